@@ -1,0 +1,88 @@
+"""Planted functional buffers (fixture spec, SURVEY.md §8d "planted" variant).
+
+A planted buffer is xorshift64 random bytes (seed 3) with a concrete instance of
+every generated string copied in twice at positions drawn from
+``random.Random(seed)``; nocase strings get a random case flip on the second
+copy.  Unlike the pure-random perf buffers these produce real matches, so the
+verifier (scan.c / re.c) and the rule conditions are exercised end to end.
+
+Everything here is deterministic (CPython ``random`` + the canonical xorshift),
+so the same bytes are rebuilt on the GPU box from the committed specs.
+"""
+import random
+import re
+
+import numpy as np
+
+_TOKEN = re.compile(r"\?\?|[0-9A-Fa-f]\?|\?[0-9A-Fa-f]|[0-9A-Fa-f]{2}|\[\d+-\d+\]")
+
+
+def _instance_hex(body: str, r: random.Random) -> bytes:
+    out = bytearray()
+    for tok in _TOKEN.findall(body):
+        if tok == "??":
+            out.append(r.getrandbits(8))
+        elif tok.startswith("["):
+            lo, hi = map(int, tok[1:-1].split("-"))
+            out.extend(r.getrandbits(8) for _ in range(r.randint(lo, hi)))
+        elif tok.endswith("?"):
+            out.append((int(tok[0], 16) << 4) | r.getrandbits(4))
+        elif tok.startswith("?"):
+            out.append((r.getrandbits(4) << 4) | int(tok[1], 16))
+        else:
+            out.append(int(tok, 16))
+    return bytes(out)
+
+
+def string_instances(rules_text: str, seed: int = 7):
+    """One concrete byte instance per string of a generated rule file.
+
+    Returns a list of (bytes, nocase) in declaration order.
+    """
+    r = random.Random(seed)
+    out = []
+    for line in rules_text.splitlines():
+        line = line.strip()
+        if not line.startswith("$"):
+            continue
+        _, rhs = line.split("=", 1)
+        rhs = rhs.strip()
+        if rhs.startswith("{"):
+            out.append((_instance_hex(rhs[1:rhs.rindex("}")], r), False))
+        else:
+            lit = rhs[1:rhs.rindex('"')]
+            out.append((lit.encode(), rhs.endswith("nocase")))
+    return out
+
+
+def _flip_case(b: bytes, r: random.Random) -> bytes:
+    return bytes((c ^ 0x20) if (65 <= c <= 90 or 97 <= c <= 122) and r.random() < 0.5 else c
+                 for c in b)
+
+
+def planted_buffer(xorshift, rules_text: str, size: int, seed: int = 3) -> np.ndarray:
+    """xorshift(size, seed) with every string instance planted twice."""
+    buf = xorshift(size, seed).copy()
+    r = random.Random(1000 + seed)
+    for data, nocase in string_instances(rules_text):
+        for copy in range(2):
+            inst = _flip_case(data, r) if (nocase and copy == 1) else data
+            pos = r.randrange(0, size - len(inst))
+            buf[pos:pos + len(inst)] = np.frombuffer(inst, dtype=np.uint8)
+    return buf
+
+
+def boundary_buffer(xorshift, atoms, size: int, period: int, seed: int = 11) -> np.ndarray:
+    """Random bytes with atoms planted so they END exactly at multiples of
+    ``period`` (and one byte either side): the adversarial slice/shard-edge case
+    of SURVEY.md Appendix A's parity-trap list."""
+    buf = xorshift(size, seed).copy()
+    r = random.Random(seed)
+    k = 0
+    for end in range(period, size, period):
+        a = atoms[k % len(atoms)]
+        k += 1
+        e = end + r.choice((-1, 0, 0, 1))
+        if e - len(a) >= 0 and e <= size:
+            buf[e - len(a):e] = np.frombuffer(a, dtype=np.uint8)
+    return buf
