@@ -1,0 +1,237 @@
+"""Benchmark: scanned GB/s per GPU of the MI355X Aho-Corasick atom scanner.
+
+Metric (BASELINE.json): "scanned GB/s per GPU (4 GiB buffer, 10k atoms) +
+bit-exact match-set vs CPU".  Workload = config C: the 10k mixed hex/ascii/
+wildcard rule set (tests/golden/tables/C.npz, compiled by stock libyara), 4 GiB
+of the canonical xorshift64 input per GPU, resident in HBM before timing.
+
+A step = one pass of the hot path over the batch: the scan kernel over the
+whole shard, candidate compaction into one ascending position array, and for
+N > 1 the RCCL gather of every rank's candidate list to rank 0 (config D:
+one logical 4N GiB buffer, rank r owns bytes [4r, 4r+4) GiB plus a 16-byte
+warm-up halo; weak scaling).
+
+    python bench.py [--gpus N] [--steps K] [--warmup W]
+    torchrun --nproc-per-node N bench.py --gpus N ...
+
+Rank 0 prints one JSON line.  value = total bytes scanned by all ranks per
+second (decimal GB/s).  roofline = the scan kernel's algorithmic HBM bytes
+(1 B per input byte) per launch / its HIP-event duration, vs
+the 8.0 TB/s HBM3E peak.  cpu_baseline = the stock reference libyara
+(oracle/_ref, yr_rules_scan_mem) on the host, 1 thread, bounded sample.
+"""
+import argparse
+import ctypes
+import json
+import os
+import sys
+import time
+
+REPO = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, REPO)
+
+GiB = 1 << 30
+HBM_PEAK_GBS = 8000.0   # MI355X HBM3E spec (MI355X_MICROARCH.md)
+
+
+def parse():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--warmup", type=int, default=3)
+    ap.add_argument("--rules", default="C", help="rule set (tests/golden/tables/<name>.npz)")
+    ap.add_argument("--gib-per-gpu", type=float, default=4.0)
+    ap.add_argument("--seed", type=int, default=1)
+    ap.add_argument("--cpu-sample-mib", type=int, default=1024)
+    ap.add_argument("--no-cpu", action="store_true")
+    ap.add_argument("--no-check", action="store_true")
+    return ap.parse_args()
+
+
+def cpu_baseline(rules: str, sample_mib: int, seed: int):
+    """Stock reference libyara yr_rules_scan_mem on the host (kind "reference"),
+    or the in-repo restatement of scanner.c:45-176 (kind "port") if the
+    reference build did not travel.  1 thread, a bounded prefix of the input."""
+    sys.path.insert(0, os.path.join(REPO, "tests", "golden"))
+    import oracle
+    n = sample_mib << 20
+    data = oracle.xorshift(n, seed)
+    ref_so = os.path.join(REPO, "oracle", "_ref", "libyara_ref.so")
+    if os.path.exists(ref_so):
+        import gen_rules
+        L = ctypes.CDLL(ref_so)
+        L.yr_initialize()
+        comp = ctypes.c_void_p()
+        assert L.yr_compiler_create(ctypes.byref(comp)) == 0
+        L.yr_compiler_add_string.argtypes = [ctypes.c_void_p, ctypes.c_char_p, ctypes.c_char_p]
+        assert L.yr_compiler_add_string(comp, gen_rules.gen(rules).encode(), None) == 0
+        rules_h = ctypes.c_void_p()
+        L.yr_compiler_get_rules.argtypes = [ctypes.c_void_p, ctypes.POINTER(ctypes.c_void_p)]
+        assert L.yr_compiler_get_rules(comp, ctypes.byref(rules_h)) == 0
+        CB = ctypes.CFUNCTYPE(ctypes.c_int, ctypes.c_void_p, ctypes.c_int, ctypes.c_void_p,
+                              ctypes.c_void_p)
+        cb = CB(lambda ctx, msg, md, ud: 0)   # CALLBACK_CONTINUE
+        L.yr_rules_scan_mem.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_size_t,
+                                        ctypes.c_int, CB, ctypes.c_void_p, ctypes.c_int]
+        t0 = time.perf_counter()
+        rc = L.yr_rules_scan_mem(rules_h, data.ctypes.data, n, 0, cb, None, 0)
+        dt = time.perf_counter() - t0
+        assert rc == 0, rc
+        kind, what = "reference", "stock libyara 4.2.1 yr_rules_scan_mem (oracle/_ref)"
+    else:
+        from conftest import ref_tables   # noqa
+        tab = ref_tables(rules)
+        t0 = time.perf_counter()
+        oracle.count_parallel(tab, data, 1)
+        dt = time.perf_counter() - t0
+        kind, what = "port", "in-repo restatement of scanner.c:45-176 (oracle/ac_oracle.c)"
+    return {"value": round(n / dt / 1e9, 4), "unit": "GB/s", "cores": 1, "kind": kind,
+            "sample": "%s, rule set %s, first %d MiB of the xorshift64 seed-%d input, 1 thread, "
+                      "%.1f s" % (what, rules, sample_mib, seed, dt)}
+
+
+def load_traffic(kernel_bytes):
+    """HBM bytes per scan-kernel launch from the committed PMC pass (profiles/)."""
+    p = os.path.join(REPO, "profiles", "pmc_traffic.json")
+    if not os.path.exists(p):
+        return None
+    try:
+        d = json.load(open(p))
+        if int(d.get("input_bytes", -1)) == kernel_bytes:
+            return int(d["hbm_bytes_per_launch"])
+    except Exception:
+        pass
+    return None
+
+
+def main():
+    args = parse()
+    sys.path.insert(0, os.path.join(REPO, "tests"))
+    import torch
+    import torch.distributed as dist
+
+    import yara_amd
+    from yara_amd._hip import memcpy
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world != args.gpus and world > 1:
+        raise SystemExit("--gpus %d but WORLD_SIZE=%d" % (args.gpus, world))
+    torch.cuda.set_device(local)
+    dev = torch.device("cuda", local)
+    if world > 1:
+        dist.init_process_group("nccl", device_id=dev)
+
+    shard = int(args.gib_per_gpu * GiB)
+    begin, end = rank * shard, (rank + 1) * shard
+    halo = 16 if begin > 0 else 0                   # >= 4-byte warm-up, 16-B aligned
+    buf = torch.empty(shard + halo + 16, dtype=torch.uint8, device=dev)
+    yara_amd.fill_xorshift64(buf.data_ptr(), shard + halo, args.seed, begin - halo)
+    torch.cuda.synchronize()
+
+    tables = yara_amd.Tables.from_npz(os.path.join(REPO, "tests", "golden", "tables",
+                                                   "%s.npz" % args.rules), device=local)
+    stream = torch.cuda.Stream(device=dev)
+    scanner = yara_amd.Scanner(tables, stream=stream.cuda_stream)
+    block = shard + halo
+
+    def step(timed_kernel=False):
+        scanner.scan_device(buf.data_ptr(), block, halo, block)
+        ptr, cnt, _ = scanner.device_result()
+        kms = scanner.kernel_ms() if timed_kernel else None
+        pos = torch.empty(max(cnt, 1), dtype=torch.int64, device=dev)
+        memcpy(pos.data_ptr(), ptr, cnt * 8, 3)
+        pos = pos[:cnt] + (begin - halo)            # global positions
+        if world > 1:
+            n_t = torch.tensor([cnt], dtype=torch.int64, device=dev)
+            counts = [torch.zeros_like(n_t) for _ in range(world)]
+            dist.all_gather(counts, n_t)
+            mx = int(max(c.item() for c in counts))
+            padded = torch.full((max(mx, 1),), -1, dtype=torch.int64, device=dev)
+            padded[:cnt] = pos
+            gathered = [torch.empty_like(padded) for _ in range(world)] if rank == 0 else None
+            dist.gather(padded, gathered, dst=0)
+            if rank == 0:
+                pos = torch.cat([g[:int(c.item())] for g, c in zip(gathered, counts)])
+        return pos, kms
+
+    for _ in range(args.warmup):
+        step()
+    scanner.set_timing(True)
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    kernel_ms = []
+    for _ in range(args.steps):
+        pos, kms = step(True)
+        kernel_ms.append(kms)
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    elapsed = time.perf_counter() - t0
+    scanner.set_timing(False)
+    if world > 1:
+        t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed = float(t.item())
+
+    total_bytes = shard * world * args.steps
+    value = total_bytes / elapsed / 1e9
+    k_avg = sum(kernel_ms) / len(kernel_ms)
+    achieved = shard / (k_avg * 1e-3) / 1e9
+
+    # parity spot check of this run's own output (rank 0): ascending and the
+    # candidate count of config C at 4 GiB recorded from the reference run
+    check = None
+    if rank == 0 and not args.no_check:
+        p = pos.cpu().numpy()
+        ok = bool((p[1:] > p[:-1]).all()) if p.size > 1 else True
+        check = {"ascending": ok, "candidates": int(p.size)}
+        if world == 1 and args.rules == "C" and shard == 4 * GiB and args.seed == 1:
+            from conftest import golden
+            import oracle
+            rec = golden()["cases"]["C_4G"]
+            check["golden_candidate_count"] = rec["candidate_count"]
+            check["match_golden"] = (int(p.size) == rec["candidate_count"] and
+                                     oracle.positions_sha(p) == rec["candidate_sha"])
+
+    if rank == 0:
+        cpu = None
+        if world == 1 and not args.no_cpu:
+            cpu = cpu_baseline(args.rules, args.cpu_sample_mib, args.seed)
+        line = {
+            "metric": "scanned GB/s per GPU (4 GiB buffer, 10k atoms) + bit-exact match-set vs CPU",
+            "value": round(value, 3),
+            "unit": "GB/s",
+            "n_gpus": world,
+            "steps": args.steps,
+            "warmup": args.warmup,
+            "ms_per_step": round(elapsed / args.steps * 1e3, 4),
+            "higher_is_better": True,
+            "scaling": "weak",
+            "vs_baseline": None,
+            "dtype": "u8",
+            "data": "synthetic (SURVEY.md App. A xorshift64 seed %d, generated in HBM)" % args.seed,
+            "config": {"workload": "config %s: %d strings -> AC tables of stock libyara 4.2.1, "
+                                   "%.0f GiB per GPU%s" % (
+                                       args.rules, {"B": 1000, "C": 10000, "E": 2000}.get(args.rules, 0),
+                                       args.gib_per_gpu,
+                                       "" if world == 1 else ", one %d GiB buffer sharded, RCCL "
+                                       "gather of candidate lists" % (args.gib_per_gpu * world)),
+                       "bytes_per_gpu": shard, "parallelism": "shard%d" % world},
+            "roofline": {"bound": "hbm", "achieved": round(achieved, 2), "peak": HBM_PEAK_GBS,
+                         "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4),
+                         "traffic": load_traffic(shard),
+                         "kernel": "scan_segments_kernel", "kernel_ms_avg": round(k_avg, 4)},
+            "cpu_baseline": cpu,
+            "check": check,
+        }
+        print(json.dumps(line), flush=True)
+    if world > 1:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

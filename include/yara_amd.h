@@ -1,0 +1,221 @@
+/*
+ * yara_amd.h -- C ABI of the MI355X (gfx950) Aho-Corasick atom scanner.
+ *
+ * Drop-in boundary for libyara's per-block AC walk.  In the reference
+ * (HoundThe/yara, libyara 4.2.1) the walk is the static function
+ *
+ *     static int _yr_scanner_scan_mem_block(YR_SCANNER* scanner,
+ *         const uint8_t* block_data, YR_MEMORY_BLOCK* block);
+ *                                          -- libyara/scanner.c:45-176
+ *
+ * called only from yr_scanner_scan_mem_blocks (scanner.c:495).  Being static it
+ * cannot be interposed; a maintainer replaces the call site with the three
+ * steps below (INTEGRATION.md shows the patch and the binding):
+ *
+ *   1. yr_amd_tables_create   once per YR_RULES: flatten the tables the rules
+ *                             compiler built (rules->ac_transition_table,
+ *                             rules->ac_match_table, rules->ac_match_pool;
+ *                             rules.c:356-363) into HBM-resident scan tables.
+ *   2. yr_amd_scan_block      per YR_MEMORY_BLOCK: the GPU walk.  Returns the
+ *                             ascending positions i in [0, size] at which the
+ *                             reference loop finds ac_match_table[state] != 0
+ *                             (scanner.c:98 and :144) -- the candidate stream.
+ *   3. yr_amd_replay          hands every candidate, in the reference's order,
+ *                             to the caller's verifier: for each i, the match
+ *                             list of state_i is walked exactly like
+ *                             scanner.c:105-121 and the callback receives
+ *                             (pool index k, offset i - backtrack) for every
+ *                             entry with backtrack <= i -- i.e. the arguments
+ *                             of yr_scan_verify_match (scan.c:992).
+ *
+ * Conventions follow libyara: every function returns an int error code
+ * (ERROR_SUCCESS = 0; codes and values from libyara/include/yara/error.h:40-109,
+ * repeated below), tables are immutable after creation and may be shared by
+ * any number of scanners/threads (as YR_RULES is, docs/capi.rst:330-347), and a
+ * scanner is used by one thread at a time (as YR_SCANNER is, scanner.h).
+ * No torch / HIP types appear in the signatures: streams are passed as void*
+ * (a hipStream_t, or NULL for the scanner's own stream).
+ */
+#ifndef YARA_AMD_H
+#define YARA_AMD_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+/* Error codes: identical values to libyara/include/yara/error.h. */
+#define YR_AMD_SUCCESS                0   /* ERROR_SUCCESS */
+#define YR_AMD_INSUFFICIENT_MEMORY    1   /* ERROR_INSUFFICIENT_MEMORY */
+#define YR_AMD_COULD_NOT_MAP_FILE     4   /* ERROR_COULD_NOT_MAP_FILE (H2D of block data failed) */
+#define YR_AMD_SCAN_TIMEOUT          26   /* ERROR_SCAN_TIMEOUT */
+#define YR_AMD_CALLBACK_ERROR        28   /* ERROR_CALLBACK_ERROR */
+#define YR_AMD_INVALID_ARGUMENT      29   /* ERROR_INVALID_ARGUMENT */
+#define YR_AMD_INTERNAL_FATAL_ERROR  31   /* ERROR_INTERNAL_FATAL_ERROR (HIP failure) */
+
+/* Max trie depth the kernels handle: YR_MAX_ATOM_LENGTH (limits.h:68). */
+#define YR_AMD_MAX_ATOM_LENGTH 4
+
+typedef struct yr_amd_tables yr_amd_tables;
+typedef struct yr_amd_scanner yr_amd_scanner;
+
+/*
+ * Build device tables from the reference's compiled AC tables.
+ *
+ *   transition_table  rules->ac_transition_table, n_slots entries
+ *                     (YR_AC_TRANSITION = uint32, ahocorasick.h:37-50)
+ *   match_table       rules->ac_match_table, n_slots entries (1-based pool
+ *                     index, 0 = no matches; ahocorasick.c:611-618)
+ *   pool_next         for k in [0, n_pool): 1-based pool index of
+ *                     rules->ac_match_pool[k].next, 0 when next == NULL
+ *   pool_backtrack    rules->ac_match_pool[k].backtrack (types.h:343)
+ *   device            HIP device ordinal the tables live on, or -1 for
+ *                     host-only tables (flattening + yr_amd_replay only; no
+ *                     scanner can be created on them)
+ *
+ * n_slots = yr_arena_get_current_offset(arena, YR_AC_TRANSITION_TABLE) /
+ *           sizeof(YR_AC_TRANSITION)                         (rules.c:442-444)
+ * Returns YR_AMD_INVALID_ARGUMENT if the trie is deeper than
+ * YR_AMD_MAX_ATOM_LENGTH or the tables are malformed.
+ */
+int yr_amd_tables_create(
+    const uint32_t* transition_table,
+    const uint32_t* match_table,
+    uint32_t n_slots,
+    const uint32_t* pool_next,
+    const uint16_t* pool_backtrack,
+    uint32_t n_pool,
+    int device,
+    yr_amd_tables** tables);
+
+int yr_amd_tables_destroy(yr_amd_tables* tables);
+
+/* Diagnostics of the flattened form (yr_rules_get_stats analogue, rules.c:438). */
+typedef struct
+{
+  uint32_t n_slots;
+  uint32_t n_states;           /* trie nodes incl. root */
+  uint32_t max_depth;
+  uint32_t states_by_depth[YR_AMD_MAX_ATOM_LENGTH + 1];
+  uint32_t accepting_states;   /* states with ac_match_table != 0 */
+  uint32_t keys_by_length[YR_AMD_MAX_ATOM_LENGTH + 1]; /* minimal accepting suffixes */
+  uint32_t root_accepting;     /* 1: every position is a candidate */
+  uint32_t filter_bits;        /* log2 of the LDS window-filter size in bits */
+  uint32_t filter_set_bits;    /* populated bits of that filter */
+  uint32_t exact_slots;        /* slots of the HBM exact-suffix hash table */
+} yr_amd_tables_info;
+
+int yr_amd_tables_get_info(const yr_amd_tables* tables, yr_amd_tables_info* info);
+
+/*
+ * A scanner owns a HIP stream and the device workspace for one scan at a time.
+ * stream: a hipStream_t to run on, or NULL to create a private stream.
+ */
+int yr_amd_scanner_create(
+    yr_amd_tables* tables,
+    void* stream,
+    yr_amd_scanner** scanner);
+
+int yr_amd_scanner_destroy(yr_amd_scanner* scanner);
+
+/*
+ * Scan one block that lives in HOST memory (the _yr_scanner_scan_mem_block
+ * replacement).  The block is copied to HBM, scanned, and the candidate
+ * stream copied back.  On success *positions points to *count ascending
+ * positions in [0, size], owned by the scanner and valid until its next scan.
+ * If *all_positions is set the rules have a non-empty root match list
+ * (ac_match_table[0] != 0): every position 0..size is a candidate and the
+ * positions array is empty.
+ */
+int yr_amd_scan_block(
+    yr_amd_scanner* scanner,
+    const uint8_t* data,
+    size_t size,
+    const uint64_t** positions,
+    uint64_t* count,
+    int* all_positions);
+
+/*
+ * Device-resident scan (the hot path the benchmark times): data is already in
+ * HBM.  Scans the bytes [byte_begin, byte_end) of a block of block_size bytes,
+ * i.e. reports candidate positions i in (byte_begin, byte_end] (position 0 is
+ * reported iff byte_begin == 0 and the root is accepting), reading up to
+ * YR_AMD_MAX_ATOM_LENGTH bytes before byte_begin as warm-up.  Shards of one
+ * block scanned this way concatenate into exactly the full block's stream.
+ *
+ * Asynchronous on the scanner's stream: results become available through
+ * yr_amd_scan_device_result after the stream is synchronised.
+ * Requirements: d_data 16-byte aligned, byte_begin % 16 == 0.
+ */
+int yr_amd_scan_device(
+    yr_amd_scanner* scanner,
+    const uint8_t* d_data,
+    uint64_t block_size,
+    uint64_t byte_begin,
+    uint64_t byte_end);
+
+/*
+ * Result of the last yr_amd_scan_device: synchronises the stream, retries
+ * once with exact output capacity if a segment overflowed, and returns a
+ * DEVICE pointer to the ascending candidate positions (uint64) and the count.
+ */
+int yr_amd_scan_device_result(
+    yr_amd_scanner* scanner,
+    const uint64_t** d_positions,
+    uint64_t* count,
+    int* all_positions);
+
+/*
+ * Verification callback: the arguments the reference passes to
+ * yr_scan_verify_match(scanner, &rules->ac_match_pool[pool_index], data,
+ * size, base, offset) (scanner.c:111-117).  A non-zero return aborts the
+ * replay and is returned by yr_amd_replay (GOTO_EXIT_ON_ERROR semantics).
+ */
+typedef int (*yr_amd_verify_fn)(void* user, uint32_t pool_index, uint64_t offset);
+
+/*
+ * Replay a candidate stream in the reference order.  For every candidate i
+ * (or every i in [0, size] when all_positions), the AC state is recomputed on
+ * the host from position max(0, i - YR_AMD_MAX_ATOM_LENGTH) (exact: the trie
+ * is at most that deep), and its match list is walked as scanner.c:105-121
+ * does.  Candidates whose state has no match list are a protocol error
+ * (YR_AMD_INTERNAL_FATAL_ERROR).
+ */
+int yr_amd_replay(
+    const yr_amd_tables* tables,
+    const uint8_t* data,
+    size_t size,
+    const uint64_t* positions,
+    uint64_t count,
+    int all_positions,
+    yr_amd_verify_fn verify,
+    void* user);
+
+/*
+ * Kernel timing (measurement support): when enabled, the scanner records HIP
+ * events around its scan kernel on its own stream; yr_amd_scanner_kernel_ms
+ * returns the duration of the last scan kernel launch (after the scan result
+ * was collected).
+ */
+int yr_amd_scanner_set_timing(yr_amd_scanner* scanner, int enable);
+int yr_amd_scanner_kernel_ms(yr_amd_scanner* scanner, float* ms);
+
+/*
+ * Benchmark/test utility (not part of the libyara path): fill a device buffer
+ * with bytes [offset, offset + n) of the canonical synthetic input of
+ * SURVEY.md Appendix A (xorshift64, byte = (uint8_t)(x >> 24),
+ * x0 = 0x9E3779B97F4A7C15 * seed), generated in parallel on the GPU with GF(2)
+ * jump-ahead.  stream: hipStream_t or NULL.
+ */
+int yr_amd_fill_xorshift64(void* d_buf, uint64_t n, uint64_t seed, uint64_t offset, void* stream);
+
+/* Library version string, e.g. "yara_amd 0.1.0 (gfx950)". */
+const char* yr_amd_version(void);
+
+#ifdef __cplusplus
+}
+#endif
+
+#endif

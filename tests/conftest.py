@@ -1,0 +1,78 @@
+"""Shared fixtures.  CPU tests run everywhere; @pytest.mark.gpu tests need a GPU.
+
+The golden vectors under tests/golden/ were produced by the stock reference
+libyara (tests/golden/make_golden.py); the reference itself is never needed
+here, so the GPU box runs all of this from the committed fixtures.
+"""
+import json
+import os
+import sys
+
+import numpy as np
+import pytest
+
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+GOLDEN = os.path.join(REPO, "tests", "golden")
+sys.path.insert(0, REPO)
+sys.path.insert(0, GOLDEN)
+
+
+def pytest_configure(config):
+    config.addinivalue_line("markers", "gpu: needs an MI355X (runs through libyara_amd.so)")
+    config.addinivalue_line("markers", "slow: multi-GiB parity cases")
+
+
+def golden():
+    with open(os.path.join(GOLDEN, "golden.json")) as f:
+        return json.load(f)
+
+
+def tables_npz(name):
+    return os.path.join(GOLDEN, "tables", "%s.npz" % name)
+
+
+def ref_tables(name):
+    """Reference tables as a plain namespace for the oracle."""
+    from oracle.tables import RefTables
+    z = np.load(tables_npz(name))
+    return RefTables(z["T"], z["M"], z["pool_next"], z["pool_string"], z["pool_backtrack"])
+
+
+def case_arrays(case):
+    p = os.path.join(GOLDEN, "cases", "%s.npz" % case)
+    return np.load(p) if os.path.exists(p) else None
+
+
+ALPHA = b"abcdxyzHeloC\x00\x01\xff"
+
+
+def case_data(rec):
+    """Rebuild the exact input bytes of a golden case (deterministic generators)."""
+    import oracle
+    import gen_rules
+    import planted
+    spec = rec["data"]
+    kind = spec[0]
+    if kind == "xs":
+        return oracle.xorshift(spec[2], spec[1])
+    if kind == "planted":
+        return planted.planted_buffer(oracle.xorshift, gen_rules.gen(spec[1]), spec[3], spec[2])
+    if kind == "alpha":
+        x = oracle.xorshift(spec[2], spec[1])
+        return np.frombuffer(ALPHA, dtype=np.uint8)[x % len(ALPHA)]
+    if kind == "file":
+        return np.frombuffer(bytes.fromhex(rec["data_bytes_hex"]), dtype=np.uint8)
+    raise ValueError(kind)
+
+
+def gpu_available():
+    try:
+        import torch
+        return torch.cuda.is_available()
+    except Exception:
+        return False
+
+
+@pytest.fixture(scope="session")
+def gold():
+    return golden()

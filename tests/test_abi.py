@@ -1,0 +1,169 @@
+"""C-ABI checks that need no GPU: exports, host-only flattening, replay order,
+error behaviour (libyara ERROR_* conventions)."""
+import ctypes
+import os
+import re
+import subprocess
+
+import numpy as np
+import pytest
+
+import oracle
+import yara_amd
+from yara_amd import _lib
+from conftest import REPO, case_arrays, case_data, golden, ref_tables, tables_npz
+
+HEADER = os.path.join(REPO, "include", "yara_amd.h")
+
+
+def declared_functions():
+    src = open(HEADER).read()
+    src = re.sub(r"/\*.*?\*/", "", src, flags=re.S)
+    return sorted(set(re.findall(r"\b(yr_amd_\w+)\s*\(", src)))
+
+
+def test_library_exports_every_declared_symbol():
+    names = declared_functions()
+    assert len(names) >= 10
+    L = _lib.lib()
+    for n in names:
+        assert hasattr(L, n), n
+    out = subprocess.run(["nm", "-D", "--defined-only", _lib.LIB_PATH], capture_output=True,
+                         text=True, check=True).stdout
+    exported = set(re.findall(r"\bT (yr_amd_\w+)", out))
+    assert set(names) <= exported
+    assert set(_lib.PROTOTYPES) == set(names)   # the Python binding covers the ABI exactly
+
+
+def test_library_is_gfx950_code():
+    """The embedded code object targets gfx950 (MI355X) and only gfx950."""
+    blob = open(_lib.LIB_PATH, "rb").read()
+    assert b"amdgcn-amd-amdhsa--gfx950" in blob
+    assert b"gfx942" not in blob and b"gfx90a" not in blob
+
+
+@pytest.mark.parametrize("name,states,depth,keys", [
+    ("B", 3244, [1, 252, 991, 1000, 1000], [0, 0, 0, 0, 1000]),
+    ("C", 29923, [1, 256, 9064, 11501, 9101], [0, 0, 0, 2426, 9101]),
+    ("E", 28983, [1, 253, 2972, 8757, 17000], [0, 0, 0, 0, 17000]),
+])
+def test_flattening_stats(name, states, depth, keys):
+    t = yara_amd.Tables.from_npz(tables_npz(name), device=-1)
+    inf = t.info()
+    assert inf["n_states"] == states
+    assert inf["states_by_depth"] == depth
+    assert inf["keys_by_length"] == keys
+    assert inf["max_depth"] == 4 and inf["root_accepting"] == 0
+    # filter density bounds the stage-2 rate
+    assert inf["filter_set_bits"] / (1 << inf["filter_bits"]) < 0.02
+
+
+def test_short_and_root_tables():
+    s = yara_amd.Tables.from_npz(tables_npz("short"), device=-1).info()
+    assert s["keys_by_length"][1] >= 1 and s["keys_by_length"][2] >= 1
+    r = yara_amd.Tables.from_npz(tables_npz("root"), device=-1).info()
+    assert r["root_accepting"] == 1
+
+
+REPLAY_CASES = ["A_sample", "B_64M", "C_64M", "short_1M", "root_4K", "C_empty", "short_3",
+                "C_planted16M"]
+
+
+@pytest.mark.parametrize("case", REPLAY_CASES)
+def test_replay_of_oracle_candidates_reproduces_reference(case):
+    """Host replay (product) fed the oracle's candidate stream == reference calls."""
+    rec = golden()["cases"][case]
+    data = case_data(rec)
+    tab = ref_tables(rec["rules"])
+    t = yara_amd.Tables.from_npz(tables_npz(rec["rules"]), device=-1)
+    allp = bool(t.info()["root_accepting"])
+    cand = None if allp else oracle.candidates(tab, data)
+    P, K = [], []
+
+    def verify(k, off):
+        K.append(k)
+        P.append(off + int(tab.pool_backtrack[k]))
+        return 0
+    assert yara_amd.replay(t, data, cand, allp, verify) == 0
+    pos, idx = np.array(P, np.uint64), np.array(K, np.uint32)
+    assert len(pos) == rec["verify_count"]
+    assert oracle.verify_stream_sha(pos, idx) == rec["verify_sha"]
+    full = case_arrays(case)
+    np.testing.assert_array_equal(pos, full["verify_pos"])
+    np.testing.assert_array_equal(idx, full["verify_idx"])
+
+
+def test_replay_propagates_verify_error():
+    """A failing verify aborts the block (GOTO_EXIT_ON_ERROR, scanner.c:111)."""
+    rec = golden()["cases"]["short_1M"]
+    data = case_data(rec)
+    t = yara_amd.Tables.from_npz(tables_npz("short"), device=-1)
+    cand = oracle.candidates(ref_tables("short"), data)
+    calls = []
+
+    def verify(k, off):
+        calls.append(k)
+        return 30 if len(calls) == 5 else 0   # ERROR_TOO_MANY_MATCHES
+    assert yara_amd.replay(t, data, cand, False, verify) == 30
+    assert len(calls) == 5
+
+
+def test_replay_rejects_unsorted_and_out_of_range():
+    data = case_data(golden()["cases"]["short_1M"])[:4096]
+    t = yara_amd.Tables.from_npz(tables_npz("short"), device=-1)
+    cand = oracle.candidates(ref_tables("short"), data)
+    assert cand.size > 3
+    bad = cand.copy()
+    bad[[1, 2]] = bad[[2, 1]]
+    assert yara_amd.replay(t, data, bad, False, lambda k, o: 0) == _lib.INVALID_ARGUMENT
+    assert yara_amd.replay(t, data, np.array([data.size + 1], np.uint64), False,
+                           lambda k, o: 0) == _lib.INVALID_ARGUMENT
+
+
+def test_replay_rejects_non_candidate():
+    data = np.zeros(64, np.uint8)   # no atom of `C` is all zeros
+    t = yara_amd.Tables.from_npz(tables_npz("C"), device=-1)
+    assert yara_amd.replay(t, data, np.array([10], np.uint64), False,
+                           lambda k, o: 0) == _lib.INTERNAL_FATAL_ERROR
+
+
+def _mk(T, M, nx=(), bt=()):
+    return yara_amd.Tables(np.array(T, np.uint32), np.array(M, np.uint32),
+                           np.array(nx, np.uint32), np.array(bt, np.uint16), device=-1)
+
+
+def test_rejects_trie_deeper_than_max_atom_length():
+    # chain of 5 states each with one child on byte 0x41 ('A'), rows 512 apart
+    n = 512 * 7
+    T = np.zeros(n, np.uint32)
+    M = np.zeros(n, np.uint32)
+    rows = [0] + [512 * (k + 1) for k in range(6)]
+    for d in range(5):
+        s, c = rows[d], rows[d + 1]
+        T[s + 0x41 + 1] = (c << 9) | (0x41 + 1)
+    M[rows[5]] = 1
+    with pytest.raises(yara_amd.YaraAmdError) as e:
+        yara_amd.Tables(T, M, np.array([0], np.uint32), np.array([5], np.uint16), device=-1)
+    assert e.value.code == _lib.INVALID_ARGUMENT
+
+
+def test_rejects_cyclic_match_pool():
+    T = np.zeros(1024, np.uint32)
+    M = np.zeros(1024, np.uint32)
+    T[0x41 + 1] = (512 << 9) | (0x41 + 1)   # root --'A'--> state at slot 512
+    M[512] = 1
+    _mk(T, M, nx=[0, 1], bt=[1, 1])          # well-formed: accepted
+    with pytest.raises(yara_amd.YaraAmdError) as e:
+        _mk(T, M, nx=[2, 1], bt=[1, 1])      # 1 -> 2 -> 1 ...
+    assert e.value.code == _lib.INVALID_ARGUMENT
+
+
+def test_scanner_on_host_only_tables_is_invalid():
+    t = yara_amd.Tables.from_npz(tables_npz("B"), device=-1)
+    with pytest.raises(yara_amd.YaraAmdError) as e:
+        yara_amd.Scanner(t)
+    assert e.value.code == _lib.INVALID_ARGUMENT
+
+
+def test_version():
+    assert "gfx950" in yara_amd.version()

@@ -1,0 +1,191 @@
+"""GPU parity: the HIP path (libyara_amd.so through its C ABI) against the
+pinned oracle and the reference's golden streams.
+
+Bar: bit-exact.  The candidate stream (ascending positions with
+ac_match_table[state] != 0) must equal the oracle's, and the verify-call
+stream produced by GPU candidates + host replay must equal the stream the
+stock libyara hot loop produced (golden SHA-256 / full arrays).
+"""
+import numpy as np
+import pytest
+
+import oracle
+import yara_amd
+from conftest import case_arrays, case_data, golden, ref_tables, tables_npz
+
+pytestmark = pytest.mark.gpu
+
+CASES = golden()["cases"]
+_TABLES = {}
+
+
+def dev_tables(name):
+    if name not in _TABLES:
+        _TABLES[name] = yara_amd.Tables.from_npz(tables_npz(name), device=0)
+    return _TABLES[name]
+
+
+def _torch():
+    import torch
+    assert torch.cuda.is_available(), "GPU tests need a GPU"
+    return torch
+
+
+def blocks(size, bsize, overlap):
+    if size == 0:
+        return [(0, 0)]
+    out, base = [], 0
+    while base < size:
+        n = min(bsize, size - base)
+        out.append((base, n))
+        base = size if base + n >= size else base + n - overlap
+    return out
+
+
+SINGLE = [k for k, v in CASES.items() if v["size"] <= (64 << 20) and not v["block"]]
+MULTI = [k for k, v in CASES.items() if v["block"]]
+
+
+@pytest.mark.parametrize("case", SINGLE)
+def test_candidates_and_verify_stream(case):
+    rec = CASES[case]
+    data = case_data(rec)
+    sc = yara_amd.Scanner(dev_tables(rec["rules"]))
+    pos, allp = sc.candidates(data)
+    if allp:
+        assert rec["rules"] == "root"
+    else:
+        assert len(pos) == rec["candidate_count"]
+        assert oracle.positions_sha(pos) == rec["candidate_sha"]
+    P, K = sc.verify_stream(data)
+    assert len(P) == rec["verify_count"]
+    assert oracle.verify_stream_sha(P, K) == rec["verify_sha"]
+    full = case_arrays(case)
+    if full is not None:
+        np.testing.assert_array_equal(P, full["verify_pos"])
+        np.testing.assert_array_equal(K, full["verify_idx"])
+
+
+@pytest.mark.parametrize("case", MULTI)
+def test_multi_block_iterator(case):
+    """State resets per YR_MEMORY_BLOCK (scanner.c:69); offsets per block base."""
+    rec = CASES[case]
+    data = case_data(rec)
+    sc = yara_amd.Scanner(dev_tables(rec["rules"]))
+    P, K, B = [], [], []
+    for base, n in blocks(data.size, rec["block"], rec["overlap"]):
+        p, k = sc.verify_stream(data[base:base + n])
+        P.append(p); K.append(k); B.append(np.full(p.size, base, np.uint64))
+    P, K, B = np.concatenate(P), np.concatenate(K), np.concatenate(B)
+    assert len(P) == rec["verify_count"]
+    assert oracle.verify_stream_sha(P, K, base=B) == rec["verify_sha"]
+
+
+@pytest.mark.parametrize("rules", ["B", "C", "E", "short"])
+@pytest.mark.parametrize("size", [0, 1, 2, 3, 4, 5, 15, 16, 17, 100, 1023, 1024, 1025,
+                                  4095, 4097, 65535, 65536, 65537, 262144 + 7, 3_000_001])
+def test_ragged_sizes_vs_oracle(rules, size):
+    """Empty and ragged blocks, tile/segment edges, tails not multiple of 16."""
+    if rules == "short":
+        x = oracle.xorshift(size, 17)
+        data = np.frombuffer(b"abcdxyzHeloC\x00\x01\xff", np.uint8)[x % 15]
+    else:
+        data = oracle.xorshift(size, 23)
+    tab = ref_tables(rules)
+    sc = yara_amd.Scanner(dev_tables(rules))
+    pos, allp = sc.candidates(data)
+    assert not allp
+    np.testing.assert_array_equal(pos, oracle.candidates(tab, data))
+
+
+@pytest.mark.parametrize("period", [16, 1024, 4096, 65536])
+def test_atoms_ending_on_slice_boundaries(period):
+    """Adversarial: atoms end exactly at lane/tile/segment edges (+-1 byte)."""
+    import planted
+    import gen_rules
+    tab = ref_tables("C")
+    inst = planted.string_instances(gen_rules.gen("C"))
+    atoms = [b for b, _ in inst if len(b) >= 4][:500]
+    data = planted.boundary_buffer(oracle.xorshift, atoms, 4 << 20, period)
+    sc = yara_amd.Scanner(dev_tables("C"))
+    pos, _ = sc.candidates(data)
+    ref = oracle.candidates(tab, data)
+    assert len(ref) > (4 << 20) // period // 2
+    np.testing.assert_array_equal(pos, ref)
+
+
+def test_periodic_data_deep_chains():
+    """'aaaa...' keeps the automaton in depth-3/4 states (failure chains)."""
+    tab = ref_tables("short")
+    sc = yara_amd.Scanner(dev_tables("short"))
+    for pat in (b"a", b"ab", b"abc", b"abcd", b"aab", b"\x00\x01", b"\xff"):
+        data = np.frombuffer(pat * (300_000 // len(pat)), np.uint8)
+        pos, _ = sc.candidates(data)
+        np.testing.assert_array_equal(pos, oracle.candidates(tab, data))
+
+
+def test_device_generator_matches_canonical():
+    torch = _torch()
+    for n in (1, 15, 16, 1000, 65536, 65536 * 3 + 5, 1 << 22):
+        d = torch.empty(max(n, 16), dtype=torch.uint8, device="cuda")
+        yara_amd.fill_xorshift64(d.data_ptr(), n, 1)
+        torch.cuda.synchronize()
+        np.testing.assert_array_equal(d[:n].cpu().numpy(), oracle.xorshift(n, 1))
+
+
+def test_device_shards_concatenate_to_full_stream():
+    """Shards [a, b) with a 4-byte warm-up read concatenate exactly (multi-GPU basis)."""
+    torch = _torch()
+    n = (16 << 20) + 12345
+    d = torch.empty(n + 16, dtype=torch.uint8, device="cuda")
+    yara_amd.fill_xorshift64(d.data_ptr(), n, 9)
+    torch.cuda.synchronize()
+    sc = yara_amd.Scanner(dev_tables("C"))
+    sc.scan_device(d.data_ptr(), n)
+    full = _d2h(torch, *sc.device_result()[:2])
+    rng = np.random.default_rng(5)
+    cuts = sorted(set([0, n] + [int(c) // 16 * 16 for c in rng.integers(0, n, 9)]))
+    parts = []
+    for a, b in zip(cuts[:-1], cuts[1:]):
+        sc.scan_device(d.data_ptr(), n, a, b)
+        parts.append(_d2h(torch, *sc.device_result()[:2]))
+    np.testing.assert_array_equal(np.concatenate(parts), full)
+    np.testing.assert_array_equal(full, oracle.candidates(ref_tables("C"), d[:n].cpu().numpy()))
+
+
+def _d2h(torch, ptr, count):
+    from yara_amd._hip import d2h_u64
+    return d2h_u64(ptr, count)
+
+
+@pytest.mark.slow
+@pytest.mark.parametrize("case", ["C_4G", "E_1G"])
+def test_full_size_against_reference(case):
+    """BASELINE sizes (4 GiB / 1 GiB): GPU candidates from device-resident data
+    equal the oracle's count/SHA recorded at golden time, and GPU candidates +
+    replay reproduce the stock libyara verify stream."""
+    torch = _torch()
+    rec = CASES[case]
+    n = rec["size"]
+    d = torch.empty(n + 16, dtype=torch.uint8, device="cuda")
+    yara_amd.fill_xorshift64(d.data_ptr(), n, rec["data"][1])
+    torch.cuda.synchronize()
+    sc = yara_amd.Scanner(dev_tables(rec["rules"]))
+    sc.scan_device(d.data_ptr(), n)
+    ptr, cnt, allp = sc.device_result()
+    pos = _d2h(torch, ptr, cnt)
+    assert cnt == rec["candidate_count"]
+    assert oracle.positions_sha(pos) == rec["candidate_sha"]
+    assert np.all(np.diff(pos.astype(np.int64)) > 0)
+    host = d[:n].cpu().numpy()
+    del d
+    P, K = [], []
+    bt = dev_tables(rec["rules"])._bt
+
+    def verify(k, off):
+        K.append(k)
+        P.append(off + int(bt[k]))
+        return 0
+    assert yara_amd.replay(dev_tables(rec["rules"]), host, pos, allp, verify) == 0
+    assert len(P) == rec["verify_count"]
+    assert oracle.verify_stream_sha(np.array(P, np.uint64), np.array(K, np.uint32)) == rec["verify_sha"]

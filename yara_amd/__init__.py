@@ -1,0 +1,215 @@
+"""yara_amd -- MI355X-native Aho-Corasick atom scanner for libyara.
+
+Python mirror of the hot-path interface (the C ABI in include/yara_amd.h is
+the product boundary; this module is a thin ctypes host layer over it, used by
+the tests, the benchmark and smoke()).
+
+Reference interface mirrored (HoundThe/yara, libyara 4.2.1):
+  * ``Tables``      <- the AC tables of a compiled YR_RULES
+                       (rules->ac_transition_table / ac_match_table /
+                       ac_match_pool, rules.c:356-363)
+  * ``Scanner.scan_mem_block(data, verify)`` <- ``_yr_scanner_scan_mem_block``
+                       (scanner.c:45-176): same dispatch order, same verify
+                       arguments (pool index, offset) as its calls to
+                       ``yr_scan_verify_match`` (scan.c:992), same int error
+                       convention (ERROR_* values of error.h).
+"""
+import ctypes
+
+import numpy as np
+
+from . import _lib
+from ._lib import (CALLBACK_ERROR, COULD_NOT_MAP_FILE, INSUFFICIENT_MEMORY,  # noqa: F401
+                   INTERNAL_FATAL_ERROR, INVALID_ARGUMENT, MAX_ATOM_LENGTH, SCAN_TIMEOUT, SUCCESS,
+                   YaraAmdError)
+
+__all__ = ["Tables", "Scanner", "replay", "fill_xorshift64", "version", "YaraAmdError"]
+
+
+def _arr(a, dt):
+    return np.ascontiguousarray(a, dtype=dt)
+
+
+def version() -> str:
+    return _lib.lib().yr_amd_version().decode()
+
+
+class Tables:
+    """Flattened, device-resident scan tables (one per compiled rule set).
+
+    ``device=-1`` builds host-only tables: flattening + replay, no scanner.
+    """
+
+    def __init__(self, T, M, pool_next, pool_backtrack, device: int = 0):
+        L = _lib.lib()
+        self._T = _arr(T, np.uint32)
+        self._M = _arr(M, np.uint32)
+        self._nx = _arr(pool_next, np.uint32)
+        self._bt = _arr(pool_backtrack, np.uint16)
+        if self._T.size != self._M.size:
+            raise ValueError("transition and match tables differ in length")
+        if self._nx.size != self._bt.size:
+            raise ValueError("pool arrays differ in length")
+        nx = self._nx if self._nx.size else np.zeros(1, np.uint32)
+        bt = self._bt if self._bt.size else np.zeros(1, np.uint16)
+        h = ctypes.c_void_p()
+        rc = L.yr_amd_tables_create(
+            self._T.ctypes.data_as(_lib._u32p), self._M.ctypes.data_as(_lib._u32p), self._T.size,
+            nx.ctypes.data_as(_lib._u32p), bt.ctypes.data_as(_lib._u16p), self._nx.size, device,
+            ctypes.byref(h))
+        _lib.check("yr_amd_tables_create", rc)
+        self._h = h
+        self.device = device
+
+    @classmethod
+    def from_npz(cls, path, device: int = 0):
+        z = np.load(path)
+        t = cls(z["T"], z["M"], z["pool_next"], z["pool_backtrack"], device=device)
+        t.pool_string = z["pool_string"] if "pool_string" in z else None
+        return t
+
+    @property
+    def handle(self):
+        return self._h
+
+    def info(self) -> dict:
+        inf = _lib.TablesInfo()
+        _lib.check("yr_amd_tables_get_info", _lib.lib().yr_amd_tables_get_info(self._h, ctypes.byref(inf)))
+        d = {}
+        for name, _ in inf._fields_:
+            v = getattr(inf, name)
+            d[name] = list(v) if not isinstance(v, int) else v
+        return d
+
+    def close(self):
+        if getattr(self, "_h", None):
+            _lib.lib().yr_amd_tables_destroy(self._h)
+            self._h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+
+def replay(tables: Tables, data: np.ndarray, positions, all_positions: bool, verify) -> int:
+    """Replay a candidate stream into ``verify(pool_index, offset) -> int``.
+
+    Returns the first non-zero verify result, or 0.  Order and arguments are
+    those of the reference's calls to yr_scan_verify_match (scanner.c:105-121).
+    """
+    d = _arr(data, np.uint8)
+    if d.size == 0:
+        d = np.zeros(1, np.uint8)
+    pos = _arr(positions if positions is not None else [], np.uint64)
+    pos_p = pos.ctypes.data_as(_lib._u64p) if pos.size else None
+    err = []
+
+    def _cb(_user, k, off):
+        try:
+            return int(verify(int(k), int(off)))
+        except Exception as e:  # never unwind through C
+            err.append(e)
+            return CALLBACK_ERROR
+
+    cb = _lib.VERIFY_FN(_cb)
+    rc = _lib.lib().yr_amd_replay(tables.handle, d.ctypes.data_as(_lib._u8p), int(data.size), pos_p,
+                                  int(pos.size), 1 if all_positions else 0, cb, None)
+    if err:
+        raise err[0]
+    return rc
+
+
+class Scanner:
+    """One scan at a time on its own HIP stream (or on ``stream``)."""
+
+    def __init__(self, tables: Tables, stream: int = 0):
+        h = ctypes.c_void_p()
+        _lib.check("yr_amd_scanner_create",
+                   _lib.lib().yr_amd_scanner_create(tables.handle, ctypes.c_void_p(stream or None),
+                                                    ctypes.byref(h)))
+        self._h = h
+        self.tables = tables
+
+    # -- host block: the _yr_scanner_scan_mem_block replacement ---------------
+    def candidates(self, data: np.ndarray):
+        """(positions uint64[], all_positions) for a block in host memory."""
+        d = _arr(data, np.uint8)
+        ptr = ctypes.POINTER(ctypes.c_uint64)()
+        cnt = ctypes.c_uint64()
+        allp = ctypes.c_int()
+        dp = d.ctypes.data_as(_lib._u8p) if d.size else None
+        _lib.check("yr_amd_scan_block",
+                   _lib.lib().yr_amd_scan_block(self._h, dp, d.size, ctypes.byref(ptr),
+                                                ctypes.byref(cnt), ctypes.byref(allp)))
+        n = cnt.value
+        pos = np.ctypeslib.as_array(ptr, shape=(n,)).copy() if n else np.zeros(0, np.uint64)
+        return pos, bool(allp.value)
+
+    def scan_mem_block(self, data: np.ndarray, verify) -> int:
+        """Mirror of _yr_scanner_scan_mem_block (scanner.c:45-176): GPU candidate
+        detection, then the reference-ordered verify calls.  Returns an ERROR_* code."""
+        try:
+            pos, allp = self.candidates(data)
+        except YaraAmdError as e:
+            return e.code
+        return replay(self.tables, data, pos, allp, verify)
+
+    def verify_stream(self, data: np.ndarray):
+        """(positions, pool indexes) of every verify call the block would make."""
+        P, K = [], []
+
+        def cb(k, off):
+            K.append(k)
+            P.append(off + int(self.tables._bt[k]))
+            return 0
+        rc = self.scan_mem_block(data, cb)
+        _lib.check("scan_mem_block", rc)
+        return np.array(P, dtype=np.uint64), np.array(K, dtype=np.uint32)
+
+    # -- device-resident block (benchmark path) -------------------------------
+    def scan_device(self, d_ptr: int, block_size: int, byte_begin: int = 0, byte_end=None):
+        if byte_end is None:
+            byte_end = block_size
+        _lib.check("yr_amd_scan_device",
+                   _lib.lib().yr_amd_scan_device(self._h, ctypes.c_void_p(d_ptr), block_size,
+                                                 byte_begin, byte_end))
+
+    def device_result(self):
+        """(device pointer to uint64 positions, count, all_positions)."""
+        p = ctypes.c_void_p()
+        cnt = ctypes.c_uint64()
+        allp = ctypes.c_int()
+        _lib.check("yr_amd_scan_device_result",
+                   _lib.lib().yr_amd_scan_device_result(self._h, ctypes.byref(p), ctypes.byref(cnt),
+                                                        ctypes.byref(allp)))
+        return p.value or 0, cnt.value, bool(allp.value)
+
+    def set_timing(self, enable: bool = True):
+        _lib.check("yr_amd_scanner_set_timing", _lib.lib().yr_amd_scanner_set_timing(self._h, int(enable)))
+
+    def kernel_ms(self) -> float:
+        """Duration of the last scan kernel launch (HIP events on the scan stream)."""
+        ms = ctypes.c_float()
+        _lib.check("yr_amd_scanner_kernel_ms", _lib.lib().yr_amd_scanner_kernel_ms(self._h, ctypes.byref(ms)))
+        return ms.value
+
+    def close(self):
+        if getattr(self, "_h", None):
+            _lib.lib().yr_amd_scanner_destroy(self._h)
+            self._h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+
+def fill_xorshift64(d_ptr: int, n: int, seed: int, offset: int = 0, stream: int = 0):
+    """Fill device memory with bytes [offset, offset+n) of the SURVEY.md App. A
+    synthetic buffer (bench/test utility)."""
+    _lib.check("yr_amd_fill_xorshift64",
+               _lib.lib().yr_amd_fill_xorshift64(ctypes.c_void_p(d_ptr), n, seed, offset,
+                                                 ctypes.c_void_p(stream or None)))

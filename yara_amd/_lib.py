@@ -1,0 +1,103 @@
+"""ctypes binding of libyara_amd.so (the C ABI declared in include/yara_amd.h).
+
+The HIP library is the product; this module only loads it.  There is no
+fallback: if the shared object is missing or fails to load, importing raises.
+"""
+import ctypes
+import os
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(_HERE, "libyara_amd.so")
+
+# error codes (libyara/include/yara/error.h values)
+SUCCESS = 0
+INSUFFICIENT_MEMORY = 1
+COULD_NOT_MAP_FILE = 4
+SCAN_TIMEOUT = 26
+CALLBACK_ERROR = 28
+INVALID_ARGUMENT = 29
+INTERNAL_FATAL_ERROR = 31
+MAX_ATOM_LENGTH = 4
+
+_u32p = ctypes.POINTER(ctypes.c_uint32)
+_u16p = ctypes.POINTER(ctypes.c_uint16)
+_u64p = ctypes.POINTER(ctypes.c_uint64)
+_u8p = ctypes.POINTER(ctypes.c_uint8)
+_vp = ctypes.c_void_p
+_int = ctypes.c_int
+
+VERIFY_FN = ctypes.CFUNCTYPE(ctypes.c_int, ctypes.c_void_p, ctypes.c_uint32, ctypes.c_uint64)
+
+
+class TablesInfo(ctypes.Structure):
+    _fields_ = [
+        ("n_slots", ctypes.c_uint32),
+        ("n_states", ctypes.c_uint32),
+        ("max_depth", ctypes.c_uint32),
+        ("states_by_depth", ctypes.c_uint32 * (MAX_ATOM_LENGTH + 1)),
+        ("accepting_states", ctypes.c_uint32),
+        ("keys_by_length", ctypes.c_uint32 * (MAX_ATOM_LENGTH + 1)),
+        ("root_accepting", ctypes.c_uint32),
+        ("filter_bits", ctypes.c_uint32),
+        ("filter_set_bits", ctypes.c_uint32),
+        ("exact_slots", ctypes.c_uint32),
+    ]
+
+
+# name -> (restype, argtypes); every function include/yara_amd.h declares
+PROTOTYPES = {
+    "yr_amd_tables_create": (_int, [_u32p, _u32p, ctypes.c_uint32, _u32p, _u16p, ctypes.c_uint32,
+                                    _int, ctypes.POINTER(_vp)]),
+    "yr_amd_tables_destroy": (_int, [_vp]),
+    "yr_amd_tables_get_info": (_int, [_vp, ctypes.POINTER(TablesInfo)]),
+    "yr_amd_scanner_create": (_int, [_vp, _vp, ctypes.POINTER(_vp)]),
+    "yr_amd_scanner_destroy": (_int, [_vp]),
+    "yr_amd_scan_block": (_int, [_vp, _u8p, ctypes.c_size_t, ctypes.POINTER(_u64p),
+                                 ctypes.POINTER(ctypes.c_uint64), ctypes.POINTER(_int)]),
+    "yr_amd_scan_device": (_int, [_vp, _vp, ctypes.c_uint64, ctypes.c_uint64, ctypes.c_uint64]),
+    "yr_amd_scan_device_result": (_int, [_vp, ctypes.POINTER(_vp), ctypes.POINTER(ctypes.c_uint64),
+                                         ctypes.POINTER(_int)]),
+    "yr_amd_replay": (_int, [_vp, _u8p, ctypes.c_size_t, _u64p, ctypes.c_uint64, _int, VERIFY_FN,
+                             _vp]),
+    "yr_amd_fill_xorshift64": (_int, [_vp, ctypes.c_uint64, ctypes.c_uint64, ctypes.c_uint64, _vp]),
+    "yr_amd_scanner_set_timing": (_int, [_vp, _int]),
+    "yr_amd_scanner_kernel_ms": (_int, [_vp, ctypes.POINTER(ctypes.c_float)]),
+    "yr_amd_version": (ctypes.c_char_p, []),
+}
+
+_lib = None
+
+
+class YaraAmdError(RuntimeError):
+    def __init__(self, fn, code):
+        super().__init__("%s failed with error %d" % (fn, code))
+        self.code = code
+
+
+def lib():
+    """Load libyara_amd.so (raises if it is missing: no CPU fallback exists)."""
+    global _lib
+    if _lib is None:
+        # Share ONE HIP runtime with PyTorch: torch ships its own libamdhip64.so.7;
+        # loading it first makes the dynamic linker bind libyara_amd.so's
+        # DT_NEEDED libamdhip64.so.7 to that same instance, so torch tensors,
+        # streams and RCCL and our kernels live in one HIP/HSA runtime.
+        try:
+            import torch  # noqa: F401
+        except ImportError:
+            pass
+        if not os.path.exists(LIB_PATH):
+            raise ImportError("libyara_amd.so not built (%s); run __graft_entry__.build() or "
+                              "make -C yara_amd/csrc" % LIB_PATH)
+        L = ctypes.CDLL(LIB_PATH)
+        for name, (res, args) in PROTOTYPES.items():
+            f = getattr(L, name)
+            f.restype = res
+            f.argtypes = args
+        _lib = L
+    return _lib
+
+
+def check(fn, code):
+    if code != SUCCESS:
+        raise YaraAmdError(fn, code)

@@ -1,0 +1,335 @@
+// gfx950 kernels of the Aho-Corasick atom scanner.
+//
+// What is computed (reference semantics, libyara/scanner.c:45-176): the
+// positions i in (byte_begin, byte_end] of a block at which the AC walk's state
+// has a non-empty match list (ac_match_table[state] != 0, scanner.c:98/:144).
+//
+// How: libyara's trie is at most 4 deep (YR_MAX_ATOM_LENGTH, limits.h:68) and
+// its match lists are closed under failure links (ahocorasick.c:254-300), so
+// ac_match_table[state_i] != 0 iff some "key" -- a minimal accepting trie
+// string, 1..4 bytes -- ends at position i (host flattening: tables.cpp).
+// That makes every position independent of every other: no sequential state
+// chain, just a window test.
+//
+//   stage 1 (every byte, LDS):  one bit of a 2^20-bit filter over the hashed
+//             3-byte window ending at the byte.  128 KiB, staged once per
+//             workgroup; one ds_read_b32 per input byte.  Superset of the keys.
+//   stage 2 (filter hits, ~1%):  hits are appended in position order to a
+//             per-wave LDS ring; full batches of 64 are checked exactly against
+//             an open-addressed hash table of the keys in HBM/L2, and survivors
+//             are compacted with a wave ballot + mbcnt into the segment's output.
+//
+// Memory: the input is streamed once, 16 B per lane (1 KiB per wave per step),
+// tile t+1 prefetched while tile t is filtered.  Roofline: HBM read bandwidth
+// (1 algorithmic byte per input byte).
+#include "internal.h"
+
+namespace yamd {
+
+__device__ __forceinline__ uint32_t lane_id() {
+  return __builtin_amdgcn_mbcnt_hi(~0u, __builtin_amdgcn_mbcnt_lo(~0u, 0u));
+}
+
+__device__ __forceinline__ uint32_t wave_inclusive_scan(uint32_t v, uint32_t lane) {
+#pragma unroll
+  for (int d = 1; d < kWave; d <<= 1) {
+    uint32_t o = __shfl_up(v, d, kWave);
+    if (lane >= (uint32_t)d) v += o;
+  }
+  return v;
+}
+
+// Exact test of one position (byte index g of the block; position g + 1):
+// does a key of length L <= min(4, g + 1) equal the L bytes ending at g?
+__device__ __noinline__ bool exact_check(const uint8_t* __restrict__ data,
+                                         const uint64_t* __restrict__ exact, uint32_t exact_mask,
+                                         uint32_t len_mask, uint64_t g) {
+  uint32_t w4 = 0;
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    int64_t idx = (int64_t)g - 3 + i;
+    uint32_t b = idx >= 0 ? (uint32_t)data[idx] : 0u;
+    w4 |= b << (8 * i);
+  }
+  const uint64_t pos = g + 1;
+  for (uint32_t L = 1; L <= 4; ++L) {
+    if (!((len_mask >> L) & 1u) || pos < L) continue;
+    const uint32_t key = L == 4 ? w4 : (w4 >> (8 * (4 - L)));
+    const uint64_t want = exact_entry(key, L);
+    uint32_t s = exact_hash(key, L) & exact_mask;
+    for (uint32_t probe = 0; probe <= exact_mask; ++probe) {
+      const uint64_t e = exact[s];
+      if (e == want) return true;
+      if (e == 0) break;
+      s = (s + 1) & exact_mask;
+    }
+  }
+  return false;
+}
+
+struct WaveQueue {
+  uint32_t* ring;   // kQueueCap entries in LDS: byte offset within segment
+  uint32_t head;    // wave-uniform counters (monotonic)
+  uint32_t tail;
+};
+
+// Exact-check up to 64 queued hits and append the survivors, in order, to the
+// segment's output.
+__device__ __forceinline__ void drain(const ScanParams& p, WaveQueue& q, uint32_t lane,
+                                      uint64_t seg_start, uint32_t* out, uint32_t& found) {
+  const uint32_t n = min(q.tail - q.head, (uint32_t)kWave);
+  __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+  bool hit = false;
+  uint32_t off = 0;
+  if (lane < n) {
+    off = q.ring[(q.head + lane) % kQueueCap];
+    hit = exact_check(p.data, p.exact, p.exact_mask, p.len_mask, seg_start + off);
+  }
+  const uint64_t b = __ballot(hit);
+  if (hit) {
+    const uint32_t idx = found + (uint32_t)__popcll(b & ((1ull << lane) - 1));
+    if (idx < p.seg_cap) out[idx] = off;
+  }
+  found += (uint32_t)__popcll(b);
+  q.head += n;
+}
+
+__device__ __forceinline__ uint4 load_tile(const uint8_t* base, uint32_t tile_off, uint32_t lane,
+                                           uint64_t avail) {
+  const uint32_t off = tile_off + lane * kBytesPerLane;
+  if (tile_off + (uint64_t)kTile <= avail) {
+    return *reinterpret_cast<const uint4*>(base + off);
+  }
+  // ragged block tail (at most one tile per launch)
+  uint4 v = make_uint4(0, 0, 0, 0);
+  if (off + (uint64_t)kBytesPerLane <= avail) {
+    v = *reinterpret_cast<const uint4*>(base + off);
+  } else if (off < avail) {
+    uint32_t w[4] = {0, 0, 0, 0};
+#pragma unroll
+    for (uint32_t i = 0; i < kBytesPerLane; ++i) {
+      const uint32_t b = off + i < avail ? (uint32_t)base[off + i] : 0u;
+      w[i >> 2] |= b << (8 * (i & 3));
+    }
+    v = make_uint4(w[0], w[1], w[2], w[3]);
+  }
+  return v;
+}
+
+__device__ void scan_segment(const ScanParams& p, const uint32_t* __restrict__ filt,
+                             WaveQueue& q, uint32_t seg, uint32_t lane) {
+  const uint64_t seg_start = p.byte_begin + (uint64_t)seg * p.seg_bytes;
+  const uint64_t seg_end = min(seg_start + p.seg_bytes, p.byte_end);
+  const uint32_t seg_len = (uint32_t)(seg_end - seg_start);
+  const uint64_t avail = p.block_size - seg_start;
+  const uint8_t* base = p.data + seg_start;
+  uint32_t* out = p.seg_out + (size_t)seg * p.seg_cap;
+  uint32_t found = 0;
+
+  // 4 bytes before the segment (warm-up halo); zeros before the block start.
+  uint32_t carry = seg_start >= 4 ? *reinterpret_cast<const uint32_t*>(base - 4) : 0u;
+  q.head = q.tail = 0;
+
+  const uint32_t ntiles = (seg_len + kTile - 1) / kTile;
+  uint4 cur = load_tile(base, 0, lane, avail);
+  for (uint32_t t = 0; t < ntiles; ++t) {
+    const uint32_t tile_off = t * kTile;
+    uint4 nxt = make_uint4(0, 0, 0, 0);
+    if (t + 1 < ntiles) nxt = load_tile(base, tile_off + kTile, lane, avail);
+
+    const uint32_t up = __shfl_up(cur.w, 1, kWave);
+    const uint32_t S0 = lane == 0 ? carry : up;
+    carry = __shfl(cur.w, kWave - 1, kWave);
+    const uint32_t S[6] = {S0, cur.x, cur.y, cur.z, cur.w, 0u};
+
+    uint32_t mask = 0;
+#pragma unroll
+    for (int k = 0; k < kBytesPerLane; ++k) {
+      // low 24 bits = bytes k-2, k-1, k of this lane (stream offset k + 2)
+      const int o = k + 2;
+      const uint32_t x = (o & 3) ? __builtin_amdgcn_alignbyte(S[(o >> 2) + 1], S[o >> 2], o & 3)
+                                 : S[o >> 2];
+      const uint32_t h = filter_hash(x);
+      const uint32_t w = filt[filter_word(h)];
+      mask |= ((w >> filter_bit(h)) & 1u) << k;
+    }
+    const uint32_t lane_off = tile_off + lane * kBytesPerLane;
+    if (lane_off + kBytesPerLane > seg_len) {
+      mask = lane_off >= seg_len ? 0u : (mask & ((1u << (seg_len - lane_off)) - 1u));
+    }
+
+    // ordered append of this tile's hits to the wave ring
+    const uint32_t c = __popc(mask);
+    const uint32_t incl = wave_inclusive_scan(c, lane);
+    const uint32_t total = __shfl(incl, kWave - 1, kWave);
+    if (total != 0) {
+      const uint32_t excl = incl - c;
+      uint32_t done = 0;
+      while (done < total) {
+        const uint32_t space = kQueueCap - (q.tail - q.head);
+        const uint32_t take = min(space, total - done);
+        uint32_t m = mask, r = excl;
+        while (m != 0 && r < done + take) {
+          const uint32_t j = __builtin_ctz(m);
+          m &= m - 1;
+          if (r >= done) q.ring[(q.tail + (r - done)) % kQueueCap] = lane_off + j;
+          ++r;
+        }
+        q.tail += take;
+        done += take;
+        while (q.tail - q.head >= (uint32_t)kWave) drain(p, q, lane, seg_start, out, found);
+      }
+    }
+    cur = nxt;
+  }
+  while (q.tail != q.head) drain(p, q, lane, seg_start, out, found);
+  if (lane == 0) p.seg_count[seg] = found;
+}
+
+__global__ __launch_bounds__(kWGThreads, 1) void scan_segments_kernel(ScanParams p) {
+  extern __shared__ __attribute__((aligned(16))) uint32_t lds[];
+  uint32_t* filt = lds;
+  {
+    const uint4* src = reinterpret_cast<const uint4*>(p.filter);
+    uint4* dst = reinterpret_cast<uint4*>(filt);
+    for (uint32_t i = threadIdx.x; i < kFilterWords / 4; i += blockDim.x) dst[i] = src[i];
+  }
+  __syncthreads();
+  const uint32_t lane = lane_id();
+  const uint32_t wid = threadIdx.x / kWave;
+  WaveQueue q;
+  q.ring = lds + kFilterWords + wid * kQueueCap;
+  const uint32_t total_waves = gridDim.x * kWavesPerWG;
+  for (uint32_t seg = blockIdx.x * kWavesPerWG + wid; seg < p.n_segments; seg += total_waves) {
+    scan_segment(p, filt, q, seg, lane);
+  }
+}
+
+// ---------------------------------------------------------------------------
+// Candidate compaction: per-segment counts -> offsets (one workgroup), then a
+// scatter of every segment's ascending entries into one ascending uint64 array.
+// ---------------------------------------------------------------------------
+__global__ __launch_bounds__(1024) void seg_offsets_kernel(const uint32_t* seg_count, uint32_t n,
+                                                           uint32_t cap, uint64_t* seg_offset,
+                                                           uint64_t* summary) {
+  __shared__ uint64_t part[1024];
+  __shared__ uint32_t pmax[1024];
+  const uint32_t t = threadIdx.x;
+  const uint32_t per = (n + 1023) / 1024;
+  const uint32_t lo = min(t * per, n), hi = min(lo + per, n);
+  uint64_t s = 0;
+  uint32_t mx = 0;
+  for (uint32_t i = lo; i < hi; ++i) {
+    const uint32_t c = seg_count[i];
+    s += min(c, cap);
+    mx = max(mx, c);
+  }
+  part[t] = s;
+  pmax[t] = mx;
+  __syncthreads();
+  for (uint32_t d = 1; d < 1024; d <<= 1) {
+    uint64_t v = t >= d ? part[t - d] : 0;
+    uint32_t m = t >= d ? pmax[t - d] : 0;
+    __syncthreads();
+    part[t] += v;
+    pmax[t] = max(pmax[t], m);
+    __syncthreads();
+  }
+  uint64_t run = part[t] - s;
+  for (uint32_t i = lo; i < hi; ++i) {
+    seg_offset[i] = run;
+    run += min(seg_count[i], cap);
+  }
+  if (t == 1023) {
+    summary[0] = part[1023];   // total entries written
+    summary[1] = pmax[1023];   // max per-segment count (overflow if > cap)
+  }
+}
+
+__global__ __launch_bounds__(256) void seg_scatter_kernel(const uint32_t* seg_count,
+                                                          const uint32_t* seg_out,
+                                                          const uint64_t* seg_offset, uint32_t cap,
+                                                          uint64_t byte_begin, uint32_t seg_bytes,
+                                                          uint64_t* positions) {
+  const uint32_t seg = blockIdx.x;
+  const uint32_t c = min(seg_count[seg], cap);
+  const uint64_t base = byte_begin + (uint64_t)seg * seg_bytes + 1;  // position = byte + 1
+  const uint32_t* src = seg_out + (size_t)seg * cap;
+  uint64_t* dst = positions + seg_offset[seg];
+  for (uint32_t i = threadIdx.x; i < c; i += blockDim.x) dst[i] = base + src[i];
+}
+
+// ---------------------------------------------------------------------------
+// Synthetic input (SURVEY.md App. A xorshift64), one chunk per thread, each
+// chunk's start state precomputed on the host by GF(2) jump-ahead.
+// ---------------------------------------------------------------------------
+__global__ __launch_bounds__(256) void xorshift_fill_kernel(uint8_t* buf, uint64_t n,
+                                                            const uint64_t* states,
+                                                            uint32_t n_chunks, uint32_t chunk) {
+  const uint32_t c = blockIdx.x * blockDim.x + threadIdx.x;
+  if (c >= n_chunks) return;
+  uint64_t x = states[c];
+  const uint64_t lo = (uint64_t)c * chunk;
+  const uint64_t hi = min(lo + chunk, n);
+  uint64_t i = lo;
+  for (; i + 16 <= hi; i += 16) {
+    uint32_t w[4];
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      uint32_t v = 0;
+#pragma unroll
+      for (int b = 0; b < 4; ++b) {
+        x ^= x << 13;
+        x ^= x >> 7;
+        x ^= x << 17;
+        v |= (uint32_t)((x >> 24) & 0xFF) << (8 * b);
+      }
+      w[j] = v;
+    }
+    *reinterpret_cast<uint4*>(buf + i) = make_uint4(w[0], w[1], w[2], w[3]);
+  }
+  for (; i < hi; ++i) {
+    x ^= x << 13;
+    x ^= x >> 7;
+    x ^= x << 17;
+    buf[i] = (uint8_t)(x >> 24);
+  }
+}
+
+}  // namespace yamd
+
+// Launch wrappers (host side, called from scanner.cpp).
+namespace yamd {
+
+hipError_t launch_scan(const ScanParams& p, int grid, hipStream_t s) {
+  const size_t lds = kFilterBytes + (size_t)kWavesPerWG * kQueueCap * 4;
+  hipLaunchKernelGGL(scan_segments_kernel, dim3(grid), dim3(kWGThreads), lds, s, p);
+  return hipGetLastError();
+}
+
+hipError_t launch_compact(const ScanParams& p, uint64_t* seg_offset, uint64_t* summary,
+                          uint64_t* positions, bool scatter, hipStream_t s) {
+  if (!scatter) {
+    hipLaunchKernelGGL(seg_offsets_kernel, dim3(1), dim3(1024), 0, s, p.seg_count, p.n_segments,
+                       p.seg_cap, seg_offset, summary);
+  } else {
+    hipLaunchKernelGGL(seg_scatter_kernel, dim3(p.n_segments), dim3(256), 0, s, p.seg_count,
+                       p.seg_out, seg_offset, p.seg_cap, p.byte_begin, p.seg_bytes, positions);
+  }
+  return hipGetLastError();
+}
+
+hipError_t launch_xorshift(uint8_t* buf, uint64_t n, const uint64_t* states, uint32_t n_chunks,
+                           uint32_t chunk, hipStream_t s) {
+  hipLaunchKernelGGL(xorshift_fill_kernel, dim3((n_chunks + 255) / 256), dim3(256), 0, s, buf, n,
+                     states, n_chunks, chunk);
+  return hipGetLastError();
+}
+
+hipError_t configure_scan_kernel() {
+  const size_t lds = kFilterBytes + (size_t)kWavesPerWG * kQueueCap * 4;
+  return hipFuncSetAttribute((const void*)scan_segments_kernel,
+                             hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+}
+
+}  // namespace yamd

@@ -1,0 +1,471 @@
+// C ABI of the MI355X Aho-Corasick atom scanner (include/yara_amd.h).
+//
+// Host orchestration of one block scan (the role of libyara's
+// _yr_scanner_scan_mem_block, scanner.c:45-176):
+//   H2D (host blocks only) -> scan_segments_kernel -> seg_offsets_kernel
+//   -> [overflow retry] -> seg_scatter_kernel -> D2H of the candidate stream.
+// and the host replay of candidates into the caller's verifier in the exact
+// order of scanner.c:98-122 / :144-163.
+#include <hip/hip_runtime.h>
+#include <string.h>
+
+#include <algorithm>
+#include <new>
+#include <vector>
+
+#include "../../include/yara_amd.h"
+#include "internal.h"
+#include "tables.h"
+
+namespace yamd {
+hipError_t launch_scan(const ScanParams& p, int grid, hipStream_t s);
+hipError_t launch_compact(const ScanParams& p, uint64_t* seg_offset, uint64_t* summary,
+                          uint64_t* positions, bool scatter, hipStream_t s);
+hipError_t launch_xorshift(uint8_t* buf, uint64_t n, const uint64_t* states, uint32_t n_chunks,
+                           uint32_t chunk, hipStream_t s);
+hipError_t configure_scan_kernel();
+}  // namespace yamd
+
+using namespace yamd;
+
+struct yr_amd_tables {
+  FlatTables flat;
+  int device = 0;
+  uint32_t* d_filter = nullptr;
+  uint64_t* d_exact = nullptr;
+  int num_cus = 256;
+};
+
+struct yr_amd_scanner {
+  yr_amd_tables* tables = nullptr;
+  hipStream_t stream = nullptr;
+  bool own_stream = false;
+
+  uint8_t* d_block = nullptr;           // staging for host blocks
+  size_t d_block_cap = 0;
+  uint32_t* d_seg_count = nullptr;
+  uint64_t* d_seg_offset = nullptr;
+  uint32_t seg_alloc = 0;               // segments the count/offset arrays hold
+  uint32_t* d_seg_out = nullptr;
+  size_t seg_out_cap = 0;               // entries
+  uint64_t* d_positions = nullptr;
+  size_t positions_cap = 0;             // entries
+  uint64_t* h_summary = nullptr;        // pinned: {total, max per segment}
+  uint64_t* d_summary = nullptr;
+
+  std::vector<uint64_t> h_positions;
+
+  // state of the last yr_amd_scan_device
+  ScanParams last{};
+  int last_grid = 0;
+  bool last_all = false;
+  bool last_empty = false;
+  bool pending = false;
+  uint64_t last_count = 0;
+
+  // optional kernel timing (HIP events on the scan stream)
+  bool timing = false;
+  hipEvent_t ev_begin = nullptr, ev_end = nullptr;
+  bool ev_valid = false;
+};
+
+#define HIP_TRY(expr)                                   \
+  do {                                                  \
+    if ((expr) != hipSuccess) return YR_AMD_INTERNAL_FATAL_ERROR; \
+  } while (0)
+
+namespace {
+
+template <typename T>
+int grow(T*& p, size_t& cap, size_t need) {
+  if (need <= cap && p != nullptr) return YR_AMD_SUCCESS;
+  if (p) (void)hipFree(p);
+  p = nullptr;
+  cap = 0;
+  size_t n = std::max<size_t>(need, 1);
+  if (hipMalloc((void**)&p, n * sizeof(T)) != hipSuccess) {
+    p = nullptr;
+    return YR_AMD_INSUFFICIENT_MEMORY;
+  }
+  cap = n;
+  return YR_AMD_SUCCESS;
+}
+
+int ensure_segments(yr_amd_scanner* s, uint32_t n_segments, uint32_t seg_cap) {
+  if (n_segments > s->seg_alloc) {
+    size_t c = 0;
+    if (s->d_seg_count) (void)hipFree(s->d_seg_count);
+    if (s->d_seg_offset) (void)hipFree(s->d_seg_offset);
+    s->d_seg_count = nullptr;
+    s->d_seg_offset = nullptr;
+    s->seg_alloc = 0;
+    if (grow(s->d_seg_count, c, n_segments)) return YR_AMD_INSUFFICIENT_MEMORY;
+    c = 0;
+    if (grow(s->d_seg_offset, c, n_segments)) return YR_AMD_INSUFFICIENT_MEMORY;
+    s->seg_alloc = n_segments;
+  }
+  return grow(s->d_seg_out, s->seg_out_cap, (size_t)n_segments * seg_cap);
+}
+
+uint32_t choose_seg_bytes(uint64_t nbytes, int num_cus) {
+  // aim for >= 1 segment per wave of a full-chip launch, 4-64 tiles each
+  const uint64_t waves = (uint64_t)num_cus * kWavesPerWG;
+  uint64_t per = (nbytes + waves - 1) / waves;
+  per = (per + kTile - 1) / kTile * kTile;
+  return (uint32_t)std::min<uint64_t>(std::max<uint64_t>(per, 4 * kTile), kSegment);
+}
+
+int run_scan(yr_amd_scanner* s) {
+  if (s->timing) HIP_TRY(hipEventRecord(s->ev_begin, s->stream));
+  HIP_TRY(launch_scan(s->last, s->last_grid, s->stream));
+  if (s->timing) {
+    HIP_TRY(hipEventRecord(s->ev_end, s->stream));
+    s->ev_valid = true;
+  }
+  HIP_TRY(launch_compact(s->last, s->d_seg_offset, s->d_summary, nullptr, false, s->stream));
+  HIP_TRY(hipMemcpyAsync(s->h_summary, s->d_summary, 2 * sizeof(uint64_t), hipMemcpyDeviceToHost,
+                         s->stream));
+  return YR_AMD_SUCCESS;
+}
+
+}  // namespace
+
+extern "C" {
+
+const char* yr_amd_version(void) { return "yara_amd 0.1.0 (gfx950)"; }
+
+int yr_amd_tables_create(const uint32_t* transition_table, const uint32_t* match_table,
+                         uint32_t n_slots, const uint32_t* pool_next,
+                         const uint16_t* pool_backtrack, uint32_t n_pool, int device,
+                         yr_amd_tables** tables) {
+  if (tables == nullptr) return YR_AMD_INVALID_ARGUMENT;
+  *tables = nullptr;
+  yr_amd_tables* t = new (std::nothrow) yr_amd_tables();
+  if (t == nullptr) return YR_AMD_INSUFFICIENT_MEMORY;
+  int r = flatten_tables(transition_table, match_table, n_slots, pool_next, pool_backtrack, n_pool,
+                         t->flat);
+  if (r != YR_AMD_SUCCESS) {
+    delete t;
+    return r;
+  }
+  t->device = device;
+  if (device < 0) {  // host-only: flattening + replay
+    *tables = t;
+    return YR_AMD_SUCCESS;
+  }
+  if (hipSetDevice(device) != hipSuccess ||
+      hipDeviceGetAttribute(&t->num_cus, hipDeviceAttributeMultiprocessorCount, device) !=
+          hipSuccess ||
+      configure_scan_kernel() != hipSuccess ||
+      hipMalloc((void**)&t->d_filter, t->flat.filter.size() * 4) != hipSuccess ||
+      hipMalloc((void**)&t->d_exact, t->flat.exact.size() * 8) != hipSuccess ||
+      hipMemcpy(t->d_filter, t->flat.filter.data(), t->flat.filter.size() * 4,
+                hipMemcpyHostToDevice) != hipSuccess ||
+      hipMemcpy(t->d_exact, t->flat.exact.data(), t->flat.exact.size() * 8,
+                hipMemcpyHostToDevice) != hipSuccess) {
+    yr_amd_tables_destroy(t);
+    return YR_AMD_INTERNAL_FATAL_ERROR;
+  }
+  *tables = t;
+  return YR_AMD_SUCCESS;
+}
+
+int yr_amd_tables_destroy(yr_amd_tables* t) {
+  if (t == nullptr) return YR_AMD_SUCCESS;
+  if (t->d_filter) (void)hipFree(t->d_filter);
+  if (t->d_exact) (void)hipFree(t->d_exact);
+  delete t;
+  return YR_AMD_SUCCESS;
+}
+
+int yr_amd_tables_get_info(const yr_amd_tables* t, yr_amd_tables_info* info) {
+  if (t == nullptr || info == nullptr) return YR_AMD_INVALID_ARGUMENT;
+  memset(info, 0, sizeof(*info));
+  const FlatTables& f = t->flat;
+  info->n_slots = f.n_slots;
+  info->n_states = f.n_states;
+  info->max_depth = f.max_depth;
+  for (int d = 0; d <= YR_AMD_MAX_ATOM_LENGTH; ++d) {
+    info->states_by_depth[d] = f.by_depth[d];
+    info->keys_by_length[d] = f.keys_by_len[d];
+  }
+  info->accepting_states = f.accepting;
+  info->root_accepting = f.root_accepting ? 1 : 0;
+  info->filter_bits = kFilterLog2Bits;
+  info->filter_set_bits = f.filter_set_bits;
+  info->exact_slots = (uint32_t)f.exact.size();
+  return YR_AMD_SUCCESS;
+}
+
+int yr_amd_scanner_create(yr_amd_tables* tables, void* stream, yr_amd_scanner** scanner) {
+  if (tables == nullptr || scanner == nullptr || tables->device < 0) return YR_AMD_INVALID_ARGUMENT;
+  *scanner = nullptr;
+  yr_amd_scanner* s = new (std::nothrow) yr_amd_scanner();
+  if (s == nullptr) return YR_AMD_INSUFFICIENT_MEMORY;
+  s->tables = tables;
+  if (hipSetDevice(tables->device) != hipSuccess) {
+    delete s;
+    return YR_AMD_INTERNAL_FATAL_ERROR;
+  }
+  if (stream != nullptr) {
+    s->stream = (hipStream_t)stream;
+  } else {
+    if (hipStreamCreateWithFlags(&s->stream, hipStreamNonBlocking) != hipSuccess) {
+      delete s;
+      return YR_AMD_INTERNAL_FATAL_ERROR;
+    }
+    s->own_stream = true;
+  }
+  if (hipHostMalloc((void**)&s->h_summary, 2 * sizeof(uint64_t), hipHostMallocDefault) !=
+          hipSuccess ||
+      hipMalloc((void**)&s->d_summary, 2 * sizeof(uint64_t)) != hipSuccess) {
+    yr_amd_scanner_destroy(s);
+    return YR_AMD_INTERNAL_FATAL_ERROR;
+  }
+  *scanner = s;
+  return YR_AMD_SUCCESS;
+}
+
+int yr_amd_scanner_destroy(yr_amd_scanner* s) {
+  if (s == nullptr) return YR_AMD_SUCCESS;
+  if (s->stream) (void)hipStreamSynchronize(s->stream);
+  for (void* p : {(void*)s->d_block, (void*)s->d_seg_count, (void*)s->d_seg_offset,
+                  (void*)s->d_seg_out, (void*)s->d_positions, (void*)s->d_summary})
+    if (p) (void)hipFree(p);
+  if (s->h_summary) (void)hipHostFree(s->h_summary);
+  if (s->ev_begin) (void)hipEventDestroy(s->ev_begin);
+  if (s->ev_end) (void)hipEventDestroy(s->ev_end);
+  if (s->own_stream && s->stream) (void)hipStreamDestroy(s->stream);
+  delete s;
+  return YR_AMD_SUCCESS;
+}
+
+int yr_amd_scanner_set_timing(yr_amd_scanner* s, int enable) {
+  if (s == nullptr) return YR_AMD_INVALID_ARGUMENT;
+  if (enable && s->ev_begin == nullptr) {
+    HIP_TRY(hipSetDevice(s->tables->device));
+    HIP_TRY(hipEventCreate(&s->ev_begin));
+    HIP_TRY(hipEventCreate(&s->ev_end));
+  }
+  s->timing = enable != 0;
+  s->ev_valid = false;
+  return YR_AMD_SUCCESS;
+}
+
+int yr_amd_scanner_kernel_ms(yr_amd_scanner* s, float* ms) {
+  if (s == nullptr || ms == nullptr || !s->ev_valid) return YR_AMD_INVALID_ARGUMENT;
+  HIP_TRY(hipEventSynchronize(s->ev_end));
+  HIP_TRY(hipEventElapsedTime(ms, s->ev_begin, s->ev_end));
+  return YR_AMD_SUCCESS;
+}
+
+int yr_amd_scan_device(yr_amd_scanner* s, const uint8_t* d_data, uint64_t block_size,
+                       uint64_t byte_begin, uint64_t byte_end) {
+  if (s == nullptr || byte_begin > byte_end || byte_end > block_size) return YR_AMD_INVALID_ARGUMENT;
+  if ((byte_begin & 15) != 0 || (((uintptr_t)d_data) & 15) != 0) return YR_AMD_INVALID_ARGUMENT;
+  const yr_amd_tables* t = s->tables;
+  s->pending = true;
+  s->last_count = 0;
+  s->ev_valid = false;
+  s->last_all = t->flat.root_accepting;
+  s->last_empty = s->last_all || byte_end == byte_begin;
+  if (s->last_empty) return YR_AMD_SUCCESS;
+  if (d_data == nullptr) return YR_AMD_INVALID_ARGUMENT;
+  HIP_TRY(hipSetDevice(t->device));
+
+  const uint64_t nbytes = byte_end - byte_begin;
+  const uint32_t seg_bytes = choose_seg_bytes(nbytes, t->num_cus);
+  const uint64_t n_segments64 = (nbytes + seg_bytes - 1) / seg_bytes;
+  if (n_segments64 > 0xFFFFFFFFull) return YR_AMD_INVALID_ARGUMENT;
+  const uint32_t n_segments = (uint32_t)n_segments64;
+  const uint32_t seg_cap = std::max<uint32_t>(64, seg_bytes / 256);
+  int r = ensure_segments(s, n_segments, seg_cap);
+  if (r) return r;
+
+  ScanParams& p = s->last;
+  p.data = d_data;
+  p.block_size = block_size;
+  p.byte_begin = byte_begin;
+  p.byte_end = byte_end;
+  p.filter = t->d_filter;
+  p.exact = t->d_exact;
+  p.exact_mask = (uint32_t)t->flat.exact.size() - 1;
+  p.len_mask = t->flat.len_mask;
+  p.n_segments = n_segments;
+  p.seg_bytes = seg_bytes;
+  p.seg_cap = seg_cap;
+  p.seg_count = s->d_seg_count;
+  p.seg_out = s->d_seg_out;
+  s->last_grid = (int)std::min<uint64_t>((n_segments + kWavesPerWG - 1) / kWavesPerWG,
+                                         (uint64_t)t->num_cus);
+  return run_scan(s);
+}
+
+int yr_amd_scan_device_result(yr_amd_scanner* s, const uint64_t** d_positions, uint64_t* count,
+                              int* all_positions) {
+  if (s == nullptr || !s->pending) return YR_AMD_INVALID_ARGUMENT;
+  if (all_positions) *all_positions = s->last_all ? 1 : 0;
+  if (s->last_empty) {
+    s->pending = false;
+    if (d_positions) *d_positions = s->d_positions;
+    if (count) *count = 0;
+    return YR_AMD_SUCCESS;
+  }
+  HIP_TRY(hipStreamSynchronize(s->stream));
+  uint64_t total = s->h_summary[0];
+  const uint64_t maxc = s->h_summary[1];
+  if (maxc > s->last.seg_cap) {
+    // some segment overflowed: rerun once with the exact capacity needed
+    const uint32_t cap = (uint32_t)maxc;
+    int r = ensure_segments(s, s->last.n_segments, cap);
+    if (r) return r;
+    s->last.seg_cap = cap;
+    s->last.seg_out = s->d_seg_out;
+    r = run_scan(s);
+    if (r) return r;
+    HIP_TRY(hipStreamSynchronize(s->stream));
+    total = s->h_summary[0];
+    if (s->h_summary[1] > cap) return YR_AMD_INTERNAL_FATAL_ERROR;
+  }
+  int r = grow(s->d_positions, s->positions_cap, total);
+  if (r) return r;
+  if (total > 0) {
+    HIP_TRY(launch_compact(s->last, s->d_seg_offset, s->d_summary, s->d_positions, true, s->stream));
+    HIP_TRY(hipStreamSynchronize(s->stream));
+  }
+  s->last_count = total;
+  s->pending = false;
+  if (d_positions) *d_positions = s->d_positions;
+  if (count) *count = total;
+  return YR_AMD_SUCCESS;
+}
+
+int yr_amd_scan_block(yr_amd_scanner* s, const uint8_t* data, size_t size,
+                      const uint64_t** positions, uint64_t* count, int* all_positions) {
+  if (s == nullptr || (data == nullptr && size > 0)) return YR_AMD_INVALID_ARGUMENT;
+  HIP_TRY(hipSetDevice(s->tables->device));
+  if (size > 0) {
+    int r = grow(s->d_block, s->d_block_cap, size);
+    if (r) return r;
+    if (hipMemcpyAsync(s->d_block, data, size, hipMemcpyHostToDevice, s->stream) != hipSuccess)
+      return YR_AMD_COULD_NOT_MAP_FILE;
+  }
+  int r = yr_amd_scan_device(s, s->d_block, size, 0, size);
+  if (r) return r;
+  const uint64_t* d_pos = nullptr;
+  uint64_t n = 0;
+  int all = 0;
+  r = yr_amd_scan_device_result(s, &d_pos, &n, &all);
+  if (r) return r;
+  s->h_positions.resize(n);
+  if (n > 0) {
+    HIP_TRY(hipMemcpyAsync(s->h_positions.data(), d_pos, n * sizeof(uint64_t),
+                           hipMemcpyDeviceToHost, s->stream));
+    HIP_TRY(hipStreamSynchronize(s->stream));
+  }
+  if (positions) *positions = s->h_positions.data();
+  if (count) *count = n;
+  if (all_positions) *all_positions = all;
+  return YR_AMD_SUCCESS;
+}
+
+int yr_amd_replay(const yr_amd_tables* t, const uint8_t* data, size_t size,
+                  const uint64_t* positions, uint64_t count, int all_positions,
+                  yr_amd_verify_fn verify, void* user) {
+  if (t == nullptr || verify == nullptr || (data == nullptr && size > 0)) return YR_AMD_INVALID_ARGUMENT;
+  if (!all_positions && count > 0 && positions == nullptr) return YR_AMD_INVALID_ARGUMENT;
+  const FlatTables& f = t->flat;
+  const uint32_t* T = f.T.data();
+  const uint32_t* M = f.M.data();
+  const uint32_t* nx = f.pool_next.data();
+  const uint16_t* bt = f.pool_backtrack.data();
+  const uint64_t n = all_positions ? (uint64_t)size + 1 : count;
+  uint64_t prev = 0;
+  for (uint64_t c = 0; c < n; ++c) {
+    const uint64_t i = all_positions ? c : positions[c];
+    if (i > size || (c > 0 && i <= prev)) return YR_AMD_INVALID_ARGUMENT;  // must ascend
+    prev = i;
+    // state at i from root over the last <= YR_MAX_ATOM_LENGTH bytes
+    uint32_t state = 0;
+    for (uint64_t j = i > YR_AMD_MAX_ATOM_LENGTH ? i - YR_AMD_MAX_ATOM_LENGTH : 0; j < i; ++j)
+      state = ac_step(T, state, data[j]);
+    if (M[state] == 0) return YR_AMD_INTERNAL_FATAL_ERROR;
+    // scanner.c:105-121
+    for (uint32_t k = M[state]; k != 0; k = nx[k - 1]) {
+      if (bt[k - 1] <= i) {
+        const int r = verify(user, k - 1, i - bt[k - 1]);
+        if (r != 0) return r;
+      }
+    }
+  }
+  return YR_AMD_SUCCESS;
+}
+
+// ---------------------------------------------------------------------------
+// xorshift64 jump-ahead: the generator is linear over GF(2)^64, so the state
+// after m steps is A^m x0; chunk start states are computed on the host.
+// ---------------------------------------------------------------------------
+namespace {
+struct Mat64 {
+  uint64_t col[64];
+};
+inline uint64_t xs_step(uint64_t x) {
+  x ^= x << 13;
+  x ^= x >> 7;
+  x ^= x << 17;
+  return x;
+}
+inline uint64_t apply(const Mat64& m, uint64_t v) {
+  uint64_t r = 0;
+  for (int j = 0; j < 64; ++j)
+    if ((v >> j) & 1) r ^= m.col[j];
+  return r;
+}
+Mat64 compose(const Mat64& a, const Mat64& b) {  // a(b(.))
+  Mat64 r;
+  for (int j = 0; j < 64; ++j) r.col[j] = apply(a, b.col[j]);
+  return r;
+}
+Mat64 power(uint64_t m) {
+  Mat64 base, acc;
+  for (int j = 0; j < 64; ++j) {
+    base.col[j] = xs_step(1ull << j);
+    acc.col[j] = 1ull << j;
+  }
+  while (m) {
+    if (m & 1) acc = compose(base, acc);
+    base = compose(base, base);
+    m >>= 1;
+  }
+  return acc;
+}
+}  // namespace
+
+int yr_amd_fill_xorshift64(void* d_buf, uint64_t n, uint64_t seed, uint64_t offset, void* stream) {
+  if (n == 0) return YR_AMD_SUCCESS;
+  if (d_buf == nullptr || (((uintptr_t)d_buf) & 15) != 0) return YR_AMD_INVALID_ARGUMENT;
+  const uint32_t chunk = 1u << 16;
+  const uint64_t n_chunks64 = (n + chunk - 1) / chunk;
+  if (n_chunks64 > 0xFFFFFFFFull) return YR_AMD_INVALID_ARGUMENT;
+  const uint32_t n_chunks = (uint32_t)n_chunks64;
+  std::vector<uint64_t> states(n_chunks);
+  const Mat64 jump = power(chunk);
+  uint64_t x = apply(power(offset), 0x9E3779B97F4A7C15ull * seed);
+  for (uint32_t c = 0; c < n_chunks; ++c) {
+    states[c] = x;
+    x = apply(jump, x);
+  }
+  uint64_t* d_states = nullptr;
+  hipStream_t st = (hipStream_t)stream;
+  HIP_TRY(hipMalloc((void**)&d_states, n_chunks * sizeof(uint64_t)));
+  int r = YR_AMD_SUCCESS;
+  if (hipMemcpyAsync(d_states, states.data(), n_chunks * sizeof(uint64_t), hipMemcpyHostToDevice,
+                     st) != hipSuccess ||
+      launch_xorshift((uint8_t*)d_buf, n, d_states, n_chunks, chunk, st) != hipSuccess ||
+      hipStreamSynchronize(st) != hipSuccess)
+    r = YR_AMD_INTERNAL_FATAL_ERROR;
+  (void)hipFree(d_states);
+  return r;
+}
+
+}  // extern "C"

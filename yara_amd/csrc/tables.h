@@ -1,0 +1,56 @@
+// Host-side flattening of libyara's compiled Aho-Corasick tables.
+#pragma once
+
+#include <stdint.h>
+
+#include <vector>
+
+namespace yamd {
+
+struct Key {
+  uint32_t bytes;  // little endian: first byte of the key in bits 0-7
+  uint32_t len;    // 1..4
+};
+
+struct FlatTables {
+  // verbatim host copies of the reference tables (used by the replay)
+  uint32_t n_slots = 0;
+  std::vector<uint32_t> T, M, pool_next;
+  std::vector<uint16_t> pool_backtrack;
+
+  // trie statistics
+  uint32_t n_states = 0, max_depth = 0, accepting = 0;
+  uint32_t by_depth[5] = {0, 0, 0, 0, 0};
+  uint32_t keys_by_len[5] = {0, 0, 0, 0, 0};
+  bool root_accepting = false;
+
+  // flattened scan form
+  std::vector<Key> keys;           // minimal accepting trie strings
+  std::vector<uint32_t> filter;    // kFilterWords
+  uint32_t filter_set_bits = 0;
+  std::vector<uint64_t> exact;     // power-of-two open-addressed table
+  uint32_t len_mask = 0;
+};
+
+// Returns a YR_AMD_* error code.
+int flatten_tables(const uint32_t* T, const uint32_t* M, uint32_t n_slots,
+                   const uint32_t* pool_next, const uint16_t* pool_backtrack, uint32_t n_pool,
+                   FlatTables& out);
+
+// One transition of the reference walk (libyara/scanner.c:124-141).
+inline uint32_t ac_step(const uint32_t* T, uint32_t state, uint8_t byte) {
+  const uint32_t index = (uint32_t)byte + 1;
+  uint32_t t = T[state + index];
+  while ((t & 0x1FFu) != index) {
+    if (state != 0) {
+      state = T[state] >> 9;
+      t = T[state + index];
+    } else {
+      t = 0;
+      break;
+    }
+  }
+  return t >> 9;
+}
+
+}  // namespace yamd
