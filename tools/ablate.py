@@ -1,0 +1,57 @@
+"""Profiling ablations of the scan kernel (diagnostic only; modes != 0 are wrong
+by construction).  Interleaved rounds in one process (guide §5.4 rule 24).
+
+    python tools/ablate.py [--gib 4] [--rules C] [--rounds 5] [--modes 0,1,2,3]
+"""
+import argparse
+import ctypes
+import json
+import os
+import statistics
+import sys
+
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, REPO)
+
+NAMES = {0: "product", 1: "no-exact-check", 2: "stage1-only", 3: "stream-only"}
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gib", type=float, default=4.0)
+    ap.add_argument("--rules", default="C")
+    ap.add_argument("--rounds", type=int, default=5)
+    ap.add_argument("--reps", type=int, default=3)
+    ap.add_argument("--modes", default="0,1,2,3")
+    a = ap.parse_args()
+    import torch
+    import yara_amd
+    from yara_amd import _lib
+    L = _lib.lib()
+    L.yr_amd__diag_kernel_mode.argtypes = [ctypes.c_void_p, ctypes.c_int]
+    n = int(a.gib * (1 << 30))
+    buf = torch.empty(n + 16, dtype=torch.uint8, device="cuda")
+    yara_amd.fill_xorshift64(buf.data_ptr(), n, 1)
+    t = yara_amd.Tables.from_npz(os.path.join(REPO, "tests", "golden", "tables", a.rules + ".npz"))
+    sc = yara_amd.Scanner(t)
+    sc.set_timing(True)
+    modes = [int(m) for m in a.modes.split(",")]
+    res = {m: [] for m in modes}
+    for _ in range(a.rounds):
+        for m in modes:
+            assert L.yr_amd__diag_kernel_mode(sc.handle if hasattr(sc, "handle") else sc._h, m) == 0
+            for _ in range(a.reps):
+                sc.scan_device(buf.data_ptr(), n)
+                sc.device_result()
+                res[m].append(sc.kernel_ms())
+    L.yr_amd__diag_kernel_mode(sc._h, 0)
+    out = {}
+    for m in modes:
+        med = statistics.median(res[m])
+        out[NAMES[m]] = {"median_ms": round(med, 4), "min_ms": round(min(res[m]), 4),
+                         "GB/s": round(n / (med * 1e-3) / 1e9, 1)}
+    print(json.dumps({"rules": a.rules, "bytes": n, "modes": out}, indent=1))
+
+
+if __name__ == "__main__":
+    main()

@@ -34,14 +34,21 @@ constexpr uint32_t kQueueCap = 256;
 
 constexpr uint32_t kHashK = 0x9E3779u;  // 24-bit odd multiplier
 
-// Filter hash of a 3-byte window.  w3 holds the window in its low 24 bits
-// (little endian: oldest byte lowest); any upper byte is ignored by the 24-bit
-// multiply (v_mul_u32_u24 on gfx950).
-__host__ __device__ inline uint32_t filter_hash(uint32_t w3) {
-  return (w3 & 0xFFFFFFu) * kHashK;  // low 32 bits; hipcc emits v_mul_u32_u24
+// Blocked-Bloom filter hash of a 3-byte window: one 32-bit filter word and two
+// bit positions inside it (k = 2 in one word: one LDS read per position).
+// w3 holds the window in its low 24 bits (little endian, oldest byte lowest);
+// any upper byte is ignored.  On gfx950 the two halves of the 48-bit product
+// are v_mul_u32_u24 and v_mul_hi_u32_u24 (full rate).
+struct FilterProbe {
+  uint32_t word;  // index into the kFilterWords-word filter
+  uint32_t b1, b2;
+};
+__host__ __device__ inline FilterProbe filter_probe(uint32_t w3) {
+  const uint32_t x = w3 & 0xFFFFFFu;
+  const uint32_t lo = x * kHashK;
+  const uint32_t hi = (uint32_t)(((uint64_t)x * kHashK) >> 32);
+  return FilterProbe{hi & (kFilterWords - 1), lo >> 27, (lo >> 22) & 31u};
 }
-__host__ __device__ inline uint32_t filter_word(uint32_t h) { return h >> (32 - (kFilterLog2Bits - 5)); }
-__host__ __device__ inline uint32_t filter_bit(uint32_t h) { return (h >> (32 - kFilterLog2Bits)) & 31u; }
 
 // Exact table: open addressing, linear probing, 64-bit slots
 //   slot = (1 << 63) | (len << 32) | key,  0 = empty

@@ -30,38 +30,64 @@ __device__ __forceinline__ uint32_t lane_id() {
   return __builtin_amdgcn_mbcnt_hi(~0u, __builtin_amdgcn_mbcnt_lo(~0u, 0u));
 }
 
-__device__ __forceinline__ uint32_t wave_inclusive_scan(uint32_t v, uint32_t lane) {
-#pragma unroll
-  for (int d = 1; d < kWave; d <<= 1) {
-    uint32_t o = __shfl_up(v, d, kWave);
-    if (lane >= (uint32_t)d) v += o;
-  }
+// Inclusive prefix sum over the 64 lanes with DPP (no LDS traffic):
+// Hillis-Steele inside each 16-lane row, then row_bcast:15 / row_bcast:31.
+__device__ __forceinline__ uint32_t wave_inclusive_scan(uint32_t v) {
+  v += __builtin_amdgcn_update_dpp(0u, v, 0x111, 0xF, 0xF, true);   // row_shr:1
+  v += __builtin_amdgcn_update_dpp(0u, v, 0x112, 0xF, 0xF, true);   // row_shr:2
+  v += __builtin_amdgcn_update_dpp(0u, v, 0x114, 0xF, 0xF, true);   // row_shr:4
+  v += __builtin_amdgcn_update_dpp(0u, v, 0x118, 0xF, 0xF, true);   // row_shr:8
+  v += __builtin_amdgcn_update_dpp(0u, v, 0x142, 0xA, 0xF, false);  // row_bcast:15
+  v += __builtin_amdgcn_update_dpp(0u, v, 0x143, 0xC, 0xF, false);  // row_bcast:31
   return v;
 }
 
 // Exact test of one position (byte index g of the block; position g + 1):
 // does a key of length L <= min(4, g + 1) equal the L bytes ending at g?
-__device__ __noinline__ bool exact_check(const uint8_t* __restrict__ data,
+// The first probe of every key length is issued before any is consumed, and
+// the table is at most 1/4 full, so a test costs ~one dependent L2 round trip
+// after the 4-byte window load.
+__device__ __noinline__ bool exact_check(const uint8_t* __restrict__ data, uint64_t block_size,
                                          const uint64_t* __restrict__ exact, uint32_t exact_mask,
                                          uint32_t len_mask, uint64_t g) {
-  uint32_t w4 = 0;
+  uint32_t w4;
+  const uint64_t a = g - 3;                       // first byte of the 4-byte window
+  if (g >= 3 && (a & ~3ull) + 8 <= block_size) {
+    const uint64_t a0 = a & ~3ull;
+    const uint32_t lo = *reinterpret_cast<const uint32_t*>(data + a0);
+    const uint32_t hi = *reinterpret_cast<const uint32_t*>(data + a0 + 4);
+    w4 = __builtin_amdgcn_alignbyte(hi, lo, (uint32_t)(a & 3));
+  } else {                                        // block head / tail: bytewise
+    w4 = 0;
 #pragma unroll
-  for (int i = 0; i < 4; ++i) {
-    int64_t idx = (int64_t)g - 3 + i;
-    uint32_t b = idx >= 0 ? (uint32_t)data[idx] : 0u;
-    w4 |= b << (8 * i);
+    for (int i = 0; i < 4; ++i) {
+      const int64_t idx = (int64_t)g - 3 + i;
+      w4 |= (idx >= 0 ? (uint32_t)data[idx] : 0u) << (8 * i);
+    }
   }
   const uint64_t pos = g + 1;
-  for (uint32_t L = 1; L <= 4; ++L) {
-    if (!((len_mask >> L) & 1u) || pos < L) continue;
+  uint32_t slot[4];
+  uint64_t want[4], e[4];
+  bool act[4];
+#pragma unroll
+  for (int L = 1; L <= 4; ++L) {
+    act[L - 1] = ((len_mask >> L) & 1u) && pos >= (uint64_t)L;
     const uint32_t key = L == 4 ? w4 : (w4 >> (8 * (4 - L)));
-    const uint64_t want = exact_entry(key, L);
-    uint32_t s = exact_hash(key, L) & exact_mask;
-    for (uint32_t probe = 0; probe <= exact_mask; ++probe) {
-      const uint64_t e = exact[s];
-      if (e == want) return true;
-      if (e == 0) break;
+    want[L - 1] = exact_entry(key, L);
+    slot[L - 1] = exact_hash(key, L) & exact_mask;
+    e[L - 1] = act[L - 1] ? exact[slot[L - 1]] : 0ull;
+  }
+#pragma unroll
+  for (int i = 0; i < 4; ++i)
+    if (act[i] && e[i] == want[i]) return true;
+  for (int i = 0; i < 4; ++i) {                   // linear-probe collisions (rare)
+    if (!act[i] || e[i] == 0) continue;
+    uint32_t s = slot[i];
+    for (uint32_t probe = 0; probe < exact_mask; ++probe) {
       s = (s + 1) & exact_mask;
+      const uint64_t v = exact[s];
+      if (v == want[i]) return true;
+      if (v == 0) break;
     }
   }
   return false;
@@ -75,6 +101,7 @@ struct WaveQueue {
 
 // Exact-check up to 64 queued hits and append the survivors, in order, to the
 // segment's output.
+template <int MODE>
 __device__ __forceinline__ void drain(const ScanParams& p, WaveQueue& q, uint32_t lane,
                                       uint64_t seg_start, uint32_t* out, uint32_t& found) {
   const uint32_t n = min(q.tail - q.head, (uint32_t)kWave);
@@ -83,7 +110,9 @@ __device__ __forceinline__ void drain(const ScanParams& p, WaveQueue& q, uint32_
   uint32_t off = 0;
   if (lane < n) {
     off = q.ring[(q.head + lane) % kQueueCap];
-    hit = exact_check(p.data, p.exact, p.exact_mask, p.len_mask, seg_start + off);
+    hit = MODE == 1 ? (off & 1023u) == 7u
+                    : exact_check(p.data, p.block_size, p.exact, p.exact_mask, p.len_mask,
+                                  seg_start + off);
   }
   const uint64_t b = __ballot(hit);
   if (hit) {
@@ -116,6 +145,57 @@ __device__ __forceinline__ uint4 load_tile(const uint8_t* base, uint32_t tile_of
   return v;
 }
 
+// Append this tile's filter hits to the wave ring in ascending position order
+// (lane-major, bit-minor == byte order).  Few hitting lanes: a scalar walk over
+// them; many: DPP prefix sum of per-lane counts and per-lane ring writes.
+template <int MODE>
+__device__ __forceinline__ void append_hits(const ScanParams& p, WaveQueue& q, uint32_t lane,
+                                            uint32_t mask, uint32_t lane_off, uint64_t seg_start,
+                                            uint32_t* out, uint32_t& found) {
+  const uint64_t any = __ballot(mask != 0);
+  if (__popcll(any) <= 4) {
+    uint64_t b = any;
+    while (b) {
+      const uint32_t l = (uint32_t)__builtin_ctzll(b);
+      b &= b - 1;
+      uint32_t m = __builtin_amdgcn_readlane(mask, l);
+      const uint32_t off = __builtin_amdgcn_readlane(lane_off, l);
+      while (m) {
+        const uint32_t j = (uint32_t)__builtin_ctz(m);
+        m &= m - 1;
+        if (q.tail - q.head == kQueueCap) drain<MODE>(p, q, lane, seg_start, out, found);
+        if (lane == 0) q.ring[q.tail % kQueueCap] = off + j;
+        ++q.tail;
+      }
+    }
+  } else {
+    const uint32_t c = __popc(mask);
+    const uint32_t incl = wave_inclusive_scan(c);
+    const uint32_t total = __builtin_amdgcn_readlane(incl, kWave - 1);
+    const uint32_t excl = incl - c;
+    uint32_t done = 0;
+    while (done < total) {
+      const uint32_t space = kQueueCap - (q.tail - q.head);
+      const uint32_t take = min(space, total - done);
+      uint32_t m = mask, r = excl;
+      while (m != 0 && r < done + take) {
+        const uint32_t j = (uint32_t)__builtin_ctz(m);
+        m &= m - 1;
+        if (r >= done) q.ring[(q.tail + (r - done)) % kQueueCap] = lane_off + j;
+        ++r;
+      }
+      q.tail += take;
+      done += take;
+      while (q.tail - q.head >= (uint32_t)kWave) drain<MODE>(p, q, lane, seg_start, out, found);
+    }
+  }
+  while (q.tail - q.head >= (uint32_t)kWave) drain<MODE>(p, q, lane, seg_start, out, found);
+}
+
+// MODE: 0 = the product kernel.  1..3 are profiling ablations only (their
+// output is wrong by construction): 1 = no exact check (drain only pops),
+// 2 = stage 1 only (no queue), 3 = input streaming only (no filter lookups).
+template <int MODE>
 __device__ void scan_segment(const ScanParams& p, const uint32_t* __restrict__ filt,
                              WaveQueue& q, uint32_t seg, uint32_t lane) {
   const uint64_t seg_start = p.byte_begin + (uint64_t)seg * p.seg_bytes;
@@ -137,9 +217,9 @@ __device__ void scan_segment(const ScanParams& p, const uint32_t* __restrict__ f
     uint4 nxt = make_uint4(0, 0, 0, 0);
     if (t + 1 < ntiles) nxt = load_tile(base, tile_off + kTile, lane, avail);
 
-    const uint32_t up = __shfl_up(cur.w, 1, kWave);
-    const uint32_t S0 = lane == 0 ? carry : up;
-    carry = __shfl(cur.w, kWave - 1, kWave);
+    // previous lane's last dword (lane 0: the previous tile's / the halo)
+    const uint32_t S0 = __builtin_amdgcn_update_dpp(carry, cur.w, 0x138, 0xF, 0xF, false);  // wave_shr:1
+    carry = __builtin_amdgcn_readlane(cur.w, kWave - 1);
     const uint32_t S[6] = {S0, cur.x, cur.y, cur.z, cur.w, 0u};
 
     uint32_t mask = 0;
@@ -149,43 +229,31 @@ __device__ void scan_segment(const ScanParams& p, const uint32_t* __restrict__ f
       const int o = k + 2;
       const uint32_t x = (o & 3) ? __builtin_amdgcn_alignbyte(S[(o >> 2) + 1], S[o >> 2], o & 3)
                                  : S[o >> 2];
-      const uint32_t h = filter_hash(x);
-      const uint32_t w = filt[filter_word(h)];
-      mask |= ((w >> filter_bit(h)) & 1u) << k;
+      if constexpr (MODE == 3) {
+        mask ^= x;
+      } else {
+        const FilterProbe fp = filter_probe(x);
+        const uint32_t w = filt[fp.word];
+        mask |= (((w >> fp.b1) & (w >> fp.b2)) & 1u) << k;
+      }
+    }
+    if constexpr (MODE >= 2) {
+      asm volatile("" ::"v"(mask));
+      cur = nxt;
+      continue;
     }
     const uint32_t lane_off = tile_off + lane * kBytesPerLane;
     if (lane_off + kBytesPerLane > seg_len) {
       mask = lane_off >= seg_len ? 0u : (mask & ((1u << (seg_len - lane_off)) - 1u));
     }
-
-    // ordered append of this tile's hits to the wave ring
-    const uint32_t c = __popc(mask);
-    const uint32_t incl = wave_inclusive_scan(c, lane);
-    const uint32_t total = __shfl(incl, kWave - 1, kWave);
-    if (total != 0) {
-      const uint32_t excl = incl - c;
-      uint32_t done = 0;
-      while (done < total) {
-        const uint32_t space = kQueueCap - (q.tail - q.head);
-        const uint32_t take = min(space, total - done);
-        uint32_t m = mask, r = excl;
-        while (m != 0 && r < done + take) {
-          const uint32_t j = __builtin_ctz(m);
-          m &= m - 1;
-          if (r >= done) q.ring[(q.tail + (r - done)) % kQueueCap] = lane_off + j;
-          ++r;
-        }
-        q.tail += take;
-        done += take;
-        while (q.tail - q.head >= (uint32_t)kWave) drain(p, q, lane, seg_start, out, found);
-      }
-    }
+    if (__ballot(mask != 0) != 0) append_hits<MODE>(p, q, lane, mask, lane_off, seg_start, out, found);
     cur = nxt;
   }
-  while (q.tail != q.head) drain(p, q, lane, seg_start, out, found);
+  while (q.tail != q.head) drain<MODE>(p, q, lane, seg_start, out, found);
   if (lane == 0) p.seg_count[seg] = found;
 }
 
+template <int MODE>
 __global__ __launch_bounds__(kWGThreads, 1) void scan_segments_kernel(ScanParams p) {
   extern __shared__ __attribute__((aligned(16))) uint32_t lds[];
   uint32_t* filt = lds;
@@ -201,7 +269,7 @@ __global__ __launch_bounds__(kWGThreads, 1) void scan_segments_kernel(ScanParams
   q.ring = lds + kFilterWords + wid * kQueueCap;
   const uint32_t total_waves = gridDim.x * kWavesPerWG;
   for (uint32_t seg = blockIdx.x * kWavesPerWG + wid; seg < p.n_segments; seg += total_waves) {
-    scan_segment(p, filt, q, seg, lane);
+    scan_segment<MODE>(p, filt, q, seg, lane);
   }
 }
 
@@ -301,9 +369,14 @@ __global__ __launch_bounds__(256) void xorshift_fill_kernel(uint8_t* buf, uint64
 // Launch wrappers (host side, called from scanner.cpp).
 namespace yamd {
 
-hipError_t launch_scan(const ScanParams& p, int grid, hipStream_t s) {
+hipError_t launch_scan(const ScanParams& p, int grid, hipStream_t s, int mode) {
   const size_t lds = kFilterBytes + (size_t)kWavesPerWG * kQueueCap * 4;
-  hipLaunchKernelGGL(scan_segments_kernel, dim3(grid), dim3(kWGThreads), lds, s, p);
+  switch (mode) {
+    case 1: hipLaunchKernelGGL(scan_segments_kernel<1>, dim3(grid), dim3(kWGThreads), lds, s, p); break;
+    case 2: hipLaunchKernelGGL(scan_segments_kernel<2>, dim3(grid), dim3(kWGThreads), lds, s, p); break;
+    case 3: hipLaunchKernelGGL(scan_segments_kernel<3>, dim3(grid), dim3(kWGThreads), lds, s, p); break;
+    default: hipLaunchKernelGGL(scan_segments_kernel<0>, dim3(grid), dim3(kWGThreads), lds, s, p); break;
+  }
   return hipGetLastError();
 }
 
@@ -327,9 +400,14 @@ hipError_t launch_xorshift(uint8_t* buf, uint64_t n, const uint64_t* states, uin
 }
 
 hipError_t configure_scan_kernel() {
-  const size_t lds = kFilterBytes + (size_t)kWavesPerWG * kQueueCap * 4;
-  return hipFuncSetAttribute((const void*)scan_segments_kernel,
-                             hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+  const int lds = (int)(kFilterBytes + (size_t)kWavesPerWG * kQueueCap * 4);
+  hipError_t e = hipSuccess;
+  for (const void* k : {(const void*)scan_segments_kernel<0>, (const void*)scan_segments_kernel<1>,
+                        (const void*)scan_segments_kernel<2>, (const void*)scan_segments_kernel<3>}) {
+    hipError_t r = hipFuncSetAttribute(k, hipFuncAttributeMaxDynamicSharedMemorySize, lds);
+    if (r != hipSuccess) e = r;
+  }
+  return e;
 }
 
 }  // namespace yamd

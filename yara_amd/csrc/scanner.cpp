@@ -18,7 +18,7 @@
 #include "tables.h"
 
 namespace yamd {
-hipError_t launch_scan(const ScanParams& p, int grid, hipStream_t s);
+hipError_t launch_scan(const ScanParams& p, int grid, hipStream_t s, int mode);
 hipError_t launch_compact(const ScanParams& p, uint64_t* seg_offset, uint64_t* summary,
                           uint64_t* positions, bool scatter, hipStream_t s);
 hipError_t launch_xorshift(uint8_t* buf, uint64_t n, const uint64_t* states, uint32_t n_chunks,
@@ -67,6 +67,8 @@ struct yr_amd_scanner {
   bool timing = false;
   hipEvent_t ev_begin = nullptr, ev_end = nullptr;
   bool ev_valid = false;
+
+  int diag_mode = 0;   // profiling ablation of the scan kernel (0 = product)
 };
 
 #define HIP_TRY(expr)                                   \
@@ -117,7 +119,7 @@ uint32_t choose_seg_bytes(uint64_t nbytes, int num_cus) {
 
 int run_scan(yr_amd_scanner* s) {
   if (s->timing) HIP_TRY(hipEventRecord(s->ev_begin, s->stream));
-  HIP_TRY(launch_scan(s->last, s->last_grid, s->stream));
+  HIP_TRY(launch_scan(s->last, s->last_grid, s->stream, s->diag_mode));
   if (s->timing) {
     HIP_TRY(hipEventRecord(s->ev_end, s->stream));
     s->ev_valid = true;
@@ -249,6 +251,14 @@ int yr_amd_scanner_set_timing(yr_amd_scanner* s, int enable) {
   }
   s->timing = enable != 0;
   s->ev_valid = false;
+  return YR_AMD_SUCCESS;
+}
+
+// Not declared in include/yara_amd.h: profiling ablations of the scan kernel
+// (tools/ablate.py).  Any mode other than 0 produces wrong results.
+int yr_amd__diag_kernel_mode(yr_amd_scanner* s, int mode) {
+  if (s == nullptr || mode < 0 || mode > 3) return YR_AMD_INVALID_ARGUMENT;
+  s->diag_mode = mode;
   return YR_AMD_SUCCESS;
 }
 
