@@ -29,39 +29,52 @@ constexpr int kFilterLog2Bits = 20;
 constexpr uint32_t kFilterWords = 1u << (kFilterLog2Bits - 5);   // 32768
 constexpr uint32_t kFilterBytes = kFilterWords * 4;              // 131072
 
-// Per-wave LDS ring of filter hits awaiting the exact check.
-constexpr uint32_t kQueueCap = 256;
+// Per-wave LDS ring of filter hits awaiting the exact check: one 32-byte entry
+// per (tile, lane) with hits = the lane's 20 bytes of window context + mask.
+constexpr uint32_t kQueueCap = 64;
+constexpr uint32_t kQueueEntryWords = 8;
+constexpr uint32_t kQueueBytes = kWavesPerWG * kQueueCap * kQueueEntryWords * 4;   // 32 KiB
+constexpr uint32_t kScanLdsBytes = kFilterBytes + kQueueBytes;                   // 160 KiB
 
-constexpr uint32_t kHashK = 0x9E3779u;  // 24-bit odd multiplier
-
-// Blocked-Bloom filter hash of a 3-byte window: one 32-bit filter word and two
-// bit positions inside it (k = 2 in one word: one LDS read per position).
-// w3 holds the window in its low 24 bits (little endian, oldest byte lowest);
-// any upper byte is ignored.  On gfx950 the two halves of the 48-bit product
-// are v_mul_u32_u24 and v_mul_hi_u32_u24 (full rate).
+// Blocked-Bloom filter probe of a 3-byte window x = a | b << 8 | c << 16
+// (a = oldest byte): one 32-bit filter word, two bit positions inside it
+// (k = 2 in one word: one LDS read per position).  Built from the key bits
+// with VOP2 shifts/logic only -- on gfx950 those issue at twice the rate of
+// v_mul_u32_u24 / v_alignbit / v_bfe -- and never reading bits 24..31, so a
+// window register may carry a neighbouring byte there:
+//   word = (x >> 9 ^ x) & 0x7FFF     device byte address: (x >> 7 ^ x << 2) & 0x1FFFC
+//   b1   = x & 31                   device: the shifter reads only bits 0..4
+//   b2   = (x >> 7) & 31            device: same register as the address term
 struct FilterProbe {
   uint32_t word;  // index into the kFilterWords-word filter
   uint32_t b1, b2;
 };
 __host__ __device__ inline FilterProbe filter_probe(uint32_t w3) {
   const uint32_t x = w3 & 0xFFFFFFu;
-  const uint32_t lo = x * kHashK;
-  const uint32_t hi = (uint32_t)(((uint64_t)x * kHashK) >> 32);
-  return FilterProbe{hi & (kFilterWords - 1), lo >> 27, (lo >> 22) & 31u};
+  return FilterProbe{((x >> 9) ^ x) & (kFilterWords - 1), x & 31u, (x >> 7) & 31u};
 }
 
-// Exact table: open addressing, linear probing, 64-bit slots
-//   slot = (1 << 63) | (len << 32) | key,  0 = empty
-// key = the last `len` bytes before the position, little endian.
-__host__ __device__ inline uint64_t exact_entry(uint32_t key, uint32_t len) {
-  return (1ull << 63) | ((uint64_t)len << 32) | key;
+// Exact key sets (second stage), one uint32 array in HBM:
+//   [0, 8)        1-byte keys: 256-bit bitmap
+//   [8, 2056)     2-byte keys: 65536-bit bitmap
+//   t3, t4        3- and 4-byte keys: two-choice bucketed hash tables, 4 keys
+//                 per 16-byte bucket; a lookup loads both candidate buckets
+//                 (two independent dwordx4 loads: one round trip, no probe
+//                 chains).  t3 stores key | 1 << 24, t4 stores the key; 0 marks
+//                 an empty slot (a 4-byte key of 0 is kept in a flag).
+// Keys are little endian: the first byte of the key in bits 0..7.
+constexpr uint32_t kExactBm1 = 0;
+constexpr uint32_t kExactBm2 = 8;
+constexpr uint32_t kExactHeadWords = 8 + 2048;
+constexpr uint32_t kExactZero4 = 1u;   // flag: the 4-byte key 0x00000000 exists
+
+__host__ __device__ inline uint32_t bucket_hash1(uint32_t key) {
+  uint32_t h = key * 0x9E3779B1u;
+  return h ^ (h >> 16);
 }
-__host__ __device__ inline uint32_t exact_hash(uint32_t key, uint32_t len) {
-  uint32_t h = key * 0x85EBCA6Bu ^ (len * 0xC2B2AE35u);
-  h ^= h >> 15;
-  h *= 0x2C1B3C6Du;
-  h ^= h >> 13;
-  return h;
+__host__ __device__ inline uint32_t bucket_hash2(uint32_t key) {
+  uint32_t h = (key ^ 0x5BD1E995u) * 0x85EBCA77u;
+  return h ^ (h >> 13);
 }
 
 struct ScanParams {
@@ -70,8 +83,10 @@ struct ScanParams {
   uint64_t byte_begin;      // first byte of this launch (multiple of 16)
   uint64_t byte_end;        // one past the last byte
   const uint32_t* filter;   // kFilterWords words
-  const uint64_t* exact;    // exact_slots entries
-  uint32_t exact_mask;      // exact_slots - 1
+  const uint32_t* exact;    // exact key sets (layout above)
+  uint32_t t3_off, t3_mask; // word offset / bucket-count mask of the 3-byte table
+  uint32_t t4_off, t4_mask; // same for the 4-byte table
+  uint32_t exact_flags;     // kExactZero4
   uint32_t len_mask;        // bit L set iff keys of length L exist
   uint32_t n_segments;
   uint32_t seg_bytes;       // bytes per segment (multiple of kTile)

@@ -42,84 +42,99 @@ __device__ __forceinline__ uint32_t wave_inclusive_scan(uint32_t v) {
   return v;
 }
 
-// Exact test of one position (byte index g of the block; position g + 1):
-// does a key of length L <= min(4, g + 1) equal the L bytes ending at g?
-// The first probe of every key length is issued before any is consumed, and
-// the table is at most 1/4 full, so a test costs ~one dependent L2 round trip
-// after the 4-byte window load.
-__device__ __noinline__ bool exact_check(const uint8_t* __restrict__ data, uint64_t block_size,
-                                         const uint64_t* __restrict__ exact, uint32_t exact_mask,
-                                         uint32_t len_mask, uint64_t g) {
-  uint32_t w4;
-  const uint64_t a = g - 3;                       // first byte of the 4-byte window
-  if (g >= 3 && (a & ~3ull) + 8 <= block_size) {
-    const uint64_t a0 = a & ~3ull;
-    const uint32_t lo = *reinterpret_cast<const uint32_t*>(data + a0);
-    const uint32_t hi = *reinterpret_cast<const uint32_t*>(data + a0 + 4);
-    w4 = __builtin_amdgcn_alignbyte(hi, lo, (uint32_t)(a & 3));
-  } else {                                        // block head / tail: bytewise
-    w4 = 0;
-#pragma unroll
-    for (int i = 0; i < 4; ++i) {
-      const int64_t idx = (int64_t)g - 3 + i;
-      w4 |= (idx >= 0 ? (uint32_t)data[idx] : 0u) << (8 * i);
+// Exact test of one position `pos` of the block: does a key of length
+// L <= min(4, pos) equal the last L bytes before it?  w4 = those 4 bytes,
+// little endian (oldest lowest; zeros before the block start).  Every load
+// (bitmap words, both candidate buckets of each table) is independent: one
+// round trip.
+__device__ __noinline__ bool exact_check(uint32_t w4, uint64_t pos, const ScanParams& p) {
+  const uint32_t* __restrict__ ex = p.exact;
+  bool hit = false;
+  const uint32_t lm = p.len_mask;
+  if ((lm & 2u) && pos >= 1) {
+    const uint32_t k = w4 >> 24;
+    hit |= (ex[kExactBm1 + (k >> 5)] >> (k & 31)) & 1u;
+  }
+  if ((lm & 4u) && pos >= 2) {
+    const uint32_t k = w4 >> 16;
+    hit |= (ex[kExactBm2 + (k >> 5)] >> (k & 31)) & 1u;
+  }
+  if ((lm & 8u) && pos >= 3) {
+    const uint32_t k = (w4 >> 8) | (1u << 24);
+    const uint4 a = *reinterpret_cast<const uint4*>(ex + p.t3_off + (bucket_hash1(k) & p.t3_mask) * 4);
+    const uint4 b = *reinterpret_cast<const uint4*>(ex + p.t3_off + (bucket_hash2(k) & p.t3_mask) * 4);
+    hit |= a.x == k || a.y == k || a.z == k || a.w == k || b.x == k || b.y == k || b.z == k || b.w == k;
+  }
+  if ((lm & 16u) && pos >= 4) {
+    const uint32_t k = w4;
+    if (k == 0) {
+      hit |= (p.exact_flags & kExactZero4) != 0;
+    } else {
+      const uint4 a = *reinterpret_cast<const uint4*>(ex + p.t4_off + (bucket_hash1(k) & p.t4_mask) * 4);
+      const uint4 b = *reinterpret_cast<const uint4*>(ex + p.t4_off + (bucket_hash2(k) & p.t4_mask) * 4);
+      hit |= a.x == k || a.y == k || a.z == k || a.w == k || b.x == k || b.y == k || b.z == k || b.w == k;
     }
   }
-  const uint64_t pos = g + 1;
-  uint32_t slot[4];
-  uint64_t want[4], e[4];
-  bool act[4];
-#pragma unroll
-  for (int L = 1; L <= 4; ++L) {
-    act[L - 1] = ((len_mask >> L) & 1u) && pos >= (uint64_t)L;
-    const uint32_t key = L == 4 ? w4 : (w4 >> (8 * (4 - L)));
-    want[L - 1] = exact_entry(key, L);
-    slot[L - 1] = exact_hash(key, L) & exact_mask;
-    e[L - 1] = act[L - 1] ? exact[slot[L - 1]] : 0ull;
-  }
-#pragma unroll
-  for (int i = 0; i < 4; ++i)
-    if (act[i] && e[i] == want[i]) return true;
-  for (int i = 0; i < 4; ++i) {                   // linear-probe collisions (rare)
-    if (!act[i] || e[i] == 0) continue;
-    uint32_t s = slot[i];
-    for (uint32_t probe = 0; probe < exact_mask; ++probe) {
-      s = (s + 1) & exact_mask;
-      const uint64_t v = exact[s];
-      if (v == want[i]) return true;
-      if (v == 0) break;
-    }
-  }
-  return false;
+  return hit;
 }
 
+// The 4 bytes ending at lane byte j (0..15) from the lane's window context
+// C[0] = the 4 bytes before the lane, C[1..4] = its 16 bytes.
+__device__ __forceinline__ uint32_t window4(const uint32_t (&C)[5], uint32_t j) {
+  const uint32_t o = j + 1, i = o >> 2;
+  uint32_t lo = C[0], hi = C[1];
+  if (i == 1) { lo = C[1]; hi = C[2]; }
+  if (i == 2) { lo = C[2]; hi = C[3]; }
+  if (i == 3) { lo = C[3]; hi = C[4]; }
+  if (i == 4) { lo = C[4]; hi = 0u; }
+  return __builtin_amdgcn_alignbyte(hi, lo, o & 3u);
+}
+
+// Per-wave LDS ring of filter hits awaiting the exact check.  One 32-byte
+// entry per (tile, lane) with at least one hit: the lane's window context
+// (4 bytes before it + its 16 bytes) and (lane byte offset in segment / 16)
+// << 16 | 16-bit hit mask.  Entries are appended in lane order, so ring order
+// is ascending position order.  The exact check then needs no global load
+// of the input, only the hash-table probes.
 struct WaveQueue {
-  uint32_t* ring;   // kQueueCap entries in LDS: byte offset within segment
+  uint32_t* ring;   // kQueueCap entries of kQueueEntryWords dwords
   uint32_t head;    // wave-uniform counters (monotonic)
   uint32_t tail;
 };
 
-// Exact-check up to 64 queued hits and append the survivors, in order, to the
-// segment's output.
+// Exact-check the hits of up to 64 ring entries and append the survivors, in
+// order, to the segment's output.
 template <int MODE>
 __device__ __forceinline__ void drain(const ScanParams& p, WaveQueue& q, uint32_t lane,
                                       uint64_t seg_start, uint32_t* out, uint32_t& found) {
   const uint32_t n = min(q.tail - q.head, (uint32_t)kWave);
   __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
-  bool hit = false;
-  uint32_t off = 0;
+  uint32_t keep = 0, off0 = 0;
   if (lane < n) {
-    off = q.ring[(q.head + lane) % kQueueCap];
-    hit = MODE == 1 ? (off & 1023u) == 7u
-                    : exact_check(p.data, p.block_size, p.exact, p.exact_mask, p.len_mask,
-                                  seg_start + off);
+    const uint32_t* ent = q.ring + ((q.head + lane) % kQueueCap) * kQueueEntryWords;
+    const uint4 a = *reinterpret_cast<const uint4*>(ent);
+    const uint4 b = *reinterpret_cast<const uint4*>(ent + 4);
+    const uint32_t C[5] = {a.x, a.y, a.z, a.w, b.x};
+    off0 = (b.y >> 16) * kBytesPerLane;
+    uint32_t m = b.y & 0xFFFFu;
+    while (m) {
+      const uint32_t j = (uint32_t)__builtin_ctz(m);
+      m &= m - 1;
+      const bool hit = MODE == 1 ? ((off0 + j) & 1023u) == 7u
+                                 : exact_check(window4(C, j), seg_start + off0 + j + 1, p);
+      keep |= (uint32_t)hit << j;
+    }
   }
-  const uint64_t b = __ballot(hit);
-  if (hit) {
-    const uint32_t idx = found + (uint32_t)__popcll(b & ((1ull << lane) - 1));
-    if (idx < p.seg_cap) out[idx] = off;
+  const uint32_t c = __popc(keep);
+  const uint32_t incl = wave_inclusive_scan(c);
+  uint32_t idx = found + incl - c;
+  while (keep) {
+    const uint32_t j = (uint32_t)__builtin_ctz(keep);
+    keep &= keep - 1;
+    if (idx < p.seg_cap) out[idx] = off0 + j;
+    ++idx;
   }
-  found += (uint32_t)__popcll(b);
+  found += __builtin_amdgcn_readlane(incl, kWave - 1);
   q.head += n;
 }
 
@@ -145,56 +160,10 @@ __device__ __forceinline__ uint4 load_tile(const uint8_t* base, uint32_t tile_of
   return v;
 }
 
-// Append this tile's filter hits to the wave ring in ascending position order
-// (lane-major, bit-minor == byte order).  Few hitting lanes: a scalar walk over
-// them; many: DPP prefix sum of per-lane counts and per-lane ring writes.
-template <int MODE>
-__device__ __forceinline__ void append_hits(const ScanParams& p, WaveQueue& q, uint32_t lane,
-                                            uint32_t mask, uint32_t lane_off, uint64_t seg_start,
-                                            uint32_t* out, uint32_t& found) {
-  const uint64_t any = __ballot(mask != 0);
-  if (__popcll(any) <= 4) {
-    uint64_t b = any;
-    while (b) {
-      const uint32_t l = (uint32_t)__builtin_ctzll(b);
-      b &= b - 1;
-      uint32_t m = __builtin_amdgcn_readlane(mask, l);
-      const uint32_t off = __builtin_amdgcn_readlane(lane_off, l);
-      while (m) {
-        const uint32_t j = (uint32_t)__builtin_ctz(m);
-        m &= m - 1;
-        if (q.tail - q.head == kQueueCap) drain<MODE>(p, q, lane, seg_start, out, found);
-        if (lane == 0) q.ring[q.tail % kQueueCap] = off + j;
-        ++q.tail;
-      }
-    }
-  } else {
-    const uint32_t c = __popc(mask);
-    const uint32_t incl = wave_inclusive_scan(c);
-    const uint32_t total = __builtin_amdgcn_readlane(incl, kWave - 1);
-    const uint32_t excl = incl - c;
-    uint32_t done = 0;
-    while (done < total) {
-      const uint32_t space = kQueueCap - (q.tail - q.head);
-      const uint32_t take = min(space, total - done);
-      uint32_t m = mask, r = excl;
-      while (m != 0 && r < done + take) {
-        const uint32_t j = (uint32_t)__builtin_ctz(m);
-        m &= m - 1;
-        if (r >= done) q.ring[(q.tail + (r - done)) % kQueueCap] = lane_off + j;
-        ++r;
-      }
-      q.tail += take;
-      done += take;
-      while (q.tail - q.head >= (uint32_t)kWave) drain<MODE>(p, q, lane, seg_start, out, found);
-    }
-  }
-  while (q.tail - q.head >= (uint32_t)kWave) drain<MODE>(p, q, lane, seg_start, out, found);
-}
-
-// MODE: 0 = the product kernel.  1..3 are profiling ablations only (their
-// output is wrong by construction): 1 = no exact check (drain only pops),
-// 2 = stage 1 only (no queue), 3 = input streaming only (no filter lookups).
+// MODE: 0 = the product kernel.  Others are profiling ablations only (their
+// output is wrong by construction): 1 = no exact check, 2 = stage 1 only
+// (no queue), 3 = input streaming only (no filter), 4 = stage 1 with
+// bank-conflict-free LDS addresses, 5 = stage 1 VALU without the LDS reads.
 template <int MODE>
 __device__ void scan_segment(const ScanParams& p, const uint32_t* __restrict__ filt,
                              WaveQueue& q, uint32_t seg, uint32_t lane) {
@@ -205,6 +174,7 @@ __device__ void scan_segment(const ScanParams& p, const uint32_t* __restrict__ f
   const uint8_t* base = p.data + seg_start;
   uint32_t* out = p.seg_out + (size_t)seg * p.seg_cap;
   uint32_t found = 0;
+  const char* filt_bytes = reinterpret_cast<const char*>(filt);
 
   // 4 bytes before the segment (warm-up halo); zeros before the block start.
   uint32_t carry = seg_start >= 4 ? *reinterpret_cast<const uint32_t*>(base - 4) : 0u;
@@ -222,31 +192,67 @@ __device__ void scan_segment(const ScanParams& p, const uint32_t* __restrict__ f
     carry = __builtin_amdgcn_readlane(cur.w, kWave - 1);
     const uint32_t S[6] = {S0, cur.x, cur.y, cur.z, cur.w, 0u};
 
-    uint32_t mask = 0;
+    // Phase A: the 16 windows of this lane and their 16 filter-word reads,
+    // all issued before any is consumed (hides LDS latency at 4 waves/SIMD).
+    uint32_t xs[kBytesPerLane], ws[kBytesPerLane];
 #pragma unroll
     for (int k = 0; k < kBytesPerLane; ++k) {
       // low 24 bits = bytes k-2, k-1, k of this lane (stream offset k + 2)
       const int o = k + 2;
-      const uint32_t x = (o & 3) ? __builtin_amdgcn_alignbyte(S[(o >> 2) + 1], S[o >> 2], o & 3)
-                                 : S[o >> 2];
+      xs[k] = (o & 3) == 0   ? S[o >> 2]
+              : (o & 3) == 1 ? S[o >> 2] >> 8
+                             : __builtin_amdgcn_alignbyte(S[(o >> 2) + 1], S[o >> 2], o & 3);
+      if constexpr (MODE != 3) {
+        const uint32_t x = xs[k];
+        uint32_t addr = ((x >> 7) ^ (x << 2)) & (kFilterBytes - 4);
+        if constexpr (MODE == 4) addr = ((lane & 31u) * 4u + (uint32_t)k * 128u) & (kFilterBytes - 4);
+        if constexpr (MODE == 5) {
+          ws[k] = addr ^ x;
+        } else {
+          ws[k] = *reinterpret_cast<const __attribute__((address_space(3))) uint32_t*>(
+              (uintptr_t)addr);   // filter sits at LDS offset 0: no base add
+        }
+      }
+    }
+    // Phase B: blocked-Bloom test of bits b1 = x[0..4], b2 = x[7..11] (the
+    // shifter reads only the low 5 bits of the amount); acc collects the 16
+    // results via v_alignbit: afterwards bit 16 + k holds position k.
+    uint32_t acc = 0;
+#pragma unroll
+    for (int k = 0; k < kBytesPerLane; ++k) {
       if constexpr (MODE == 3) {
-        mask ^= x;
+        acc ^= xs[k];
       } else {
-        const FilterProbe fp = filter_probe(x);
-        const uint32_t w = filt[fp.word];
-        mask |= (((w >> fp.b1) & (w >> fp.b2)) & 1u) << k;
+        const uint32_t x = xs[k], w = ws[k];
+        const uint32_t t2 = (w >> (x & 31u)) & (w >> ((x >> 7) & 31u));
+        acc = __builtin_amdgcn_alignbit(t2, acc, 1);
       }
     }
     if constexpr (MODE >= 2) {
-      asm volatile("" ::"v"(mask));
+      asm volatile("" ::"v"(acc));
       cur = nxt;
       continue;
     }
+    uint32_t mask = acc >> 16;
     const uint32_t lane_off = tile_off + lane * kBytesPerLane;
     if (lane_off + kBytesPerLane > seg_len) {
       mask = lane_off >= seg_len ? 0u : (mask & ((1u << (seg_len - lane_off)) - 1u));
     }
-    if (__ballot(mask != 0) != 0) append_hits<MODE>(p, q, lane, mask, lane_off, seg_start, out, found);
+    const uint64_t any = __ballot(mask != 0);
+    if (any != 0) {
+      const uint32_t n = (uint32_t)__popcll(any);
+      while (q.tail - q.head + n > kQueueCap) drain<MODE>(p, q, lane, seg_start, out, found);
+      if (mask != 0) {
+        const uint32_t below = __builtin_amdgcn_mbcnt_hi((uint32_t)(any >> 32),
+                                                         __builtin_amdgcn_mbcnt_lo((uint32_t)any, 0u));
+        uint32_t* ent = q.ring + ((q.tail + below) % kQueueCap) * kQueueEntryWords;
+        *reinterpret_cast<uint4*>(ent) = make_uint4(S[0], S[1], S[2], S[3]);
+        *reinterpret_cast<uint4*>(ent + 4) =
+            make_uint4(S[4], ((lane_off / kBytesPerLane) << 16) | mask, 0u, 0u);
+      }
+      q.tail += n;
+      if (q.tail - q.head >= kQueueCap) drain<MODE>(p, q, lane, seg_start, out, found);
+    }
     cur = nxt;
   }
   while (q.tail != q.head) drain<MODE>(p, q, lane, seg_start, out, found);
@@ -266,7 +272,7 @@ __global__ __launch_bounds__(kWGThreads, 1) void scan_segments_kernel(ScanParams
   const uint32_t lane = lane_id();
   const uint32_t wid = threadIdx.x / kWave;
   WaveQueue q;
-  q.ring = lds + kFilterWords + wid * kQueueCap;
+  q.ring = lds + kFilterWords + wid * kQueueCap * kQueueEntryWords;
   const uint32_t total_waves = gridDim.x * kWavesPerWG;
   for (uint32_t seg = blockIdx.x * kWavesPerWG + wid; seg < p.n_segments; seg += total_waves) {
     scan_segment<MODE>(p, filt, q, seg, lane);
@@ -370,11 +376,13 @@ __global__ __launch_bounds__(256) void xorshift_fill_kernel(uint8_t* buf, uint64
 namespace yamd {
 
 hipError_t launch_scan(const ScanParams& p, int grid, hipStream_t s, int mode) {
-  const size_t lds = kFilterBytes + (size_t)kWavesPerWG * kQueueCap * 4;
+  const size_t lds = kScanLdsBytes;
   switch (mode) {
     case 1: hipLaunchKernelGGL(scan_segments_kernel<1>, dim3(grid), dim3(kWGThreads), lds, s, p); break;
     case 2: hipLaunchKernelGGL(scan_segments_kernel<2>, dim3(grid), dim3(kWGThreads), lds, s, p); break;
     case 3: hipLaunchKernelGGL(scan_segments_kernel<3>, dim3(grid), dim3(kWGThreads), lds, s, p); break;
+    case 4: hipLaunchKernelGGL(scan_segments_kernel<4>, dim3(grid), dim3(kWGThreads), lds, s, p); break;
+    case 5: hipLaunchKernelGGL(scan_segments_kernel<5>, dim3(grid), dim3(kWGThreads), lds, s, p); break;
     default: hipLaunchKernelGGL(scan_segments_kernel<0>, dim3(grid), dim3(kWGThreads), lds, s, p); break;
   }
   return hipGetLastError();
@@ -400,10 +408,11 @@ hipError_t launch_xorshift(uint8_t* buf, uint64_t n, const uint64_t* states, uin
 }
 
 hipError_t configure_scan_kernel() {
-  const int lds = (int)(kFilterBytes + (size_t)kWavesPerWG * kQueueCap * 4);
+  const int lds = (int)kScanLdsBytes;
   hipError_t e = hipSuccess;
   for (const void* k : {(const void*)scan_segments_kernel<0>, (const void*)scan_segments_kernel<1>,
-                        (const void*)scan_segments_kernel<2>, (const void*)scan_segments_kernel<3>}) {
+                        (const void*)scan_segments_kernel<2>, (const void*)scan_segments_kernel<3>,
+                        (const void*)scan_segments_kernel<4>, (const void*)scan_segments_kernel<5>}) {
     hipError_t r = hipFuncSetAttribute(k, hipFuncAttributeMaxDynamicSharedMemorySize, lds);
     if (r != hipSuccess) e = r;
   }

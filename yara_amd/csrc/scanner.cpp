@@ -32,7 +32,7 @@ struct yr_amd_tables {
   FlatTables flat;
   int device = 0;
   uint32_t* d_filter = nullptr;
-  uint64_t* d_exact = nullptr;
+  uint32_t* d_exact = nullptr;
   int num_cus = 256;
 };
 
@@ -160,10 +160,10 @@ int yr_amd_tables_create(const uint32_t* transition_table, const uint32_t* match
           hipSuccess ||
       configure_scan_kernel() != hipSuccess ||
       hipMalloc((void**)&t->d_filter, t->flat.filter.size() * 4) != hipSuccess ||
-      hipMalloc((void**)&t->d_exact, t->flat.exact.size() * 8) != hipSuccess ||
+      hipMalloc((void**)&t->d_exact, t->flat.exact.size() * 4) != hipSuccess ||
       hipMemcpy(t->d_filter, t->flat.filter.data(), t->flat.filter.size() * 4,
                 hipMemcpyHostToDevice) != hipSuccess ||
-      hipMemcpy(t->d_exact, t->flat.exact.data(), t->flat.exact.size() * 8,
+      hipMemcpy(t->d_exact, t->flat.exact.data(), t->flat.exact.size() * 4,
                 hipMemcpyHostToDevice) != hipSuccess) {
     yr_amd_tables_destroy(t);
     return YR_AMD_INTERNAL_FATAL_ERROR;
@@ -195,7 +195,7 @@ int yr_amd_tables_get_info(const yr_amd_tables* t, yr_amd_tables_info* info) {
   info->root_accepting = f.root_accepting ? 1 : 0;
   info->filter_bits = kFilterLog2Bits;
   info->filter_set_bits = f.filter_set_bits;
-  info->exact_slots = (uint32_t)f.exact.size();
+  info->exact_slots = 4 * (f.t3_mask + 1 + f.t4_mask + 1);
   return YR_AMD_SUCCESS;
 }
 
@@ -257,7 +257,7 @@ int yr_amd_scanner_set_timing(yr_amd_scanner* s, int enable) {
 // Not declared in include/yara_amd.h: profiling ablations of the scan kernel
 // (tools/ablate.py).  Any mode other than 0 produces wrong results.
 int yr_amd__diag_kernel_mode(yr_amd_scanner* s, int mode) {
-  if (s == nullptr || mode < 0 || mode > 3) return YR_AMD_INVALID_ARGUMENT;
+  if (s == nullptr || mode < 0 || mode > 5) return YR_AMD_INVALID_ARGUMENT;
   s->diag_mode = mode;
   return YR_AMD_SUCCESS;
 }
@@ -299,7 +299,11 @@ int yr_amd_scan_device(yr_amd_scanner* s, const uint8_t* d_data, uint64_t block_
   p.byte_end = byte_end;
   p.filter = t->d_filter;
   p.exact = t->d_exact;
-  p.exact_mask = (uint32_t)t->flat.exact.size() - 1;
+  p.t3_off = t->flat.t3_off;
+  p.t3_mask = t->flat.t3_mask;
+  p.t4_off = t->flat.t4_off;
+  p.t4_mask = t->flat.t4_mask;
+  p.exact_flags = t->flat.exact_flags;
   p.len_mask = t->flat.len_mask;
   p.n_segments = n_segments;
   p.seg_bytes = seg_bytes;

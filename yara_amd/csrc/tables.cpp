@@ -43,6 +43,46 @@ void filter_set(std::vector<uint32_t>& f, uint32_t w3) {
   f[fp.word] |= (1u << fp.b1) | (1u << fp.b2);
 }
 
+// Two-choice, 4-way bucketed cuckoo table of non-zero keys.  Load <= 1/2 to
+// start; the bucket count doubles until every key is placed.
+bool build_bucket_table(const std::vector<uint32_t>& keys, std::vector<uint32_t>& table,
+                        uint32_t& n_buckets) {
+  uint32_t nb = 4;
+  while (nb * 4 < 2 * keys.size()) nb <<= 1;
+  for (; nb <= (1u << 26); nb <<= 1) {
+    table.assign((size_t)nb * 4, 0u);
+    uint32_t rng = 0x2545F491u;
+    bool ok = true;
+    for (uint32_t key0 : keys) {
+      uint32_t key = key0;
+      bool placed = false;
+      for (int kick = 0; kick < 512 && !placed; ++kick) {
+        const uint32_t b[2] = {bucket_hash1(key) & (nb - 1), bucket_hash2(key) & (nb - 1)};
+        for (int c = 0; c < 2 && !placed; ++c) {
+          for (int s = 0; s < 4; ++s) {
+            uint32_t& slot = table[(size_t)b[c] * 4 + s];
+            if (slot == key) { placed = true; break; }   // duplicate
+            if (slot == 0) { slot = key; placed = true; break; }
+          }
+        }
+        if (!placed) {   // evict a random resident of one of the two buckets
+          rng ^= rng << 13; rng ^= rng >> 17; rng ^= rng << 5;
+          uint32_t& victim = table[(size_t)b[rng & 1] * 4 + ((rng >> 1) & 3)];
+          const uint32_t v = victim;
+          victim = key;
+          key = v;
+        }
+      }
+      if (!placed) { ok = false; break; }
+    }
+    if (ok) {
+      n_buckets = nb;
+      return true;
+    }
+  }
+  return false;
+}
+
 }  // namespace
 
 int flatten_tables(const uint32_t* T, const uint32_t* M, uint32_t n_slots,
@@ -148,15 +188,31 @@ int flatten_tables(const uint32_t* T, const uint32_t* M, uint32_t n_slots,
   }
   for (uint32_t w : out.filter) out.filter_set_bits += (uint32_t)__builtin_popcount(w);
 
-  // 3b. exact keys, load factor <= 1/4 (a miss costs ~1.2 probes)
-  uint32_t slots = 64;
-  while (slots < 4 * out.keys.size()) slots <<= 1;
-  out.exact.assign(slots, 0ull);
+  // 3b. exact key sets: bitmaps for 1-2 byte keys, two-choice bucketed
+  //     hash tables for 3-4 byte keys
+  std::vector<uint32_t> k3, k4;
+  out.exact.assign(kExactHeadWords, 0u);
   for (const Key& k : out.keys) {
-    uint32_t s = exact_hash(k.bytes, k.len) & (slots - 1);
-    while (out.exact[s] != 0) s = (s + 1) & (slots - 1);
-    out.exact[s] = exact_entry(k.bytes, k.len);
+    switch (k.len) {
+      case 1: out.exact[kExactBm1 + (k.bytes >> 5)] |= 1u << (k.bytes & 31); break;
+      case 2: out.exact[kExactBm2 + (k.bytes >> 5)] |= 1u << (k.bytes & 31); break;
+      case 3: k3.push_back(k.bytes | (1u << 24)); break;
+      case 4:
+        if (k.bytes == 0) out.exact_flags |= kExactZero4;
+        else k4.push_back(k.bytes);
+        break;
+    }
   }
+  std::vector<uint32_t> t3, t4;
+  uint32_t nb3 = 0, nb4 = 0;
+  if (!build_bucket_table(k3, t3, nb3) || !build_bucket_table(k4, t4, nb4))
+    return YR_AMD_INTERNAL_FATAL_ERROR;
+  out.t3_off = (uint32_t)out.exact.size();
+  out.t3_mask = nb3 - 1;
+  out.exact.insert(out.exact.end(), t3.begin(), t3.end());
+  out.t4_off = (uint32_t)out.exact.size();
+  out.t4_mask = nb4 - 1;
+  out.exact.insert(out.exact.end(), t4.begin(), t4.end());
   return YR_AMD_SUCCESS;
 }
 

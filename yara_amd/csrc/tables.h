@@ -28,7 +28,8 @@ struct FlatTables {
   std::vector<Key> keys;           // minimal accepting trie strings
   std::vector<uint32_t> filter;    // kFilterWords
   uint32_t filter_set_bits = 0;
-  std::vector<uint64_t> exact;     // power-of-two open-addressed table
+  std::vector<uint32_t> exact;     // exact key sets (internal.h layout)
+  uint32_t t3_off = 0, t3_mask = 0, t4_off = 0, t4_mask = 0, exact_flags = 0;
   uint32_t len_mask = 0;
 };
 
