@@ -14,7 +14,8 @@ REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, REPO)
 
 NAMES = {0: "product", 1: "no-exact-check", 2: "stage1-only", 3: "stream-only",
-         4: "stage1-conflict-free-lds", 5: "stage1-valu-no-lds"}
+         4: "stage1-conflict-free-lds", 5: "stage1-valu-no-lds",
+         6: "stage1-lds-no-test"}
 
 
 def main():
@@ -23,7 +24,7 @@ def main():
     ap.add_argument("--rules", default="C")
     ap.add_argument("--rounds", type=int, default=5)
     ap.add_argument("--reps", type=int, default=3)
-    ap.add_argument("--modes", default="0,1,2,3,4,5")
+    ap.add_argument("--modes", default="0,1,2,3,4,5,6")
     a = ap.parse_args()
     import torch
     import yara_amd

@@ -47,7 +47,7 @@ __device__ __forceinline__ uint32_t wave_inclusive_scan(uint32_t v) {
 // little endian (oldest lowest; zeros before the block start).  Every load
 // (bitmap words, both candidate buckets of each table) is independent: one
 // round trip.
-__device__ __noinline__ bool exact_check(uint32_t w4, uint64_t pos, const ScanParams& p) {
+__device__ __forceinline__ bool exact_check(uint32_t w4, uint64_t pos, const ScanParams& p) {
   const uint32_t* __restrict__ ex = p.exact;
   bool hit = false;
   const uint32_t lm = p.len_mask;
@@ -142,7 +142,11 @@ __device__ __forceinline__ uint4 load_tile(const uint8_t* base, uint32_t tile_of
                                            uint64_t avail) {
   const uint32_t off = tile_off + lane * kBytesPerLane;
   if (tile_off + (uint64_t)kTile <= avail) {
-    return *reinterpret_cast<const uint4*>(base + off);
+    // read-once stream: non-temporal, so the filter staging and the exact
+    // tables keep their L2 lines
+    typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
+    const u32x4 v = __builtin_nontemporal_load(reinterpret_cast<const u32x4*>(base + off));
+    return make_uint4(v.x, v.y, v.z, v.w);
   }
   // ragged block tail (at most one tile per launch)
   uint4 v = make_uint4(0, 0, 0, 0);
@@ -163,7 +167,8 @@ __device__ __forceinline__ uint4 load_tile(const uint8_t* base, uint32_t tile_of
 // MODE: 0 = the product kernel.  Others are profiling ablations only (their
 // output is wrong by construction): 1 = no exact check, 2 = stage 1 only
 // (no queue), 3 = input streaming only (no filter), 4 = stage 1 with
-// bank-conflict-free LDS addresses, 5 = stage 1 VALU without the LDS reads.
+// bank-conflict-free LDS addresses, 5 = stage 1 VALU without the LDS reads,
+// 6 = stage 1 addresses + LDS reads without the bit tests.
 template <int MODE>
 __device__ void scan_segment(const ScanParams& p, const uint32_t* __restrict__ filt,
                              WaveQueue& q, uint32_t seg, uint32_t lane) {
@@ -204,7 +209,7 @@ __device__ void scan_segment(const ScanParams& p, const uint32_t* __restrict__ f
                              : __builtin_amdgcn_alignbyte(S[(o >> 2) + 1], S[o >> 2], o & 3);
       if constexpr (MODE != 3) {
         const uint32_t x = xs[k];
-        uint32_t addr = ((x >> 7) ^ (x << 2)) & (kFilterBytes - 4);
+        uint32_t addr = (x >> 7) & (kFilterBytes - 4);
         if constexpr (MODE == 4) addr = ((lane & 31u) * 4u + (uint32_t)k * 128u) & (kFilterBytes - 4);
         if constexpr (MODE == 5) {
           ws[k] = addr ^ x;
@@ -214,7 +219,7 @@ __device__ void scan_segment(const ScanParams& p, const uint32_t* __restrict__ f
         }
       }
     }
-    // Phase B: blocked-Bloom test of bits b1 = x[0..4], b2 = x[7..11] (the
+    // Phase B: blocked-Bloom test of bits b1 = x[0..4], b2 = x[4..8] (the
     // shifter reads only the low 5 bits of the amount); acc collects the 16
     // results via v_alignbit: afterwards bit 16 + k holds position k.
     uint32_t acc = 0;
@@ -222,9 +227,11 @@ __device__ void scan_segment(const ScanParams& p, const uint32_t* __restrict__ f
     for (int k = 0; k < kBytesPerLane; ++k) {
       if constexpr (MODE == 3) {
         acc ^= xs[k];
+      } else if constexpr (MODE == 6) {
+        acc ^= ws[k];
       } else {
         const uint32_t x = xs[k], w = ws[k];
-        const uint32_t t2 = (w >> (x & 31u)) & (w >> ((x >> 7) & 31u));
+        const uint32_t t2 = (w >> (x & 31u)) & (w >> ((x >> 4) & 31u));
         acc = __builtin_amdgcn_alignbit(t2, acc, 1);
       }
     }
@@ -383,6 +390,7 @@ hipError_t launch_scan(const ScanParams& p, int grid, hipStream_t s, int mode) {
     case 3: hipLaunchKernelGGL(scan_segments_kernel<3>, dim3(grid), dim3(kWGThreads), lds, s, p); break;
     case 4: hipLaunchKernelGGL(scan_segments_kernel<4>, dim3(grid), dim3(kWGThreads), lds, s, p); break;
     case 5: hipLaunchKernelGGL(scan_segments_kernel<5>, dim3(grid), dim3(kWGThreads), lds, s, p); break;
+    case 6: hipLaunchKernelGGL(scan_segments_kernel<6>, dim3(grid), dim3(kWGThreads), lds, s, p); break;
     default: hipLaunchKernelGGL(scan_segments_kernel<0>, dim3(grid), dim3(kWGThreads), lds, s, p); break;
   }
   return hipGetLastError();
@@ -412,7 +420,8 @@ hipError_t configure_scan_kernel() {
   hipError_t e = hipSuccess;
   for (const void* k : {(const void*)scan_segments_kernel<0>, (const void*)scan_segments_kernel<1>,
                         (const void*)scan_segments_kernel<2>, (const void*)scan_segments_kernel<3>,
-                        (const void*)scan_segments_kernel<4>, (const void*)scan_segments_kernel<5>}) {
+                        (const void*)scan_segments_kernel<4>, (const void*)scan_segments_kernel<5>,
+                        (const void*)scan_segments_kernel<6>}) {
     hipError_t r = hipFuncSetAttribute(k, hipFuncAttributeMaxDynamicSharedMemorySize, lds);
     if (r != hipSuccess) e = r;
   }
