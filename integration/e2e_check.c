@@ -1,0 +1,248 @@
+/*
+ * e2e_check -- end-to-end match-set parity: stock libyara vs the GPU driver.
+ *
+ * Test infrastructure: compiles a rule file with the stock libyara compiler,
+ * scans the same data twice --
+ *   stock:  yr_scanner_scan_mem[_blocks]          (scanner.c:417/:633)
+ *   gpu:    yr_gpu_scanner_scan_mem[_blocks]      (integration/yr_gpu_scanner.c)
+ * -- and compares the complete match sets ({string idx, base+offset, length,
+ * xor key} of every match of every string, private ones included) and the
+ * per-rule RULE_MATCHING / RULE_NOT_MATCHING reports.  Prints one JSON line.
+ *
+ *   e2e_check <rules.yar> <data file | xs:SEED:SIZE> [block_size overlap]
+ */
+#include <stdint.h>
+#include <stdio.h>
+#include <stdlib.h>
+#include <string.h>
+#include <time.h>
+#include <yara.h>
+
+#include "yr_gpu_scanner.h"
+
+typedef struct
+{
+  uint32_t s;
+  uint64_t off;
+  uint32_t len, xk;
+} rec;
+
+typedef struct
+{
+  YR_RULES* rules;
+  rec* r;
+  size_t n, cap;
+  uint8_t* rule_msg; /* 1 matching, 2 not matching */
+  int dumped;
+  int finished;
+} collect;
+
+static void push(collect* c, rec x)
+{
+  if (c->n == c->cap)
+  {
+    c->cap = c->cap ? 2 * c->cap : 1024;
+    c->r = (rec*) realloc(c->r, c->cap * sizeof(rec));
+  }
+  c->r[c->n++] = x;
+}
+
+static int cb(YR_SCAN_CONTEXT* ctx, int msg, void* data, void* user)
+{
+  collect* c = (collect*) user;
+  if (msg == CALLBACK_MSG_RULE_MATCHING || msg == CALLBACK_MSG_RULE_NOT_MATCHING)
+  {
+    YR_RULE* rule = (YR_RULE*) data;
+    c->rule_msg[rule - c->rules->rules_table] =
+        msg == CALLBACK_MSG_RULE_MATCHING ? 1 : 2;
+    if (!c->dumped)
+    {
+      for (uint32_t k = 0; k < c->rules->num_strings; k++)
+        for (YR_MATCH* m = ctx->matches[k].head; m != NULL; m = m->next)
+        {
+          rec x = {k, (uint64_t) (m->base + m->offset), (uint32_t) m->match_length,
+                   m->xor_key};
+          push(c, x);
+        }
+      c->dumped = 1;
+    }
+  }
+  else if (msg == CALLBACK_MSG_SCAN_FINISHED)
+  {
+    c->finished = 1;
+  }
+  return CALLBACK_CONTINUE;
+}
+
+static void xorshift_fill(uint8_t* buf, size_t n, uint64_t seed)
+{
+  uint64_t x = 0x9E3779B97F4A7C15ull * seed;
+  for (size_t i = 0; i < n; i++)
+  {
+    x ^= x << 13;
+    x ^= x >> 7;
+    x ^= x << 17;
+    buf[i] = (uint8_t) (x >> 24);
+  }
+}
+
+static uint8_t* load(const char* spec, size_t* n)
+{
+  if (strncmp(spec, "xs:", 3) == 0)
+  {
+    unsigned long long seed, sz;
+    sscanf(spec + 3, "%llu:%llu", &seed, &sz);
+    uint8_t* b = (uint8_t*) malloc(sz ? sz : 1);
+    xorshift_fill(b, sz, seed);
+    *n = sz;
+    return b;
+  }
+  FILE* f = fopen(spec, "rb");
+  if (!f) return NULL;
+  fseek(f, 0, SEEK_END);
+  long sz = ftell(f);
+  fseek(f, 0, SEEK_SET);
+  uint8_t* b = (uint8_t*) malloc(sz ? sz : 1);
+  if (fread(b, 1, sz, f) != (size_t) sz) return NULL;
+  fclose(f);
+  *n = (size_t) sz;
+  return b;
+}
+
+/* overlapping block iterator (tests/util.c:136-209 semantics) */
+typedef struct
+{
+  const uint8_t* data;
+  size_t size, bsize, overlap, next_base;
+  YR_MEMORY_BLOCK blk;
+} blk_iter;
+
+static const uint8_t* blk_fetch(YR_MEMORY_BLOCK* b)
+{
+  return ((blk_iter*) b->context)->data + b->base;
+}
+
+static YR_MEMORY_BLOCK* blk_next(YR_MEMORY_BLOCK_ITERATOR* iter)
+{
+  blk_iter* it = (blk_iter*) iter->context;
+  if (it->next_base >= it->size) return NULL;
+  size_t base = it->next_base;
+  size_t len = it->size - base < it->bsize ? it->size - base : it->bsize;
+  it->blk.base = base;
+  it->blk.size = len;
+  it->blk.context = it;
+  it->blk.fetch_data = blk_fetch;
+  it->next_base = base + len >= it->size ? it->size : base + len - it->overlap;
+  return &it->blk;
+}
+
+static YR_MEMORY_BLOCK* blk_first(YR_MEMORY_BLOCK_ITERATOR* iter)
+{
+  ((blk_iter*) iter->context)->next_base = 0;
+  return blk_next(iter);
+}
+
+static uint64_t blk_file_size(YR_MEMORY_BLOCK_ITERATOR* iter)
+{
+  return ((blk_iter*) iter->context)->size;
+}
+
+static int cmp_rec(const void* a, const void* b)
+{
+  return memcmp(a, b, sizeof(rec));
+}
+
+static double now(void)
+{
+  struct timespec t;
+  clock_gettime(CLOCK_MONOTONIC, &t);
+  return t.tv_sec + 1e-9 * t.tv_nsec;
+}
+
+static int run(YR_RULES* rules, YR_GPU_SCANNER* gs, const uint8_t* data, size_t n,
+               size_t bsize, size_t overlap, collect* c, double* secs)
+{
+  YR_SCANNER* sc;
+  int r = yr_scanner_create(rules, &sc);
+  if (r) return r;
+  yr_scanner_set_flags(sc, SCAN_FLAGS_REPORT_RULES_MATCHING | SCAN_FLAGS_REPORT_RULES_NOT_MATCHING);
+  yr_scanner_set_callback(sc, cb, c);
+  double t0 = now();
+  if (bsize == 0)
+  {
+    r = gs ? yr_gpu_scanner_scan_mem(sc, gs, data, n) : yr_scanner_scan_mem(sc, data, n);
+  }
+  else
+  {
+    blk_iter it = {data, n, bsize, overlap, 0};
+    YR_MEMORY_BLOCK_ITERATOR iter = {&it, blk_first, blk_next, blk_file_size, ERROR_SUCCESS};
+    r = gs ? yr_gpu_scanner_scan_mem_blocks(sc, gs, &iter) : yr_scanner_scan_mem_blocks(sc, &iter);
+  }
+  *secs = now() - t0;
+  yr_scanner_destroy(sc);
+  return r;
+}
+
+int main(int argc, char** argv)
+{
+  if (argc < 3)
+  {
+    fprintf(stderr, "usage: e2e_check rules data [block overlap]\n");
+    return 2;
+  }
+  size_t bsize = argc > 4 ? strtoull(argv[3], NULL, 10) : 0;
+  size_t overlap = argc > 4 ? strtoull(argv[4], NULL, 10) : 0;
+  yr_initialize();
+  YR_COMPILER* comp;
+  YR_RULES* rules;
+  FILE* f = fopen(argv[1], "r");
+  if (!f || yr_compiler_create(&comp) || yr_compiler_add_file(comp, f, NULL, argv[1]) ||
+      yr_compiler_get_rules(comp, &rules))
+  {
+    fprintf(stderr, "rule compilation failed\n");
+    return 2;
+  }
+  size_t n;
+  uint8_t* data = load(argv[2], &n);
+  if (!data)
+  {
+    fprintf(stderr, "cannot load data\n");
+    return 2;
+  }
+  YR_GPU_RULES* gr;
+  YR_GPU_SCANNER* gs;
+  int r = yr_gpu_rules_create(rules, 0, &gr);
+  if (r == 0) r = yr_gpu_scanner_create(gr, &gs);
+  if (r)
+  {
+    fprintf(stderr, "gpu setup failed: %d\n", r);
+    return 3;
+  }
+  collect a = {rules}, b = {rules};
+  a.rule_msg = (uint8_t*) calloc(rules->num_rules + 1, 1);
+  b.rule_msg = (uint8_t*) calloc(rules->num_rules + 1, 1);
+  double ts, tg, tw;
+  collect warm = {rules};
+  warm.rule_msg = (uint8_t*) calloc(rules->num_rules + 1, 1);
+  run(rules, gs, data, n < 4096 ? n : 4096, 0, 0, &warm, &tw); /* GPU warm-up */
+  int rs = run(rules, NULL, data, n, bsize, overlap, &a, &ts);
+  int rg = run(rules, gs, data, n, bsize, overlap, &b, &tg);
+  qsort(a.r, a.n, sizeof(rec), cmp_rec);
+  qsort(b.r, b.n, sizeof(rec), cmp_rec);
+  int same_matches = a.n == b.n && (a.n == 0 || memcmp(a.r, b.r, a.n * sizeof(rec)) == 0);
+  int same_rules = memcmp(a.rule_msg, b.rule_msg, rules->num_rules) == 0;
+  int n_match_rules = 0;
+  for (uint32_t i = 0; i < rules->num_rules; i++) n_match_rules += a.rule_msg[i] == 1;
+  printf("{\"size\": %zu, \"block\": %zu, \"rc_stock\": %d, \"rc_gpu\": %d, "
+         "\"matches_stock\": %zu, \"matches_gpu\": %zu, \"rules_matching\": %d, "
+         "\"same_matches\": %s, \"same_rule_reports\": %s, \"finished\": [%d, %d], "
+         "\"stock_s\": %.4f, \"gpu_s\": %.4f}\n",
+         n, bsize, rs, rg, a.n, b.n, n_match_rules, same_matches ? "true" : "false",
+         same_rules ? "true" : "false", a.finished, b.finished, ts, tg);
+  yr_gpu_scanner_destroy(gs);
+  yr_gpu_rules_destroy(gr);
+  yr_rules_destroy(rules);
+  yr_compiler_destroy(comp);
+  yr_finalize();
+  return (rs == rg && same_matches && same_rules) ? 0 : 1;
+}

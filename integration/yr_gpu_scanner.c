@@ -1,0 +1,384 @@
+/*
+ * yr_gpu_scanner.c -- libyara-side integration of the MI355X atom scanner.
+ *
+ * This is the code a libyara maintainer adds: it is compiled
+ * against libyara's own headers and linked with an UNMODIFIED libyara (here
+ * the stock reference build, oracle/_ref/libyara_ref.so) and libyara_amd.so.
+ *
+ * libyara's per-block walk _yr_scanner_scan_mem_block (scanner.c:45-176) is
+ * static, so the driver that calls it, yr_scanner_scan_mem_blocks
+ * (scanner.c:417-583), is re-hosted here step for step; the only change is
+ * the per-block call (scanner.c:493-496), which becomes
+ *     GPU candidate stream (yr_amd_scan_block)
+ *  -> reference-ordered replay (yr_amd_replay)
+ *  -> the unmodified verifier yr_scan_verify_match (scan.c:992)
+ * followed, as in the reference, by yr_execute_code (exec.c:418) and the
+ * rule-report loop (scanner.c:524-556).
+ */
+#include "yr_gpu_scanner.h"
+
+#include <stdlib.h>
+#include <string.h>
+#include <yara.h>
+#include <yara/arena.h>
+#include <yara/compiler.h>
+#include <yara/exec.h>
+#include <yara/exefiles.h>
+#include <yara/notebook.h>
+#include <yara/scan.h>
+#include <yara/stopwatch.h>
+
+#include "exception.h" /* libyara/exception.h: YR_TRYCATCH (exception.h:150-185) */
+
+struct YR_GPU_RULES
+{
+  YR_RULES* rules;
+  yr_amd_tables* tables;
+};
+
+struct YR_GPU_SCANNER
+{
+  YR_GPU_RULES* gpu_rules;
+  yr_amd_scanner* scanner;
+  uint8_t* staging; /* host copy of the block being scanned */
+  size_t staging_size;
+};
+
+int yr_gpu_rules_create(YR_RULES* rules, int device, YR_GPU_RULES** out)
+{
+  *out = NULL;
+  YR_GPU_RULES* g = (YR_GPU_RULES*) calloc(1, sizeof(YR_GPU_RULES));
+  if (g == NULL) return ERROR_INSUFFICIENT_MEMORY;
+
+  /* table sizes exactly as yr_rules_get_stats computes them (rules.c:442) */
+  uint32_t n_slots = (uint32_t) (yr_arena_get_current_offset(
+                                     rules->arena, YR_AC_TRANSITION_TABLE) /
+                                 sizeof(YR_AC_TRANSITION));
+  uint32_t n_pool = (uint32_t) (yr_arena_get_current_offset(
+                                    rules->arena, YR_AC_STATE_MATCHES_POOL) /
+                                sizeof(YR_AC_MATCH));
+
+  uint32_t* nx = (uint32_t*) malloc(sizeof(uint32_t) * (n_pool ? n_pool : 1));
+  uint16_t* bt = (uint16_t*) malloc(sizeof(uint16_t) * (n_pool ? n_pool : 1));
+  if (nx == NULL || bt == NULL)
+  {
+    free(nx);
+    free(bt);
+    free(g);
+    return ERROR_INSUFFICIENT_MEMORY;
+  }
+  for (uint32_t k = 0; k < n_pool; k++)
+  {
+    YR_AC_MATCH* m = &rules->ac_match_pool[k];
+    nx[k] = m->next ? (uint32_t) (m->next - rules->ac_match_pool) + 1 : 0;
+    bt[k] = m->backtrack;
+  }
+  int r = yr_amd_tables_create(
+      rules->ac_transition_table,
+      rules->ac_match_table,
+      n_slots,
+      nx,
+      bt,
+      n_pool,
+      device,
+      &g->tables);
+  free(nx);
+  free(bt);
+  if (r != ERROR_SUCCESS)
+  {
+    free(g);
+    return r;
+  }
+  g->rules = rules;
+  *out = g;
+  return ERROR_SUCCESS;
+}
+
+void yr_gpu_rules_destroy(YR_GPU_RULES* g)
+{
+  if (g == NULL) return;
+  yr_amd_tables_destroy(g->tables);
+  free(g);
+}
+
+int yr_gpu_scanner_create(YR_GPU_RULES* g, YR_GPU_SCANNER** out)
+{
+  *out = NULL;
+  YR_GPU_SCANNER* s = (YR_GPU_SCANNER*) calloc(1, sizeof(YR_GPU_SCANNER));
+  if (s == NULL) return ERROR_INSUFFICIENT_MEMORY;
+  int r = yr_amd_scanner_create(g->tables, NULL, &s->scanner);
+  if (r != ERROR_SUCCESS)
+  {
+    free(s);
+    return r;
+  }
+  s->gpu_rules = g;
+  *out = s;
+  return ERROR_SUCCESS;
+}
+
+void yr_gpu_scanner_destroy(YR_GPU_SCANNER* s)
+{
+  if (s == NULL) return;
+  yr_amd_scanner_destroy(s->scanner);
+  free(s->staging);
+  free(s);
+}
+
+typedef struct
+{
+  YR_SCANNER* scanner;
+  const uint8_t* data;
+  size_t size;
+  uint64_t base;
+} verify_ctx;
+
+/* The reference's own call, scanner.c:111-117 / :153-159. */
+static int _verify(void* user, uint32_t pool_index, uint64_t offset)
+{
+  verify_ctx* c = (verify_ctx*) user;
+  return yr_scan_verify_match(
+      c->scanner,
+      &c->scanner->rules->ac_match_pool[pool_index],
+      c->data,
+      c->size,
+      c->base,
+      (size_t) offset);
+}
+
+/* Replacement of _yr_scanner_scan_mem_block (scanner.c:45-176). */
+static int _yr_gpu_scan_mem_block(
+    YR_SCANNER* scanner,
+    YR_GPU_SCANNER* gs,
+    const uint8_t* block_data,
+    YR_MEMORY_BLOCK* block)
+{
+  int result = ERROR_SUCCESS;
+
+  /* The reference checks the timeout every 4096 bytes (scanner.c:74-81); the
+   * GPU path checks before and after the whole-block candidate pass. */
+  if (scanner->timeout > 0 &&
+      yr_stopwatch_elapsed_ns(&scanner->stopwatch) > scanner->timeout)
+    return ERROR_SCAN_TIMEOUT;
+
+  /* Block bytes may live in an mmap (filemap.c:56): copy them in the scanning
+   * thread inside the trycatch so a SIGBUS/SIGSEGV maps to
+   * ERROR_COULD_NOT_MAP_FILE exactly as at scanner.c:493-496. */
+  if (block->size > gs->staging_size)
+  {
+    uint8_t* p = (uint8_t*) realloc(gs->staging, block->size);
+    if (p == NULL) return ERROR_INSUFFICIENT_MEMORY;
+    gs->staging = p;
+    gs->staging_size = block->size;
+  }
+  YR_TRYCATCH(
+      !(scanner->flags & SCAN_FLAGS_NO_TRYCATCH),
+      { memcpy(gs->staging, block_data, block->size); },
+      { result = ERROR_COULD_NOT_MAP_FILE; });
+  if (result != ERROR_SUCCESS) return result;
+
+  const uint64_t* positions = NULL;
+  uint64_t count = 0;
+  int all_positions = 0;
+  FAIL_ON_ERROR(yr_amd_scan_block(
+      gs->scanner,
+      gs->staging,
+      block->size,
+      &positions,
+      &count,
+      &all_positions));
+
+  if (scanner->timeout > 0 &&
+      yr_stopwatch_elapsed_ns(&scanner->stopwatch) > scanner->timeout)
+    return ERROR_SCAN_TIMEOUT;
+
+  verify_ctx ctx = {scanner, gs->staging, block->size, block->base};
+  return yr_amd_replay(
+      gs->gpu_rules->tables,
+      gs->staging,
+      block->size,
+      positions,
+      count,
+      all_positions,
+      _verify,
+      &ctx);
+}
+
+/* _yr_scanner_clean_matches (scanner.c:178-203) is static: same memsets. */
+static void _clean_matches(YR_SCANNER* scanner)
+{
+  memset(
+      scanner->rule_matches_flags,
+      0,
+      sizeof(YR_BITMASK) * YR_BITMASK_SIZE(scanner->rules->num_rules));
+  memset(
+      scanner->ns_unsatisfied_flags,
+      0,
+      sizeof(YR_BITMASK) * YR_BITMASK_SIZE(scanner->rules->num_namespaces));
+  memset(
+      scanner->strings_temp_disabled,
+      0,
+      sizeof(YR_BITMASK) * YR_BITMASK_SIZE(scanner->rules->num_strings));
+  memset(scanner->matches, 0, sizeof(YR_MATCHES) * scanner->rules->num_strings);
+  memset(
+      scanner->unconfirmed_matches,
+      0,
+      sizeof(YR_MATCHES) * scanner->rules->num_strings);
+}
+
+/* yr_scanner_scan_mem_blocks (scanner.c:417-583) with the GPU block scan. */
+int yr_gpu_scanner_scan_mem_blocks(
+    YR_SCANNER* scanner,
+    YR_GPU_SCANNER* gs,
+    YR_MEMORY_BLOCK_ITERATOR* iterator)
+{
+  YR_RULES* rules;
+  YR_RULE* rule;
+  YR_MEMORY_BLOCK* block;
+  int i, result = ERROR_SUCCESS;
+
+  if (scanner->callback == NULL) return ERROR_CALLBACK_REQUIRED;
+
+  scanner->iterator = iterator;
+  rules = scanner->rules;
+
+  if (iterator->last_error == ERROR_BLOCK_NOT_READY)
+  {
+    block = iterator->next(iterator);
+  }
+  else
+  {
+    uint32_t max_match_data;
+    FAIL_ON_ERROR(
+        yr_get_configuration_uint32(YR_CONFIG_MAX_MATCH_DATA, &max_match_data));
+    result = yr_notebook_create(
+        1024 * (sizeof(YR_MATCH) + max_match_data), &scanner->matches_notebook);
+    if (result != ERROR_SUCCESS) goto _exit;
+    yr_stopwatch_start(&scanner->stopwatch);
+    block = iterator->first(iterator);
+  }
+
+  while (block != NULL)
+  {
+    const uint8_t* data = block->fetch_data(block);
+    if (data == NULL)
+    {
+      block = iterator->next(iterator);
+      continue;
+    }
+    if (scanner->entry_point == YR_UNDEFINED)
+    {
+      YR_TRYCATCH(
+          !(scanner->flags & SCAN_FLAGS_NO_TRYCATCH),
+          {
+            if (scanner->flags & SCAN_FLAGS_PROCESS_MEMORY)
+              scanner->entry_point = yr_get_entry_point_address(
+                  data, block->size, block->base);
+            else
+              scanner->entry_point = yr_get_entry_point_offset(
+                  data, block->size);
+          },
+          {});
+    }
+
+    result = _yr_gpu_scan_mem_block(scanner, gs, data, block);
+    if (result != ERROR_SUCCESS) goto _exit;
+    block = iterator->next(iterator);
+  }
+
+  result = iterator->last_error;
+  if (result != ERROR_SUCCESS) goto _exit;
+
+  if (iterator->file_size != NULL)
+    scanner->file_size = iterator->file_size(iterator);
+  else
+    scanner->file_size = YR_UNDEFINED;
+
+  YR_TRYCATCH(
+      !(scanner->flags & SCAN_FLAGS_NO_TRYCATCH),
+      { result = yr_execute_code(scanner); },
+      { result = ERROR_COULD_NOT_MAP_FILE; });
+  if (result != ERROR_SUCCESS) goto _exit;
+
+  for (i = 0, rule = rules->rules_table; !RULE_IS_NULL(rule); i++, rule++)
+  {
+    int message = 0;
+    if (yr_bitmask_is_set(scanner->rule_matches_flags, i) &&
+        yr_bitmask_is_not_set(scanner->ns_unsatisfied_flags, rule->ns->idx))
+    {
+      if (scanner->flags & SCAN_FLAGS_REPORT_RULES_MATCHING)
+        message = CALLBACK_MSG_RULE_MATCHING;
+    }
+    else
+    {
+      if (scanner->flags & SCAN_FLAGS_REPORT_RULES_NOT_MATCHING)
+        message = CALLBACK_MSG_RULE_NOT_MATCHING;
+    }
+    if (message != 0 && !RULE_IS_PRIVATE(rule))
+    {
+      switch (scanner->callback(scanner, message, rule, scanner->user_data))
+      {
+      case CALLBACK_ABORT:
+        result = ERROR_SUCCESS;
+        goto _exit;
+      case CALLBACK_ERROR:
+        result = ERROR_CALLBACK_ERROR;
+        goto _exit;
+      }
+    }
+  }
+  scanner->callback(scanner, CALLBACK_MSG_SCAN_FINISHED, NULL, scanner->user_data);
+
+_exit:
+  if (result != ERROR_BLOCK_NOT_READY)
+  {
+    _clean_matches(scanner);
+    if (scanner->matches_notebook != NULL)
+    {
+      yr_notebook_destroy(scanner->matches_notebook);
+      scanner->matches_notebook = NULL;
+    }
+  }
+  return result;
+}
+
+static YR_MEMORY_BLOCK* _first_block(YR_MEMORY_BLOCK_ITERATOR* it)
+{
+  return (YR_MEMORY_BLOCK*) it->context;
+}
+
+static YR_MEMORY_BLOCK* _next_block(YR_MEMORY_BLOCK_ITERATOR* it)
+{
+  return NULL;
+}
+
+static uint64_t _file_size(YR_MEMORY_BLOCK_ITERATOR* it)
+{
+  return ((YR_MEMORY_BLOCK*) it->context)->size;
+}
+
+static const uint8_t* _fetch(YR_MEMORY_BLOCK* b)
+{
+  return (const uint8_t*) b->context;
+}
+
+/* yr_scanner_scan_mem (scanner.c:633-671) with the GPU driver. */
+int yr_gpu_scanner_scan_mem(
+    YR_SCANNER* scanner,
+    YR_GPU_SCANNER* gs,
+    const uint8_t* buffer,
+    size_t buffer_size)
+{
+  YR_MEMORY_BLOCK block;
+  YR_MEMORY_BLOCK_ITERATOR iterator;
+  block.size = buffer_size;
+  block.base = 0;
+  block.fetch_data = _fetch;
+  block.context = (void*) buffer;
+  iterator.context = &block;
+  iterator.first = _first_block;
+  iterator.next = _next_block;
+  iterator.file_size = _file_size;
+  iterator.last_error = ERROR_SUCCESS;
+  return yr_gpu_scanner_scan_mem_blocks(scanner, gs, &iterator);
+}

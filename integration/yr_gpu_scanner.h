@@ -1,0 +1,40 @@
+/*
+ * yr_gpu_scanner.h -- libyara-side integration of the MI355X atom scanner
+ * (see yr_gpu_scanner.c and INTEGRATION.md).  Include after <yara.h>.
+ */
+#ifndef YR_GPU_SCANNER_H
+#define YR_GPU_SCANNER_H
+
+#include <yara.h>
+
+#include "../include/yara_amd.h"
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+typedef struct YR_GPU_RULES YR_GPU_RULES;     /* device tables of one YR_RULES */
+typedef struct YR_GPU_SCANNER YR_GPU_SCANNER; /* one per YR_SCANNER / thread */
+
+int yr_gpu_rules_create(YR_RULES* rules, int device, YR_GPU_RULES** out);
+void yr_gpu_rules_destroy(YR_GPU_RULES* g);
+int yr_gpu_scanner_create(YR_GPU_RULES* g, YR_GPU_SCANNER** out);
+void yr_gpu_scanner_destroy(YR_GPU_SCANNER* s);
+
+/* Drop-in counterparts of yr_scanner_scan_mem_blocks / yr_scanner_scan_mem
+ * (scanner.c:417, :633): same arguments, callbacks, flags and error codes. */
+int yr_gpu_scanner_scan_mem_blocks(
+    YR_SCANNER* scanner,
+    YR_GPU_SCANNER* gs,
+    YR_MEMORY_BLOCK_ITERATOR* iterator);
+int yr_gpu_scanner_scan_mem(
+    YR_SCANNER* scanner,
+    YR_GPU_SCANNER* gs,
+    const uint8_t* buffer,
+    size_t buffer_size);
+
+#ifdef __cplusplus
+}
+#endif
+
+#endif

@@ -1,0 +1,86 @@
+"""End-to-end match-set parity against the stock reference libyara.
+
+integration/_build/e2e_check compiles the rules with the stock libyara
+compiler and scans the same bytes twice: through stock yr_scanner_scan_mem
+(scanner.c:633) and through the re-hosted driver of integration/yr_gpu_scanner.c
+(GPU candidate stream -> reference-ordered replay -> the unmodified
+yr_scan_verify_match / yr_execute_code of that same libyara).  Every match of
+every string ({string, base+offset, length, xor key}) and every rule report
+must be identical.  The reference build (oracle/_ref) and the shim are built
+in the build container and travel to the GPU box as shared objects.
+"""
+import json
+import os
+import subprocess
+
+import numpy as np
+import pytest
+
+import gen_rules
+import oracle
+import planted
+from conftest import ALPHA, GOLDEN, REPO
+
+pytestmark = pytest.mark.gpu
+
+CHECK = os.path.join(REPO, "integration", "_build", "e2e_check")
+needs_check = pytest.mark.skipif(not os.path.exists(CHECK),
+                                 reason="integration/_build/e2e_check not built "
+                                        "(needs the reference headers at build time)")
+
+
+def _rules_file(tmp_path, name):
+    p = tmp_path / ("%s.yar" % name)
+    if name in ("short", "root"):
+        p.write_text(open(os.path.join(GOLDEN, "rules", name + ".yar")).read())
+    else:
+        p.write_text(gen_rules.gen(name))
+    return str(p)
+
+
+def _run(rules, data_spec, block=0, overlap=0):
+    cmd = [CHECK, rules, data_spec] + ([str(block), str(overlap)] if block else [])
+    r = subprocess.run(cmd, capture_output=True, text=True, timeout=600)
+    assert r.stdout, r.stderr
+    res = json.loads(r.stdout.strip().splitlines()[-1])
+    return r.returncode, res
+
+
+def _data_file(tmp_path, arr, name):
+    p = tmp_path / name
+    np.asarray(arr, dtype=np.uint8).tofile(str(p))
+    return str(p)
+
+
+CASES = [
+    ("B", "planted", 16 << 20, 0, 0),
+    ("C", "planted", 16 << 20, 0, 0),
+    ("E", "planted", 16 << 20, 0, 0),
+    ("C", "xs", 64 << 20, 0, 0),
+    ("B", "planted", 4 << 20, 1024, 256),
+    ("C", "planted", 2 << 20, 4096, 512),
+    ("short", "alpha", 1 << 20, 0, 0),
+    ("short", "alpha", 1 << 20, 1024, 256),
+    ("root", "alpha", 4096, 0, 0),
+]
+
+
+@needs_check
+@pytest.mark.parametrize("rules,kind,size,block,overlap", CASES)
+def test_match_set_equals_stock_libyara(tmp_path, rules, kind, size, block, overlap):
+    rf = _rules_file(tmp_path, rules)
+    if kind == "xs":
+        spec = "xs:1:%d" % size
+    elif kind == "planted":
+        spec = _data_file(tmp_path, planted.planted_buffer(oracle.xorshift, gen_rules.gen(rules),
+                                                           size, 3), "d.bin")
+    else:
+        x = oracle.xorshift(size, 5)
+        spec = _data_file(tmp_path, np.frombuffer(ALPHA, np.uint8)[x % len(ALPHA)], "d.bin")
+    rc, res = _run(rf, spec, block, overlap)
+    assert res["rc_stock"] == 0 and res["rc_gpu"] == 0, res
+    assert res["same_matches"] and res["same_rule_reports"], res
+    assert res["finished"] == [1, 1], res
+    if kind == "planted":
+        assert res["matches_stock"] > 0 and res["rules_matching"] > 0, res
+    assert rc == 0
