@@ -22,9 +22,8 @@
 
 typedef struct
 {
-  uint32_t s;
   uint64_t off;
-  uint32_t len, xk;
+  uint32_t s, len, xk, pad; /* no implicit padding: records are memcmp'd */
 } rec;
 
 typedef struct
@@ -60,8 +59,8 @@ static int cb(YR_SCAN_CONTEXT* ctx, int msg, void* data, void* user)
       for (uint32_t k = 0; k < c->rules->num_strings; k++)
         for (YR_MATCH* m = ctx->matches[k].head; m != NULL; m = m->next)
         {
-          rec x = {k, (uint64_t) (m->base + m->offset), (uint32_t) m->match_length,
-                   m->xor_key};
+          rec x = {(uint64_t) (m->base + m->offset), k, (uint32_t) m->match_length,
+                   m->xor_key, 0};
           push(c, x);
         }
       c->dumped = 1;
