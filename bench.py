@@ -45,6 +45,7 @@ def parse():
     ap.add_argument("--cpu-sample-mib", type=int, default=1024)
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--no-check", action="store_true")
+    ap.add_argument("--backend", default="nccl", help="nccl (= RCCL) or gloo (rehearsal)")
     return ap.parse_args()
 
 
@@ -118,23 +119,29 @@ def main():
     local = int(os.environ.get("LOCAL_RANK", "0"))
     if world != args.gpus and world > 1:
         raise SystemExit("--gpus %d but WORLD_SIZE=%d" % (args.gpus, world))
-    torch.cuda.set_device(local)
-    dev = torch.device("cuda", local)
+    ndev = torch.cuda.device_count()
+    dev = torch.device("cuda", local % ndev)   # % ndev: gloo rehearsals on fewer GPUs
+    torch.cuda.set_device(dev)
     if world > 1:
-        dist.init_process_group("nccl", device_id=dev)
+        if args.backend == "nccl":
+            dist.init_process_group("nccl", device_id=dev)
+        else:
+            dist.init_process_group(args.backend)
 
+    from yara_amd import dist as ydist
     shard = int(args.gib_per_gpu * GiB)
-    begin, end = rank * shard, (rank + 1) * shard
-    halo = 16 if begin > 0 else 0                   # >= 4-byte warm-up, 16-B aligned
-    buf = torch.empty(shard + halo + 16, dtype=torch.uint8, device=dev)
-    yara_amd.fill_xorshift64(buf.data_ptr(), shard + halo, args.seed, begin - halo)
+    total = shard * world                           # one logical block, sharded
+    begin, end = ydist.shard_bounds(total, world, rank)
+    lo, halo = ydist.local_window(begin, end)       # >= 4-byte warm-up, 16-B aligned
+    buf = torch.empty(end - lo + 16, dtype=torch.uint8, device=dev)
+    yara_amd.fill_xorshift64(buf.data_ptr(), end - lo, args.seed, lo)
     torch.cuda.synchronize()
 
     tables = yara_amd.Tables.from_npz(os.path.join(REPO, "tests", "golden", "tables",
-                                                   "%s.npz" % args.rules), device=local)
+                                                   "%s.npz" % args.rules), device=dev.index)
     stream = torch.cuda.Stream(device=dev)
     scanner = yara_amd.Scanner(tables, stream=stream.cuda_stream)
-    block = shard + halo
+    block = end - lo
 
     def step(timed_kernel=False):
         scanner.scan_device(buf.data_ptr(), block, halo, block)
@@ -142,18 +149,9 @@ def main():
         kms = scanner.kernel_ms() if timed_kernel else None
         pos = torch.empty(max(cnt, 1), dtype=torch.int64, device=dev)
         memcpy(pos.data_ptr(), ptr, cnt * 8, 3)
-        pos = pos[:cnt] + (begin - halo)            # global positions
+        pos = pos[:cnt] + lo                        # global positions
         if world > 1:
-            n_t = torch.tensor([cnt], dtype=torch.int64, device=dev)
-            counts = [torch.zeros_like(n_t) for _ in range(world)]
-            dist.all_gather(counts, n_t)
-            mx = int(max(c.item() for c in counts))
-            padded = torch.full((max(mx, 1),), -1, dtype=torch.int64, device=dev)
-            padded[:cnt] = pos
-            gathered = [torch.empty_like(padded) for _ in range(world)] if rank == 0 else None
-            dist.gather(padded, gathered, dst=0)
-            if rank == 0:
-                pos = torch.cat([g[:int(c.item())] for g, c in zip(gathered, counts)])
+            pos = ydist.gather_positions(pos)       # RCCL: counts + padded gather
         return pos, kms
 
     for _ in range(args.warmup):
@@ -173,11 +171,12 @@ def main():
     elapsed = time.perf_counter() - t0
     scanner.set_timing(False)
     if world > 1:
-        t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
+        t = torch.tensor([elapsed], dtype=torch.float64,
+                         device=dev if args.backend == "nccl" else "cpu")
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed = float(t.item())
 
-    total_bytes = shard * world * args.steps
+    total_bytes = total * args.steps
     value = total_bytes / elapsed / 1e9
     k_avg = sum(kernel_ms) / len(kernel_ms)
     achieved = shard / (k_avg * 1e-3) / 1e9
