@@ -138,6 +138,15 @@ __device__ __forceinline__ void drain(const ScanParams& p, WaveQueue& q, uint32_
   q.head += n;
 }
 
+// A tile entirely inside the block: one 16-byte non-temporal load per lane
+// (read-once stream; keeps the exact tables' L2 lines).
+__device__ __forceinline__ uint4 load_tile_full(const uint8_t* base, uint32_t tile_off, uint32_t lane) {
+  typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
+  const u32x4 v = __builtin_nontemporal_load(
+      reinterpret_cast<const u32x4*>(base + tile_off + lane * kBytesPerLane));
+  return make_uint4(v.x, v.y, v.z, v.w);
+}
+
 __device__ __forceinline__ uint4 load_tile(const uint8_t* base, uint32_t tile_off, uint32_t lane,
                                            uint64_t avail) {
   const uint32_t off = tile_off + lane * kBytesPerLane;
@@ -164,106 +173,130 @@ __device__ __forceinline__ uint4 load_tile(const uint8_t* base, uint32_t tile_of
   return v;
 }
 
+struct SegState {
+  uint64_t seg_start;
+  uint32_t seg_len;
+  uint32_t* out;
+  uint32_t found;
+  uint32_t carry;   // the 4 bytes before the current tile (lane 0's window head)
+};
+
+// One 1 KiB tile: stage-1 filter over its 1024 byte positions, then the ordered
+// append of the hits to the wave ring.  TAIL: the segment's last, partial tile
+// (positions past seg_len are masked off).
+template <int MODE, bool TAIL>
+__device__ __forceinline__ void tile_step(const ScanParams& p, WaveQueue& q, SegState& st,
+                                          uint4 cur, uint32_t tile_off, uint32_t lane) {
+  // previous lane's last dword (lane 0: the previous tile's / the halo)
+  const uint32_t S0 = __builtin_amdgcn_update_dpp(st.carry, cur.w, 0x138, 0xF, 0xF, false);  // wave_shr:1
+  st.carry = __builtin_amdgcn_readlane(cur.w, kWave - 1);
+  const uint32_t S[6] = {S0, cur.x, cur.y, cur.z, cur.w, 0u};
+
+  // Phase A: the 16 windows of this lane and their 16 filter-word reads, all
+  // issued before any is consumed (LDS latency hiding at 4 waves/SIMD).
+  uint32_t xs[kBytesPerLane], ws[kBytesPerLane];
+#pragma unroll
+  for (int k = 0; k < kBytesPerLane; ++k) {
+    // low 24 bits = bytes k-2, k-1, k of this lane (stream offset k + 2)
+    const int o = k + 2;
+    xs[k] = (o & 3) == 0   ? S[o >> 2]
+            : (o & 3) == 1 ? S[o >> 2] >> 8
+                           : __builtin_amdgcn_alignbyte(S[(o >> 2) + 1], S[o >> 2], o & 3);
+    if constexpr (MODE != 3) {
+      const uint32_t x = xs[k];
+      uint32_t addr = (x >> 7) & (kFilterBytes - 4);
+      if constexpr (MODE == 4) addr = ((lane & 31u) * 4u + (uint32_t)k * 128u) & (kFilterBytes - 4);
+      if constexpr (MODE == 5) {
+        ws[k] = addr ^ x;
+      } else {
+        ws[k] = *reinterpret_cast<const __attribute__((address_space(3))) uint32_t*>(
+            (uintptr_t)addr);   // filter sits at LDS offset 0: no base add
+      }
+    }
+  }
+  // Phase B: blocked-Bloom test of bits b1 = x[0..4], b2 = x[4..8] (the
+  // shifter reads only the low 5 bits of the amount); acc collects the 16
+  // results via v_alignbit: afterwards bit 16 + k holds position k.
+  uint32_t acc = 0;
+#pragma unroll
+  for (int k = 0; k < kBytesPerLane; ++k) {
+    if constexpr (MODE == 3) {
+      acc ^= xs[k];
+    } else if constexpr (MODE == 6) {
+      acc ^= ws[k];
+    } else {
+      const uint32_t x = xs[k], w = ws[k];
+      const uint32_t t2 = (w >> (x & 31u)) & (w >> ((x >> 4) & 31u));
+      acc = __builtin_amdgcn_alignbit(t2, acc, 1);
+    }
+  }
+  if constexpr (MODE >= 2) {
+    asm volatile("" ::"v"(acc));
+    return;
+  }
+  uint32_t mask = acc >> 16;
+  const uint32_t lane_off = tile_off + lane * kBytesPerLane;
+  if constexpr (TAIL) {
+    if (lane_off + kBytesPerLane > st.seg_len)
+      mask = lane_off >= st.seg_len ? 0u : (mask & ((1u << (st.seg_len - lane_off)) - 1u));
+  }
+  const uint64_t any = __ballot(mask != 0);
+  if (any != 0) {
+    const uint32_t n = (uint32_t)__popcll(any);
+    if (q.tail - q.head + n > kQueueCap) drain<MODE>(p, q, lane, st.seg_start, st.out, st.found);
+    if (mask != 0) {
+      const uint32_t below = __builtin_amdgcn_mbcnt_hi((uint32_t)(any >> 32),
+                                                       __builtin_amdgcn_mbcnt_lo((uint32_t)any, 0u));
+      uint32_t* ent = q.ring + ((q.tail + below) % kQueueCap) * kQueueEntryWords;
+      *reinterpret_cast<uint4*>(ent) = make_uint4(S[0], S[1], S[2], S[3]);
+      *reinterpret_cast<uint4*>(ent + 4) =
+          make_uint4(S[4], ((lane_off / kBytesPerLane) << 16) | mask, 0u, 0u);
+    }
+    q.tail += n;
+  }
+}
+
+// Stream one segment [seg_start, seg_start + seg_len) of the block: full tiles
+// in the main loop (unmasked, one tile of loads in flight), then the partial
+// tail tile if any.
 // MODE: 0 = the product kernel.  Others are profiling ablations only (their
 // output is wrong by construction): 1 = no exact check, 2 = stage 1 only
 // (no queue), 3 = input streaming only (no filter), 4 = stage 1 with
 // bank-conflict-free LDS addresses, 5 = stage 1 VALU without the LDS reads,
 // 6 = stage 1 addresses + LDS reads without the bit tests.
 template <int MODE>
-__device__ void scan_segment(const ScanParams& p, const uint32_t* __restrict__ filt,
-                             WaveQueue& q, uint32_t seg, uint32_t lane) {
-  const uint64_t seg_start = p.byte_begin + (uint64_t)seg * p.seg_bytes;
-  const uint64_t seg_end = min(seg_start + p.seg_bytes, p.byte_end);
-  const uint32_t seg_len = (uint32_t)(seg_end - seg_start);
-  const uint64_t avail = p.block_size - seg_start;
-  const uint8_t* base = p.data + seg_start;
-  uint32_t* out = p.seg_out + (size_t)seg * p.seg_cap;
-  uint32_t found = 0;
-  const char* filt_bytes = reinterpret_cast<const char*>(filt);
+__device__ void scan_segment(const ScanParams& p, WaveQueue& q, uint32_t seg, uint32_t lane) {
+  SegState st;
+  st.seg_start = p.byte_begin + (uint64_t)seg * p.seg_bytes;
+  const uint64_t seg_end = min(st.seg_start + p.seg_bytes, p.byte_end);
+  st.seg_len = (uint32_t)(seg_end - st.seg_start);
+  st.out = p.seg_out + (size_t)seg * p.seg_cap;
+  st.found = 0;
+  const uint64_t avail = p.block_size - st.seg_start;
+  const uint8_t* base = p.data + st.seg_start;
 
   // 4 bytes before the segment (warm-up halo); zeros before the block start.
-  uint32_t carry = seg_start >= 4 ? *reinterpret_cast<const uint32_t*>(base - 4) : 0u;
+  st.carry = st.seg_start >= 4 ? *reinterpret_cast<const uint32_t*>(base - 4) : 0u;
   q.head = q.tail = 0;
 
-  const uint32_t ntiles = (seg_len + kTile - 1) / kTile;
-  uint4 cur = load_tile(base, 0, lane, avail);
-  for (uint32_t t = 0; t < ntiles; ++t) {
+  const uint32_t n_full = st.seg_len / kTile;            // tiles needing no mask / bounds
+  const uint32_t n_all = (st.seg_len + kTile - 1) / kTile;
+  uint4 cur = n_full > 0 ? load_tile_full(base, 0, lane) : load_tile(base, 0, lane, avail);
+  for (uint32_t t = 0; t < n_full; ++t) {
     const uint32_t tile_off = t * kTile;
     uint4 nxt = make_uint4(0, 0, 0, 0);
-    if (t + 1 < ntiles) nxt = load_tile(base, tile_off + kTile, lane, avail);
-
-    // previous lane's last dword (lane 0: the previous tile's / the halo)
-    const uint32_t S0 = __builtin_amdgcn_update_dpp(carry, cur.w, 0x138, 0xF, 0xF, false);  // wave_shr:1
-    carry = __builtin_amdgcn_readlane(cur.w, kWave - 1);
-    const uint32_t S[6] = {S0, cur.x, cur.y, cur.z, cur.w, 0u};
-
-    // Phase A: the 16 windows of this lane and their 16 filter-word reads,
-    // all issued before any is consumed (hides LDS latency at 4 waves/SIMD).
-    uint32_t xs[kBytesPerLane], ws[kBytesPerLane];
-#pragma unroll
-    for (int k = 0; k < kBytesPerLane; ++k) {
-      // low 24 bits = bytes k-2, k-1, k of this lane (stream offset k + 2)
-      const int o = k + 2;
-      xs[k] = (o & 3) == 0   ? S[o >> 2]
-              : (o & 3) == 1 ? S[o >> 2] >> 8
-                             : __builtin_amdgcn_alignbyte(S[(o >> 2) + 1], S[o >> 2], o & 3);
-      if constexpr (MODE != 3) {
-        const uint32_t x = xs[k];
-        uint32_t addr = (x >> 7) & (kFilterBytes - 4);
-        if constexpr (MODE == 4) addr = ((lane & 31u) * 4u + (uint32_t)k * 128u) & (kFilterBytes - 4);
-        if constexpr (MODE == 5) {
-          ws[k] = addr ^ x;
-        } else {
-          ws[k] = *reinterpret_cast<const __attribute__((address_space(3))) uint32_t*>(
-              (uintptr_t)addr);   // filter sits at LDS offset 0: no base add
-        }
-      }
+    if (t + 1 < n_full) {
+      nxt = load_tile_full(base, tile_off + kTile, lane);
+    } else if (t + 1 < n_all) {
+      nxt = load_tile(base, tile_off + kTile, lane, avail);
     }
-    // Phase B: blocked-Bloom test of bits b1 = x[0..4], b2 = x[4..8] (the
-    // shifter reads only the low 5 bits of the amount); acc collects the 16
-    // results via v_alignbit: afterwards bit 16 + k holds position k.
-    uint32_t acc = 0;
-#pragma unroll
-    for (int k = 0; k < kBytesPerLane; ++k) {
-      if constexpr (MODE == 3) {
-        acc ^= xs[k];
-      } else if constexpr (MODE == 6) {
-        acc ^= ws[k];
-      } else {
-        const uint32_t x = xs[k], w = ws[k];
-        const uint32_t t2 = (w >> (x & 31u)) & (w >> ((x >> 4) & 31u));
-        acc = __builtin_amdgcn_alignbit(t2, acc, 1);
-      }
-    }
-    if constexpr (MODE >= 2) {
-      asm volatile("" ::"v"(acc));
-      cur = nxt;
-      continue;
-    }
-    uint32_t mask = acc >> 16;
-    const uint32_t lane_off = tile_off + lane * kBytesPerLane;
-    if (lane_off + kBytesPerLane > seg_len) {
-      mask = lane_off >= seg_len ? 0u : (mask & ((1u << (seg_len - lane_off)) - 1u));
-    }
-    const uint64_t any = __ballot(mask != 0);
-    if (any != 0) {
-      const uint32_t n = (uint32_t)__popcll(any);
-      while (q.tail - q.head + n > kQueueCap) drain<MODE>(p, q, lane, seg_start, out, found);
-      if (mask != 0) {
-        const uint32_t below = __builtin_amdgcn_mbcnt_hi((uint32_t)(any >> 32),
-                                                         __builtin_amdgcn_mbcnt_lo((uint32_t)any, 0u));
-        uint32_t* ent = q.ring + ((q.tail + below) % kQueueCap) * kQueueEntryWords;
-        *reinterpret_cast<uint4*>(ent) = make_uint4(S[0], S[1], S[2], S[3]);
-        *reinterpret_cast<uint4*>(ent + 4) =
-            make_uint4(S[4], ((lane_off / kBytesPerLane) << 16) | mask, 0u, 0u);
-      }
-      q.tail += n;
-      if (q.tail - q.head >= kQueueCap) drain<MODE>(p, q, lane, seg_start, out, found);
-    }
+    tile_step<MODE, false>(p, q, st, cur, tile_off, lane);
+    if (q.tail - q.head >= kQueueCap) drain<MODE>(p, q, lane, st.seg_start, st.out, st.found);
     cur = nxt;
   }
-  while (q.tail != q.head) drain<MODE>(p, q, lane, seg_start, out, found);
-  if (lane == 0) p.seg_count[seg] = found;
+  if (n_all > n_full) tile_step<MODE, true>(p, q, st, cur, n_full * kTile, lane);
+  while (q.tail != q.head) drain<MODE>(p, q, lane, st.seg_start, st.out, st.found);
+  if (lane == 0) p.seg_count[seg] = st.found;
 }
 
 template <int MODE>
@@ -282,7 +315,7 @@ __global__ __launch_bounds__(kWGThreads, 1) void scan_segments_kernel(ScanParams
   q.ring = lds + kFilterWords + wid * kQueueCap * kQueueEntryWords;
   const uint32_t total_waves = gridDim.x * kWavesPerWG;
   for (uint32_t seg = blockIdx.x * kWavesPerWG + wid; seg < p.n_segments; seg += total_waves) {
-    scan_segment<MODE>(p, filt, q, seg, lane);
+    scan_segment<MODE>(p, q, seg, lane);
   }
 }
 
