@@ -310,7 +310,9 @@ __global__ __launch_bounds__(kWGThreads, 1) void scan_segments_kernel(ScanParams
   }
   __syncthreads();
   const uint32_t lane = lane_id();
-  const uint32_t wid = threadIdx.x / kWave;
+  // wave index, provably wave-uniform: everything derived from it (segment
+  // bounds, loop counts, ring base) stays in SGPRs with scalar branches
+  const uint32_t wid = __builtin_amdgcn_readfirstlane(threadIdx.x / kWave);
   WaveQueue q;
   q.ring = lds + kFilterWords + wid * kQueueCap * kQueueEntryWords;
   const uint32_t total_waves = gridDim.x * kWavesPerWG;
