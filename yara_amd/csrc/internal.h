@@ -23,7 +23,7 @@ constexpr uint32_t kSegment = 1u << 20;   // max segment: 1 MiB (ring entries ho
 constexpr int kWavesPerWG = 16;
 constexpr int kWGThreads = kWave * kWavesPerWG;     // 1024
 
-// LDS window filter: 2^20 bits = 128 KiB, one bit per hashed 3-byte window.
+// LDS window filter: 2^20 bits = 128 KiB over the 3-byte windows (filter_probe).
 constexpr int kFilterLog2Bits = 20;
 constexpr uint32_t kFilterWords = 1u << (kFilterLog2Bits - 5);   // 32768
 constexpr uint32_t kFilterBytes = kFilterWords * 4;              // 131072
@@ -35,25 +35,26 @@ constexpr uint32_t kQueueEntryWords = 8;
 constexpr uint32_t kQueueBytes = kWavesPerWG * kQueueCap * kQueueEntryWords * 4;   // 32 KiB
 constexpr uint32_t kScanLdsBytes = kFilterBytes + kQueueBytes;                   // 160 KiB
 
-// Blocked-Bloom filter probe of a 3-byte window x = a | b << 8 | c << 16
-// (a = oldest byte): one 32-bit filter word, two bit positions inside it
-// (k = 2 in one word: one LDS read per position).  Plain bit fields -- VOP2
-// shifts and masks only, which gfx950 issues at twice the rate of
-// v_mul_u32_u24 / v_alignbit / v_bfe; the word comes from the two newest
-// bytes, the bits from the oldest, so the fields are independent (on the
-// benchmark rule sets this matches a fully mixed hash: 0.24% false positives
-// for config C).  Bits 24..31 of a window register are never read, so it may
-// carry a neighbouring byte there.
-//   word = x[9..23]    device byte address: (x >> 7) & 0x1FFFC
-//   b1   = x[0..4]     device: the shifter reads only bits 0..4 of x
-//   b2   = x[4..8]     device: x >> 4, same
+// Split-block Bloom filter probe of a 3-byte window x = a | b << 8 | c << 16
+// (a = oldest byte).  The filter is 2^14 blocks of two 32-bit words (lo, hi);
+// a key sets one bit in each word of its block, and a position passes when
+// both are set: one ds_read_b64 and the same VOP2 shift/and work per position
+// as a single-word block with k = 2, but each bit now lives in a 32-position
+// space of its own, so a block holding one key passes 1/1024 of random
+// windows instead of 1/256 (config C: 0.15% false positives vs 0.24%).  The
+// three fields are disjoint and cover the window exactly:
+//   block = x[10..23]   device byte address: (x >> 7) & 0x1FFF8
+//   b_lo  = x[0..4]     device: the shifter reads only bits 0..4 of x
+//   b_hi  = x[5..9]     device: x >> 5, same
+// Bits 24..31 of a window register are never read, so it may carry a
+// neighbouring byte there.
 struct FilterProbe {
-  uint32_t word;  // index into the kFilterWords-word filter
-  uint32_t b1, b2;
+  uint32_t block;  // index into the kFilterWords / 2 blocks; words 2*block, 2*block+1
+  uint32_t b_lo, b_hi;
 };
 __host__ __device__ inline FilterProbe filter_probe(uint32_t w3) {
   const uint32_t x = w3 & 0xFFFFFFu;
-  return FilterProbe{(x >> 9) & (kFilterWords - 1), x & 31u, (x >> 4) & 31u};
+  return FilterProbe{x >> 10, x & 31u, (x >> 5) & 31u};
 }
 
 // Exact key sets (second stage), one uint32 array in HBM:

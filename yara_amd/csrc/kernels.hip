@@ -11,16 +11,17 @@
 // That makes every position independent of every other: no sequential state
 // chain, just a window test.
 //
-//   stage 1 (every byte, LDS):  one bit of a 2^20-bit filter over the hashed
-//             3-byte window ending at the byte.  128 KiB, staged once per
-//             workgroup; one ds_read_b32 per input byte.  Superset of the keys.
-//   stage 2 (filter hits, ~1%):  hits are appended in position order to a
-//             per-wave LDS ring; full batches of 64 are checked exactly against
-//             an open-addressed hash table of the keys in HBM/L2, and survivors
+//   stage 1 (every byte, LDS):  a split-block Bloom filter (2^20 bits) over
+//             the 3-byte window ending at the byte (internal.h filter_probe).
+//             128 KiB, staged once per workgroup; one ds_read_b64 per input
+//             byte.  Superset of the keys (config C: 0.15% of positions pass).
+//   stage 2 (filter hits):  hits are appended in position order to a per-wave
+//             LDS ring; full batches of 64 are checked exactly against the key
+//             sets (bitmaps / bucketed cuckoo tables in HBM/L2), and survivors
 //             are compacted with a wave ballot + mbcnt into the segment's output.
 //
 // Memory: the input is streamed once, 16 B per lane (1 KiB per wave per step),
-// tile t+1 prefetched while tile t is filtered.  Roofline: HBM read bandwidth
+// tiles t+1 and t+2 in flight while tile t is filtered.  Roofline: HBM read bandwidth
 // (1 algorithmic byte per input byte).
 #include "internal.h"
 
@@ -192,9 +193,9 @@ __device__ __forceinline__ void tile_step(const ScanParams& p, WaveQueue& q, Seg
   st.carry = __builtin_amdgcn_readlane(cur.w, kWave - 1);
   const uint32_t S[6] = {S0, cur.x, cur.y, cur.z, cur.w, 0u};
 
-  // Phase A: the 16 windows of this lane and their 16 filter-word reads, all
-  // issued before any is consumed (LDS latency hiding at 4 waves/SIMD).
-  uint32_t xs[kBytesPerLane], ws[kBytesPerLane];
+  // Phase A: the 16 windows of this lane and their 16 filter-block reads.
+  uint32_t xs[kBytesPerLane];
+  uint2 ws[kBytesPerLane];
 #pragma unroll
   for (int k = 0; k < kBytesPerLane; ++k) {
     // low 24 bits = bytes k-2, k-1, k of this lane (stream offset k + 2)
@@ -204,29 +205,32 @@ __device__ __forceinline__ void tile_step(const ScanParams& p, WaveQueue& q, Seg
                            : __builtin_amdgcn_alignbyte(S[(o >> 2) + 1], S[o >> 2], o & 3);
     if constexpr (MODE != 3) {
       const uint32_t x = xs[k];
-      uint32_t addr = (x >> 7) & (kFilterBytes - 4);
-      if constexpr (MODE == 4) addr = ((lane & 31u) * 4u + (uint32_t)k * 128u) & (kFilterBytes - 4);
+      uint32_t addr = (x >> 7) & (kFilterBytes - 8);   // block x[10..23], 8 B each
+      if constexpr (MODE == 4) addr = ((lane & 31u) * 8u + (uint32_t)k * 256u) & (kFilterBytes - 8);
       if constexpr (MODE == 5) {
-        ws[k] = addr ^ x;
+        ws[k] = make_uint2(addr ^ x, addr + x);
       } else {
-        ws[k] = *reinterpret_cast<const __attribute__((address_space(3))) uint32_t*>(
+        typedef uint32_t u32x2 __attribute__((ext_vector_type(2)));
+        const u32x2 v = *reinterpret_cast<const __attribute__((address_space(3))) u32x2*>(
             (uintptr_t)addr);   // filter sits at LDS offset 0: no base add
+        ws[k] = make_uint2(v.x, v.y);
       }
     }
   }
-  // Phase B: blocked-Bloom test of bits b1 = x[0..4], b2 = x[4..8] (the
-  // shifter reads only the low 5 bits of the amount); acc collects the 16
-  // results via v_alignbit: afterwards bit 16 + k holds position k.
+  // Phase B: split-block test, bit x[0..4] of the lo word and bit x[5..9] of
+  // the hi word (the shifter reads only the low 5 bits of the amount); acc
+  // collects the 16 results via v_alignbit: afterwards bit 16 + k holds
+  // position k.
   uint32_t acc = 0;
 #pragma unroll
   for (int k = 0; k < kBytesPerLane; ++k) {
     if constexpr (MODE == 3) {
       acc ^= xs[k];
     } else if constexpr (MODE == 6) {
-      acc ^= ws[k];
+      acc ^= ws[k].x ^ ws[k].y;
     } else {
-      const uint32_t x = xs[k], w = ws[k];
-      const uint32_t t2 = (w >> (x & 31u)) & (w >> ((x >> 4) & 31u));
+      const uint32_t x = xs[k];
+      const uint32_t t2 = (ws[k].x >> (x & 31u)) & (ws[k].y >> ((x >> 5) & 31u));
       acc = __builtin_amdgcn_alignbit(t2, acc, 1);
     }
   }
@@ -257,7 +261,7 @@ __device__ __forceinline__ void tile_step(const ScanParams& p, WaveQueue& q, Seg
 }
 
 // Stream one segment [seg_start, seg_start + seg_len) of the block: full tiles
-// in the main loop (unmasked, one tile of loads in flight), then the partial
+// in the main loop (unmasked, two tiles of loads in flight), then the partial
 // tail tile if any.
 // MODE: 0 = the product kernel.  Others are profiling ablations only (their
 // output is wrong by construction): 1 = no exact check, 2 = stage 1 only
@@ -281,18 +285,19 @@ __device__ void scan_segment(const ScanParams& p, WaveQueue& q, uint32_t seg, ui
 
   const uint32_t n_full = st.seg_len / kTile;            // tiles needing no mask / bounds
   const uint32_t n_all = (st.seg_len + kTile - 1) / kTile;
-  uint4 cur = n_full > 0 ? load_tile_full(base, 0, lane) : load_tile(base, 0, lane, avail);
+  // two tiles of loads in flight ahead of the one being filtered
+  auto fetch = [&](uint32_t t) {
+    return t < n_full ? load_tile_full(base, t * kTile, lane)
+                      : (t < n_all ? load_tile(base, t * kTile, lane, avail) : make_uint4(0, 0, 0, 0));
+  };
+  uint4 cur = fetch(0);
+  uint4 nxt = fetch(1);
   for (uint32_t t = 0; t < n_full; ++t) {
-    const uint32_t tile_off = t * kTile;
-    uint4 nxt = make_uint4(0, 0, 0, 0);
-    if (t + 1 < n_full) {
-      nxt = load_tile_full(base, tile_off + kTile, lane);
-    } else if (t + 1 < n_all) {
-      nxt = load_tile(base, tile_off + kTile, lane, avail);
-    }
-    tile_step<MODE, false>(p, q, st, cur, tile_off, lane);
+    const uint4 nxt2 = fetch(t + 2);
+    tile_step<MODE, false>(p, q, st, cur, t * kTile, lane);
     if (q.tail - q.head >= kQueueCap) drain<MODE>(p, q, lane, st.seg_start, st.out, st.found);
     cur = nxt;
+    nxt = nxt2;
   }
   if (n_all > n_full) tile_step<MODE, true>(p, q, st, cur, n_full * kTile, lane);
   while (q.tail != q.head) drain<MODE>(p, q, lane, st.seg_start, st.out, st.found);

@@ -40,7 +40,8 @@ inline uint64_t node_key(uint32_t bytes, uint32_t depth) { return ((uint64_t)dep
 
 void filter_set(std::vector<uint32_t>& f, uint32_t w3) {
   const FilterProbe fp = filter_probe(w3);
-  f[fp.word] |= (1u << fp.b1) | (1u << fp.b2);
+  f[2 * fp.block] |= 1u << fp.b_lo;
+  f[2 * fp.block + 1] |= 1u << fp.b_hi;
 }
 
 // Two-choice, 4-way bucketed cuckoo table of non-zero keys.  Load <= 1/2 to
