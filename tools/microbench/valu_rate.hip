@@ -24,6 +24,12 @@ __global__ __launch_bounds__(1024) void k(uint32_t* out, uint32_t iters, uint32_
         if constexpr (OP == 7) a[i] = __builtin_amdgcn_ubfe(a[(i + 1) & 7], a[i], 1) ^ a[i];       // bfe + xor
         if constexpr (OP == 8) a[i] = ((a[i] >> 7) ^ (a[(i + 1) & 7] << 2)) & 0x1FFFCu;            // lshr,lshl,bitop3
         if constexpr (OP == 9) a[i] = (a[(i + 1) & 7] << (i + 1)) | a[i];                          // lshl_or
+        if constexpr (OP == 10)  // v_and_b32_sdwa into byte 1, preserving the rest
+          asm("v_and_b32_sdwa %0, %1, %2 dst_sel:BYTE_1 dst_unused:UNUSED_PRESERVE src0_sel:DWORD src1_sel:DWORD"
+              : "+v"(a[i]) : "v"(a[(i + 1) & 7]), "v"(a[(i + 2) & 7]));
+        if constexpr (OP == 11)  // v_lshrrev_b32_sdwa, amount = byte 1 of a register
+          asm("v_lshrrev_b32_sdwa %0, %1, %0 dst_sel:DWORD dst_unused:UNUSED_PAD src0_sel:BYTE_1 src1_sel:DWORD"
+              : "+v"(a[i]) : "v"(a[(i + 1) & 7]));
       }
     }
   }
@@ -49,15 +55,15 @@ int main() {
   uint32_t* out; hipMalloc(&out, 4);
   int cus; hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, 0);
   const uint32_t iters = 4096;
-  const char* names[] = {"alignbit", "mul_u24+xor", "mul_hi_u24+add", "lshr+xor", "add", "alignbyte", "perm", "bfe+xor", "lshr,lshl,bitop3", "lshl_or"};
+  const char* names[] = {"alignbit", "mul_u24+xor", "mul_hi_u24+add", "lshr+xor", "add", "alignbyte", "perm", "bfe+xor", "lshr,lshl,bitop3", "lshl_or", "and_sdwa_byte", "lshr_sdwa_src"};
   for (int g : {cus, 2 * cus}) {
-    double ms[10] = {run<0>(out, g, iters), run<1>(out, g, iters), run<2>(out, g, iters),
+    double ms[12] = {run<0>(out, g, iters), run<1>(out, g, iters), run<2>(out, g, iters),
                     run<3>(out, g, iters), run<4>(out, g, iters), run<5>(out, g, iters),
                     run<6>(out, g, iters), run<7>(out, g, iters), run<8>(out, g, iters),
-                    run<9>(out, g, iters)};
-    for (int o = 0; o < 10; ++o) {
+                    run<9>(out, g, iters), run<10>(out, g, iters), run<11>(out, g, iters)};
+    for (int o = 0; o < 12; ++o) {
       // wave-instructions executed per chain-step
-      const double nops[10] = {1, 2, 2, 2, 1, 1, 1, 2, 3, 1};
+      const double nops[12] = {1, 2, 2, 2, 1, 1, 1, 2, 3, 1, 1, 1};
       double ops = nops[o];
       double winstr = (double)g * 16 * iters * 64 * ops;
       printf("grid %d  %-15s %8.3f ms  %.3f wave-instr/clk/CU @2.4GHz  (%.1f G lane-op/s/CU)\n", g,

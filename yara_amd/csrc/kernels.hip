@@ -91,10 +91,13 @@ __device__ __forceinline__ uint32_t window4(const uint32_t (&C)[5], uint32_t j) 
   return __builtin_amdgcn_alignbyte(hi, lo, o & 3u);
 }
 
+// Lane byte (0..15) of bit b of a tile hit mask: bit 8n + r <=> byte 4n + r.
+__device__ __forceinline__ uint32_t mask_position(uint32_t b) { return ((b >> 3) << 2) | (b & 3u); }
+
 // Per-wave LDS ring of filter hits awaiting the exact check.  One 32-byte
 // entry per (tile, lane) with at least one hit: the lane's window context
-// (4 bytes before it + its 16 bytes) and (lane byte offset in segment / 16)
-// << 16 | 16-bit hit mask.  Entries are appended in lane order, so ring order
+// (4 bytes before it + its 16 bytes), lane byte offset in segment / 16, and
+// the hit mask (mask_position() layout).  Entries are appended in lane order, so ring order
 // is ascending position order.  The exact check then needs no global load
 // of the input, only the hash-table probes.
 struct WaveQueue {
@@ -116,10 +119,10 @@ __device__ __forceinline__ void drain(const ScanParams& p, WaveQueue& q, uint32_
     const uint4 a = *reinterpret_cast<const uint4*>(ent);
     const uint4 b = *reinterpret_cast<const uint4*>(ent + 4);
     const uint32_t C[5] = {a.x, a.y, a.z, a.w, b.x};
-    off0 = (b.y >> 16) * kBytesPerLane;
-    uint32_t m = b.y & 0xFFFFu;
+    off0 = b.y * kBytesPerLane;
+    uint32_t m = b.z;
     while (m) {
-      const uint32_t j = (uint32_t)__builtin_ctz(m);
+      const uint32_t j = mask_position((uint32_t)__builtin_ctz(m));
       m &= m - 1;
       const bool hit = MODE == 1 ? ((off0 + j) & 1023u) == 7u
                                  : exact_check(window4(C, j), seg_start + off0 + j + 1, p);
@@ -218,31 +221,48 @@ __device__ __forceinline__ void tile_step(const ScanParams& p, WaveQueue& q, Seg
     }
   }
   // Phase B: split-block test, bit x[0..4] of the lo word and bit x[5..9] of
-  // the hi word (the shifter reads only the low 5 bits of the amount); acc
-  // collects the 16 results via v_alignbit: afterwards bit 16 + k holds
-  // position k.
-  uint32_t acc = 0;
+  // the hi word (the shifter reads only the low 5 bits of the amount).  The
+  // AND of the two shifted words is written by one SDWA v_and straight into
+  // byte n of accumulator r (k = 4n + r), so bit 0 of that byte is position
+  // k's result and no separate accumulate instruction is needed; bits 1..7
+  // of each byte are don't-care and masked off once per tile below.
+  uint32_t acc[4];   // every byte is written below: no initial value needed
 #pragma unroll
   for (int k = 0; k < kBytesPerLane; ++k) {
     if constexpr (MODE == 3) {
-      acc ^= xs[k];
+      acc[k & 3] ^= xs[k];
     } else if constexpr (MODE == 6) {
-      acc ^= ws[k].x ^ ws[k].y;
+      acc[k & 3] ^= ws[k].x ^ ws[k].y;
     } else {
       const uint32_t x = xs[k];
-      const uint32_t t2 = (ws[k].x >> (x & 31u)) & (ws[k].y >> ((x >> 5) & 31u));
-      acc = __builtin_amdgcn_alignbit(t2, acc, 1);
+      const uint32_t u = ws[k].x >> (x & 31u), v = ws[k].y >> ((x >> 5) & 31u);
+      switch (k >> 2) {
+        case 0: asm("v_and_b32_sdwa %0, %1, %2 dst_sel:BYTE_0 dst_unused:UNUSED_PRESERVE src0_sel:DWORD src1_sel:DWORD"
+                    : "+v"(acc[k & 3]) : "v"(u), "v"(v)); break;
+        case 1: asm("v_and_b32_sdwa %0, %1, %2 dst_sel:BYTE_1 dst_unused:UNUSED_PRESERVE src0_sel:DWORD src1_sel:DWORD"
+                    : "+v"(acc[k & 3]) : "v"(u), "v"(v)); break;
+        case 2: asm("v_and_b32_sdwa %0, %1, %2 dst_sel:BYTE_2 dst_unused:UNUSED_PRESERVE src0_sel:DWORD src1_sel:DWORD"
+                    : "+v"(acc[k & 3]) : "v"(u), "v"(v)); break;
+        default: asm("v_and_b32_sdwa %0, %1, %2 dst_sel:BYTE_3 dst_unused:UNUSED_PRESERVE src0_sel:DWORD src1_sel:DWORD"
+                     : "+v"(acc[k & 3]) : "v"(u), "v"(v)); break;
+      }
     }
   }
   if constexpr (MODE >= 2) {
-    asm volatile("" ::"v"(acc));
+    asm volatile("" ::"v"(acc[0] ^ acc[1] ^ acc[2] ^ acc[3]));
     return;
   }
-  uint32_t mask = acc >> 16;
+  // hit mask: bit 8n + r <=> position 4n + r of the lane (mask_position())
+  uint32_t mask = (acc[0] & 0x01010101u) | ((acc[1] & 0x01010101u) << 1) |
+                  ((acc[2] & 0x01010101u) << 2) | ((acc[3] & 0x01010101u) << 3);
   const uint32_t lane_off = tile_off + lane * kBytesPerLane;
   if constexpr (TAIL) {
-    if (lane_off + kBytesPerLane > st.seg_len)
-      mask = lane_off >= st.seg_len ? 0u : (mask & ((1u << (st.seg_len - lane_off)) - 1u));
+    if (lane_off + kBytesPerLane > st.seg_len) {
+      const uint32_t lim = lane_off >= st.seg_len ? 0u : st.seg_len - lane_off;
+      uint32_t keep = 0;
+      for (uint32_t j = 0; j < lim; ++j) keep |= 1u << (((j >> 2) << 3) | (j & 3u));
+      mask &= keep;
+    }
   }
   const uint64_t any = __ballot(mask != 0);
   if (any != 0) {
@@ -254,7 +274,7 @@ __device__ __forceinline__ void tile_step(const ScanParams& p, WaveQueue& q, Seg
       uint32_t* ent = q.ring + ((q.tail + below) % kQueueCap) * kQueueEntryWords;
       *reinterpret_cast<uint4*>(ent) = make_uint4(S[0], S[1], S[2], S[3]);
       *reinterpret_cast<uint4*>(ent + 4) =
-          make_uint4(S[4], ((lane_off / kBytesPerLane) << 16) | mask, 0u, 0u);
+          make_uint4(S[4], lane_off / kBytesPerLane, mask, 0u);
     }
     q.tail += n;
   }
