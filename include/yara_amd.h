@@ -194,6 +194,85 @@ int yr_amd_replay(
     void* user);
 
 /*
+ * ---- On-device literal pre-verification ----
+ *
+ * The string records of the rules (YR_STRING, libyara/include/yara/types.h),
+ * indexed like rules->strings_table, for the on-device evaluation of
+ * _yr_scan_verify_literal_match (scan.c:887-990).
+ */
+typedef struct
+{
+  uint32_t flags;          /* YR_STRING.flags (STRING_FLAGS_* values, types.h:66-88) */
+  uint32_t length;         /* YR_STRING.length */
+  int64_t fixed_offset;    /* YR_STRING.fixed_offset */
+  uint64_t bytes_offset;   /* where YR_STRING.string starts in the byte blob */
+} yr_amd_string;
+
+/*
+ * Attach the string records to the tables (once, before any scanner verifies
+ * on them).  pool_string[k] = index (into strings) of
+ * rules->ac_match_pool[k].string; n_pool must equal the tables' pool size.
+ * lowercase = the host's yr_lowercase[256] table (libyara.c:258), so nocase
+ * comparisons use exactly the host's case folding.
+ */
+int yr_amd_tables_set_strings(
+    yr_amd_tables* tables,
+    const uint32_t* pool_string,
+    uint32_t n_pool,
+    const yr_amd_string* strings,
+    uint32_t n_strings,
+    const uint8_t* bytes,
+    uint64_t n_bytes,
+    const uint8_t* lowercase);
+
+/*
+ * One call of the replay that can have an effect: the host calls
+ * yr_scan_verify_match(scanner, &rules->ac_match_pool[pool_index], data,
+ * size, base, offset).  candidate = index of the candidate position in the
+ * scan's stream that produced it.
+ */
+typedef struct
+{
+  uint64_t offset;
+  uint32_t pool_index;
+  uint32_t candidate;
+} yr_amd_verify_rec;
+
+/*
+ * Pre-verify the candidate stream of the last completed scan of this scanner
+ * (yr_amd_scan_device + yr_amd_scan_device_result, on the same block) on the
+ * GPU.  Produces, in the exact order yr_amd_replay would make them, the calls
+ * of the reference loop (scanner.c:105-121) minus those that provably return
+ * without effect: a literal string whose comparison fails
+ * (_yr_scan_verify_literal_match returns before _yr_scan_match_callback,
+ * scan.c:974-975), a FIXED_OFFSET string at another offset (scan.c:1023), and
+ * offset == size (scan.c:1013).  Non-literal strings are always kept (their
+ * verification is re.c's, on the host).  data_base = YR_MEMORY_BLOCK.base.
+ * On success *d_records is a DEVICE pointer owned by the scanner (valid until
+ * its next verify) to *count records.  Synchronous.
+ * Requires yr_amd_tables_set_strings; YR_AMD_INVALID_ARGUMENT otherwise.
+ */
+int yr_amd_verify_device(
+    yr_amd_scanner* scanner,
+    uint64_t data_base,
+    const yr_amd_verify_rec** d_records,
+    uint64_t* count);
+
+/*
+ * Host-block convenience: H2D, scan, pre-verify, D2H.  *records points to
+ * *count host records owned by the scanner (valid until its next call).
+ * Replaying them in order into yr_scan_verify_match yields the same scan
+ * state as replaying the full candidate stream with yr_amd_replay.
+ */
+int yr_amd_scan_block_verified(
+    yr_amd_scanner* scanner,
+    const uint8_t* data,
+    size_t size,
+    uint64_t data_base,
+    const yr_amd_verify_rec** records,
+    uint64_t* count);
+
+/*
  * Kernel timing (measurement support): when enabled, the scanner records HIP
  * events around its scan kernel on its own stream; yr_amd_scanner_kernel_ms
  * returns the duration of the last scan kernel launch (after the scan result

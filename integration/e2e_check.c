@@ -10,6 +10,7 @@
  * per-rule RULE_MATCHING / RULE_NOT_MATCHING reports.  Prints one JSON line.
  *
  *   e2e_check <rules.yar> <data file | xs:SEED:SIZE> [block_size overlap]
+ *   (E2E_PREVERIFY=0: GPU path without the on-device literal pre-verification)
  */
 #include <stdint.h>
 #include <stdio.h>
@@ -212,6 +213,8 @@ int main(int argc, char** argv)
   YR_GPU_SCANNER* gs;
   int r = yr_gpu_rules_create(rules, 0, &gr);
   if (r == 0) r = yr_gpu_scanner_create(gr, &gs);
+  const char* pv = getenv("E2E_PREVERIFY"); /* "0": replay the full candidate stream */
+  if (r == 0 && pv != NULL && strcmp(pv, "0") == 0) yr_gpu_scanner_set_preverify(gs, 0);
   if (r)
   {
     fprintf(stderr, "gpu setup failed: %d\n", r);

@@ -9,9 +9,13 @@
  * static, so the driver that calls it, yr_scanner_scan_mem_blocks
  * (scanner.c:417-583), is re-hosted here step for step; the only change is
  * the per-block call (scanner.c:493-496), which becomes
- *     GPU candidate stream (yr_amd_scan_block)
- *  -> reference-ordered replay (yr_amd_replay)
- *  -> the unmodified verifier yr_scan_verify_match (scan.c:992)
+ *     GPU candidate stream + on-device literal pre-verification
+ *       (yr_amd_scan_block_verified: drops the calls that provably have no
+ *       effect, scan.c:887-990 / :1013 / :1023)
+ *  -> the remaining calls, in the reference's order, into the unmodified
+ *     verifier yr_scan_verify_match (scan.c:992)
+ * or, with pre-verification off, the full candidate stream (yr_amd_scan_block)
+ * replayed by yr_amd_replay.
  * followed, as in the reference, by yr_execute_code (exec.c:418) and the
  * rule-report loop (scanner.c:524-556).
  */
@@ -24,6 +28,7 @@
 #include <yara/compiler.h>
 #include <yara/exec.h>
 #include <yara/exefiles.h>
+#include <yara/globals.h>
 #include <yara/notebook.h>
 #include <yara/scan.h>
 #include <yara/stopwatch.h>
@@ -42,7 +47,41 @@ struct YR_GPU_SCANNER
   yr_amd_scanner* scanner;
   uint8_t* staging; /* host copy of the block being scanned */
   size_t staging_size;
+  int preverify;    /* on-device literal pre-verification (default on) */
 };
+
+/* YR_STRING records for yr_amd_tables_set_strings (types.h YR_STRING). */
+static int _attach_strings(YR_RULES* rules, uint32_t n_pool, yr_amd_tables* t)
+{
+  uint32_t n_str = rules->num_strings;
+  uint64_t n_bytes = 0;
+  for (uint32_t k = 0; k < n_str; k++) n_bytes += rules->strings_table[k].length;
+  uint32_t* ps = (uint32_t*) malloc(sizeof(uint32_t) * (n_pool ? n_pool : 1));
+  yr_amd_string* st = (yr_amd_string*) malloc(sizeof(yr_amd_string) * (n_str ? n_str : 1));
+  uint8_t* blob = (uint8_t*) malloc(n_bytes ? n_bytes : 1);
+  int r = ERROR_INSUFFICIENT_MEMORY;
+  if (ps != NULL && st != NULL && blob != NULL)
+  {
+    for (uint32_t k = 0; k < n_pool; k++)
+      ps[k] = (uint32_t) (rules->ac_match_pool[k].string - rules->strings_table);
+    uint64_t off = 0;
+    for (uint32_t k = 0; k < n_str; k++)
+    {
+      YR_STRING* s = &rules->strings_table[k];
+      st[k].flags = s->flags;
+      st[k].length = (uint32_t) s->length;
+      st[k].fixed_offset = s->fixed_offset;
+      st[k].bytes_offset = off;
+      if (s->length > 0) memcpy(blob + off, s->string, s->length);
+      off += s->length;
+    }
+    r = yr_amd_tables_set_strings(t, ps, n_pool, st, n_str, blob, n_bytes, yr_lowercase);
+  }
+  free(ps);
+  free(st);
+  free(blob);
+  return r;
+}
 
 int yr_gpu_rules_create(YR_RULES* rules, int device, YR_GPU_RULES** out)
 {
@@ -84,8 +123,10 @@ int yr_gpu_rules_create(YR_RULES* rules, int device, YR_GPU_RULES** out)
       &g->tables);
   free(nx);
   free(bt);
+  if (r == ERROR_SUCCESS && device >= 0) r = _attach_strings(rules, n_pool, g->tables);
   if (r != ERROR_SUCCESS)
   {
+    yr_amd_tables_destroy(g->tables);
     free(g);
     return r;
   }
@@ -113,8 +154,14 @@ int yr_gpu_scanner_create(YR_GPU_RULES* g, YR_GPU_SCANNER** out)
     return r;
   }
   s->gpu_rules = g;
+  s->preverify = 1;
   *out = s;
   return ERROR_SUCCESS;
+}
+
+void yr_gpu_scanner_set_preverify(YR_GPU_SCANNER* s, int enable)
+{
+  s->preverify = enable != 0;
 }
 
 void yr_gpu_scanner_destroy(YR_GPU_SCANNER* s)
@@ -176,6 +223,27 @@ static int _yr_gpu_scan_mem_block(
       { memcpy(gs->staging, block_data, block->size); },
       { result = ERROR_COULD_NOT_MAP_FILE; });
   if (result != ERROR_SUCCESS) return result;
+
+  if (gs->preverify)
+  {
+    const yr_amd_verify_rec* recs = NULL;
+    uint64_t n = 0;
+    FAIL_ON_ERROR(yr_amd_scan_block_verified(
+        gs->scanner, gs->staging, block->size, block->base, &recs, &n));
+    if (scanner->timeout > 0 &&
+        yr_stopwatch_elapsed_ns(&scanner->stopwatch) > scanner->timeout)
+      return ERROR_SCAN_TIMEOUT;
+    /* the calls of scanner.c:111-117 / :153-159 that can have an effect */
+    for (uint64_t c = 0; c < n; c++)
+      FAIL_ON_ERROR(yr_scan_verify_match(
+          scanner,
+          &scanner->rules->ac_match_pool[recs[c].pool_index],
+          gs->staging,
+          block->size,
+          block->base,
+          (size_t) recs[c].offset));
+    return ERROR_SUCCESS;
+  }
 
   const uint64_t* positions = NULL;
   uint64_t count = 0;

@@ -21,6 +21,11 @@ void yr_gpu_rules_destroy(YR_GPU_RULES* g);
 int yr_gpu_scanner_create(YR_GPU_RULES* g, YR_GPU_SCANNER** out);
 void yr_gpu_scanner_destroy(YR_GPU_SCANNER* s);
 
+/* On-device literal pre-verification (default on): only the verify calls that
+ * can have an effect reach yr_scan_verify_match.  Off: every call of the
+ * reference loop is replayed (yr_amd_replay). */
+void yr_gpu_scanner_set_preverify(YR_GPU_SCANNER* s, int enable);
+
 /* Drop-in counterparts of yr_scanner_scan_mem_blocks / yr_scanner_scan_mem
  * (scanner.c:417, :633): same arguments, callbacks, flags and error codes. */
 int yr_gpu_scanner_scan_mem_blocks(

@@ -53,6 +53,10 @@ def lib():
         L.oracle_count_parallel.argtypes = [_u32p, _u32p, _u8p, ctypes.c_uint64, ctypes.c_int]
         L.oracle_xorshift_fill.restype = None
         L.oracle_xorshift_fill.argtypes = [_u8p, ctypes.c_uint64, ctypes.c_uint64]
+        L.oracle_literal_effect.restype = ctypes.c_int64
+        L.oracle_literal_effect.argtypes = [_u64p, _u32p, ctypes.c_uint64, _u16p, _u32p, _u32p,
+                                            _u32p, ctypes.POINTER(ctypes.c_int64), _u64p, _u8p,
+                                            _u8p, _u8p, ctypes.c_uint64, ctypes.c_uint64, _u8p]
         L.oracle_step.restype = ctypes.c_uint32
         L.oracle_step.argtypes = [_u32p, ctypes.c_uint32, ctypes.c_uint8]
         _lib = L
@@ -136,3 +140,36 @@ def verify_stream_sha(pos, idx, base=None) -> str:
 
 def positions_sha(pos) -> str:
     return hashlib.sha256(np.asarray(pos, dtype="<u8").tobytes()).hexdigest()
+
+
+def ascii_lowercase() -> np.ndarray:
+    """libyara's yr_lowercase under the C locale (libyara.c:258, tolower)."""
+    low = np.arange(256, dtype=np.uint8)
+    low[ord("A"):ord("Z") + 1] += 32
+    return low
+
+
+def literal_effect(npz, pos, idx, data: np.ndarray, base: int = 0, lowercase=None) -> np.ndarray:
+    """Keep-mask of a verify-call stream (positions, pool indexes): True where
+    yr_scan_verify_match can have an effect (ac_oracle.c oracle_literal_effect).
+    ``npz`` = a tests/golden/tables/*.npz mapping (pool + YR_STRING records)."""
+    pos = _c(pos, np.uint64)
+    idx = _c(idx, np.uint32)
+    n = pos.size
+    out = np.zeros(max(n, 1), np.uint8)
+    offs = _c(npz["str_offsets"], np.int64)
+    str_off = _c(offs[:-1], np.uint64) if offs.size > 1 else np.zeros(1, np.uint64)
+    str_len = _c(np.diff(offs), np.uint32) if offs.size > 1 else np.zeros(1, np.uint32)
+    flags = _c(npz["str_flags"], np.uint32) if len(npz["str_flags"]) else np.zeros(1, np.uint32)
+    fixed = _c(npz["str_fixed_offset"], np.int64) if len(npz["str_fixed_offset"]) else np.zeros(1, np.int64)
+    blob = _c(npz["str_bytes"], np.uint8) if len(npz["str_bytes"]) else np.zeros(1, np.uint8)
+    bt = _c(npz["pool_backtrack"], np.uint16)
+    ps = _c(npz["pool_string"], np.uint32)
+    low = _c(ascii_lowercase() if lowercase is None else lowercase, np.uint8)
+    d = _c(data, np.uint8) if data.size else np.zeros(1, np.uint8)
+    lib().oracle_literal_effect(
+        _p(pos, _u64p) if n else None, _p(idx, _u32p) if n else None, n, _p(bt, _u16p),
+        _p(ps, _u32p), _p(flags, _u32p), _p(str_len, _u32p),
+        fixed.ctypes.data_as(ctypes.POINTER(ctypes.c_int64)), _p(str_off, _u64p),
+        _p(blob, _u8p), _p(low, _u8p), _p(d, _u8p), int(data.size), base, _p(out, _u8p))
+    return out[:n].astype(bool)

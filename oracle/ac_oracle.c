@@ -207,3 +207,109 @@ void oracle_xorshift_fill(uint8_t* buf, uint64_t n, uint64_t seed)
     buf[i] = (uint8_t) (x >> 24);
   }
 }
+
+/*
+ * Literal pre-verification oracle.  For every
+ * call (position i, pool index k) of a verify-call stream, decide whether
+ * yr_scan_verify_match(ctx, &pool[k], data, size, base, i - backtrack[k]) can
+ * have an effect, restating:
+ *   - yr_scan_verify_match early outs (libyara/scan.c:1013 offset == size,
+ *     :1023-1025 FIXED_OFFSET mismatch), literal vs re.c dispatch (:1036-1046);
+ *   - _yr_scan_verify_literal_match (scan.c:887-990): FITS_IN_ATOM ->
+ *     forward_matches = backtrack; NO_CASE -> ascii icompare then wide
+ *     wicompare; else ascii compare, wide wcompare, then (XOR) wide xor then
+ *     xor; no effect iff forward_matches == 0 (:974-975);
+ *   - the comparisons _yr_scan_compare / icompare / wcompare / wicompare /
+ *     xor_compare / xor_wcompare (scan.c:62-255), lowercase = yr_lowercase.
+ * Base64 literal strings are not restated: always kept (as on the device).
+ * out[c] = 1 keep, 0 no effect.
+ */
+#define SF_NO_CASE 0x04u
+#define SF_ASCII 0x08u
+#define SF_WIDE 0x10u
+#define SF_LITERAL 0x400u
+#define SF_FITS_IN_ATOM 0x800u
+#define SF_FIXED_OFFSET 0x8000u
+#define SF_XOR 0x80000u
+#define SF_BASE64_ANY (0x200000u | 0x400000u)
+
+static uint64_t fwd_plain(const uint8_t* d, uint64_t avail, const uint8_t* s, uint32_t n,
+                          const uint8_t* low)
+{
+  if (avail < n) return 0;
+  uint32_t i = 0;
+  while (i < n && (low ? low[d[i]] == low[s[i]] : d[i] == s[i])) i++;
+  return i == n ? n : 0;
+}
+
+static uint64_t fwd_wide(const uint8_t* d, uint64_t avail, const uint8_t* s, uint32_t n,
+                         const uint8_t* low)
+{
+  if (avail < 2ull * n) return 0;
+  uint32_t i = 0;
+  while (i < n && (low ? low[d[2 * i]] == low[s[i]] : d[2 * i] == s[i]) && d[2 * i + 1] == 0) i++;
+  return i == n ? 2ull * n : 0;
+}
+
+static uint64_t fwd_xor(const uint8_t* d, uint64_t avail, const uint8_t* s, uint32_t n, int wide)
+{
+  if (avail < (wide ? 2ull * n : (uint64_t) n)) return 0;
+  uint8_t k = d[0] ^ s[0];
+  uint32_t i = 0;
+  if (wide)
+    while (i < n && d[2 * i] == (uint8_t) (s[i] ^ k) && (uint8_t) (d[2 * i + 1] ^ k) == 0) i++;
+  else
+    while (i < n && d[i] == (uint8_t) (s[i] ^ k)) i++;
+  return i == n ? (wide ? 2ull * n : n) : 0;
+}
+
+int64_t oracle_literal_effect(
+    const uint64_t* pos, const uint32_t* pool_idx, uint64_t n_calls,
+    const uint16_t* backtrack, const uint32_t* pool_string,
+    const uint32_t* str_flags, const uint32_t* str_len, const int64_t* str_fixed,
+    const uint64_t* str_off, const uint8_t* blob, const uint8_t* lowercase,
+    const uint8_t* data, uint64_t size, uint64_t base, uint8_t* out)
+{
+  int64_t kept = 0;
+  for (uint64_t c = 0; c < n_calls; c++)
+  {
+    uint32_t k = pool_idx[c];
+    uint64_t off = pos[c] - backtrack[k];
+    uint32_t s = pool_string[k];
+    uint32_t f = str_flags[s];
+    uint64_t fm = 1; /* forward_matches != 0, or "not decided here" */
+    if (off == size)
+      fm = 0;
+    else if ((f & SF_FIXED_OFFSET) && str_fixed[s] != (int64_t) (base + off))
+      fm = 0;
+    else if ((f & SF_LITERAL) && !(f & SF_BASE64_ANY))
+    {
+      const uint8_t* d = data + off;
+      uint64_t avail = size - off;
+      const uint8_t* str = blob + str_off[s];
+      uint32_t n = str_len[s];
+      if (f & SF_FITS_IN_ATOM)
+        fm = backtrack[k];
+      else if (f & SF_NO_CASE)
+      {
+        fm = 0;
+        if (f & SF_ASCII) fm = fwd_plain(d, avail, str, n, lowercase);
+        if ((f & SF_WIDE) && fm == 0) fm = fwd_wide(d, avail, str, n, lowercase);
+      }
+      else
+      {
+        fm = 0;
+        if (f & SF_ASCII) fm = fwd_plain(d, avail, str, n, NULL);
+        if ((f & SF_WIDE) && fm == 0) fm = fwd_wide(d, avail, str, n, NULL);
+        if ((f & SF_XOR) && fm == 0)
+        {
+          if (f & SF_WIDE) fm = fwd_xor(d, avail, str, n, 1);
+          if (fm == 0) fm = fwd_xor(d, avail, str, n, 0);
+        }
+      }
+    }
+    out[c] = fm != 0;
+    kept += fm != 0;
+  }
+  return kept;
+}

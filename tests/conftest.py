@@ -60,6 +60,8 @@ def case_data(rec):
     if kind == "alpha":
         x = oracle.xorshift(spec[2], spec[1])
         return np.frombuffer(ALPHA, dtype=np.uint8)[x % len(ALPHA)]
+    if kind == "lit":
+        return planted.lit_buffer(oracle.xorshift, spec[2], spec[1])
     if kind == "file":
         return np.frombuffer(bytes.fromhex(rec["data_bytes_hex"]), dtype=np.uint8)
     raise ValueError(kind)

@@ -86,3 +86,54 @@ def boundary_buffer(xorshift, atoms, size: int, period: int, seed: int = 11) -> 
         if e - len(a) >= 0 and e <= size:
             buf[e - len(a):e] = np.frombuffer(a, dtype=np.uint8)
     return buf
+
+
+# --- literal-variety buffer (tests/golden/rules/lit.yar) ---------------------
+# Every literal form the on-device pre-verification restates (scan.c:62-255,
+# 887-990) is planted as a match and as near misses that pass the atom but fail
+# the comparison: ascii / wide / nocase / xor (narrow and wide, several keys) /
+# fixed offset / fullword / base64 / hex with wildcards and jumps.
+LIT_WORDS = [b"HelloWorld", b"xyzzy1234", b"ab", b"Quartz", b"WideString", b"AsciiAndWide",
+             b"CaseLess", b"NoCaseWide", b"zz", b"XorMe!", b"XorWide", b"XorRange",
+             b"FixedHere", b"word", b"secretstr"]
+
+
+def _wide(b: bytes) -> bytes:
+    return bytes(x for c in b for x in (c, 0))
+
+
+def _near(b: bytes, r: random.Random) -> bytes:
+    """Same first 4 bytes (atom still hits), one later byte changed."""
+    if len(b) <= 4:
+        return b[:-1] + bytes([b[-1] ^ 0x01])
+    j = r.randrange(4, len(b))
+    return b[:j] + bytes([b[j] ^ 0x5A]) + b[j + 1:]
+
+
+def lit_buffer(xorshift, size: int, seed: int = 13) -> np.ndarray:
+    import base64
+    buf = xorshift(size, seed).copy()
+    r = random.Random(seed)
+    pieces = []
+    for w in LIT_WORDS:
+        pieces += [w, _wide(w), _flip_case(w, r), _near(w, r), _wide(_near(w, r))]
+        for key in (0x01, 0x10, 0x5A, 0xFF):
+            pieces.append(bytes(c ^ key for c in w))
+            pieces.append(bytes(c ^ key for c in _wide(w)))
+            pieces.append(bytes(c ^ key for c in _near(w, r)))
+    pieces += [b" word ", b"swordfish", b"word.", b"(word)", b"words"]
+    for t in (b"base64text", b"xbase64text", b"xxbase64text"):
+        pieces.append(base64.b64encode(t))
+    pieces += [bytes.fromhex("414243444546"), bytes.fromhex("4142434445FF"),
+               bytes.fromhex("6162AA6465"), bytes.fromhex("6162AA6466"),
+               bytes.fromhex("313233AABB3738"), bytes.fromhex("313233AABBCCDD3738"),
+               bytes.fromhex("313233AA3738")]
+    for p in pieces:
+        for _ in range(2):
+            pos = r.randrange(0, size - len(p))
+            buf[pos:pos + len(p)] = np.frombuffer(p, dtype=np.uint8)
+    fixed = b"FixedHere"
+    if size > 8192:
+        buf[4096:4096 + len(fixed)] = np.frombuffer(fixed, dtype=np.uint8)
+        buf[6000:6000 + len(fixed)] = np.frombuffer(fixed, dtype=np.uint8)
+    return buf

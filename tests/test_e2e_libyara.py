@@ -31,16 +31,17 @@ needs_check = pytest.mark.skipif(not os.path.exists(CHECK),
 
 def _rules_file(tmp_path, name):
     p = tmp_path / ("%s.yar" % name)
-    if name in ("short", "root"):
+    if name in ("short", "root", "lit"):
         p.write_text(open(os.path.join(GOLDEN, "rules", name + ".yar")).read())
     else:
         p.write_text(gen_rules.gen(name))
     return str(p)
 
 
-def _run(rules, data_spec, block=0, overlap=0):
+def _run(rules, data_spec, block=0, overlap=0, preverify=True):
     cmd = [CHECK, rules, data_spec] + ([str(block), str(overlap)] if block else [])
-    r = subprocess.run(cmd, capture_output=True, text=True, timeout=600)
+    env = dict(os.environ, E2E_PREVERIFY="1" if preverify else "0")
+    r = subprocess.run(cmd, capture_output=True, text=True, timeout=600, env=env)
     assert r.stdout, r.stderr
     res = json.loads(r.stdout.strip().splitlines()[-1])
     return r.returncode, res
@@ -62,25 +63,31 @@ CASES = [
     ("short", "alpha", 1 << 20, 0, 0),
     ("short", "alpha", 1 << 20, 1024, 256),
     ("root", "alpha", 4096, 0, 0),
+    ("lit", "lit", 1 << 20, 0, 0),
+    ("lit", "lit", 1 << 20, 4096, 512),
+    ("lit", "lit", 8 << 20, 65536, 100),
 ]
 
 
 @needs_check
+@pytest.mark.parametrize("preverify", [True, False], ids=["preverify", "full-replay"])
 @pytest.mark.parametrize("rules,kind,size,block,overlap", CASES)
-def test_match_set_equals_stock_libyara(tmp_path, rules, kind, size, block, overlap):
+def test_match_set_equals_stock_libyara(tmp_path, rules, kind, size, block, overlap, preverify):
     rf = _rules_file(tmp_path, rules)
     if kind == "xs":
         spec = "xs:1:%d" % size
+    elif kind == "lit":
+        spec = _data_file(tmp_path, planted.lit_buffer(oracle.xorshift, size, 13), "d.bin")
     elif kind == "planted":
         spec = _data_file(tmp_path, planted.planted_buffer(oracle.xorshift, gen_rules.gen(rules),
                                                            size, 3), "d.bin")
     else:
         x = oracle.xorshift(size, 5)
         spec = _data_file(tmp_path, np.frombuffer(ALPHA, np.uint8)[x % len(ALPHA)], "d.bin")
-    rc, res = _run(rf, spec, block, overlap)
+    rc, res = _run(rf, spec, block, overlap, preverify)
     assert res["rc_stock"] == 0 and res["rc_gpu"] == 0, res
     assert res["same_matches"] and res["same_rule_reports"], res
     assert res["finished"] == [1, 1], res
-    if kind == "planted":
+    if kind in ("planted", "lit"):
         assert res["matches_stock"] > 0 and res["rules_matching"] > 0, res
     assert rc == 0

@@ -1,0 +1,127 @@
+"""On-device literal pre-verification.
+
+The GPU emits, in the reference's call order, only the yr_scan_verify_match
+calls that can have an effect (scan.c:887-990, :1013, :1023).  Parity:
+  * CPU: the oracle's keep-mask (oracle_literal_effect, a restatement of the
+    scan.c comparisons) never drops a call that produced one of the matches the
+    stock libyara reported (golden match sets) -- it is pinned to the reference
+    through its final output;
+  * GPU: the device records equal the golden verify-call stream filtered by the
+    oracle's mask, bit-exact (offset, pool index), for every golden case,
+    single- and multi-block (fixed-offset strings see the block base);
+  * the end-to-end match sets through the libyara shim with pre-verification
+    on are identical to stock libyara (tests/test_e2e_libyara.py).
+"""
+import numpy as np
+import pytest
+
+import oracle
+from conftest import case_arrays, case_data, golden, tables_npz
+
+CASES = golden()["cases"]
+FULL = [k for k in CASES if case_arrays(k) is not None]
+SF_LITERAL = 0x400
+
+
+def _expected(rec, arr, data):
+    """Golden verify stream -> (keep mask, offsets, pool idx, bases)."""
+    z = np.load(tables_npz(rec["rules"]))
+    pos, idx = arr["verify_pos"], arr["verify_idx"]
+    base = arr["verify_base"]
+    bt = z["pool_backtrack"]
+    keep = np.zeros(len(pos), bool)
+    if rec["block"]:
+        for b in np.unique(base):
+            sel = base == b
+            blk = data[int(b):int(b) + rec["block"]]
+            keep[sel] = oracle.literal_effect(z, pos[sel], idx[sel], blk, base=int(b))
+    else:
+        keep = oracle.literal_effect(z, pos, idx, data)
+    off = pos.astype(np.uint64) - bt[idx].astype(np.uint64)
+    return z, keep, off, idx, base
+
+
+@pytest.mark.parametrize("case", FULL)
+def test_oracle_keeps_every_reported_match(case):
+    rec = CASES[case]
+    arr = case_arrays(case)
+    data = case_data(rec)
+    z, keep, off, idx, base = _expected(rec, arr, data)
+    ps = z["pool_string"]
+    kept = set(zip((base[keep] + off[keep]).tolist(), ps[idx[keep]].tolist()))
+    flags = z["str_flags"]
+    for s, o in zip(arr["match_string"].tolist(), arr["match_offset"].tolist()):
+        if flags[s] & SF_LITERAL:
+            assert (o, s) in kept, (case, s, o)
+    # the filter is not a no-op where literal near misses exist
+    if case.startswith("lit"):
+        assert keep.sum() < len(keep)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("case", FULL)
+def test_device_records_equal_oracle_filtered_reference_stream(case):
+    import yara_amd
+    rec = CASES[case]
+    arr = case_arrays(case)
+    data = case_data(rec)
+    z, keep, off, idx, base = _expected(rec, arr, data)
+    tab = yara_amd.Tables.from_npz(tables_npz(rec["rules"]), device=0, strings=True)
+    sc = yara_amd.Scanner(tab)
+    if rec["block"]:
+        from test_gpu_parity import blocks
+        got_off, got_idx, got_base = [], [], []
+        for b, n in blocks(rec["size"], rec["block"], rec["overlap"]):
+            r = sc.verify_calls(data[b:b + n], data_base=b)
+            got_off.append(r["offset"])
+            got_idx.append(r["pool_index"])
+            got_base.append(np.full(len(r), b, np.uint64))
+        g_off, g_idx = np.concatenate(got_off), np.concatenate(got_idx)
+        g_base = np.concatenate(got_base)
+        assert np.array_equal(g_base, base[keep])
+    else:
+        r = sc.verify_calls(data)
+        g_off, g_idx = r["offset"], r["pool_index"]
+    assert len(g_off) == int(keep.sum()), (case, len(g_off), int(keep.sum()))
+    assert np.array_equal(g_off, off[keep])
+    assert np.array_equal(g_idx, idx[keep])
+
+
+@pytest.mark.gpu
+def test_device_verify_after_sharded_device_scan():
+    """yr_amd_verify_device on a device-resident block scanned in two shards
+    equals the whole-block host path."""
+    import torch
+    import yara_amd
+    from yara_amd._hip import memcpy
+    rec = CASES["lit_1M"]
+    data = case_data(rec)
+    tab = yara_amd.Tables.from_npz(tables_npz("lit"), device=0, strings=True)
+    sc = yara_amd.Scanner(tab)
+    want = sc.verify_calls(data)
+    d = torch.from_numpy(data.copy()).cuda()
+    half = (len(data) // 2) & ~15
+    got = []
+    for lo, hi in ((0, half), (half, len(data))):
+        sc.scan_device(d.data_ptr(), len(data), lo, hi)
+        sc.device_result()
+        p, n = sc.verify_device(0)
+        out = np.zeros(n, dtype=yara_amd._lib.VERIFY_REC_DTYPE)
+        if n:
+            h = torch.empty(n * 16, dtype=torch.uint8, device="cuda")
+            memcpy(h.data_ptr(), p, n * 16, 3)
+            out = np.frombuffer(h.cpu().numpy().tobytes(), dtype=yara_amd._lib.VERIFY_REC_DTYPE)
+        got.append(out)
+    g = np.concatenate(got)
+    assert np.array_equal(g["offset"], want["offset"])
+    assert np.array_equal(g["pool_index"], want["pool_index"])
+
+
+@pytest.mark.gpu
+def test_preverify_requires_strings():
+    import yara_amd
+    tab = yara_amd.Tables.from_npz(tables_npz("lit"), device=0)
+    sc = yara_amd.Scanner(tab)
+    with pytest.raises(yara_amd.YaraAmdError) as e:
+        sc.verify_calls(np.zeros(16, np.uint8))
+    assert e.value.code == yara_amd.INVALID_ARGUMENT

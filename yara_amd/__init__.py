@@ -62,11 +62,39 @@ class Tables:
         self.device = device
 
     @classmethod
-    def from_npz(cls, path, device: int = 0):
+    def from_npz(cls, path, device: int = 0, strings: bool = False):
+        """Tables from a tests/golden/tables/*.npz dump; ``strings=True`` also
+        attaches the YR_STRING records (needed by Scanner.verify_calls)."""
         z = np.load(path)
         t = cls(z["T"], z["M"], z["pool_next"], z["pool_backtrack"], device=device)
         t.pool_string = z["pool_string"] if "pool_string" in z else None
+        if strings:
+            offs = z["str_offsets"]
+            t.set_strings(z["pool_string"], z["str_flags"], np.diff(offs), z["str_fixed_offset"],
+                          z["str_bytes"], offs[:-1])
         return t
+
+    def set_strings(self, pool_string, flags, lengths, fixed_offsets, blob, bytes_offsets,
+                    lowercase=None):
+        """Attach YR_STRING records (yr_amd_tables_set_strings).  ``lowercase``
+        defaults to C-locale tolower, i.e. libyara's yr_lowercase (libyara.c:258)."""
+        n = len(flags)
+        recs = (_lib.String * max(n, 1))()
+        for k in range(n):
+            recs[k].flags = int(flags[k])
+            recs[k].length = int(lengths[k])
+            recs[k].fixed_offset = int(fixed_offsets[k])
+            recs[k].bytes_offset = int(bytes_offsets[k])
+        if lowercase is None:
+            lowercase = np.arange(256, dtype=np.uint8)
+            lowercase[ord("A"):ord("Z") + 1] += 32
+        self._ps = _arr(pool_string, np.uint32)
+        self._blob = _arr(blob, np.uint8) if len(blob) else np.zeros(1, np.uint8)
+        self._lower = _arr(lowercase, np.uint8)
+        ps = self._ps if self._ps.size else np.zeros(1, np.uint32)
+        _lib.check("yr_amd_tables_set_strings", _lib.lib().yr_amd_tables_set_strings(
+            self._h, ps.ctypes.data_as(_lib._u32p), self._ps.size, recs, n,
+            self._blob.ctypes.data_as(_lib._u8p), len(blob), self._lower.ctypes.data_as(_lib._u8p)))
 
     @property
     def handle(self):
@@ -167,6 +195,33 @@ class Scanner:
         rc = self.scan_mem_block(data, cb)
         _lib.check("scan_mem_block", rc)
         return np.array(P, dtype=np.uint64), np.array(K, dtype=np.uint32)
+
+    def verify_calls(self, data: np.ndarray, data_base: int = 0):
+        """On-device pre-verification (yr_amd_scan_block_verified): the verify
+        calls of the block that can have an effect, in the reference's order,
+        as a structured array {offset, pool_index, candidate}."""
+        d = _arr(data, np.uint8)
+        ptr = ctypes.POINTER(_lib.VerifyRec)()
+        cnt = ctypes.c_uint64()
+        dp = d.ctypes.data_as(_lib._u8p) if d.size else None
+        _lib.check("yr_amd_scan_block_verified",
+                   _lib.lib().yr_amd_scan_block_verified(self._h, dp, d.size, data_base,
+                                                         ctypes.byref(ptr), ctypes.byref(cnt)))
+        n = cnt.value
+        out = np.zeros(n, dtype=_lib.VERIFY_REC_DTYPE)
+        if n:
+            ctypes.memmove(out.ctypes.data, ptr, n * 16)
+        return out
+
+    def verify_device(self, data_base: int = 0):
+        """(device pointer to yr_amd_verify_rec[], count) for the last
+        completed device scan (yr_amd_verify_device)."""
+        p = ctypes.c_void_p()
+        cnt = ctypes.c_uint64()
+        _lib.check("yr_amd_verify_device",
+                   _lib.lib().yr_amd_verify_device(self._h, data_base, ctypes.byref(p),
+                                                   ctypes.byref(cnt)))
+        return p.value or 0, cnt.value
 
     # -- device-resident block (benchmark path) -------------------------------
     def scan_device(self, d_ptr: int, block_size: int, byte_begin: int = 0, byte_end=None):

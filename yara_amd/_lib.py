@@ -44,6 +44,20 @@ class TablesInfo(ctypes.Structure):
     ]
 
 
+class String(ctypes.Structure):
+    """yr_amd_string (include/yara_amd.h)."""
+    _fields_ = [("flags", ctypes.c_uint32), ("length", ctypes.c_uint32),
+                ("fixed_offset", ctypes.c_int64), ("bytes_offset", ctypes.c_uint64)]
+
+
+class VerifyRec(ctypes.Structure):
+    """yr_amd_verify_rec (include/yara_amd.h)."""
+    _fields_ = [("offset", ctypes.c_uint64), ("pool_index", ctypes.c_uint32),
+                ("candidate", ctypes.c_uint32)]
+
+
+VERIFY_REC_DTYPE = [("offset", "<u8"), ("pool_index", "<u4"), ("candidate", "<u4")]
+
 # name -> (restype, argtypes); every function include/yara_amd.h declares
 PROTOTYPES = {
     "yr_amd_tables_create": (_int, [_u32p, _u32p, ctypes.c_uint32, _u32p, _u16p, ctypes.c_uint32,
@@ -63,6 +77,13 @@ PROTOTYPES = {
     "yr_amd_scanner_set_timing": (_int, [_vp, _int]),
     "yr_amd_scanner_kernel_ms": (_int, [_vp, ctypes.POINTER(ctypes.c_float)]),
     "yr_amd_version": (ctypes.c_char_p, []),
+    "yr_amd_tables_set_strings": (_int, [_vp, _u32p, ctypes.c_uint32, ctypes.POINTER(String),
+                                         ctypes.c_uint32, _u8p, ctypes.c_uint64, _u8p]),
+    "yr_amd_verify_device": (_int, [_vp, ctypes.c_uint64, ctypes.POINTER(_vp),
+                                    ctypes.POINTER(ctypes.c_uint64)]),
+    "yr_amd_scan_block_verified": (_int, [_vp, _u8p, ctypes.c_size_t, ctypes.c_uint64,
+                                          ctypes.POINTER(ctypes.POINTER(VerifyRec)),
+                                          ctypes.POINTER(ctypes.c_uint64)]),
 }
 
 _lib = None

@@ -16,6 +16,7 @@
 #include "../../include/yara_amd.h"
 #include "internal.h"
 #include "tables.h"
+#include "verify.h"
 
 namespace yamd {
 hipError_t launch_scan(const ScanParams& p, int grid, hipStream_t s, int mode);
@@ -34,6 +35,17 @@ struct yr_amd_tables {
   uint32_t* d_filter = nullptr;
   uint32_t* d_exact = nullptr;
   int num_cus = 256;
+
+  // on-device literal pre-verification (yr_amd_tables_set_strings)
+  bool has_strings = false;
+  uint32_t* d_T = nullptr;
+  uint32_t* d_M = nullptr;
+  uint32_t* d_pool_next = nullptr;
+  uint16_t* d_pool_backtrack = nullptr;
+  uint32_t* d_pool_string = nullptr;
+  DevString* d_strings = nullptr;
+  uint8_t* d_str_bytes = nullptr;
+  uint8_t* d_lowercase = nullptr;
 };
 
 struct yr_amd_scanner {
@@ -69,7 +81,20 @@ struct yr_amd_scanner {
   bool ev_valid = false;
 
   int diag_mode = 0;   // profiling ablation of the scan kernel (0 = product)
+
+  // pre-verification workspace
+  uint32_t* d_vcount = nullptr;
+  size_t vcount_cap = 0;
+  uint64_t* d_voffset = nullptr;
+  size_t voffset_cap = 0;
+  uint64_t* d_vchunk = nullptr;
+  size_t vchunk_cap = 0;
+  VerifyRec* d_vrec = nullptr;
+  size_t vrec_cap = 0;
+  std::vector<yr_amd_verify_rec> h_vrec;
 };
+
+static_assert(sizeof(VerifyRec) == sizeof(yr_amd_verify_rec), "record layout");
 
 #define HIP_TRY(expr)                                   \
   do {                                                  \
@@ -174,8 +199,10 @@ int yr_amd_tables_create(const uint32_t* transition_table, const uint32_t* match
 
 int yr_amd_tables_destroy(yr_amd_tables* t) {
   if (t == nullptr) return YR_AMD_SUCCESS;
-  if (t->d_filter) (void)hipFree(t->d_filter);
-  if (t->d_exact) (void)hipFree(t->d_exact);
+  for (void* p : {(void*)t->d_filter, (void*)t->d_exact, (void*)t->d_T, (void*)t->d_M,
+                  (void*)t->d_pool_next, (void*)t->d_pool_backtrack, (void*)t->d_pool_string,
+                  (void*)t->d_strings, (void*)t->d_str_bytes, (void*)t->d_lowercase})
+    if (p) (void)hipFree(p);
   delete t;
   return YR_AMD_SUCCESS;
 }
@@ -232,7 +259,8 @@ int yr_amd_scanner_destroy(yr_amd_scanner* s) {
   if (s == nullptr) return YR_AMD_SUCCESS;
   if (s->stream) (void)hipStreamSynchronize(s->stream);
   for (void* p : {(void*)s->d_block, (void*)s->d_seg_count, (void*)s->d_seg_offset,
-                  (void*)s->d_seg_out, (void*)s->d_positions, (void*)s->d_summary})
+                  (void*)s->d_seg_out, (void*)s->d_positions, (void*)s->d_summary,
+                  (void*)s->d_vcount, (void*)s->d_voffset, (void*)s->d_vchunk, (void*)s->d_vrec})
     if (p) (void)hipFree(p);
   if (s->h_summary) (void)hipHostFree(s->h_summary);
   if (s->ev_begin) (void)hipEventDestroy(s->ev_begin);
@@ -277,6 +305,10 @@ int yr_amd_scan_device(yr_amd_scanner* s, const uint8_t* d_data, uint64_t block_
   s->pending = true;
   s->last_count = 0;
   s->ev_valid = false;
+  s->last.data = d_data;
+  s->last.block_size = block_size;
+  s->last.byte_begin = byte_begin;
+  s->last.byte_end = byte_end;
   s->last_all = t->flat.root_accepting;
   s->last_empty = s->last_all || byte_end == byte_begin;
   if (s->last_empty) return YR_AMD_SUCCESS;
@@ -380,6 +412,141 @@ int yr_amd_scan_block(yr_amd_scanner* s, const uint8_t* data, size_t size,
   if (positions) *positions = s->h_positions.data();
   if (count) *count = n;
   if (all_positions) *all_positions = all;
+  return YR_AMD_SUCCESS;
+}
+
+extern "C++" {
+namespace {
+template <typename T>
+int upload(T*& d, const T* h, size_t n) {
+  if (hipMalloc((void**)&d, std::max<size_t>(n, 1) * sizeof(T)) != hipSuccess) {
+    d = nullptr;
+    return YR_AMD_INSUFFICIENT_MEMORY;
+  }
+  if (n > 0 && hipMemcpy(d, h, n * sizeof(T), hipMemcpyHostToDevice) != hipSuccess)
+    return YR_AMD_INTERNAL_FATAL_ERROR;
+  return YR_AMD_SUCCESS;
+}
+}  // namespace
+}  // extern "C++"
+
+int yr_amd_tables_set_strings(yr_amd_tables* t, const uint32_t* pool_string, uint32_t n_pool,
+                              const yr_amd_string* strings, uint32_t n_strings,
+                              const uint8_t* bytes, uint64_t n_bytes, const uint8_t* lowercase) {
+  if (t == nullptr || lowercase == nullptr || t->has_strings) return YR_AMD_INVALID_ARGUMENT;
+  if (n_pool != t->flat.pool_next.size()) return YR_AMD_INVALID_ARGUMENT;
+  if ((n_pool > 0 && pool_string == nullptr) || (n_strings > 0 && strings == nullptr) ||
+      (n_bytes > 0 && bytes == nullptr))
+    return YR_AMD_INVALID_ARGUMENT;
+  for (uint32_t k = 0; k < n_pool; ++k)
+    if (pool_string[k] >= n_strings) return YR_AMD_INVALID_ARGUMENT;
+  std::vector<DevString> ds(n_strings);
+  for (uint32_t k = 0; k < n_strings; ++k) {
+    const yr_amd_string& x = strings[k];
+    if (x.bytes_offset > n_bytes || x.length > n_bytes - x.bytes_offset)
+      return YR_AMD_INVALID_ARGUMENT;
+    ds[k] = DevString{x.flags, x.length, x.fixed_offset, x.bytes_offset};
+  }
+  if (t->device < 0) return YR_AMD_INVALID_ARGUMENT;   // device feature
+  HIP_TRY(hipSetDevice(t->device));
+  const FlatTables& f = t->flat;
+  int r = YR_AMD_SUCCESS;
+  if (!r) r = upload(t->d_T, f.T.data(), f.T.size());
+  if (!r) r = upload(t->d_M, f.M.data(), f.M.size());
+  if (!r) r = upload(t->d_pool_next, f.pool_next.data(), f.pool_next.size());
+  if (!r) r = upload(t->d_pool_backtrack, f.pool_backtrack.data(), f.pool_backtrack.size());
+  if (!r) r = upload(t->d_pool_string, pool_string, n_pool);
+  if (!r) r = upload(t->d_strings, ds.data(), ds.size());
+  if (!r) r = upload(t->d_str_bytes, bytes, n_bytes);
+  if (!r) r = upload(t->d_lowercase, lowercase, 256);
+  if (r) return r;   // partial uploads are freed with the tables
+  t->has_strings = true;
+  return YR_AMD_SUCCESS;
+}
+
+int yr_amd_verify_device(yr_amd_scanner* s, uint64_t data_base, const yr_amd_verify_rec** d_records,
+                         uint64_t* count) {
+  if (s == nullptr || s->pending || !s->tables->has_strings) return YR_AMD_INVALID_ARGUMENT;
+  const yr_amd_tables* t = s->tables;
+  const ScanParams& L = s->last;
+  HIP_TRY(hipSetDevice(t->device));
+  VerifyParams v{};
+  v.data = L.data;
+  v.size = L.block_size;
+  v.data_base = data_base;
+  v.all = s->last_all ? 1 : 0;
+  if (v.all) {
+    // every position of the scanned range: (byte_begin, byte_end], plus 0
+    v.all_first = L.byte_begin == 0 ? 0 : L.byte_begin + 1;
+    v.count = L.byte_end + 1 - v.all_first;
+    if (L.byte_begin == L.byte_end && L.byte_begin != 0) v.count = 0;
+  } else {
+    v.positions = s->d_positions;
+    v.count = s->last_count;
+  }
+  v.T = t->d_T;
+  v.M = t->d_M;
+  v.pool_next = t->d_pool_next;
+  v.pool_backtrack = t->d_pool_backtrack;
+  v.pool_string = t->d_pool_string;
+  v.strings = t->d_strings;
+  v.str_bytes = t->d_str_bytes;
+  v.lowercase = t->d_lowercase;
+  uint64_t total = 0;
+  if (v.count > 0) {
+    if (v.data == nullptr) return YR_AMD_INVALID_ARGUMENT;
+    int r = grow(s->d_vcount, s->vcount_cap, v.count);
+    if (!r) r = grow(s->d_voffset, s->voffset_cap, v.count);
+    if (!r) r = grow(s->d_vchunk, s->vchunk_cap, exclusive_scan_chunks(v.count));
+    if (r) return r;
+    v.counts = s->d_vcount;
+    v.offsets = s->d_voffset;
+    HIP_TRY(launch_verify(v, 0, s->stream));
+    HIP_TRY(launch_exclusive_scan(s->d_vcount, v.count, s->d_vchunk, s->d_voffset, s->d_summary,
+                                  s->stream));
+    HIP_TRY(hipMemcpyAsync(s->h_summary, s->d_summary, sizeof(uint64_t), hipMemcpyDeviceToHost,
+                           s->stream));
+    HIP_TRY(hipStreamSynchronize(s->stream));
+    total = s->h_summary[0];
+    r = grow(s->d_vrec, s->vrec_cap, total);
+    if (r) return r;
+    if (total > 0) {
+      v.out = s->d_vrec;
+      HIP_TRY(launch_verify(v, 1, s->stream));
+      HIP_TRY(hipStreamSynchronize(s->stream));
+    }
+  }
+  if (d_records) *d_records = reinterpret_cast<const yr_amd_verify_rec*>(s->d_vrec);
+  if (count) *count = total;
+  return YR_AMD_SUCCESS;
+}
+
+int yr_amd_scan_block_verified(yr_amd_scanner* s, const uint8_t* data, size_t size,
+                               uint64_t data_base, const yr_amd_verify_rec** records,
+                               uint64_t* count) {
+  if (s == nullptr || (data == nullptr && size > 0)) return YR_AMD_INVALID_ARGUMENT;
+  if (!s->tables->has_strings) return YR_AMD_INVALID_ARGUMENT;
+  HIP_TRY(hipSetDevice(s->tables->device));
+  if (size > 0) {
+    int r = grow(s->d_block, s->d_block_cap, size);
+    if (r) return r;
+    if (hipMemcpyAsync(s->d_block, data, size, hipMemcpyHostToDevice, s->stream) != hipSuccess)
+      return YR_AMD_COULD_NOT_MAP_FILE;
+  }
+  int r = yr_amd_scan_device(s, s->d_block, size, 0, size);
+  if (!r) r = yr_amd_scan_device_result(s, nullptr, nullptr, nullptr);
+  const yr_amd_verify_rec* d_rec = nullptr;
+  uint64_t n = 0;
+  if (!r) r = yr_amd_verify_device(s, data_base, &d_rec, &n);
+  if (r) return r;
+  s->h_vrec.resize(n);
+  if (n > 0) {
+    HIP_TRY(hipMemcpyAsync(s->h_vrec.data(), d_rec, n * sizeof(yr_amd_verify_rec),
+                           hipMemcpyDeviceToHost, s->stream));
+    HIP_TRY(hipStreamSynchronize(s->stream));
+  }
+  if (records) *records = s->h_vrec.data();
+  if (count) *count = n;
   return YR_AMD_SUCCESS;
 }
 

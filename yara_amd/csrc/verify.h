@@ -1,0 +1,61 @@
+// Device data of the on-device literal pre-verification (verify.hip).
+#pragma once
+
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+namespace yamd {
+
+// YR_STRING.flags bits (libyara/include/yara/types.h:66-88).
+constexpr uint32_t kStrNoCase = 0x04;
+constexpr uint32_t kStrAscii = 0x08;
+constexpr uint32_t kStrWide = 0x10;
+constexpr uint32_t kStrLiteral = 0x400;
+constexpr uint32_t kStrFitsInAtom = 0x800;
+constexpr uint32_t kStrFixedOffset = 0x8000;
+constexpr uint32_t kStrXor = 0x80000;
+// literal flags whose comparison is not restated on the device: such calls
+// are always handed to the host (base64 / base64wide)
+constexpr uint32_t kStrUnmodelled = 0x200000 | 0x400000;
+
+struct DevString {
+  uint32_t flags;
+  uint32_t length;
+  int64_t fixed_offset;
+  uint64_t bytes_off;   // into the string byte blob
+};
+
+// Same layout as yr_amd_verify_rec (include/yara_amd.h).
+struct VerifyRec {
+  uint64_t offset;
+  uint32_t pool_index;
+  uint32_t candidate;
+};
+
+struct VerifyParams {
+  const uint8_t* data;        // block in HBM
+  uint64_t size;              // block size
+  uint64_t data_base;         // YR_MEMORY_BLOCK.base (fixed-offset strings)
+  const uint64_t* positions;  // ascending candidates (unused when all)
+  uint64_t count;             // candidates (size + 1 when all)
+  int all;                    // every position of a range is a candidate:
+  uint64_t all_first;         //   i = all_first + c
+  const uint32_t* T;          // ac_transition_table
+  const uint32_t* M;          // ac_match_table
+  const uint32_t* pool_next;  // 1-based, 0 = end
+  const uint16_t* pool_backtrack;
+  const uint32_t* pool_string;
+  const DevString* strings;
+  const uint8_t* str_bytes;
+  const uint8_t* lowercase;   // the host's yr_lowercase[256]
+  uint32_t* counts;           // [count] records per candidate (pass 0)
+  const uint64_t* offsets;    // [count] exclusive scan of counts (pass 1)
+  VerifyRec* out;             // records (pass 1)
+};
+
+hipError_t launch_verify(const VerifyParams& p, int pass, hipStream_t s);
+hipError_t launch_exclusive_scan(const uint32_t* counts, uint64_t n, uint64_t* chunk_sum,
+                                 uint64_t* offsets, uint64_t* total, hipStream_t s);
+uint64_t exclusive_scan_chunks(uint64_t n);
+
+}  // namespace yamd

@@ -1,0 +1,242 @@
+// gfx950 kernels of the on-device literal pre-verification.
+//
+// Input: the candidate stream of a block scan (ascending positions i with
+// ac_match_table[state_i] != 0).  For every candidate the reference loop
+// (libyara/scanner.c:98-122, :144-163) calls
+//     yr_scan_verify_match(ctx, m, data, size, base, i - m->backtrack)
+// for each entry m of state_i's match list with backtrack <= i.  For a literal
+// string (STRING_FLAGS_LITERAL) that call is a pure function of the bytes
+// until the comparison succeeds: yr_scan_verify_match (scan.c:992-1089) only
+// returns early, and _yr_scan_verify_literal_match (scan.c:887-990) returns
+// ERROR_SUCCESS without touching the scan context when forward_matches == 0.
+// These kernels evaluate exactly that comparison on the GPU and emit the
+// calls that can have an effect -- every call on a non-literal string (regex /
+// hex with jumps: decided on the host by re.c), and every literal call whose
+// comparison succeeds -- as {offset, pool index} records in the reference's
+// call order.  The host replays the records into the unmodified
+// yr_scan_verify_match, so the final match set is unchanged while the host no
+// longer walks lists or compares bytes for the (vast majority of) candidates
+// that are atom hits only.
+//
+// Work per candidate (one lane each): recompute state_i by the reference
+// transition rule from max(0, i - 4) (the trie is at most 4 deep, limits.h:68),
+// walk the pool list, compare.  Candidates are ~0.015% of positions (config
+// C): this is latency-bound pointer chasing in L2, microseconds per block, so
+// the kernels are simple two-pass (count, exclusive scan, write).
+#include "internal.h"
+#include "verify.h"
+
+namespace yamd {
+
+// libyara/scanner.c:124-141 (the transition rule; T resident in L2).
+__device__ __forceinline__ uint32_t dev_ac_step(const uint32_t* __restrict__ T, uint32_t state,
+                                                uint32_t byte) {
+  const uint32_t index = byte + 1;
+  uint32_t t = T[state + index];
+  while ((t & 0x1FFu) != index) {
+    if (state == 0) return 0;
+    state = T[state] >> 9;
+    t = T[state + index];
+  }
+  return t >> 9;
+}
+
+// _yr_scan_compare / _yr_scan_icompare (scan.c:142-179): forward match length
+// of the ascii form, 0 if none.
+__device__ bool cmp_ascii(const uint8_t* d, uint64_t avail, const uint8_t* s, uint32_t n,
+                          const uint8_t* lower) {
+  if (avail < n) return false;
+  if (lower == nullptr) {
+    for (uint32_t i = 0; i < n; ++i)
+      if (d[i] != s[i]) return false;
+  } else {
+    for (uint32_t i = 0; i < n; ++i)
+      if (lower[d[i]] != lower[s[i]]) return false;
+  }
+  return true;
+}
+
+// _yr_scan_wcompare / _yr_scan_wicompare (scan.c:181-255): the wide form
+// (every character followed by 0x00).
+__device__ bool cmp_wide(const uint8_t* d, uint64_t avail, const uint8_t* s, uint32_t n,
+                         const uint8_t* lower) {
+  if (avail < 2ull * n) return false;
+  for (uint32_t i = 0; i < n; ++i) {
+    const uint8_t a = d[2 * i], b = s[i];
+    if ((lower == nullptr ? a != b : lower[a] != lower[b]) || d[2 * i + 1] != 0) return false;
+  }
+  return true;
+}
+
+// _yr_scan_xor_compare (scan.c:62-101) and _yr_scan_xor_wcompare (:103-140):
+// key k = data[0] ^ string[0], then every byte (and, wide, every 0x00 ^ k).
+__device__ bool cmp_xor(const uint8_t* d, uint64_t avail, const uint8_t* s, uint32_t n, bool wide) {
+  if (avail < (wide ? 2ull * n : (uint64_t)n)) return false;
+  if (n == 0) return false;   // both reference loops yield 0 for an empty string
+  const uint8_t k = d[0] ^ s[0];
+  for (uint32_t i = 0; i < n; ++i) {
+    if (wide) {
+      if (d[2 * i] != (uint8_t)(s[i] ^ k) || (uint8_t)(d[2 * i + 1] ^ k) != 0) return false;
+    } else if (d[i] != (uint8_t)(s[i] ^ k)) {
+      return false;
+    }
+  }
+  return true;
+}
+
+// Does yr_scan_verify_match(ctx, &pool[k], data, size, base, offset) possibly
+// have an effect?  false only where the reference provably returns without
+// touching the context.
+__device__ bool call_matters(const VerifyParams& p, uint32_t k, uint64_t offset) {
+  // scan.c:1013: data_size - offset <= 0 (size_t) <=> offset == size
+  if (offset >= p.size) return false;
+  const DevString st = p.strings[p.pool_string[k]];
+  // scan.c:1023-1025
+  if ((st.flags & kStrFixedOffset) && st.fixed_offset != (int64_t)(p.data_base + offset))
+    return false;
+  if (!(st.flags & kStrLiteral)) return true;            // re.c verification on the host
+  if (st.flags & kStrUnmodelled) return true;            // conservative
+  // _yr_scan_verify_literal_match, scan.c:907-972
+  if (st.flags & kStrFitsInAtom) return p.pool_backtrack[k] != 0;
+  const uint8_t* d = p.data + offset;
+  const uint64_t avail = p.size - offset;
+  const uint8_t* s = p.str_bytes + st.bytes_off;
+  const uint32_t n = st.length;
+  if (st.flags & kStrNoCase) {
+    if ((st.flags & kStrAscii) && cmp_ascii(d, avail, s, n, p.lowercase)) return n != 0;
+    if ((st.flags & kStrWide) && cmp_wide(d, avail, s, n, p.lowercase)) return n != 0;
+    return false;
+  }
+  if ((st.flags & kStrAscii) && cmp_ascii(d, avail, s, n, nullptr)) return n != 0;
+  if ((st.flags & kStrWide) && cmp_wide(d, avail, s, n, nullptr)) return n != 0;
+  if (st.flags & kStrXor) {
+    if ((st.flags & kStrWide) && cmp_xor(d, avail, s, n, true)) return true;
+    if (cmp_xor(d, avail, s, n, false)) return true;
+  }
+  return false;
+}
+
+// PASS 0: count the records of each candidate; PASS 1: write them.
+template <int PASS>
+__global__ __launch_bounds__(256) void verify_kernel(VerifyParams p) {
+  const uint64_t c = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (c >= p.count) return;
+  const uint64_t i = p.all ? p.all_first + c : p.positions[c];
+  uint32_t state = 0;
+  for (uint64_t j = i > 4 ? i - 4 : 0; j < i; ++j) state = dev_ac_step(p.T, state, p.data[j]);
+  uint32_t n = 0;
+  uint64_t o = PASS ? p.offsets[c] : 0;
+  // scanner.c:105-121: the list of state_i in pool order
+  for (uint32_t k = p.M[state]; k != 0; k = p.pool_next[k - 1]) {
+    const uint32_t bt = p.pool_backtrack[k - 1];
+    if (bt > i) continue;
+    if (!call_matters(p, k - 1, i - bt)) continue;
+    if (PASS) {
+      VerifyRec r;
+      r.offset = i - bt;
+      r.pool_index = k - 1;
+      r.candidate = (uint32_t)c;
+      p.out[o++] = r;
+    }
+    ++n;
+  }
+  if (!PASS) p.counts[c] = n;
+}
+
+// Exclusive scan of n uint32 counts into uint64 offsets, three launches:
+// per-chunk sums, one-workgroup scan of the chunk sums (+ total), chunk scans.
+constexpr uint32_t kScanChunk = 4096;   // 256 threads x 16
+
+__global__ __launch_bounds__(256) void chunk_sum_kernel(const uint32_t* counts, uint64_t n,
+                                                        uint64_t* chunk_sum) {
+  __shared__ uint64_t red[256];
+  const uint64_t base = (uint64_t)blockIdx.x * kScanChunk;
+  uint64_t s = 0;
+  for (uint32_t j = threadIdx.x; j < kScanChunk; j += 256)
+    if (base + j < n) s += counts[base + j];
+  red[threadIdx.x] = s;
+  __syncthreads();
+  for (uint32_t d = 128; d > 0; d >>= 1) {
+    if (threadIdx.x < d) red[threadIdx.x] += red[threadIdx.x + d];
+    __syncthreads();
+  }
+  if (threadIdx.x == 0) chunk_sum[blockIdx.x] = red[0];
+}
+
+__global__ __launch_bounds__(1024) void chunk_offsets_kernel(uint64_t* chunk_sum, uint64_t n_chunks,
+                                                             uint64_t* total) {
+  __shared__ uint64_t part[1024];
+  const uint32_t t = threadIdx.x;
+  const uint64_t per = (n_chunks + 1023) / 1024;
+  const uint64_t lo = min(t * per, n_chunks), hi = min(lo + per, n_chunks);
+  uint64_t s = 0;
+  for (uint64_t i = lo; i < hi; ++i) s += chunk_sum[i];
+  part[t] = s;
+  __syncthreads();
+  for (uint32_t d = 1; d < 1024; d <<= 1) {
+    const uint64_t v = t >= d ? part[t - d] : 0;
+    __syncthreads();
+    part[t] += v;
+    __syncthreads();
+  }
+  uint64_t run = part[t] - s;
+  for (uint64_t i = lo; i < hi; ++i) {
+    const uint64_t c = chunk_sum[i];
+    chunk_sum[i] = run;
+    run += c;
+  }
+  if (t == 1023) *total = part[1023];
+}
+
+__global__ __launch_bounds__(256) void chunk_scan_kernel(const uint32_t* counts, uint64_t n,
+                                                         const uint64_t* chunk_off,
+                                                         uint64_t* offsets) {
+  __shared__ uint64_t part[256];
+  const uint64_t base = (uint64_t)blockIdx.x * kScanChunk + (uint64_t)threadIdx.x * 16;
+  uint32_t v[16];
+  uint64_t s = 0;
+#pragma unroll
+  for (int j = 0; j < 16; ++j) {
+    v[j] = base + j < n ? counts[base + j] : 0u;
+    s += v[j];
+  }
+  part[threadIdx.x] = s;
+  __syncthreads();
+  for (uint32_t d = 1; d < 256; d <<= 1) {
+    const uint64_t x = threadIdx.x >= d ? part[threadIdx.x - d] : 0;
+    __syncthreads();
+    part[threadIdx.x] += x;
+    __syncthreads();
+  }
+  uint64_t run = chunk_off[blockIdx.x] + part[threadIdx.x] - s;
+#pragma unroll
+  for (int j = 0; j < 16; ++j) {
+    if (base + j < n) offsets[base + j] = run;
+    run += v[j];
+  }
+}
+
+hipError_t launch_verify(const VerifyParams& p, int pass, hipStream_t s) {
+  if (p.count == 0) return hipSuccess;
+  const uint64_t blocks = (p.count + 255) / 256;
+  if (pass == 0)
+    hipLaunchKernelGGL(verify_kernel<0>, dim3((uint32_t)blocks), dim3(256), 0, s, p);
+  else
+    hipLaunchKernelGGL(verify_kernel<1>, dim3((uint32_t)blocks), dim3(256), 0, s, p);
+  return hipGetLastError();
+}
+
+hipError_t launch_exclusive_scan(const uint32_t* counts, uint64_t n, uint64_t* chunk_sum,
+                                 uint64_t* offsets, uint64_t* total, hipStream_t s) {
+  const uint64_t chunks = (n + kScanChunk - 1) / kScanChunk;
+  if (chunks == 0) return hipMemsetAsync(total, 0, sizeof(uint64_t), s);
+  hipLaunchKernelGGL(chunk_sum_kernel, dim3((uint32_t)chunks), dim3(256), 0, s, counts, n, chunk_sum);
+  hipLaunchKernelGGL(chunk_offsets_kernel, dim3(1), dim3(1024), 0, s, chunk_sum, chunks, total);
+  hipLaunchKernelGGL(chunk_scan_kernel, dim3((uint32_t)chunks), dim3(256), 0, s, counts, n, chunk_sum,
+                     offsets);
+  return hipGetLastError();
+}
+
+uint64_t exclusive_scan_chunks(uint64_t n) { return (n + kScanChunk - 1) / kScanChunk; }
+
+}  // namespace yamd
