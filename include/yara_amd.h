@@ -273,6 +273,56 @@ int yr_amd_scan_block_verified(
     uint64_t* count);
 
 /*
+ * ---- Block pipeline ----
+ *
+ * The block driver of libyara (yr_scanner_scan_mem_blocks, scanner.c:417-583;
+ * files via filemap.c, processes via proc/linux.c) scans one
+ * YR_MEMORY_BLOCK at a time.  A pipeline keeps up to `depth` blocks in flight
+ * (each: copy to a pinned buffer, H2D, scan, on-device pre-verification on
+ * its own HIP stream and worker thread) while the caller replays the oldest
+ * one, so end-to-end scans of many blocks overlap PCIe, GPU and host replay.
+ * Requires yr_amd_tables_set_strings.  One pipeline per YR_SCANNER.
+ */
+typedef struct yr_amd_pipeline yr_amd_pipeline;
+
+/* depth: blocks in flight, 1..8 (2 double-buffers). */
+int yr_amd_pipeline_create(yr_amd_tables* tables, uint32_t depth, yr_amd_pipeline** pipeline);
+
+/* Waits for the workers to finish, frees everything. */
+int yr_amd_pipeline_destroy(yr_amd_pipeline* pipeline);
+
+/*
+ * Copy a block (the caller's buffer may be reused on return; the copy runs in
+ * the calling thread, so a fault on an mmap'ed block surfaces in the caller,
+ * inside its YR_TRYCATCH) and start its GPU work.  At most `depth` blocks may
+ * be in flight: YR_AMD_INVALID_ARGUMENT otherwise (call yr_amd_pipeline_next).
+ * base = YR_MEMORY_BLOCK.base.
+ */
+int yr_amd_pipeline_submit(
+    yr_amd_pipeline* pipeline,
+    const uint8_t* data,
+    size_t size,
+    uint64_t base);
+
+/*
+ * Wait for the oldest submitted block.  Returns its scan status; on success
+ * *records / *count are its effective verify calls (yr_amd_scan_block_verified
+ * semantics) and *data / *size / *base its pipeline-owned bytes, all valid
+ * until the next yr_amd_pipeline_next / _drain / _destroy.  Blocks come back
+ * in submission order.
+ */
+int yr_amd_pipeline_next(
+    yr_amd_pipeline* pipeline,
+    const yr_amd_verify_rec** records,
+    uint64_t* count,
+    const uint8_t** data,
+    size_t* size,
+    uint64_t* base);
+
+/* Wait for and discard every block in flight (error paths). */
+int yr_amd_pipeline_drain(yr_amd_pipeline* pipeline);
+
+/*
  * Kernel timing (measurement support): when enabled, the scanner records HIP
  * events around its scan kernel on its own stream; yr_amd_scanner_kernel_ms
  * returns the duration of the last scan kernel launch (after the scan result

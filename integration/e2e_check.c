@@ -11,12 +11,19 @@
  *
  *   e2e_check <rules.yar> <data file | xs:SEED:SIZE> [block_size overlap]
  *   (E2E_PREVERIFY=0: GPU path without the on-device literal pre-verification)
+ *   E2E_MODE = mem (default) | file | fd | proc: the entry point compared --
+ *   yr_scanner_scan_mem[_blocks] / _scan_file / _scan_fd / _scan_proc against
+ *   the shim's twins (scanner.c:417-722).  proc scans a stopped child process
+ *   that holds the data (forked before any GPU initialisation).
  */
 #include <stdint.h>
 #include <stdio.h>
 #include <stdlib.h>
 #include <string.h>
+#include <signal.h>
+#include <sys/wait.h>
 #include <time.h>
+#include <unistd.h>
 #include <yara.h>
 
 #include "yr_gpu_scanner.h"
@@ -159,6 +166,10 @@ static double now(void)
   return t.tv_sec + 1e-9 * t.tv_nsec;
 }
 
+static const char* g_mode = "mem";
+static const char* g_path = NULL; /* file / fd modes */
+static int g_pid = 0;             /* proc mode */
+
 static int run(YR_RULES* rules, YR_GPU_SCANNER* gs, const uint8_t* data, size_t n,
                size_t bsize, size_t overlap, collect* c, double* secs)
 {
@@ -168,7 +179,21 @@ static int run(YR_RULES* rules, YR_GPU_SCANNER* gs, const uint8_t* data, size_t 
   yr_scanner_set_flags(sc, SCAN_FLAGS_REPORT_RULES_MATCHING | SCAN_FLAGS_REPORT_RULES_NOT_MATCHING);
   yr_scanner_set_callback(sc, cb, c);
   double t0 = now();
-  if (bsize == 0)
+  if (strcmp(g_mode, "file") == 0 && c->rules != NULL && data == NULL)
+  {
+    r = gs ? yr_gpu_scanner_scan_file(sc, gs, g_path) : yr_scanner_scan_file(sc, g_path);
+  }
+  else if (strcmp(g_mode, "fd") == 0 && data == NULL)
+  {
+    FILE* f = fopen(g_path, "rb");
+    r = gs ? yr_gpu_scanner_scan_fd(sc, gs, fileno(f)) : yr_scanner_scan_fd(sc, fileno(f));
+    fclose(f);
+  }
+  else if (strcmp(g_mode, "proc") == 0 && data == NULL)
+  {
+    r = gs ? yr_gpu_scanner_scan_proc(sc, gs, g_pid) : yr_scanner_scan_proc(sc, g_pid);
+  }
+  else if (bsize == 0)
   {
     r = gs ? yr_gpu_scanner_scan_mem(sc, gs, data, n) : yr_scanner_scan_mem(sc, data, n);
   }
@@ -209,6 +234,33 @@ int main(int argc, char** argv)
     fprintf(stderr, "cannot load data\n");
     return 2;
   }
+  if (getenv("E2E_MODE")) g_mode = getenv("E2E_MODE");
+  char tmpl[] = "/tmp/e2e_check_XXXXXX";
+  if (strcmp(g_mode, "file") == 0 || strcmp(g_mode, "fd") == 0)
+  {
+    int fd = mkstemp(tmpl);
+    if (fd < 0 || write(fd, data, n) != (ssize_t) n) return 2;
+    close(fd);
+    g_path = tmpl;
+  }
+  else if (strcmp(g_mode, "proc") == 0)
+  {
+    /* before any GPU initialisation: the child's address space holds the
+     * data and no device mappings */
+    g_pid = fork();
+    if (g_pid < 0) return 2;
+    if (g_pid == 0)
+    {
+      volatile uint8_t sink = 0;
+      for (size_t i = 0; i < n; i += 4096) sink ^= data[i]; /* keep it resident */
+      (void) sink;
+      raise(SIGSTOP);
+      _exit(0);
+    }
+    int st;
+    waitpid(g_pid, &st, WUNTRACED);
+  }
+  int scan_whole = strcmp(g_mode, "mem") != 0; /* entry points take no data pointer */
   YR_GPU_RULES* gr;
   YR_GPU_SCANNER* gs;
   int r = yr_gpu_rules_create(rules, 0, &gr);
@@ -226,20 +278,30 @@ int main(int argc, char** argv)
   double ts, tg, tw;
   collect warm = {rules};
   warm.rule_msg = (uint8_t*) calloc(rules->num_rules + 1, 1);
+  const char* mode = g_mode;
+  g_mode = "mem";
   run(rules, gs, data, n < 4096 ? n : 4096, 0, 0, &warm, &tw); /* GPU warm-up */
-  int rs = run(rules, NULL, data, n, bsize, overlap, &a, &ts);
-  int rg = run(rules, gs, data, n, bsize, overlap, &b, &tg);
+  g_mode = mode;
+  const uint8_t* d_arg = scan_whole ? NULL : data;
+  int rs = run(rules, NULL, d_arg, n, bsize, overlap, &a, &ts);
+  int rg = run(rules, gs, d_arg, n, bsize, overlap, &b, &tg);
+  if (g_pid > 0)
+  {
+    kill(g_pid, SIGKILL);
+    waitpid(g_pid, NULL, 0);
+  }
+  if (g_path) unlink(g_path);
   qsort(a.r, a.n, sizeof(rec), cmp_rec);
   qsort(b.r, b.n, sizeof(rec), cmp_rec);
   int same_matches = a.n == b.n && (a.n == 0 || memcmp(a.r, b.r, a.n * sizeof(rec)) == 0);
   int same_rules = memcmp(a.rule_msg, b.rule_msg, rules->num_rules) == 0;
   int n_match_rules = 0;
   for (uint32_t i = 0; i < rules->num_rules; i++) n_match_rules += a.rule_msg[i] == 1;
-  printf("{\"size\": %zu, \"block\": %zu, \"rc_stock\": %d, \"rc_gpu\": %d, "
+  printf("{\"mode\": \"%s\", \"size\": %zu, \"block\": %zu, \"rc_stock\": %d, \"rc_gpu\": %d, "
          "\"matches_stock\": %zu, \"matches_gpu\": %zu, \"rules_matching\": %d, "
          "\"same_matches\": %s, \"same_rule_reports\": %s, \"finished\": [%d, %d], "
          "\"stock_s\": %.4f, \"gpu_s\": %.4f}\n",
-         n, bsize, rs, rg, a.n, b.n, n_match_rules, same_matches ? "true" : "false",
+         g_mode, n, bsize, rs, rg, a.n, b.n, n_match_rules, same_matches ? "true" : "false",
          same_rules ? "true" : "false", a.finished, b.finished, ts, tg);
   yr_gpu_scanner_destroy(gs);
   yr_gpu_rules_destroy(gr);

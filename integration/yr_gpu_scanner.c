@@ -9,15 +9,17 @@
  * static, so the driver that calls it, yr_scanner_scan_mem_blocks
  * (scanner.c:417-583), is re-hosted here step for step; the only change is
  * the per-block call (scanner.c:493-496), which becomes
- *     GPU candidate stream + on-device literal pre-verification
- *       (yr_amd_scan_block_verified: drops the calls that provably have no
- *       effect, scan.c:887-990 / :1013 / :1023)
+ *     the block pipeline (yr_amd_pipeline_*: copy, H2D, GPU candidate stream
+ *       and on-device literal pre-verification, which drops the calls that
+ *       provably have no effect, scan.c:887-990 / :1013 / :1023), two blocks
+ *       in flight while the host replays the previous one
  *  -> the remaining calls, in the reference's order, into the unmodified
  *     verifier yr_scan_verify_match (scan.c:992)
- * or, with pre-verification off, the full candidate stream (yr_amd_scan_block)
- * replayed by yr_amd_replay.
- * followed, as in the reference, by yr_execute_code (exec.c:418) and the
- * rule-report loop (scanner.c:524-556).
+ * or, with pre-verification off, one block at a time: the full candidate
+ * stream (yr_amd_scan_block) replayed by yr_amd_replay.  Either way followed,
+ * as in the reference, by yr_execute_code (exec.c:418) and the rule-report
+ * loop (scanner.c:524-556).  scan_file / scan_fd / scan_proc wrap it exactly
+ * like scanner.c:674-722.
  */
 #include "yr_gpu_scanner.h"
 
@@ -29,7 +31,9 @@
 #include <yara/exec.h>
 #include <yara/exefiles.h>
 #include <yara/globals.h>
+#include <yara/filemap.h>
 #include <yara/notebook.h>
+#include <yara/proc.h>
 #include <yara/scan.h>
 #include <yara/stopwatch.h>
 
@@ -48,6 +52,9 @@ struct YR_GPU_SCANNER
   uint8_t* staging; /* host copy of the block being scanned */
   size_t staging_size;
   int preverify;    /* on-device literal pre-verification (default on) */
+  yr_amd_pipeline* pipe; /* blocks in flight on the GPU (preverify path) */
+  uint32_t depth;
+  uint32_t inflight;
 };
 
 /* YR_STRING records for yr_amd_tables_set_strings (types.h YR_STRING). */
@@ -148,6 +155,12 @@ int yr_gpu_scanner_create(YR_GPU_RULES* g, YR_GPU_SCANNER** out)
   YR_GPU_SCANNER* s = (YR_GPU_SCANNER*) calloc(1, sizeof(YR_GPU_SCANNER));
   if (s == NULL) return ERROR_INSUFFICIENT_MEMORY;
   int r = yr_amd_scanner_create(g->tables, NULL, &s->scanner);
+  if (r == ERROR_SUCCESS)
+  {
+    s->depth = 2;
+    r = yr_amd_pipeline_create(g->tables, s->depth, &s->pipe);
+    if (r != ERROR_SUCCESS) yr_amd_scanner_destroy(s->scanner);
+  }
   if (r != ERROR_SUCCESS)
   {
     free(s);
@@ -167,6 +180,7 @@ void yr_gpu_scanner_set_preverify(YR_GPU_SCANNER* s, int enable)
 void yr_gpu_scanner_destroy(YR_GPU_SCANNER* s)
 {
   if (s == NULL) return;
+  yr_amd_pipeline_destroy(s->pipe);
   yr_amd_scanner_destroy(s->scanner);
   free(s->staging);
   free(s);
@@ -224,27 +238,6 @@ static int _yr_gpu_scan_mem_block(
       { result = ERROR_COULD_NOT_MAP_FILE; });
   if (result != ERROR_SUCCESS) return result;
 
-  if (gs->preverify)
-  {
-    const yr_amd_verify_rec* recs = NULL;
-    uint64_t n = 0;
-    FAIL_ON_ERROR(yr_amd_scan_block_verified(
-        gs->scanner, gs->staging, block->size, block->base, &recs, &n));
-    if (scanner->timeout > 0 &&
-        yr_stopwatch_elapsed_ns(&scanner->stopwatch) > scanner->timeout)
-      return ERROR_SCAN_TIMEOUT;
-    /* the calls of scanner.c:111-117 / :153-159 that can have an effect */
-    for (uint64_t c = 0; c < n; c++)
-      FAIL_ON_ERROR(yr_scan_verify_match(
-          scanner,
-          &scanner->rules->ac_match_pool[recs[c].pool_index],
-          gs->staging,
-          block->size,
-          block->base,
-          (size_t) recs[c].offset));
-    return ERROR_SUCCESS;
-  }
-
   const uint64_t* positions = NULL;
   uint64_t count = 0;
   int all_positions = 0;
@@ -270,6 +263,56 @@ static int _yr_gpu_scan_mem_block(
       all_positions,
       _verify,
       &ctx);
+}
+
+/* Replay the oldest block of the pipeline: its effective verify calls, in the
+ * reference's order (scanner.c:111-117 / :153-159), into the unmodified
+ * yr_scan_verify_match. */
+static int _replay_next(YR_SCANNER* scanner, YR_GPU_SCANNER* gs)
+{
+  const yr_amd_verify_rec* recs = NULL;
+  uint64_t n = 0;
+  const uint8_t* data = NULL;
+  size_t size = 0;
+  uint64_t base = 0;
+  int result = yr_amd_pipeline_next(gs->pipe, &recs, &n, &data, &size, &base);
+  gs->inflight--;
+  if (result != ERROR_SUCCESS) return result;
+  if (scanner->timeout > 0 &&
+      yr_stopwatch_elapsed_ns(&scanner->stopwatch) > scanner->timeout)
+    return ERROR_SCAN_TIMEOUT;
+  for (uint64_t c = 0; c < n; c++)
+    FAIL_ON_ERROR(yr_scan_verify_match(
+        scanner,
+        &scanner->rules->ac_match_pool[recs[c].pool_index],
+        data,
+        size,
+        base,
+        (size_t) recs[c].offset));
+  return ERROR_SUCCESS;
+}
+
+/* One block into the pipeline; replays the oldest when `depth` are in flight. */
+static int _pipeline_block(
+    YR_SCANNER* scanner,
+    YR_GPU_SCANNER* gs,
+    const uint8_t* data,
+    YR_MEMORY_BLOCK* block)
+{
+  int result = ERROR_SUCCESS;
+  if (scanner->timeout > 0 &&
+      yr_stopwatch_elapsed_ns(&scanner->stopwatch) > scanner->timeout)
+    return ERROR_SCAN_TIMEOUT;
+  /* the block copy may fault on an mmap: same mapping to
+   * ERROR_COULD_NOT_MAP_FILE as scanner.c:493-496 */
+  YR_TRYCATCH(
+      !(scanner->flags & SCAN_FLAGS_NO_TRYCATCH),
+      { result = yr_amd_pipeline_submit(gs->pipe, data, block->size, block->base); },
+      { result = ERROR_COULD_NOT_MAP_FILE; });
+  if (result != ERROR_SUCCESS) return result;
+  gs->inflight++;
+  if (gs->inflight == gs->depth) return _replay_next(scanner, gs);
+  return ERROR_SUCCESS;
 }
 
 /* _yr_scanner_clean_matches (scanner.c:178-203) is static: same memsets. */
@@ -349,9 +392,17 @@ int yr_gpu_scanner_scan_mem_blocks(
           {});
     }
 
-    result = _yr_gpu_scan_mem_block(scanner, gs, data, block);
+    result = gs->preverify ? _pipeline_block(scanner, gs, data, block)
+                           : _yr_gpu_scan_mem_block(scanner, gs, data, block);
     if (result != ERROR_SUCCESS) goto _exit;
     block = iterator->next(iterator);
+  }
+
+  /* the blocks still on the GPU, in order */
+  while (gs->inflight > 0)
+  {
+    result = _replay_next(scanner, gs);
+    if (result != ERROR_SUCCESS) goto _exit;
   }
 
   result = iterator->last_error;
@@ -398,6 +449,11 @@ int yr_gpu_scanner_scan_mem_blocks(
   scanner->callback(scanner, CALLBACK_MSG_SCAN_FINISHED, NULL, scanner->user_data);
 
 _exit:
+  if (gs->inflight > 0)
+  {
+    yr_amd_pipeline_drain(gs->pipe);
+    gs->inflight = 0;
+  }
   if (result != ERROR_BLOCK_NOT_READY)
   {
     _clean_matches(scanner);
@@ -449,4 +505,47 @@ int yr_gpu_scanner_scan_mem(
   iterator.file_size = _file_size;
   iterator.last_error = ERROR_SUCCESS;
   return yr_gpu_scanner_scan_mem_blocks(scanner, gs, &iterator);
+}
+
+/* yr_scanner_scan_file (scanner.c:674-688): map, scan, unmap. */
+int yr_gpu_scanner_scan_file(YR_SCANNER* scanner, YR_GPU_SCANNER* gs, const char* filename)
+{
+  YR_MAPPED_FILE mfile;
+  int result = yr_filemap_map(filename, &mfile);
+  if (result == ERROR_SUCCESS)
+  {
+    result = yr_gpu_scanner_scan_mem(scanner, gs, mfile.data, mfile.size);
+    yr_filemap_unmap(&mfile);
+  }
+  return result;
+}
+
+/* yr_scanner_scan_fd (scanner.c:690-704). */
+int yr_gpu_scanner_scan_fd(YR_SCANNER* scanner, YR_GPU_SCANNER* gs, YR_FILE_DESCRIPTOR fd)
+{
+  YR_MAPPED_FILE mfile;
+  int result = yr_filemap_map_fd(fd, 0, 0, &mfile);
+  if (result == ERROR_SUCCESS)
+  {
+    result = yr_gpu_scanner_scan_mem(scanner, gs, mfile.data, mfile.size);
+    yr_filemap_unmap_fd(&mfile);
+  }
+  return result;
+}
+
+/* yr_scanner_scan_proc (scanner.c:706-722): the process's memory regions are
+ * the blocks (proc/linux.c iterator), SCAN_FLAGS_PROCESS_MEMORY set. */
+int yr_gpu_scanner_scan_proc(YR_SCANNER* scanner, YR_GPU_SCANNER* gs, int pid)
+{
+  YR_MEMORY_BLOCK_ITERATOR iterator;
+  int result = yr_process_open_iterator(pid, &iterator);
+  if (result == ERROR_SUCCESS)
+  {
+    int prev_flags = scanner->flags;
+    scanner->flags |= SCAN_FLAGS_PROCESS_MEMORY;
+    result = yr_gpu_scanner_scan_mem_blocks(scanner, gs, &iterator);
+    scanner->flags = prev_flags;
+    yr_process_close_iterator(&iterator);
+  }
+  return result;
 }

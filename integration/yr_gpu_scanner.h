@@ -21,9 +21,11 @@ void yr_gpu_rules_destroy(YR_GPU_RULES* g);
 int yr_gpu_scanner_create(YR_GPU_RULES* g, YR_GPU_SCANNER** out);
 void yr_gpu_scanner_destroy(YR_GPU_SCANNER* s);
 
-/* On-device literal pre-verification (default on): only the verify calls that
- * can have an effect reach yr_scan_verify_match.  Off: every call of the
- * reference loop is replayed (yr_amd_replay). */
+/* On-device literal pre-verification + block pipeline (default on): blocks
+ * are copied, scanned and pre-verified two at a time on the GPU while the
+ * host replays the previous one, and only the verify calls that can have an
+ * effect reach yr_scan_verify_match.  Off: one block at a time, every call of
+ * the reference loop replayed (yr_amd_scan_block + yr_amd_replay). */
 void yr_gpu_scanner_set_preverify(YR_GPU_SCANNER* s, int enable);
 
 /* Drop-in counterparts of yr_scanner_scan_mem_blocks / yr_scanner_scan_mem
@@ -37,6 +39,11 @@ int yr_gpu_scanner_scan_mem(
     YR_GPU_SCANNER* gs,
     const uint8_t* buffer,
     size_t buffer_size);
+
+/* ... and of yr_scanner_scan_file / _fd / _proc (scanner.c:674-722). */
+int yr_gpu_scanner_scan_file(YR_SCANNER* scanner, YR_GPU_SCANNER* gs, const char* filename);
+int yr_gpu_scanner_scan_fd(YR_SCANNER* scanner, YR_GPU_SCANNER* gs, YR_FILE_DESCRIPTOR fd);
+int yr_gpu_scanner_scan_proc(YR_SCANNER* scanner, YR_GPU_SCANNER* gs, int pid);
 
 #ifdef __cplusplus
 }

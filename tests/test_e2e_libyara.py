@@ -38,9 +38,9 @@ def _rules_file(tmp_path, name):
     return str(p)
 
 
-def _run(rules, data_spec, block=0, overlap=0, preverify=True):
+def _run(rules, data_spec, block=0, overlap=0, preverify=True, mode="mem"):
     cmd = [CHECK, rules, data_spec] + ([str(block), str(overlap)] if block else [])
-    env = dict(os.environ, E2E_PREVERIFY="1" if preverify else "0")
+    env = dict(os.environ, E2E_PREVERIFY="1" if preverify else "0", E2E_MODE=mode)
     r = subprocess.run(cmd, capture_output=True, text=True, timeout=600, env=env)
     assert r.stdout, r.stderr
     res = json.loads(r.stdout.strip().splitlines()[-1])
@@ -90,4 +90,27 @@ def test_match_set_equals_stock_libyara(tmp_path, rules, kind, size, block, over
     assert res["finished"] == [1, 1], res
     if kind in ("planted", "lit"):
         assert res["matches_stock"] > 0 and res["rules_matching"] > 0, res
+    assert rc == 0
+
+
+@needs_check
+@pytest.mark.parametrize("mode", ["file", "fd", "proc"])
+@pytest.mark.parametrize("rules", ["lit", "C"])
+def test_file_fd_proc_entry_points_equal_stock(tmp_path, rules, mode):
+    """yr_gpu_scanner_scan_file / _fd / _proc vs yr_scanner_scan_file / _fd /
+    _proc (scanner.c:674-722): mmap'ed files and a stopped process's memory
+    regions (proc/linux.c iterator: many blocks through the pipeline)."""
+    rf = _rules_file(tmp_path, rules)
+    if rules == "lit":
+        buf = planted.lit_buffer(oracle.xorshift, 4 << 20, 13)
+    else:
+        buf = planted.planted_buffer(oracle.xorshift, gen_rules.gen("C"), 4 << 20, 3)
+    spec = _data_file(tmp_path, buf, "d.bin")
+    rc, res = _run(rf, spec, mode=mode)
+    if mode == "proc" and res["rc_stock"] != 0:
+        pytest.skip("process memory not readable here (rc %d)" % res["rc_stock"])
+    assert res["mode"] == mode
+    assert res["rc_stock"] == 0 and res["rc_gpu"] == 0, res
+    assert res["same_matches"] and res["same_rule_reports"], res
+    assert res["matches_stock"] > 0, res
     assert rc == 0

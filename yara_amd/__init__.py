@@ -23,7 +23,8 @@ from ._lib import (CALLBACK_ERROR, COULD_NOT_MAP_FILE, INSUFFICIENT_MEMORY,  # n
                    INTERNAL_FATAL_ERROR, INVALID_ARGUMENT, MAX_ATOM_LENGTH, SCAN_TIMEOUT, SUCCESS,
                    YaraAmdError)
 
-__all__ = ["Tables", "Scanner", "replay", "fill_xorshift64", "version", "YaraAmdError"]
+__all__ = ["Tables", "Scanner", "Pipeline", "replay", "fill_xorshift64", "version",
+           "YaraAmdError"]
 
 
 def _arr(a, dt):
@@ -268,3 +269,58 @@ def fill_xorshift64(d_ptr: int, n: int, seed: int, offset: int = 0, stream: int 
     _lib.check("yr_amd_fill_xorshift64",
                _lib.lib().yr_amd_fill_xorshift64(ctypes.c_void_p(d_ptr), n, seed, offset,
                                                  ctypes.c_void_p(stream or None)))
+
+
+class Pipeline:
+    """Block pipeline (yr_amd_pipeline_*): up to ``depth`` blocks copied,
+    scanned and pre-verified on the GPU while the caller consumes the oldest.
+    Mirrors the block loop of yr_scanner_scan_mem_blocks (scanner.c:417-583)."""
+
+    def __init__(self, tables: Tables, depth: int = 2):
+        h = ctypes.c_void_p()
+        _lib.check("yr_amd_pipeline_create",
+                   _lib.lib().yr_amd_pipeline_create(tables.handle, depth, ctypes.byref(h)))
+        self._h = h
+        self.depth = depth
+        self.tables = tables
+
+    def submit(self, data: np.ndarray, base: int = 0):
+        d = _arr(data, np.uint8)
+        dp = d.ctypes.data_as(_lib._u8p) if d.size else None
+        _lib.check("yr_amd_pipeline_submit",
+                   _lib.lib().yr_amd_pipeline_submit(self._h, dp, d.size, base))
+
+    def next(self):
+        """(records {offset, pool_index, candidate}, block bytes copy, base) of
+        the oldest submitted block."""
+        recs = ctypes.POINTER(_lib.VerifyRec)()
+        cnt = ctypes.c_uint64()
+        data = ctypes.POINTER(ctypes.c_uint8)()
+        size = ctypes.c_size_t()
+        base = ctypes.c_uint64()
+        _lib.check("yr_amd_pipeline_next",
+                   _lib.lib().yr_amd_pipeline_next(self._h, ctypes.byref(recs), ctypes.byref(cnt),
+                                                   ctypes.byref(data), ctypes.byref(size),
+                                                   ctypes.byref(base)))
+        n = cnt.value
+        out = np.zeros(n, dtype=_lib.VERIFY_REC_DTYPE)
+        if n:
+            ctypes.memmove(out.ctypes.data, recs, n * 16)
+        b = np.zeros(size.value, np.uint8)
+        if size.value:
+            ctypes.memmove(b.ctypes.data, data, size.value)
+        return out, b, base.value
+
+    def drain(self):
+        _lib.check("yr_amd_pipeline_drain", _lib.lib().yr_amd_pipeline_drain(self._h))
+
+    def close(self):
+        if getattr(self, "_h", None):
+            _lib.lib().yr_amd_pipeline_destroy(self._h)
+            self._h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass

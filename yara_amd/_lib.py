@@ -81,6 +81,13 @@ PROTOTYPES = {
                                          ctypes.c_uint32, _u8p, ctypes.c_uint64, _u8p]),
     "yr_amd_verify_device": (_int, [_vp, ctypes.c_uint64, ctypes.POINTER(_vp),
                                     ctypes.POINTER(ctypes.c_uint64)]),
+    "yr_amd_pipeline_create": (_int, [_vp, ctypes.c_uint32, ctypes.POINTER(_vp)]),
+    "yr_amd_pipeline_destroy": (_int, [_vp]),
+    "yr_amd_pipeline_submit": (_int, [_vp, _u8p, ctypes.c_size_t, ctypes.c_uint64]),
+    "yr_amd_pipeline_next": (_int, [_vp, ctypes.POINTER(ctypes.POINTER(VerifyRec)),
+                                    ctypes.POINTER(ctypes.c_uint64), ctypes.POINTER(_u8p),
+                                    ctypes.POINTER(ctypes.c_size_t), ctypes.POINTER(ctypes.c_uint64)]),
+    "yr_amd_pipeline_drain": (_int, [_vp]),
     "yr_amd_scan_block_verified": (_int, [_vp, _u8p, ctypes.c_size_t, ctypes.c_uint64,
                                           ctypes.POINTER(ctypes.POINTER(VerifyRec)),
                                           ctypes.POINTER(ctypes.c_uint64)]),
