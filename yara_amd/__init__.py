@@ -290,9 +290,9 @@ class Pipeline:
         _lib.check("yr_amd_pipeline_submit",
                    _lib.lib().yr_amd_pipeline_submit(self._h, dp, d.size, base))
 
-    def next(self):
-        """(records {offset, pool_index, candidate}, block bytes copy, base) of
-        the oldest submitted block."""
+    def next(self, copy_data: bool = True):
+        """(records {offset, pool_index, candidate}, block bytes copy or None,
+        base) of the oldest submitted block."""
         recs = ctypes.POINTER(_lib.VerifyRec)()
         cnt = ctypes.c_uint64()
         data = ctypes.POINTER(ctypes.c_uint8)()
@@ -306,9 +306,11 @@ class Pipeline:
         out = np.zeros(n, dtype=_lib.VERIFY_REC_DTYPE)
         if n:
             ctypes.memmove(out.ctypes.data, recs, n * 16)
-        b = np.zeros(size.value, np.uint8)
-        if size.value:
-            ctypes.memmove(b.ctypes.data, data, size.value)
+        b = None
+        if copy_data:
+            b = np.empty(size.value, np.uint8)
+            if size.value:
+                ctypes.memmove(b.ctypes.data, data, size.value)
         return out, b, base.value
 
     def drain(self):

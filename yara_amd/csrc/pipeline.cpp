@@ -6,11 +6,12 @@
 // replay of the surviving calls on the host; the pipeline overlaps them: while
 // the host replays block k, blocks k+1 .. k+depth are copied and scanned.
 //
-// Each slot owns a scanner (its own HIP stream and device workspace), a pinned
-// host copy of its block and a worker thread that runs
+// Each slot owns a scanner (its own HIP stream and device workspace), a host
+// copy of its block and a worker thread that runs
 // yr_amd_scan_block_verified for it.  Results are handed back strictly in
 // submission order, so the replay order is the reference's block order.
 #include <hip/hip_runtime.h>
+#include <stdlib.h>
 #include <string.h>
 
 #include <condition_variable>
@@ -27,7 +28,9 @@ enum SlotState { kIdle, kSubmitted, kDone, kHeld };
 
 struct Slot {
   yr_amd_scanner* scanner = nullptr;
-  uint8_t* buf = nullptr;       // pinned host copy of the block
+  uint8_t* buf = nullptr;       // host copy of the block (pageable: the H2D
+                                // path of the runtime is faster than a host
+                                // memcpy into pinned memory)
   size_t cap = 0;
   size_t size = 0;
   uint64_t base = 0;
@@ -93,7 +96,7 @@ int yr_amd_pipeline_destroy(yr_amd_pipeline* p) {
   for (Slot& s : p->slots) {
     if (s.worker.joinable()) s.worker.join();
     if (s.scanner) yr_amd_scanner_destroy(s.scanner);
-    if (s.buf) (void)hipHostFree(s.buf);
+    free(s.buf);
   }
   delete p;
   return YR_AMD_SUCCESS;
@@ -130,13 +133,10 @@ int yr_amd_pipeline_submit(yr_amd_pipeline* p, const uint8_t* data, size_t size,
   }
   Slot& s = p->slots[idx];
   if (size > s.cap) {
-    if (s.buf) (void)hipHostFree(s.buf);
-    s.buf = nullptr;
+    free(s.buf);
     s.cap = 0;
-    if (hipHostMalloc((void**)&s.buf, size, hipHostMallocDefault) != hipSuccess) {
-      s.buf = nullptr;
-      return YR_AMD_INSUFFICIENT_MEMORY;
-    }
+    s.buf = (uint8_t*)malloc(size);
+    if (s.buf == nullptr) return YR_AMD_INSUFFICIENT_MEMORY;
     s.cap = size;
   }
   // The copy runs in the caller's thread with no lock held: a fault on an
