@@ -226,6 +226,27 @@ int yr_amd_tables_set_strings(
     const uint8_t* lowercase);
 
 /*
+ * Attach the fast-exec regex programs so that
+ * calls on hex strings (STRING_FLAGS_FAST_REGEXP) are pre-verified too.  For
+ * pool entry k, forward code = code[fwd_off[k] .. + fwd_len[k]) (a copy of
+ * rules->ac_match_pool[k].forward_code up to and including RE_OPCODE_MATCH),
+ * backward code likewise (bwd_len[k] = 0: backward_code == NULL);
+ * fwd_len[k] = 0: no program (the call is always kept).  Programs may only use
+ * the opcodes yr_re_fast_exec executes (re.c:2150-2391): ANY, LITERAL,
+ * NOT_LITERAL, MASKED_LITERAL, MASKED_NOT_LITERAL, REPEAT_ANY_UNGREEDY, MATCH;
+ * YR_AMD_INVALID_ARGUMENT otherwise.  Requires yr_amd_tables_set_strings first.
+ */
+int yr_amd_tables_set_re_code(
+    yr_amd_tables* tables,
+    uint32_t n_pool,
+    const uint32_t* fwd_off,
+    const uint32_t* fwd_len,
+    const uint32_t* bwd_off,
+    const uint32_t* bwd_len,
+    const uint8_t* code,
+    uint64_t code_len);
+
+/*
  * One call of the replay that can have an effect: the host calls
  * yr_scan_verify_match(scanner, &rules->ac_match_pool[pool_index], data,
  * size, base, offset).  candidate = index of the candidate position in the
@@ -245,9 +266,11 @@ typedef struct
  * of the reference loop (scanner.c:105-121) minus those that provably return
  * without effect: a literal string whose comparison fails
  * (_yr_scan_verify_literal_match returns before _yr_scan_match_callback,
- * scan.c:974-975), a FIXED_OFFSET string at another offset (scan.c:1023), and
- * offset == size (scan.c:1013).  Non-literal strings are always kept (their
- * verification is re.c's, on the host).  data_base = YR_MEMORY_BLOCK.base.
+ * scan.c:974-975), a FIXED_OFFSET string at another offset (scan.c:1023),
+ * offset == size (scan.c:1013), and -- with yr_amd_tables_set_re_code -- a
+ * hex string whose forward or backward fast-exec program cannot reach MATCH
+ * (_yr_scan_verify_re_match, scan.c:778-880).  Other non-literal strings are
+ * always kept (their verification is re.c's, on the host).  data_base = YR_MEMORY_BLOCK.base.
  * On success *d_records is a DEVICE pointer owned by the scanner (valid until
  * its next verify) to *count records.  Synchronous.
  * Requires yr_amd_tables_set_strings; YR_AMD_INVALID_ARGUMENT otherwise.

@@ -34,6 +34,7 @@
 #include <yara/filemap.h>
 #include <yara/notebook.h>
 #include <yara/proc.h>
+#include <yara/re.h>
 #include <yara/scan.h>
 #include <yara/stopwatch.h>
 
@@ -56,6 +57,78 @@ struct YR_GPU_SCANNER
   uint32_t depth;
   uint32_t inflight;
 };
+
+/* Length (incl. MATCH) of a linear fast-exec program (the opcodes
+ * yr_re_fast_exec runs, re.c:2150-2391), or 0. */
+static uint32_t _fast_code_len(const uint8_t* code)
+{
+  uint32_t n = 0;
+  while (n < 65536)
+  {
+    switch (code[n])
+    {
+    case RE_OPCODE_ANY: n += 1; break;
+    case RE_OPCODE_LITERAL: case RE_OPCODE_NOT_LITERAL: n += 2; break;
+    case RE_OPCODE_MASKED_LITERAL: case RE_OPCODE_MASKED_NOT_LITERAL: n += 3; break;
+    case RE_OPCODE_REPEAT_ANY_UNGREEDY: n += 5; break;
+    case RE_OPCODE_MATCH: return n + 1;
+    default: return 0;
+    }
+  }
+  return 0;
+}
+
+/* Forward/backward fast-exec programs of the hex strings' pool entries for
+ * yr_amd_tables_set_re_code (YR_AC_MATCH.forward_code / backward_code). */
+static int _attach_re_code(YR_RULES* rules, uint32_t n_pool, yr_amd_tables* t)
+{
+  uint32_t* a = (uint32_t*) calloc(4 * (size_t) (n_pool ? n_pool : 1), sizeof(uint32_t));
+  if (a == NULL) return ERROR_INSUFFICIENT_MEMORY;
+  uint32_t *fo = a, *fl = a + n_pool, *bo = a + 2 * n_pool, *bl = a + 3 * n_pool;
+  uint64_t total = 0;
+  for (uint32_t pass = 0; pass < 2; pass++)
+  {
+    uint8_t* code = pass ? (uint8_t*) malloc(total ? total : 1) : NULL;
+    if (pass && code == NULL)
+    {
+      free(a);
+      return ERROR_INSUFFICIENT_MEMORY;
+    }
+    uint64_t off = 0;
+    for (uint32_t k = 0; k < n_pool; k++)
+    {
+      YR_AC_MATCH* m = &rules->ac_match_pool[k];
+      uint32_t f = 0, b = 0;
+      if ((m->string->flags & STRING_FLAGS_FAST_REGEXP) && m->forward_code != NULL)
+      {
+        f = _fast_code_len(m->forward_code);
+        b = m->backward_code ? _fast_code_len(m->backward_code) : 0;
+        if (f == 0 || (m->backward_code != NULL && b == 0)) f = b = 0;
+      }
+      if (pass)
+      {
+        fo[k] = (uint32_t) off;
+        fl[k] = f;
+        if (f) memcpy(code + off, m->forward_code, f);
+        bo[k] = (uint32_t) (off + f);
+        bl[k] = b;
+        if (b) memcpy(code + off + f, m->backward_code, b);
+      }
+      off += f + b;
+    }
+    if (!pass)
+    {
+      total = off;
+      continue;
+    }
+    int r = yr_amd_tables_set_re_code(t, n_pool, fo, fl, bo, bl, code, total);
+    free(code);
+    free(a);
+    return r;
+  }
+  free(a);
+  return ERROR_INTERNAL_FATAL_ERROR;
+}
 
 /* YR_STRING records for yr_amd_tables_set_strings (types.h YR_STRING). */
 static int _attach_strings(YR_RULES* rules, uint32_t n_pool, yr_amd_tables* t)
@@ -131,6 +204,7 @@ int yr_gpu_rules_create(YR_RULES* rules, int device, YR_GPU_RULES** out)
   free(nx);
   free(bt);
   if (r == ERROR_SUCCESS && device >= 0) r = _attach_strings(rules, n_pool, g->tables);
+  if (r == ERROR_SUCCESS && device >= 0) r = _attach_re_code(rules, n_pool, g->tables);
   if (r != ERROR_SUCCESS)
   {
     yr_amd_tables_destroy(g->tables);

@@ -56,7 +56,8 @@ def lib():
         L.oracle_literal_effect.restype = ctypes.c_int64
         L.oracle_literal_effect.argtypes = [_u64p, _u32p, ctypes.c_uint64, _u16p, _u32p, _u32p,
                                             _u32p, ctypes.POINTER(ctypes.c_int64), _u64p, _u8p,
-                                            _u8p, _u8p, ctypes.c_uint64, ctypes.c_uint64, _u8p]
+                                            _u8p, _u8p, ctypes.c_uint64, ctypes.c_uint64, _u8p,
+                                            _u8p, _u32p, _u32p, _u32p, _u32p, _u8p]
         L.oracle_step.restype = ctypes.c_uint32
         L.oracle_step.argtypes = [_u32p, ctypes.c_uint32, ctypes.c_uint8]
         _lib = L
@@ -149,10 +150,13 @@ def ascii_lowercase() -> np.ndarray:
     return low
 
 
-def literal_effect(npz, pos, idx, data: np.ndarray, base: int = 0, lowercase=None) -> np.ndarray:
+def literal_effect(npz, pos, idx, data: np.ndarray, base: int = 0, lowercase=None,
+                   regex: bool = True) -> np.ndarray:
     """Keep-mask of a verify-call stream (positions, pool indexes): True where
-    yr_scan_verify_match can have an effect (ac_oracle.c oracle_literal_effect).
-    ``npz`` = a tests/golden/tables/*.npz mapping (pool + YR_STRING records)."""
+    yr_scan_verify_match can have an effect (ac_oracle.c oracle_literal_effect:
+    literal comparisons, and with ``regex`` the fast-exec hex programs).
+    ``npz`` = a tests/golden/tables/*.npz mapping (pool + YR_STRING records +
+    RE programs)."""
     pos = _c(pos, np.uint64)
     idx = _c(idx, np.uint32)
     n = pos.size
@@ -167,9 +171,16 @@ def literal_effect(npz, pos, idx, data: np.ndarray, base: int = 0, lowercase=Non
     ps = _c(npz["pool_string"], np.uint32)
     low = _c(ascii_lowercase() if lowercase is None else lowercase, np.uint8)
     d = _c(data, np.uint8) if data.size else np.zeros(1, np.uint8)
+    re = [None] * 6
+    if regex and "re_kind" in npz:
+        re = [_c(npz["re_kind"], np.uint8), _c(npz["re_fwd_off"], np.uint32),
+              _c(npz["re_fwd_len"], np.uint32), _c(npz["re_bwd_off"], np.uint32),
+              _c(npz["re_bwd_len"], np.uint32), _c(npz["re_code"], np.uint8)]
+    re_p = [None if a is None else _p(a, t) for a, t in
+            zip(re, [_u8p, _u32p, _u32p, _u32p, _u32p, _u8p])]
     lib().oracle_literal_effect(
         _p(pos, _u64p) if n else None, _p(idx, _u32p) if n else None, n, _p(bt, _u16p),
         _p(ps, _u32p), _p(flags, _u32p), _p(str_len, _u32p),
         fixed.ctypes.data_as(ctypes.POINTER(ctypes.c_int64)), _p(str_off, _u64p),
-        _p(blob, _u8p), _p(low, _u8p), _p(d, _u8p), int(data.size), base, _p(out, _u8p))
+        _p(blob, _u8p), _p(low, _u8p), _p(d, _u8p), int(data.size), base, _p(out, _u8p), *re_p)
     return out[:n].astype(bool)

@@ -222,6 +222,8 @@ void oracle_xorshift_fill(uint8_t* buf, uint64_t n, uint64_t seed)
  *   - the comparisons _yr_scan_compare / icompare / wcompare / wicompare /
  *     xor_compare / xor_wcompare (scan.c:62-255), lowercase = yr_lowercase.
  * Base64 literal strings are not restated: always kept (as on the device).
+ * Non-literal strings: decided by re_call_effect when the pool entry has a
+ * fast-exec program (re_kind[k] == 1, tests/golden tables v2), else kept.
  * out[c] = 1 keep, 0 no effect.
  */
 #define SF_NO_CASE 0x04u
@@ -263,12 +265,112 @@ static uint64_t fwd_xor(const uint8_t* d, uint64_t avail, const uint8_t* s, uint
   return i == n ? (wide ? 2ull * n : n) : 0;
 }
 
+/*
+ * Fast-exec regex restatement (hex strings, STRING_FLAGS_FAST_REGEXP): the
+ * program is the linear opcode sequence yr_re_fast_exec runs (re.c:2150-2391).
+ * The reference keeps a list of input positions and applies one opcode per
+ * round to all of them; here the same rounds run over the SET of
+ * bytes_matched values (a bitset over [0, YR_RE_SCAN_LIMIT]):
+ *   ANY / LITERAL / NOT_LITERAL / MASKED_(NOT_)LITERAL: b -> b + 1 if
+ *     b < max_bytes_matched and the byte at distance b (forward: input[b],
+ *     backward: input[-1-b]) passes;
+ *   REPEAT_ANY_UNGREEDY {min, max}: b -> b + min (if b < max_bytes_matched),
+ *     and b + j for min < j <= max while b + j < max_bytes_matched;
+ *   MATCH: a match iff the set is non-empty.
+ * max_bytes_matched = min(available bytes in that direction, 4096)
+ * (limits.h:163).  Returns 1 if a match is reachable, 0 otherwise.  (The set
+ * is exact "exists a path" semantics, a superset of what the reference's
+ * de-duplicating position list can reach: never says 0 where the reference
+ * would match.)
+ */
+#define RE_SCAN_LIMIT 4096
+#define RE_SET_WORDS ((RE_SCAN_LIMIT + 1 + 31) / 32 + 1)
+
+static int fast_re_reachable(const uint8_t* code, uint32_t len, const uint8_t* input,
+                             uint64_t avail, int backwards)
+{
+  uint32_t cur[RE_SET_WORDS], nxt[RE_SET_WORDS];
+  int maxb = (int) (avail < RE_SCAN_LIMIT ? avail : RE_SCAN_LIMIT);
+  memset(cur, 0, sizeof(cur));
+  cur[0] = 1; /* bytes_matched = 0 */
+  uint32_t ip = 0;
+  while (ip < len)
+  {
+    uint8_t op = code[ip];
+    if (op == 0xAD) /* MATCH */
+    {
+      for (int w = 0; w < RE_SET_WORDS; w++)
+        if (cur[w]) return 1;
+      return 0;
+    }
+    memset(nxt, 0, sizeof(nxt));
+    int any = 0;
+    for (int b = 0; b <= RE_SCAN_LIMIT; b++)
+    {
+      if (!((cur[b >> 5] >> (b & 31)) & 1)) continue;
+      if (b >= maxb) continue; /* every opcode here needs b < max_bytes_matched */
+      uint8_t c = backwards ? input[-1 - (int64_t) b] : input[b];
+      int pass = 0;
+      switch (op)
+      {
+      case 0xA0: pass = 1; break;
+      case 0xA2: pass = c == code[ip + 1]; break;
+      case 0xAE: pass = c != code[ip + 1]; break;
+      case 0xA4: pass = (c & code[ip + 2]) == code[ip + 1]; break;
+      case 0xAF: pass = (c & code[ip + 2]) != code[ip + 1]; break;
+      case 0xB5:
+      {
+        int mn = code[ip + 1] | (code[ip + 2] << 8);
+        int mx = code[ip + 3] | (code[ip + 4] << 8);
+        if (b + mn <= RE_SCAN_LIMIT) nxt[(b + mn) >> 5] |= 1u << ((b + mn) & 31);
+        for (int j = mn + 1; j <= mx && b + j < maxb; j++)
+          nxt[(b + j) >> 5] |= 1u << ((b + j) & 31);
+        any = 1;
+        continue;
+      }
+      default: return 1; /* not a fast program: cannot rule a match out */
+      }
+      if (pass)
+      {
+        nxt[(b + 1) >> 5] |= 1u << ((b + 1) & 31);
+        any = 1;
+      }
+    }
+    if (!any) return 0;
+    memcpy(cur, nxt, sizeof(cur));
+    ip += op == 0xA0 ? 1 : (op == 0xA2 || op == 0xAE) ? 2 : (op == 0xA4 || op == 0xAF) ? 3 : 5;
+  }
+  return 1;
+}
+
+/*
+ * Does the regex call (non-literal string, pool entry k at offset off) have a
+ * possible effect?  _yr_scan_verify_re_match (scan.c:778-880): the forward
+ * program from `off` must match (forward_matches != -1), then, if a backward
+ * program exists, it must match backwards from `off` (its MATCHes are what
+ * reach _yr_scan_match_callback); forward_matches == 0 without a backward
+ * program returns early too.  Only FAST ascii hex strings are decided.
+ */
+static int re_call_effect(uint32_t flags, const uint8_t* fwd, uint32_t fl, const uint8_t* bwd,
+                          uint32_t bl, const uint8_t* data, uint64_t size, uint64_t off)
+{
+  if (!(flags & 0x40u) || !(flags & SF_ASCII) || (flags & (SF_WIDE | SF_BASE64_ANY)))
+    return 1;
+  if (fl == 1) /* forward program = MATCH: forward_matches = 0 */
+    return bl > 0 ? fast_re_reachable(bwd, bl, data + off, off, 1) : 0;
+  if (!fast_re_reachable(fwd, fl, data + off, size - off, 0)) return 0;
+  if (bl > 0 && !fast_re_reachable(bwd, bl, data + off, off, 1)) return 0;
+  return 1;
+}
+
 int64_t oracle_literal_effect(
     const uint64_t* pos, const uint32_t* pool_idx, uint64_t n_calls,
     const uint16_t* backtrack, const uint32_t* pool_string,
     const uint32_t* str_flags, const uint32_t* str_len, const int64_t* str_fixed,
     const uint64_t* str_off, const uint8_t* blob, const uint8_t* lowercase,
-    const uint8_t* data, uint64_t size, uint64_t base, uint8_t* out)
+    const uint8_t* data, uint64_t size, uint64_t base, uint8_t* out,
+    const uint8_t* re_kind, const uint32_t* re_fwd_off, const uint32_t* re_fwd_len,
+    const uint32_t* re_bwd_off, const uint32_t* re_bwd_len, const uint8_t* re_code)
 {
   int64_t kept = 0;
   for (uint64_t c = 0; c < n_calls; c++)
@@ -307,6 +409,11 @@ int64_t oracle_literal_effect(
           if (fm == 0) fm = fwd_xor(d, avail, str, n, 0);
         }
       }
+    }
+    else if (!(f & SF_LITERAL) && re_kind != NULL && re_kind[k])
+    {
+      fm = re_call_effect(f, re_code + re_fwd_off[k], re_fwd_len[k], re_code + re_bwd_off[k],
+                          re_bwd_len[k], data, size, off);
     }
     out[c] = fm != 0;
     kept += fm != 0;

@@ -7,7 +7,10 @@
  *       Aho-Corasick tables exactly as YR_RULES exposes them (rules.c:356-363):
  *       T = ac_transition_table, M = ac_match_table, and the YR_AC_MATCH pool
  *       (types.h:324-344) with `next` turned into a 1-based pool index.  Also
- *       dumps the YR_STRING records (types.h:238-287) the verifier uses.
+ *       dumps the YR_STRING records (types.h:238-287) the verifier uses and,
+ *       for FAST_REGEXP strings (hex strings), each pool entry's forward and
+ *       backward RE code (re.c fast-exec opcodes, decoded linearly up to
+ *       RE_OPCODE_MATCH).
  *
  *   refdump scan <rules.yar> <data> <out_prefix> [block_size overlap]
  *       <data> is a file path or "xs:<seed>:<size>" (SURVEY.md App. A
@@ -85,6 +88,26 @@ static uint32_t n_pool_of(YR_RULES* rules)
                      sizeof(YR_AC_MATCH));
 }
 
+/* Length (incl. the final MATCH) of a linear fast-exec program (the opcodes
+ * yr_re_fast_exec accepts, re.c:2150-2391), or 0 if `code` is not one. */
+static uint32_t fast_code_len(const uint8_t* code)
+{
+  uint32_t n = 0;
+  while (n < 65536)
+  {
+    switch (code[n])
+    {
+    case 0xA0: n += 1; break;             /* ANY */
+    case 0xA2: case 0xAE: n += 2; break;  /* LITERAL, NOT_LITERAL */
+    case 0xA4: case 0xAF: n += 3; break;  /* MASKED_LITERAL, MASKED_NOT_LITERAL */
+    case 0xB5: n += 5; break;             /* REPEAT_ANY_UNGREEDY {u16 min, u16 max} */
+    case 0xAD: return n + 1;              /* MATCH */
+    default: return 0;
+    }
+  }
+  return 0;
+}
+
 static void w32(FILE* f, uint32_t v) { fwrite(&v, 4, 1, f); }
 static void w64(FILE* f, uint64_t v) { fwrite(&v, 8, 1, f); }
 
@@ -95,7 +118,7 @@ static int cmd_tables(const char* rules_path, const char* out)
   FILE* f = fopen(out, "wb");
   if (!f) die("cannot open output", 0);
   fwrite("YRTB", 4, 1, f);
-  w32(f, 1);
+  w32(f, 2);
   w32(f, ns);
   w32(f, np);
   w32(f, rules->num_strings);
@@ -122,6 +145,28 @@ static int cmd_tables(const char* rules_path, const char* out)
     fwrite(s->string, 1, s->length, f);
     static const uint8_t pad[4] = {0, 0, 0, 0};
     fwrite(pad, 1, (4 - (s->length & 3)) & 3, f);
+  }
+  /* v2: per pool entry {u32 kind, u32 fwd_len, u32 bwd_len, fwd, bwd, pad};
+   * kind 1 = FAST_REGEXP string with linear forward (and, if bwd_len > 0,
+   * backward) programs; kind 0 = anything else (no code dumped). */
+  for (uint32_t k = 0; k < np; k++)
+  {
+    YR_AC_MATCH* m = &rules->ac_match_pool[k];
+    uint32_t kind = 0, fl = 0, bl = 0;
+    if ((m->string->flags & STRING_FLAGS_FAST_REGEXP) && m->forward_code != NULL)
+    {
+      fl = fast_code_len(m->forward_code);
+      bl = m->backward_code ? fast_code_len(m->backward_code) : 0;
+      kind = fl > 0 && (m->backward_code == NULL || bl > 0);
+      if (!kind) fl = bl = 0;
+    }
+    w32(f, kind);
+    w32(f, fl);
+    w32(f, bl);
+    if (fl) fwrite(m->forward_code, 1, fl, f);
+    if (bl) fwrite(m->backward_code, 1, bl, f);
+    static const uint8_t pad[4] = {0, 0, 0, 0};
+    fwrite(pad, 1, (4 - ((fl + bl) & 3)) & 3, f);
   }
   fclose(f);
   printf("slots=%u pool=%u strings=%u rules=%u\n", ns, np, rules->num_strings,

@@ -19,6 +19,10 @@ class RefTables:
     pool_backtrack: np.ndarray    # uint16[n_pool]
     strings: list = field(default_factory=list)
     n_rules: int = 0
+    # v2: fast-exec RE programs per pool entry (kind 1) -- re.c:2150
+    re_kind: np.ndarray = None    # uint8[n_pool]
+    re_fwd: list = None           # bytes per pool entry (b"" if none)
+    re_bwd: list = None
 
 
 def read_tables(path: str) -> RefTables:
@@ -26,7 +30,7 @@ def read_tables(path: str) -> RefTables:
         buf = f.read()
     assert buf[:4] == b"YRTB", "not a refdump table file"
     ver, ns, npool, nstr, nrules = struct.unpack_from("<5I", buf, 4)
-    assert ver == 1
+    assert ver in (1, 2)
     off = 24
     T = np.frombuffer(buf, dtype="<u4", count=ns, offset=off).copy(); off += 4 * ns
     M = np.frombuffer(buf, dtype="<u4", count=ns, offset=off).copy(); off += 4 * ns
@@ -42,6 +46,15 @@ def read_tables(path: str) -> RefTables:
         strings.append(dict(flags=flags, rule_idx=rule_idx, length=length,
                             chained_to=None if chained == 0xFFFFFFFF else chained,
                             gap_min=gmin, gap_max=gmax, fixed_offset=fixed, data=data))
+    kinds, fwd, bwd = np.zeros(npool, np.uint8), [], []
+    if ver >= 2:
+        for k in range(npool):
+            kind, fl, bl = struct.unpack_from("<3I", buf, off)
+            off += 12
+            kinds[k] = kind
+            fwd.append(buf[off:off + fl])
+            bwd.append(buf[off + fl:off + fl + bl])
+            off += fl + bl + ((4 - ((fl + bl) & 3)) & 3)
     assert off == len(buf)
     return RefTables(T, M, pool[:, 0].copy(), pool[:, 1].copy(),
-                     pool[:, 2].astype(np.uint16), strings, nrules)
+                     pool[:, 2].astype(np.uint16), strings, nrules, kinds, fwd, bwd)

@@ -62,6 +62,8 @@ def case_data(rec):
         return np.frombuffer(ALPHA, dtype=np.uint8)[x % len(ALPHA)]
     if kind == "lit":
         return planted.lit_buffer(oracle.xorshift, spec[2], spec[1])
+    if kind == "hex":
+        return planted.hex_buffer(oracle.xorshift, spec[2], spec[1])
     if kind == "file":
         return np.frombuffer(bytes.fromhex(rec["data_bytes_hex"]), dtype=np.uint8)
     raise ValueError(kind)

@@ -137,3 +137,46 @@ def lit_buffer(xorshift, size: int, seed: int = 13) -> np.ndarray:
         buf[4096:4096 + len(fixed)] = np.frombuffer(fixed, dtype=np.uint8)
         buf[6000:6000 + len(fixed)] = np.frombuffer(fixed, dtype=np.uint8)
     return buf
+
+
+# --- hex-with-jumps buffer (tests/golden/rules/hex.yar) ----------------------
+# Instances and near misses of every hex string (the fast-exec programs of
+# re.c:2150-2391): jumps at their bounds and one past, masked nibbles, ~XX,
+# atoms near the block start/end (backward / forward limits), a long jump.
+def hex_buffer(xorshift, size: int, seed: int = 17) -> np.ndarray:
+    buf = xorshift(size, seed).copy()
+    r = random.Random(seed)
+    H = bytes.fromhex
+    pieces = []
+    for gap in range(1, 9):
+        pieces.append(H("4D5A01025045") + bytes(gap) + H("1122"))
+    for g1 in range(0, 5):
+        for g2 in range(0, 4):
+            pieces.append(H("AABBCCDD") + b"\x77" * g1 + H("EE") + b"\x66" * g2 + H("FF01"))
+    for g in (3, 4, 5):
+        pieces.append(H("1020") + bytes(g) + H("30405060"))
+    for g in (0, 1, 5, 10, 11):
+        pieces.append(H("71727374A57B") + b"\x33" * g + H("75"))
+        pieces.append(H("71727374A67B") + b"\x33" * g + H("75"))   # masked miss
+    for x in (0x02, 0x03, 0x04):
+        pieces.append(H("0102") + bytes([x]) + H("040506"))
+    for a, b_, c in ((1, 1, 1), (2, 2, 2), (1, 2, 3), (3, 1, 1)):
+        pieces.append(H("81828384") + bytes(a) + H("85") + bytes(b_) + H("86") + bytes(c) + H("87"))
+    for g in (0, 1, 4, 5):
+        pieces.append(H("9A9B") + b"\x44" * g + H("C1C2C3C4"))
+        pieces.append(H("9A9C") + b"\x44" * g + H("C1C2C3C4"))      # backward miss
+    for g in (1, 2, 3, 4):
+        pieces.append(H("E100E3") + b"\x55" * g + H("F1F2F3F4F5"))
+    pieces += [H("5A6B7C8D91929394"), H("5A6B7C9D91929394"), H("5A6B7C8D91929395")]
+    for g in (99, 100, 2999, 3000, 3001):
+        pieces.append(H("31415926") + bytes(g) + H("53589793"))
+    for p in pieces:
+        for _ in range(2):
+            pos = r.randrange(16, size - len(p) - 16)
+            buf[pos:pos + len(p)] = np.frombuffer(p, dtype=np.uint8)
+    # block-edge cases: a string whose atom sits right at the start / end
+    edge = H("C1C2C3C4")
+    buf[0:4] = np.frombuffer(edge, np.uint8)                  # no room for the prefix
+    tail = H("4D5A01025045") + bytes(2) + H("11")           # truncated at the end
+    buf[size - len(tail):] = np.frombuffer(tail, np.uint8)
+    return buf

@@ -63,9 +63,10 @@ class Tables:
         self.device = device
 
     @classmethod
-    def from_npz(cls, path, device: int = 0, strings: bool = False):
+    def from_npz(cls, path, device: int = 0, strings: bool = False, regex: bool = True):
         """Tables from a tests/golden/tables/*.npz dump; ``strings=True`` also
-        attaches the YR_STRING records (needed by Scanner.verify_calls)."""
+        attaches the YR_STRING records (needed by Scanner.verify_calls) and,
+        with ``regex``, the fast-exec programs of the hex strings."""
         z = np.load(path)
         t = cls(z["T"], z["M"], z["pool_next"], z["pool_backtrack"], device=device)
         t.pool_string = z["pool_string"] if "pool_string" in z else None
@@ -73,7 +74,19 @@ class Tables:
             offs = z["str_offsets"]
             t.set_strings(z["pool_string"], z["str_flags"], np.diff(offs), z["str_fixed_offset"],
                           z["str_bytes"], offs[:-1])
+            if regex and "re_kind" in z:
+                fl = np.where(z["re_kind"] != 0, z["re_fwd_len"], 0)
+                t.set_re_code(z["re_fwd_off"], fl, z["re_bwd_off"], z["re_bwd_len"], z["re_code"])
         return t
+
+    def set_re_code(self, fwd_off, fwd_len, bwd_off, bwd_len, code):
+        """Attach fast-exec RE programs (yr_amd_tables_set_re_code)."""
+        arrs = [_arr(a, np.uint32) for a in (fwd_off, fwd_len, bwd_off, bwd_len)]
+        arrs = [a if a.size else np.zeros(1, np.uint32) for a in arrs]
+        self._re = arrs + [_arr(code, np.uint8) if len(code) else np.zeros(1, np.uint8)]
+        _lib.check("yr_amd_tables_set_re_code", _lib.lib().yr_amd_tables_set_re_code(
+            self._h, len(fwd_off), *[a.ctypes.data_as(_lib._u32p) for a in arrs],
+            self._re[4].ctypes.data_as(_lib._u8p), len(code)))
 
     def set_strings(self, pool_string, flags, lengths, fixed_offsets, blob, bytes_offsets,
                     lowercase=None):

@@ -46,6 +46,8 @@ struct yr_amd_tables {
   DevString* d_strings = nullptr;
   uint8_t* d_str_bytes = nullptr;
   uint8_t* d_lowercase = nullptr;
+  DevRe* d_re = nullptr;          // yr_amd_tables_set_re_code
+  uint8_t* d_re_code = nullptr;
 };
 
 struct yr_amd_scanner {
@@ -201,7 +203,8 @@ int yr_amd_tables_destroy(yr_amd_tables* t) {
   if (t == nullptr) return YR_AMD_SUCCESS;
   for (void* p : {(void*)t->d_filter, (void*)t->d_exact, (void*)t->d_T, (void*)t->d_M,
                   (void*)t->d_pool_next, (void*)t->d_pool_backtrack, (void*)t->d_pool_string,
-                  (void*)t->d_strings, (void*)t->d_str_bytes, (void*)t->d_lowercase})
+                  (void*)t->d_strings, (void*)t->d_str_bytes, (void*)t->d_lowercase,
+                  (void*)t->d_re, (void*)t->d_re_code})
     if (p) (void)hipFree(p);
   delete t;
   return YR_AMD_SUCCESS;
@@ -464,6 +467,60 @@ int yr_amd_tables_set_strings(yr_amd_tables* t, const uint32_t* pool_string, uin
   return YR_AMD_SUCCESS;
 }
 
+namespace {
+// Length of a linear fast-exec program (opcodes of yr_re_fast_exec,
+// re.c:2150-2391) that ends with MATCH exactly at `len`, else 0.
+uint32_t fast_program_ok(const uint8_t* c, uint32_t len) {
+  uint32_t n = 0;
+  while (n < len) {
+    switch (c[n]) {
+      case kReAny: n += 1; break;
+      case kReLiteral: case kReNotLiteral: n += 2; break;
+      case kReMaskedLiteral: case kReMaskedNotLiteral: n += 3; break;
+      case kReRepeatAnyUngreedy: {
+        if (n + 5 > len) return 0;
+        const uint32_t mn = c[n + 1] | (c[n + 2] << 8), mx = c[n + 3] | (c[n + 4] << 8);
+        if (mn > mx) return 0;
+        n += 5;
+        break;
+      }
+      case kReMatch: return n + 1 == len ? len : 0;
+      default: return 0;
+    }
+  }
+  return 0;
+}
+}  // namespace
+
+int yr_amd_tables_set_re_code(yr_amd_tables* t, uint32_t n_pool, const uint32_t* fwd_off,
+                              const uint32_t* fwd_len, const uint32_t* bwd_off,
+                              const uint32_t* bwd_len, const uint8_t* code, uint64_t code_len) {
+  if (t == nullptr || !t->has_strings || t->d_re != nullptr || t->d_re_code != nullptr)
+    return YR_AMD_INVALID_ARGUMENT;
+  if (n_pool != t->flat.pool_next.size()) return YR_AMD_INVALID_ARGUMENT;
+  if (n_pool > 0 && (fwd_off == nullptr || fwd_len == nullptr || bwd_off == nullptr ||
+                     bwd_len == nullptr))
+    return YR_AMD_INVALID_ARGUMENT;
+  if (code_len > 0 && code == nullptr) return YR_AMD_INVALID_ARGUMENT;
+  std::vector<DevRe> re(n_pool);
+  for (uint32_t k = 0; k < n_pool; ++k) {
+    re[k] = DevRe{fwd_off[k], fwd_len[k], bwd_off[k], bwd_len[k]};
+    if (fwd_len[k] == 0) {
+      re[k] = DevRe{0, 0, 0, 0};
+      continue;
+    }
+    if ((uint64_t)fwd_off[k] + fwd_len[k] > code_len || (uint64_t)bwd_off[k] + bwd_len[k] > code_len)
+      return YR_AMD_INVALID_ARGUMENT;
+    if (!fast_program_ok(code + fwd_off[k], fwd_len[k])) return YR_AMD_INVALID_ARGUMENT;
+    if (bwd_len[k] > 0 && !fast_program_ok(code + bwd_off[k], bwd_len[k]))
+      return YR_AMD_INVALID_ARGUMENT;
+  }
+  HIP_TRY(hipSetDevice(t->device));
+  int r = upload(t->d_re_code, code, (size_t)code_len);
+  if (!r) r = upload(t->d_re, re.data(), re.size());
+  return r;
+}
+
 int yr_amd_verify_device(yr_amd_scanner* s, uint64_t data_base, const yr_amd_verify_rec** d_records,
                          uint64_t* count) {
   if (s == nullptr || s->pending || !s->tables->has_strings) return YR_AMD_INVALID_ARGUMENT;
@@ -492,6 +549,8 @@ int yr_amd_verify_device(yr_amd_scanner* s, uint64_t data_base, const yr_amd_ver
   v.strings = t->d_strings;
   v.str_bytes = t->d_str_bytes;
   v.lowercase = t->d_lowercase;
+  v.re = t->d_re;
+  v.re_code = t->d_re_code;
   uint64_t total = 0;
   if (v.count > 0) {
     if (v.data == nullptr) return YR_AMD_INVALID_ARGUMENT;

@@ -18,6 +18,20 @@ constexpr uint32_t kStrXor = 0x80000;
 // are always handed to the host (base64 / base64wide)
 constexpr uint32_t kStrUnmodelled = 0x200000 | 0x400000;
 
+constexpr uint32_t kStrFastRegexp = 0x40;
+constexpr uint32_t kStrBase64Any = 0x200000 | 0x400000;
+
+// Fast-exec RE programs (hex strings) of one pool entry: forward code at
+// re_code[fwd_off, +fwd_len), backward code likewise; fwd_len == 0 = none.
+struct DevRe {
+  uint32_t fwd_off, fwd_len, bwd_off, bwd_len;
+};
+
+// re.c opcodes of the fast executor (libyara/include/yara/re.h:65-92).
+constexpr uint8_t kReAny = 0xA0, kReLiteral = 0xA2, kReMaskedLiteral = 0xA4, kReMatch = 0xAD,
+                  kReNotLiteral = 0xAE, kReMaskedNotLiteral = 0xAF, kReRepeatAnyUngreedy = 0xB5;
+constexpr int kReScanLimit = 4096;   // YR_RE_SCAN_LIMIT (limits.h:163)
+
 struct DevString {
   uint32_t flags;
   uint32_t length;
@@ -48,6 +62,8 @@ struct VerifyParams {
   const DevString* strings;
   const uint8_t* str_bytes;
   const uint8_t* lowercase;   // the host's yr_lowercase[256]
+  const DevRe* re;            // per pool entry, or null (no regex decisions)
+  const uint8_t* re_code;
   uint32_t* counts;           // [count] records per candidate (pass 0)
   const uint64_t* offsets;    // [count] exclusive scan of counts (pass 1)
   VerifyRec* out;             // records (pass 1)

@@ -1,4 +1,4 @@
-// gfx950 kernels of the on-device literal pre-verification.
+// gfx950 kernels of the on-device pre-verification.
 //
 // Input: the candidate stream of a block scan (ascending positions i with
 // ac_match_table[state_i] != 0).  For every candidate the reference loop
@@ -11,12 +11,12 @@
 // ERROR_SUCCESS without touching the scan context when forward_matches == 0.
 // These kernels evaluate exactly that comparison on the GPU and emit the
 // calls that can have an effect -- every call on a non-literal string (regex /
-// hex with jumps: decided on the host by re.c), and every literal call whose
-// comparison succeeds -- as {offset, pool index} records in the reference's
-// call order.  The host replays the records into the unmodified
-// yr_scan_verify_match, so the final match set is unchanged while the host no
-// longer walks lists or compares bytes for the (vast majority of) candidates
-// that are atom hits only.
+// hex with jumps, unless its fast-exec program provably cannot match: see
+// fast_re_reachable), and every literal call whose comparison succeeds -- as
+// {offset, pool index} records in the reference's call order.  The host
+// replays the records into the unmodified yr_scan_verify_match, so the final
+// match set is unchanged while the host no longer walks lists, compares bytes
+// or runs re.c for the (vast majority of) candidates that are atom hits only.
 //
 // Work per candidate (one lane each): recompute state_i by the reference
 // transition rule from max(0, i - 4) (the trie is at most 4 deep, limits.h:68),
@@ -84,6 +84,88 @@ __device__ bool cmp_xor(const uint8_t* d, uint64_t avail, const uint8_t* s, uint
   return true;
 }
 
+// yr_re_fast_exec (re.c:2150-2391) as a reachability question: is MATCH
+// reachable from bytes_matched = 0?  The reference runs the linear program
+// over a list of input positions; here a depth-first search over the choices
+// of RE_OPCODE_REPEAT_ANY_UNGREEDY (b -> b + min unconditionally, b + j for
+// min < j <= max while b + j < max_bytes_matched) with every consuming opcode
+// requiring b < max_bytes_matched.  "Exists a path" semantics, i.e. a superset
+// of what the reference's de-duplicating list reaches; out of stack or step
+// budget -> true (keep the call).
+__device__ bool fast_re_reachable(const uint8_t* __restrict__ code, uint32_t len,
+                                  const uint8_t* __restrict__ input, uint64_t avail,
+                                  bool backwards) {
+  constexpr int kMaxChoices = 8;
+  struct Choice {
+    uint32_t ip;
+    int b, j, jmax;
+  } st[kMaxChoices];
+  int sp = 0;
+  const int maxb = (int)min<uint64_t>(avail, (uint64_t)kReScanLimit);
+  uint32_t ip = 0;
+  int b = 0;
+  for (int budget = 0; budget < 8192; ++budget) {
+    if (ip >= len) return true;
+    const uint8_t op = code[ip];
+    if (op == kReMatch) return true;
+    bool ok = false;
+    if (b < maxb) {
+      const uint8_t c = backwards ? input[-1 - (int64_t)b] : input[b];
+      switch (op) {
+        case kReAny: ok = true; ip += 1; break;
+        case kReLiteral: ok = c == code[ip + 1]; ip += 2; break;
+        case kReNotLiteral: ok = c != code[ip + 1]; ip += 2; break;
+        case kReMaskedLiteral: ok = (c & code[ip + 2]) == code[ip + 1]; ip += 3; break;
+        case kReMaskedNotLiteral: ok = (c & code[ip + 2]) != code[ip + 1]; ip += 3; break;
+        case kReRepeatAnyUngreedy: {
+          const int mn = code[ip + 1] | (code[ip + 2] << 8);
+          const int mx = code[ip + 3] | (code[ip + 4] << 8);
+          ip += 5;
+          const int jmax = min(mx, maxb - 1 - b);
+          if (mn + 1 <= jmax) {
+            if (sp == kMaxChoices) return true;
+            st[sp++] = Choice{ip, b, mn + 1, jmax};
+          }
+          b += mn;
+          continue;   // position advanced by min, unconditionally
+        }
+        default: return true;   // not a fast program
+      }
+      if (ok) {
+        b += 1;
+        continue;
+      }
+    }
+    // dead position: resume the most recent open choice
+    if (sp == 0) return false;
+    Choice& t = st[sp - 1];
+    ip = t.ip;
+    b = t.b + t.j;
+    if (++t.j > t.jmax) --sp;
+  }
+  return true;
+}
+
+// _yr_scan_verify_re_match (scan.c:778-880) for FAST ascii hex strings: the
+// forward program from `offset` must reach MATCH (else forward_matches == -1:
+// return), a zero-length forward match needs a backward program, and with a
+// backward program its MATCHes are the only way to _yr_scan_match_callback.
+__device__ bool re_call_matters(const VerifyParams& p, uint32_t k, uint32_t flags,
+                                uint64_t offset) {
+  if (p.re == nullptr) return true;
+  if (!(flags & kStrFastRegexp) || !(flags & kStrAscii) || (flags & (kStrWide | kStrBase64Any)))
+    return true;
+  const DevRe r = p.re[k];
+  if (r.fwd_len == 0) return true;
+  const uint8_t* d = p.data + offset;
+  if (r.fwd_len == 1)   // forward program = MATCH: forward_matches = 0
+    return r.bwd_len > 0 && fast_re_reachable(p.re_code + r.bwd_off, r.bwd_len, d, offset, true);
+  if (!fast_re_reachable(p.re_code + r.fwd_off, r.fwd_len, d, p.size - offset, false)) return false;
+  if (r.bwd_len > 0 && !fast_re_reachable(p.re_code + r.bwd_off, r.bwd_len, d, offset, true))
+    return false;
+  return true;
+}
+
 // Does yr_scan_verify_match(ctx, &pool[k], data, size, base, offset) possibly
 // have an effect?  false only where the reference provably returns without
 // touching the context.
@@ -94,7 +176,7 @@ __device__ bool call_matters(const VerifyParams& p, uint32_t k, uint64_t offset)
   // scan.c:1023-1025
   if ((st.flags & kStrFixedOffset) && st.fixed_offset != (int64_t)(p.data_base + offset))
     return false;
-  if (!(st.flags & kStrLiteral)) return true;            // re.c verification on the host
+  if (!(st.flags & kStrLiteral)) return re_call_matters(p, k, st.flags, offset);
   if (st.flags & kStrUnmodelled) return true;            // conservative
   // _yr_scan_verify_literal_match, scan.c:907-972
   if (st.flags & kStrFitsInAtom) return p.pool_backtrack[k] != 0;
