@@ -92,6 +92,21 @@ int yr_amd_tables_create(
 
 int yr_amd_tables_destroy(yr_amd_tables* tables);
 
+/*
+ * The same tables straight from a compiled rules file (SURVEY.md section 8f,
+ * row 3): the bytes of a .yarc written by yarac / yr_rules_save (arena format
+ * version 19, arena.c:543-700, sections compiler.h:58-69), parsed without
+ * libyara.  With device >= 0 the string records and the hex strings' regex
+ * programs are attached too (yr_amd_tables_set_strings with C-locale case
+ * folding, yr_amd_tables_set_re_code), so pre-verification works directly.
+ * YR_AMD_INVALID_ARGUMENT for anything that is not a well-formed v19 arena.
+ */
+int yr_amd_tables_load_yarc(
+    const uint8_t* file,
+    size_t file_size,
+    int device,
+    yr_amd_tables** tables);
+
 /* Diagnostics of the flattened form (yr_rules_get_stats analogue, rules.c:438). */
 typedef struct
 {

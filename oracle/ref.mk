@@ -9,6 +9,7 @@
 # Outputs (git-ignored, but travel to the GPU box with the gpurun snapshot):
 #   oracle/_ref/libyara_ref.so   stock libyara (scanner.c, scan.c, exec.c, ... as-is)
 #   oracle/_ref/yara             stock CLI (config A plumbing check)
+#   oracle/_ref/yarac            stock rules compiler (.yarc fixtures)
 #
 # The generated parsers (grammar.c, lexer.c, re_*.c, hex_*.c) are checked in
 # upstream, so no bison/flex/autotools are needed.
@@ -37,7 +38,7 @@ CLI := args common threading yara
 
 HOOKED_OBJS := $(filter-out $(OBJ)/scanner.o,$(OBJS)) $(OBJ)/scanner_hooked.o $(OBJ)/refhook.o
 
-all: $(OUT)/libyara_ref.so $(OUT)/libyara_ref_hooked.so $(OUT)/yara $(OUT)/refdump
+all: $(OUT)/libyara_ref.so $(OUT)/libyara_ref_hooked.so $(OUT)/yara $(OUT)/yarac $(OUT)/refdump
 
 define OBJ_RULE
 $(OBJ)/$(subst /,_,$(1)).o: $(REF)/libyara/$(1).c | $(OBJ)
@@ -69,6 +70,12 @@ $(OUT)/libyara_ref.so: $(OBJS)
 $(OUT)/yara: $(OUT)/libyara_ref.so $(patsubst %,$(REF)/cli/%.c,$(CLI))
 	$(CC) -O2 -D_GNU_SOURCE -w -I$(REF)/libyara/include -I$(REF)/cli -I$(REF) \
 	  $(patsubst %,$(REF)/cli/%.c,$(CLI)) -o $@ -L$(OUT) -lyara_ref \
+	  -Wl,-rpath,'$$ORIGIN' -lpthread -lm
+
+# stock rules compiler: writes the .yarc fixtures of tests/golden/yarc/
+$(OUT)/yarac: $(OUT)/libyara_ref.so $(REF)/cli/yarac.c $(REF)/cli/args.c $(REF)/cli/common.c
+	$(CC) -O2 -D_GNU_SOURCE -w -I$(REF)/libyara/include -I$(REF)/cli -I$(REF) \
+	  $(REF)/cli/yarac.c $(REF)/cli/args.c $(REF)/cli/common.c -o $@ -L$(OUT) -lyara_ref \
 	  -Wl,-rpath,'$$ORIGIN' -lpthread -lm
 
 clean:

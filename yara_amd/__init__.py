@@ -41,7 +41,12 @@ class Tables:
     ``device=-1`` builds host-only tables: flattening + replay, no scanner.
     """
 
-    def __init__(self, T, M, pool_next, pool_backtrack, device: int = 0):
+    def __init__(self, T=None, M=None, pool_next=None, pool_backtrack=None, device: int = 0,
+                 _handle=None):
+        if _handle is not None:          # from_yarc
+            self._h = _handle
+            self.device = device
+            return
         L = _lib.lib()
         self._T = _arr(T, np.uint32)
         self._M = _arr(M, np.uint32)
@@ -61,6 +66,19 @@ class Tables:
         _lib.check("yr_amd_tables_create", rc)
         self._h = h
         self.device = device
+
+    @classmethod
+    def from_yarc(cls, data, device: int = 0):
+        """Tables from the bytes (or path) of a compiled rules file (yarac
+        output; yr_amd_tables_load_yarc) -- no libyara involved."""
+        if isinstance(data, (str, bytes)) and not isinstance(data, bytes):
+            with open(data, "rb") as f:
+                data = f.read()
+        buf = np.frombuffer(data, dtype=np.uint8) if len(data) else np.zeros(1, np.uint8)
+        h = ctypes.c_void_p()
+        _lib.check("yr_amd_tables_load_yarc", _lib.lib().yr_amd_tables_load_yarc(
+            buf.ctypes.data_as(_lib._u8p), len(data), device, ctypes.byref(h)))
+        return cls(device=device, _handle=h)
 
     @classmethod
     def from_npz(cls, path, device: int = 0, strings: bool = False, regex: bool = True):

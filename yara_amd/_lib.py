@@ -63,6 +63,7 @@ PROTOTYPES = {
     "yr_amd_tables_create": (_int, [_u32p, _u32p, ctypes.c_uint32, _u32p, _u16p, ctypes.c_uint32,
                                     _int, ctypes.POINTER(_vp)]),
     "yr_amd_tables_destroy": (_int, [_vp]),
+    "yr_amd_tables_load_yarc": (_int, [_u8p, ctypes.c_size_t, _int, ctypes.POINTER(_vp)]),
     "yr_amd_tables_get_info": (_int, [_vp, ctypes.POINTER(TablesInfo)]),
     "yr_amd_scanner_create": (_int, [_vp, _vp, ctypes.POINTER(_vp)]),
     "yr_amd_scanner_destroy": (_int, [_vp]),
