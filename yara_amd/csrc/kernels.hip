@@ -112,6 +112,10 @@ template <int MODE>
 __device__ __forceinline__ void drain(const ScanParams& p, WaveQueue& q, uint32_t lane,
                                       uint64_t seg_start, uint32_t* out, uint32_t& found) {
   const uint32_t n = min(q.tail - q.head, (uint32_t)kWave);
+  if constexpr (MODE == 7) {   // ablation: ring appends only, entries dropped
+    q.head += n;
+    return;
+  }
   __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
   uint32_t keep = 0, off0 = 0;
   if (lane < n) {
@@ -248,7 +252,7 @@ __device__ __forceinline__ void tile_step(const ScanParams& p, WaveQueue& q, Seg
       }
     }
   }
-  if constexpr (MODE >= 2) {
+  if constexpr (MODE >= 2 && MODE <= 6) {
     asm volatile("" ::"v"(acc[0] ^ acc[1] ^ acc[2] ^ acc[3]));
     return;
   }
@@ -287,7 +291,8 @@ __device__ __forceinline__ void tile_step(const ScanParams& p, WaveQueue& q, Seg
 // output is wrong by construction): 1 = no exact check, 2 = stage 1 only
 // (no queue), 3 = input streaming only (no filter), 4 = stage 1 with
 // bank-conflict-free LDS addresses, 5 = stage 1 VALU without the LDS reads,
-// 6 = stage 1 addresses + LDS reads without the bit tests.
+// 6 = stage 1 addresses + LDS reads without the bit tests, 7 = stage 1 +
+// ring appends, drains drop the entries.
 template <int MODE>
 __device__ void scan_segment(const ScanParams& p, WaveQueue& q, uint32_t seg, uint32_t lane) {
   SegState st;
@@ -315,7 +320,6 @@ __device__ void scan_segment(const ScanParams& p, WaveQueue& q, uint32_t seg, ui
   for (uint32_t t = 0; t < n_full; ++t) {
     const uint4 nxt2 = fetch(t + 2);
     tile_step<MODE, false>(p, q, st, cur, t * kTile, lane);
-    if (q.tail - q.head >= kQueueCap) drain<MODE>(p, q, lane, st.seg_start, st.out, st.found);
     cur = nxt;
     nxt = nxt2;
   }
@@ -451,6 +455,7 @@ hipError_t launch_scan(const ScanParams& p, int grid, hipStream_t s, int mode) {
     case 4: hipLaunchKernelGGL(scan_segments_kernel<4>, dim3(grid), dim3(kWGThreads), lds, s, p); break;
     case 5: hipLaunchKernelGGL(scan_segments_kernel<5>, dim3(grid), dim3(kWGThreads), lds, s, p); break;
     case 6: hipLaunchKernelGGL(scan_segments_kernel<6>, dim3(grid), dim3(kWGThreads), lds, s, p); break;
+    case 7: hipLaunchKernelGGL(scan_segments_kernel<7>, dim3(grid), dim3(kWGThreads), lds, s, p); break;
     default: hipLaunchKernelGGL(scan_segments_kernel<0>, dim3(grid), dim3(kWGThreads), lds, s, p); break;
   }
   return hipGetLastError();
@@ -481,7 +486,7 @@ hipError_t configure_scan_kernel() {
   for (const void* k : {(const void*)scan_segments_kernel<0>, (const void*)scan_segments_kernel<1>,
                         (const void*)scan_segments_kernel<2>, (const void*)scan_segments_kernel<3>,
                         (const void*)scan_segments_kernel<4>, (const void*)scan_segments_kernel<5>,
-                        (const void*)scan_segments_kernel<6>}) {
+                        (const void*)scan_segments_kernel<6>, (const void*)scan_segments_kernel<7>}) {
     hipError_t r = hipFuncSetAttribute(k, hipFuncAttributeMaxDynamicSharedMemorySize, lds);
     if (r != hipSuccess) e = r;
   }
