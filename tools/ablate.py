@@ -15,7 +15,7 @@ sys.path.insert(0, REPO)
 
 NAMES = {0: "product", 1: "no-exact-check", 2: "stage1-only", 3: "stream-only",
          4: "stage1-conflict-free-lds", 5: "stage1-valu-no-lds",
-         6: "stage1-lds-no-test", 7: "stage1+appends-no-drain"}
+         6: "stage1-lds-no-test", 7: "stage1+appends-no-drain", 8: "product-global-ring"}
 
 
 def main():
@@ -39,19 +39,20 @@ def main():
     sc.set_timing(True)
     modes = [int(m) for m in a.modes.split(",")]
     res = {m: [] for m in modes}
+    counts = {}
     for _ in range(a.rounds):
         for m in modes:
             assert L.yr_amd__diag_kernel_mode(sc.handle if hasattr(sc, "handle") else sc._h, m) == 0
             for _ in range(a.reps):
                 sc.scan_device(buf.data_ptr(), n)
-                sc.device_result()
+                counts[m] = sc.device_result()[1]
                 res[m].append(sc.kernel_ms())
     L.yr_amd__diag_kernel_mode(sc._h, 0)
     out = {}
     for m in modes:
         med = statistics.median(res[m])
         out[NAMES[m]] = {"median_ms": round(med, 4), "min_ms": round(min(res[m]), 4),
-                         "GB/s": round(n / (med * 1e-3) / 1e9, 1)}
+                         "GB/s": round(n / (med * 1e-3) / 1e9, 1), "candidates": counts[m]}
     print(json.dumps({"rules": a.rules, "bytes": n, "modes": out}, indent=1))
 
 

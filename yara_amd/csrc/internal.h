@@ -96,6 +96,7 @@ struct ScanParams {
   uint32_t seg_cap;         // output capacity (entries) per segment
   uint32_t* seg_count;      // [n_segments] candidates found (may exceed cap)
   uint32_t* seg_out;        // [n_segments * seg_cap] byte offset within segment
+  uint32_t* gring;          // hit rings in global memory (one per wave of the grid), or null
 };
 
 }  // namespace yamd

@@ -116,7 +116,10 @@ __device__ __forceinline__ void drain(const ScanParams& p, WaveQueue& q, uint32_
     q.head += n;
     return;
   }
-  __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+  if constexpr (MODE == 8)
+    __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "workgroup");   // ring in global memory
+  else
+    __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
   uint32_t keep = 0, off0 = 0;
   if (lane < n) {
     const uint32_t* ent = q.ring + ((q.head + lane) % kQueueCap) * kQueueEntryWords;
@@ -292,7 +295,8 @@ __device__ __forceinline__ void tile_step(const ScanParams& p, WaveQueue& q, Seg
 // (no queue), 3 = input streaming only (no filter), 4 = stage 1 with
 // bank-conflict-free LDS addresses, 5 = stage 1 VALU without the LDS reads,
 // 6 = stage 1 addresses + LDS reads without the bit tests, 7 = stage 1 +
-// ring appends, drains drop the entries.
+// ring appends, drains drop the entries, 8 = product with the hit rings in
+// global memory (L2) instead of LDS.
 template <int MODE>
 __device__ void scan_segment(const ScanParams& p, WaveQueue& q, uint32_t seg, uint32_t lane) {
   SegState st;
@@ -343,7 +347,10 @@ __global__ __launch_bounds__(kWGThreads, 1) void scan_segments_kernel(ScanParams
   // bounds, loop counts, ring base) stays in SGPRs with scalar branches
   const uint32_t wid = __builtin_amdgcn_readfirstlane(threadIdx.x / kWave);
   WaveQueue q;
-  q.ring = lds + kFilterWords + wid * kQueueCap * kQueueEntryWords;
+  if constexpr (MODE == 8)
+    q.ring = p.gring + ((size_t)blockIdx.x * kWavesPerWG + wid) * kQueueCap * kQueueEntryWords;
+  else
+    q.ring = lds + kFilterWords + wid * kQueueCap * kQueueEntryWords;
   const uint32_t total_waves = gridDim.x * kWavesPerWG;
   for (uint32_t seg = blockIdx.x * kWavesPerWG + wid; seg < p.n_segments; seg += total_waves) {
     scan_segment<MODE>(p, q, seg, lane);
@@ -456,6 +463,7 @@ hipError_t launch_scan(const ScanParams& p, int grid, hipStream_t s, int mode) {
     case 5: hipLaunchKernelGGL(scan_segments_kernel<5>, dim3(grid), dim3(kWGThreads), lds, s, p); break;
     case 6: hipLaunchKernelGGL(scan_segments_kernel<6>, dim3(grid), dim3(kWGThreads), lds, s, p); break;
     case 7: hipLaunchKernelGGL(scan_segments_kernel<7>, dim3(grid), dim3(kWGThreads), lds, s, p); break;
+    case 8: hipLaunchKernelGGL(scan_segments_kernel<8>, dim3(grid), dim3(kWGThreads), kFilterBytes, s, p); break;
     default: hipLaunchKernelGGL(scan_segments_kernel<0>, dim3(grid), dim3(kWGThreads), lds, s, p); break;
   }
   return hipGetLastError();
@@ -486,7 +494,8 @@ hipError_t configure_scan_kernel() {
   for (const void* k : {(const void*)scan_segments_kernel<0>, (const void*)scan_segments_kernel<1>,
                         (const void*)scan_segments_kernel<2>, (const void*)scan_segments_kernel<3>,
                         (const void*)scan_segments_kernel<4>, (const void*)scan_segments_kernel<5>,
-                        (const void*)scan_segments_kernel<6>, (const void*)scan_segments_kernel<7>}) {
+                        (const void*)scan_segments_kernel<6>, (const void*)scan_segments_kernel<7>,
+                        (const void*)scan_segments_kernel<8>}) {
     hipError_t r = hipFuncSetAttribute(k, hipFuncAttributeMaxDynamicSharedMemorySize, lds);
     if (r != hipSuccess) e = r;
   }

@@ -83,6 +83,8 @@ struct yr_amd_scanner {
   bool ev_valid = false;
 
   int diag_mode = 0;   // profiling ablation of the scan kernel (0 = product)
+  uint32_t* d_gring = nullptr;   // global-memory hit rings (diag mode 8)
+  size_t gring_cap = 0;
 
   // pre-verification workspace
   uint32_t* d_vcount = nullptr;
@@ -263,7 +265,8 @@ int yr_amd_scanner_destroy(yr_amd_scanner* s) {
   if (s->stream) (void)hipStreamSynchronize(s->stream);
   for (void* p : {(void*)s->d_block, (void*)s->d_seg_count, (void*)s->d_seg_offset,
                   (void*)s->d_seg_out, (void*)s->d_positions, (void*)s->d_summary,
-                  (void*)s->d_vcount, (void*)s->d_voffset, (void*)s->d_vchunk, (void*)s->d_vrec})
+                  (void*)s->d_vcount, (void*)s->d_voffset, (void*)s->d_vchunk, (void*)s->d_vrec,
+                  (void*)s->d_gring})
     if (p) (void)hipFree(p);
   if (s->h_summary) (void)hipHostFree(s->h_summary);
   if (s->ev_begin) (void)hipEventDestroy(s->ev_begin);
@@ -288,7 +291,7 @@ int yr_amd_scanner_set_timing(yr_amd_scanner* s, int enable) {
 // Not declared in include/yara_amd.h: profiling ablations of the scan kernel
 // (tools/ablate.py).  Any mode other than 0 produces wrong results.
 int yr_amd__diag_kernel_mode(yr_amd_scanner* s, int mode) {
-  if (s == nullptr || mode < 0 || mode > 7) return YR_AMD_INVALID_ARGUMENT;
+  if (s == nullptr || mode < 0 || mode > 8) return YR_AMD_INVALID_ARGUMENT;
   s->diag_mode = mode;
   return YR_AMD_SUCCESS;
 }
@@ -345,6 +348,13 @@ int yr_amd_scan_device(yr_amd_scanner* s, const uint8_t* d_data, uint64_t block_
   p.seg_cap = seg_cap;
   p.seg_count = s->d_seg_count;
   p.seg_out = s->d_seg_out;
+  p.gring = nullptr;
+  if (s->diag_mode == 8) {
+    r = grow(s->d_gring, s->gring_cap,
+             (size_t)t->num_cus * kWavesPerWG * kQueueCap * kQueueEntryWords);
+    if (r) return r;
+    p.gring = s->d_gring;
+  }
   s->last_grid = (int)std::min<uint64_t>((n_segments + kWavesPerWG - 1) / kWavesPerWG,
                                          (uint64_t)t->num_cus);
   return run_scan(s);
