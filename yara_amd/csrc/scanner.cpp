@@ -3,7 +3,8 @@
 // Host orchestration of one block scan (the role of libyara's
 // _yr_scanner_scan_mem_block, scanner.c:45-176):
 //   H2D (host blocks only) -> scan_segments_kernel -> seg_offsets_kernel
-//   -> [overflow retry] -> seg_scatter_kernel -> D2H of the candidate stream.
+//   -> seg_scatter_kernel (all queued; one host synchronisation)
+//   -> [overflow retry] -> D2H of the candidate stream.
 // and the host replay of candidates into the caller's verifier in the exact
 // order of scanner.c:98-122 / :144-163.
 #include <hip/hip_runtime.h>
@@ -147,13 +148,20 @@ uint32_t choose_seg_bytes(uint64_t nbytes, int num_cus) {
 }
 
 int run_scan(yr_amd_scanner* s) {
+  // scan, per-segment offsets and the scatter are queued back to back: the
+  // output is sized for the clipped worst case (every segment at capacity),
+  // so the host synchronises once, in yr_amd_scan_device_result
+  const ScanParams& p = s->last;
+  int r = grow(s->d_positions, s->positions_cap, (size_t)p.n_segments * p.seg_cap);
+  if (r) return r;
   if (s->timing) HIP_TRY(hipEventRecord(s->ev_begin, s->stream));
-  HIP_TRY(launch_scan(s->last, s->last_grid, s->stream, s->diag_mode));
+  HIP_TRY(launch_scan(p, s->last_grid, s->stream, s->diag_mode));
   if (s->timing) {
     HIP_TRY(hipEventRecord(s->ev_end, s->stream));
     s->ev_valid = true;
   }
-  HIP_TRY(launch_compact(s->last, s->d_seg_offset, s->d_summary, nullptr, false, s->stream));
+  HIP_TRY(launch_compact(p, s->d_seg_offset, s->d_summary, nullptr, false, s->stream));
+  HIP_TRY(launch_compact(p, s->d_seg_offset, s->d_summary, s->d_positions, true, s->stream));
   HIP_TRY(hipMemcpyAsync(s->h_summary, s->d_summary, 2 * sizeof(uint64_t), hipMemcpyDeviceToHost,
                          s->stream));
   return YR_AMD_SUCCESS;
@@ -385,12 +393,6 @@ int yr_amd_scan_device_result(yr_amd_scanner* s, const uint64_t** d_positions, u
     HIP_TRY(hipStreamSynchronize(s->stream));
     total = s->h_summary[0];
     if (s->h_summary[1] > cap) return YR_AMD_INTERNAL_FATAL_ERROR;
-  }
-  int r = grow(s->d_positions, s->positions_cap, total);
-  if (r) return r;
-  if (total > 0) {
-    HIP_TRY(launch_compact(s->last, s->d_seg_offset, s->d_summary, s->d_positions, true, s->stream));
-    HIP_TRY(hipStreamSynchronize(s->stream));
   }
   s->last_count = total;
   s->pending = false;
