@@ -91,6 +91,23 @@ def cpu_baseline(rules: str, sample_mib: int, seed: int):
                       "%.1f s" % (what, rules, sample_mib, seed, dt)}
 
 
+def cpu_parallel(rules: str, sample_mib: int, seed: int, threads: int):
+    """the in-repo restatement of scanner.c:45-176, one walker
+    per contiguous slice with a 4-byte warm-up, `threads` threads (reported
+    beside cpu_baseline; not the baseline itself)."""
+    sys.path.insert(0, os.path.join(REPO, "tests", "golden"))
+    import oracle
+    from conftest import ref_tables   # noqa
+    data = oracle.xorshift(sample_mib << 20, seed)
+    tab = ref_tables(rules)
+    t0 = time.perf_counter()
+    oracle.count_parallel(tab, data, threads)
+    dt = time.perf_counter() - t0
+    return {"value": round(data.size / dt / 1e9, 4), "unit": "GB/s", "cores": threads,
+            "kind": "port", "sample": "oracle/ac_oracle.c slice walkers, rule set %s, first %d MiB"
+            % (rules, sample_mib)}
+
+
 def load_traffic(kernel_bytes):
     """HBM bytes per scan-kernel launch from the committed PMC pass (profiles/)."""
     p = os.path.join(REPO, "profiles", "pmc_traffic.json")
@@ -203,9 +220,11 @@ def main():
                                      oracle.positions_sha(p) == rec["candidate_sha"])
 
     if rank == 0:
-        cpu = None
+        cpu = cpu_par = None
         if world == 1 and not args.no_cpu:
             cpu = cpu_baseline(args.rules, args.cpu_sample_mib, args.seed)
+            cpu_par = cpu_parallel(args.rules, args.cpu_sample_mib, args.seed,
+                                   min(16, os.cpu_count() or 1))
         line = {
             "metric": "scanned GB/s per GPU (4 GiB buffer, 10k atoms) + bit-exact match-set vs CPU",
             "value": round(value, 3),
@@ -231,6 +250,7 @@ def main():
                          "traffic": load_traffic(shard),
                          "kernel": "scan_segments_kernel", "kernel_ms_avg": round(k_avg, 4)},
             "cpu_baseline": cpu,
+            "cpu_port_parallel": cpu_par,
             "check": check,
         }
         print(json.dumps(line), flush=True)
