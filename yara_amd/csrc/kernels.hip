@@ -21,7 +21,7 @@
 //             are compacted with a wave ballot + mbcnt into the segment's output.
 //
 // Memory: the input is streamed once, 16 B per lane (1 KiB per wave per step),
-// tiles t+1 and t+2 in flight while tile t is filtered.  Roofline: HBM read bandwidth
+// tile t+1 in flight while tile t is filtered.  Roofline: HBM read bandwidth
 // (1 algorithmic byte per input byte).
 #include "internal.h"
 
@@ -288,8 +288,8 @@ __device__ __forceinline__ void tile_step(const ScanParams& p, WaveQueue& q, Seg
 }
 
 // Stream one segment [seg_start, seg_start + seg_len) of the block: full tiles
-// in the main loop (unmasked, two tiles of loads in flight), then the partial
-// tail tile if any.
+// in the main loop (unmasked, the next tile's loads in flight), then the
+// partial tail tile if any.
 // MODE: 0 = the product kernel.  Others are profiling ablations only (their
 // output is wrong by construction): 1 = no exact check, 2 = stage 1 only
 // (no queue), 3 = input streaming only (no filter), 4 = stage 1 with
@@ -314,18 +314,16 @@ __device__ void scan_segment(const ScanParams& p, WaveQueue& q, uint32_t seg, ui
 
   const uint32_t n_full = st.seg_len / kTile;            // tiles needing no mask / bounds
   const uint32_t n_all = (st.seg_len + kTile - 1) / kTile;
-  // two tiles of loads in flight ahead of the one being filtered
+  // the next tile's loads in flight while this one is filtered
   auto fetch = [&](uint32_t t) {
     return t < n_full ? load_tile_full(base, t * kTile, lane)
                       : (t < n_all ? load_tile(base, t * kTile, lane, avail) : make_uint4(0, 0, 0, 0));
   };
   uint4 cur = fetch(0);
-  uint4 nxt = fetch(1);
   for (uint32_t t = 0; t < n_full; ++t) {
-    const uint4 nxt2 = fetch(t + 2);
+    const uint4 nxt = fetch(t + 1);
     tile_step<MODE, false>(p, q, st, cur, t * kTile, lane);
     cur = nxt;
-    nxt = nxt2;
   }
   if (n_all > n_full) tile_step<MODE, true>(p, q, st, cur, n_full * kTile, lane);
   while (q.tail != q.head) drain<MODE>(p, q, lane, st.seg_start, st.out, st.found);
