@@ -16,6 +16,8 @@
  *   the shim's twins (scanner.c:417-722).  proc scans a stopped child process
  *   that holds the data (forked before any GPU initialisation).
  *   E2E_REPEAT = N: time N more runs of each side, report the minimum.
+ *   E2E_FAST=1: SCAN_FLAGS_FAST_MODE; E2E_ABORT=n: the callback returns
+ *   CALLBACK_ABORT on the n-th matching rule (scanner.c:540-548).
  */
 #include <stdint.h>
 #include <stdio.h>
@@ -43,6 +45,9 @@ typedef struct
   uint8_t* rule_msg; /* 1 matching, 2 not matching */
   int dumped;
   int finished;
+  int abort_after; /* E2E_ABORT=n: CALLBACK_ABORT on the n-th RULE_MATCHING */
+  int n_matching;
+  int too_many;    /* CALLBACK_MSG_TOO_MANY_MATCHES messages seen */
 } collect;
 
 static void push(collect* c, rec x)
@@ -79,6 +84,13 @@ static int cb(YR_SCAN_CONTEXT* ctx, int msg, void* data, void* user)
   {
     c->finished = 1;
   }
+  else if (msg == CALLBACK_MSG_TOO_MANY_MATCHES)
+  {
+    c->too_many++;
+  }
+  if (msg == CALLBACK_MSG_RULE_MATCHING && c->abort_after > 0 &&
+      ++c->n_matching >= c->abort_after)
+    return CALLBACK_ABORT;
   return CALLBACK_CONTINUE;
 }
 
@@ -177,7 +189,10 @@ static int run(YR_RULES* rules, YR_GPU_SCANNER* gs, const uint8_t* data, size_t 
   YR_SCANNER* sc;
   int r = yr_scanner_create(rules, &sc);
   if (r) return r;
-  yr_scanner_set_flags(sc, SCAN_FLAGS_REPORT_RULES_MATCHING | SCAN_FLAGS_REPORT_RULES_NOT_MATCHING);
+  int flags = SCAN_FLAGS_REPORT_RULES_MATCHING | SCAN_FLAGS_REPORT_RULES_NOT_MATCHING;
+  if (getenv("E2E_FAST") && strcmp(getenv("E2E_FAST"), "1") == 0) flags |= SCAN_FLAGS_FAST_MODE;
+  yr_scanner_set_flags(sc, flags);
+  c->abort_after = getenv("E2E_ABORT") ? atoi(getenv("E2E_ABORT")) : 0;
   yr_scanner_set_callback(sc, cb, c);
   double t0 = now();
   if (strcmp(g_mode, "file") == 0 && c->rules != NULL && data == NULL)
@@ -320,9 +335,9 @@ int main(int argc, char** argv)
   printf("{\"mode\": \"%s\", \"size\": %zu, \"block\": %zu, \"rc_stock\": %d, \"rc_gpu\": %d, "
          "\"matches_stock\": %zu, \"matches_gpu\": %zu, \"rules_matching\": %d, "
          "\"same_matches\": %s, \"same_rule_reports\": %s, \"finished\": [%d, %d], "
-         "\"stock_s\": %.4f, \"gpu_s\": %.4f}\n",
+         "\"stock_s\": %.4f, \"gpu_s\": %.4f, \"too_many\": [%d, %d]}\n",
          g_mode, n, bsize, rs, rg, a.n, b.n, n_match_rules, same_matches ? "true" : "false",
-         same_rules ? "true" : "false", a.finished, b.finished, ts, tg);
+         same_rules ? "true" : "false", a.finished, b.finished, ts, tg, a.too_many, b.too_many);
   yr_gpu_scanner_destroy(gs);
   yr_gpu_rules_destroy(gr);
   yr_rules_destroy(rules);

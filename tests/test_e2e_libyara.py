@@ -38,9 +38,9 @@ def _rules_file(tmp_path, name):
     return str(p)
 
 
-def _run(rules, data_spec, block=0, overlap=0, preverify=True, mode="mem"):
+def _run(rules, data_spec, block=0, overlap=0, preverify=True, mode="mem", **extra):
     cmd = [CHECK, rules, data_spec] + ([str(block), str(overlap)] if block else [])
-    env = dict(os.environ, E2E_PREVERIFY="1" if preverify else "0", E2E_MODE=mode)
+    env = dict(os.environ, E2E_PREVERIFY="1" if preverify else "0", E2E_MODE=mode, **extra)
     r = subprocess.run(cmd, capture_output=True, text=True, timeout=600, env=env)
     assert r.stdout, r.stderr
     res = json.loads(r.stdout.strip().splitlines()[-1])
@@ -119,3 +119,28 @@ def test_file_fd_proc_entry_points_equal_stock(tmp_path, rules, mode):
     assert res["same_matches"] and res["same_rule_reports"], res
     assert res["matches_stock"] > 0, res
     assert rc == 0
+
+
+@needs_check
+@pytest.mark.parametrize("preverify", [True, False], ids=["preverify", "full-replay"])
+def test_fast_mode_abort_and_too_many_matches(tmp_path, preverify):
+    """Scanner semantics that depend on the order and effect of the verify
+    calls: SCAN_FLAGS_FAST_MODE (scan.c:1019-1021), CALLBACK_ABORT from the
+    rule-report loop (scanner.c:540-548), and strings disabled after
+    YR_MAX_STRING_MATCHES with CALLBACK_MSG_TOO_MANY_MATCHES (scan.c:1055-1076)."""
+    lit = _rules_file(tmp_path, "lit")
+    spec = _data_file(tmp_path, planted.lit_buffer(oracle.xorshift, 2 << 20, 13), "d.bin")
+    for extra in ({"E2E_FAST": "1"}, {"E2E_ABORT": "2"}, {"E2E_FAST": "1", "E2E_ABORT": "3"}):
+        rc, res = _run(lit, spec, preverify=preverify, **extra)
+        assert res["rc_stock"] == 0 and res["rc_gpu"] == 0, (extra, res)
+        assert res["same_matches"] and res["same_rule_reports"], (extra, res)
+        want_finished = [0, 0] if "E2E_ABORT" in extra else [1, 1]
+        assert res["finished"] == want_finished, (extra, res)
+    # > 1,000,000 matches of "a" in 16 MiB of the 15-letter alphabet buffer
+    short = _rules_file(tmp_path, "short")
+    x = oracle.xorshift(16 << 20, 5)
+    spec = _data_file(tmp_path, np.frombuffer(ALPHA, np.uint8)[x % len(ALPHA)], "a.bin")
+    rc, res = _run(short, spec, preverify=preverify)
+    assert res["rc_stock"] == 0 and res["rc_gpu"] == 0, res
+    assert res["too_many"][0] > 0 and res["too_many"] == [res["too_many"][0]] * 2, res
+    assert res["same_matches"] and res["same_rule_reports"], res
