@@ -98,6 +98,27 @@ def test_ragged_sizes_vs_oracle(rules, size):
     np.testing.assert_array_equal(pos, oracle.candidates(tab, data))
 
 
+@pytest.mark.parametrize("hot_mib", [1, 3])
+def test_skewed_candidate_density(hot_mib):
+    """One dense region (every byte a candidate of a 1-byte key) inside random
+    data: a few segments overflow their capacity by orders of magnitude; the
+    exact-offset rerun must still give the oracle's stream, and the scanner
+    must stay usable for a normal block afterwards."""
+    size = 64 << 20
+    data = oracle.xorshift(size, 31).copy()
+    lo = 20 << 20
+    data[lo:lo + (hot_mib << 20)] = ord("a")
+    tab = ref_tables("short")
+    sc = yara_amd.Scanner(dev_tables("short"))
+    pos, allp = sc.candidates(data)
+    assert not allp
+    ref = oracle.candidates(tab, data)
+    assert len(pos) > (hot_mib << 20)
+    np.testing.assert_array_equal(pos, ref)
+    small = oracle.xorshift(1 << 20, 32)
+    np.testing.assert_array_equal(sc.candidates(small)[0], oracle.candidates(tab, small))
+
+
 @pytest.mark.parametrize("period", [16, 1024, 4096, 65536])
 def test_atoms_ending_on_slice_boundaries(period):
     """Adversarial: atoms end exactly at lane/tile/segment edges (+-1 byte)."""

@@ -303,7 +303,7 @@ __device__ void scan_segment(const ScanParams& p, WaveQueue& q, uint32_t seg, ui
   st.seg_start = p.byte_begin + (uint64_t)seg * p.seg_bytes;
   const uint64_t seg_end = min(st.seg_start + p.seg_bytes, p.byte_end);
   st.seg_len = (uint32_t)(seg_end - st.seg_start);
-  st.out = p.seg_out + (size_t)seg * p.seg_cap;
+  st.out = p.seg_out + (p.seg_base ? p.seg_base[seg] : (size_t)seg * p.seg_cap);
   st.found = 0;
   const uint64_t avail = p.block_size - st.seg_start;
   const uint8_t* base = p.data + st.seg_start;
@@ -398,13 +398,14 @@ __global__ __launch_bounds__(1024) void seg_offsets_kernel(const uint32_t* seg_c
 
 __global__ __launch_bounds__(256) void seg_scatter_kernel(const uint32_t* seg_count,
                                                           const uint32_t* seg_out,
+                                                          const uint64_t* seg_base,
                                                           const uint64_t* seg_offset, uint32_t cap,
                                                           uint64_t byte_begin, uint32_t seg_bytes,
                                                           uint64_t* positions) {
   const uint32_t seg = blockIdx.x;
   const uint32_t c = min(seg_count[seg], cap);
   const uint64_t base = byte_begin + (uint64_t)seg * seg_bytes + 1;  // position = byte + 1
-  const uint32_t* src = seg_out + (size_t)seg * cap;
+  const uint32_t* src = seg_out + (seg_base ? seg_base[seg] : (size_t)seg * cap);
   uint64_t* dst = positions + seg_offset[seg];
   for (uint32_t i = threadIdx.x; i < c; i += blockDim.x) dst[i] = base + src[i];
 }
@@ -474,7 +475,8 @@ hipError_t launch_compact(const ScanParams& p, uint64_t* seg_offset, uint64_t* s
                        p.seg_cap, seg_offset, summary);
   } else {
     hipLaunchKernelGGL(seg_scatter_kernel, dim3(p.n_segments), dim3(256), 0, s, p.seg_count,
-                       p.seg_out, seg_offset, p.seg_cap, p.byte_begin, p.seg_bytes, positions);
+                       p.seg_out, p.seg_base, seg_offset, p.seg_cap, p.byte_begin, p.seg_bytes,
+                       positions);
   }
   return hipGetLastError();
 }

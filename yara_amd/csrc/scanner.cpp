@@ -86,6 +86,9 @@ struct yr_amd_scanner {
   int diag_mode = 0;   // profiling ablation of the scan kernel (0 = product)
   uint32_t* d_gring = nullptr;   // global-memory hit rings (diag mode 8)
   size_t gring_cap = 0;
+  uint64_t* d_seg_base = nullptr; // exact per-segment output offsets (overflow rerun)
+  size_t seg_base_cap = 0;
+  uint64_t rerun_total = 0;
 
   // pre-verification workspace
   uint32_t* d_vcount = nullptr;
@@ -152,7 +155,8 @@ int run_scan(yr_amd_scanner* s) {
   // output is sized for the clipped worst case (every segment at capacity),
   // so the host synchronises once, in yr_amd_scan_device_result
   const ScanParams& p = s->last;
-  int r = grow(s->d_positions, s->positions_cap, (size_t)p.n_segments * p.seg_cap);
+  int r = grow(s->d_positions, s->positions_cap,
+               p.seg_base ? s->rerun_total : (size_t)p.n_segments * p.seg_cap);
   if (r) return r;
   if (s->timing) HIP_TRY(hipEventRecord(s->ev_begin, s->stream));
   HIP_TRY(launch_scan(p, s->last_grid, s->stream, s->diag_mode));
@@ -274,7 +278,7 @@ int yr_amd_scanner_destroy(yr_amd_scanner* s) {
   for (void* p : {(void*)s->d_block, (void*)s->d_seg_count, (void*)s->d_seg_offset,
                   (void*)s->d_seg_out, (void*)s->d_positions, (void*)s->d_summary,
                   (void*)s->d_vcount, (void*)s->d_voffset, (void*)s->d_vchunk, (void*)s->d_vrec,
-                  (void*)s->d_gring})
+                  (void*)s->d_gring, (void*)s->d_seg_base})
     if (p) (void)hipFree(p);
   if (s->h_summary) (void)hipHostFree(s->h_summary);
   if (s->ev_begin) (void)hipEventDestroy(s->ev_begin);
@@ -357,6 +361,7 @@ int yr_amd_scan_device(yr_amd_scanner* s, const uint8_t* d_data, uint64_t block_
   p.seg_count = s->d_seg_count;
   p.seg_out = s->d_seg_out;
   p.gring = nullptr;
+  p.seg_base = nullptr;
   if (s->diag_mode == 8) {
     r = grow(s->d_gring, s->gring_cap,
              (size_t)t->num_cus * kWavesPerWG * kQueueCap * kQueueEntryWords);
@@ -382,17 +387,29 @@ int yr_amd_scan_device_result(yr_amd_scanner* s, const uint64_t** d_positions, u
   uint64_t total = s->h_summary[0];
   const uint64_t maxc = s->h_summary[1];
   if (maxc > s->last.seg_cap) {
-    // some segment overflowed: rerun once with the exact capacity needed
-    const uint32_t cap = (uint32_t)maxc;
-    int r = ensure_segments(s, s->last.n_segments, cap);
+    // some segment overflowed its capacity: rerun once with every segment
+    // writing at its exact offset (counts are kept past the capacity), so the
+    // workspace is exactly the candidate count however skewed the segments
+    ScanParams exact = s->last;
+    exact.seg_cap = 0xFFFFFFFFu;
+    HIP_TRY(launch_compact(exact, s->d_seg_offset, s->d_summary, nullptr, false, s->stream));
+    HIP_TRY(hipMemcpyAsync(s->h_summary, s->d_summary, 2 * sizeof(uint64_t),
+                           hipMemcpyDeviceToHost, s->stream));
+    HIP_TRY(hipStreamSynchronize(s->stream));
+    total = s->h_summary[0];
+    int r = grow(s->d_seg_out, s->seg_out_cap, std::max<uint64_t>(total, 1));
+    if (!r) r = grow(s->d_seg_base, s->seg_base_cap, s->last.n_segments);
     if (r) return r;
-    s->last.seg_cap = cap;
+    HIP_TRY(hipMemcpyAsync(s->d_seg_base, s->d_seg_offset, s->last.n_segments * sizeof(uint64_t),
+                           hipMemcpyDeviceToDevice, s->stream));
     s->last.seg_out = s->d_seg_out;
+    s->last.seg_base = s->d_seg_base;
+    s->last.seg_cap = 0xFFFFFFFFu;
+    s->rerun_total = std::max<uint64_t>(total, 1);
     r = run_scan(s);
     if (r) return r;
     HIP_TRY(hipStreamSynchronize(s->stream));
-    total = s->h_summary[0];
-    if (s->h_summary[1] > cap) return YR_AMD_INTERNAL_FATAL_ERROR;
+    if (s->h_summary[0] != total) return YR_AMD_INTERNAL_FATAL_ERROR;
   }
   s->last_count = total;
   s->pending = false;
