@@ -42,7 +42,7 @@ def parse():
     ap.add_argument("--rules", default="C", help="rule set (tests/golden/tables/<name>.npz)")
     ap.add_argument("--gib-per-gpu", type=float, default=4.0)
     ap.add_argument("--seed", type=int, default=1)
-    ap.add_argument("--cpu-sample-mib", type=int, default=1024)
+    ap.add_argument("--cpu-sample-mib", type=int, default=3072)
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--no-check", action="store_true")
     ap.add_argument("--backend", default="nccl", help="nccl (= RCCL) or gloo (rehearsal)")

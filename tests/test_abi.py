@@ -167,3 +167,68 @@ def test_scanner_on_host_only_tables_is_invalid():
 
 def test_version():
     assert "gfx950" in yara_amd.version()
+
+
+def _host_tables(name="lit"):
+    return yara_amd.Tables.from_npz(tables_npz(name), device=-1)
+
+
+def test_set_strings_validates_before_touching_the_device():
+    """yr_amd_tables_set_strings: pool/string indexes and byte ranges are checked
+    (ERROR_INVALID_ARGUMENT), and host-only tables cannot carry device strings."""
+    L = _lib.lib()
+    z = np.load(tables_npz("lit"))
+    t = _host_tables()
+    n_pool, n_str = len(z["pool_string"]), len(z["str_flags"])
+    recs = (_lib.String * n_str)()
+    blob = np.zeros(64, np.uint8)
+    low = np.arange(256, dtype=np.uint8)
+    ps = np.ascontiguousarray(z["pool_string"], np.uint32)
+    u8 = lambda a: a.ctypes.data_as(_lib._u8p)  # noqa: E731
+    u32 = lambda a: a.ctypes.data_as(_lib._u32p)  # noqa: E731
+    # wrong pool size
+    assert L.yr_amd_tables_set_strings(t.handle, u32(ps), n_pool - 1, recs, n_str, u8(blob), 64,
+                                       u8(low)) == yara_amd.INVALID_ARGUMENT
+    # string index out of range
+    bad = ps.copy()
+    bad[0] = n_str
+    assert L.yr_amd_tables_set_strings(t.handle, u32(bad), n_pool, recs, n_str, u8(blob), 64,
+                                       u8(low)) == yara_amd.INVALID_ARGUMENT
+    # bytes out of range
+    recs[0].length, recs[0].bytes_offset = 10, 60
+    assert L.yr_amd_tables_set_strings(t.handle, u32(ps), n_pool, recs, n_str, u8(blob), 64,
+                                       u8(low)) == yara_amd.INVALID_ARGUMENT
+    recs[0].length, recs[0].bytes_offset = 0, 0
+    # valid, but host-only tables
+    assert L.yr_amd_tables_set_strings(t.handle, u32(ps), n_pool, recs, n_str, u8(blob), 64,
+                                       u8(low)) == yara_amd.INVALID_ARGUMENT
+    # missing lowercase table / null tables
+    assert L.yr_amd_tables_set_strings(t.handle, u32(ps), n_pool, recs, n_str, u8(blob), 64,
+                                       None) == yara_amd.INVALID_ARGUMENT
+    assert L.yr_amd_tables_set_strings(None, u32(ps), n_pool, recs, n_str, u8(blob), 64,
+                                       u8(low)) == yara_amd.INVALID_ARGUMENT
+
+
+def test_set_re_code_requires_strings():
+    L = _lib.lib()
+    t = _host_tables("hex")
+    n = len(np.load(tables_npz("hex"))["pool_next"])
+    z = np.zeros(n, np.uint32)
+    code = np.array([0xAD], np.uint8)
+    assert L.yr_amd_tables_set_re_code(
+        t.handle, n, *[z.ctypes.data_as(_lib._u32p)] * 4, code.ctypes.data_as(_lib._u8p),
+        1) == yara_amd.INVALID_ARGUMENT
+
+
+def test_pipeline_and_verify_reject_bad_handles():
+    L = _lib.lib()
+    p = ctypes.c_void_p()
+    assert L.yr_amd_pipeline_create(None, 2, ctypes.byref(p)) == yara_amd.INVALID_ARGUMENT
+    t = _host_tables()
+    assert L.yr_amd_pipeline_create(t.handle, 0, ctypes.byref(p)) == yara_amd.INVALID_ARGUMENT
+    assert L.yr_amd_pipeline_create(t.handle, 9, ctypes.byref(p)) == yara_amd.INVALID_ARGUMENT
+    assert L.yr_amd_pipeline_submit(None, None, 0, 0) == yara_amd.INVALID_ARGUMENT
+    assert L.yr_amd_pipeline_next(None, None, None, None, None, None) == yara_amd.INVALID_ARGUMENT
+    assert L.yr_amd_pipeline_destroy(None) == yara_amd.SUCCESS
+    assert L.yr_amd_verify_device(None, 0, None, None) == yara_amd.INVALID_ARGUMENT
+    assert L.yr_amd_scan_block_verified(None, None, 0, 0, None, None) == yara_amd.INVALID_ARGUMENT
