@@ -94,10 +94,10 @@ __device__ __forceinline__ uint32_t window4(const uint32_t (&C)[5], uint32_t j) 
 // Lane byte (0..15) of bit b of a tile hit mask: bit 8n + r <=> byte 4n + r.
 __device__ __forceinline__ uint32_t mask_position(uint32_t b) { return ((b >> 3) << 2) | (b & 3u); }
 
-// Per-wave LDS ring of filter hits awaiting the exact check.  One 32-byte
-// entry per (tile, lane) with at least one hit: the lane's window context
-// (4 bytes before it + its 16 bytes), lane byte offset in segment / 16, and
-// the hit mask (mask_position() layout).  Entries are appended in lane order, so ring order
+// Per-wave LDS ring of filter hits awaiting the exact check.  One entry (32-byte
+// slot, 24 bytes written) per (tile, lane) with at least one hit: the lane's
+// window context (4 bytes before it + its 16 bytes) and (lane byte offset in
+// segment / 16) | (16-bit hit mask, bit j = lane byte j) << 16.  Entries are appended in lane order, so ring order
 // is ascending position order.  The exact check then needs no global load
 // of the input, only the hash-table probes.
 struct WaveQueue {
@@ -124,12 +124,12 @@ __device__ __forceinline__ void drain(const ScanParams& p, WaveQueue& q, uint32_
   if (lane < n) {
     const uint32_t* ent = q.ring + ((q.head + lane) % kQueueCap) * kQueueEntryWords;
     const uint4 a = *reinterpret_cast<const uint4*>(ent);
-    const uint4 b = *reinterpret_cast<const uint4*>(ent + 4);
+    const uint2 b = *reinterpret_cast<const uint2*>(ent + 4);
     const uint32_t C[5] = {a.x, a.y, a.z, a.w, b.x};
-    off0 = b.y * kBytesPerLane;
-    uint32_t m = b.z;
+    off0 = (b.y & 0xFFFFu) * kBytesPerLane;
+    uint32_t m = b.y >> 16;   // 16-bit mask, bit j = lane byte j
     while (m) {
-      const uint32_t j = mask_position((uint32_t)__builtin_ctz(m));
+      const uint32_t j = (uint32_t)__builtin_ctz(m);
       m &= m - 1;
       const bool hit = MODE == 1 ? ((off0 + j) & 1023u) == 7u
                                  : exact_check(window4(C, j), seg_start + off0 + j + 1, p);
@@ -279,9 +279,13 @@ __device__ __forceinline__ void tile_step(const ScanParams& p, WaveQueue& q, Seg
       const uint32_t below = __builtin_amdgcn_mbcnt_hi((uint32_t)(any >> 32),
                                                        __builtin_amdgcn_mbcnt_lo((uint32_t)any, 0u));
       uint32_t* ent = q.ring + ((q.tail + below) % kQueueCap) * kQueueEntryWords;
+      // 24-byte entry (b128 + b64: 19 LDS transfer cycles instead of 26):
+      // context, then (lane index in segment) | (16-bit mask) << 16; the mask's
+      // nibbles (bit 8n + r) are packed: t = m | m >> 4 has them in bytes 0, 2
+      const uint32_t t = mask | (mask >> 4);
+      const uint32_t m16 = __builtin_amdgcn_perm(0u, t, 0x0c0c0200u);   // bytes 0, 2
       *reinterpret_cast<uint4*>(ent) = make_uint4(S[0], S[1], S[2], S[3]);
-      *reinterpret_cast<uint4*>(ent + 4) =
-          make_uint4(S[4], lane_off / kBytesPerLane, mask, 0u);
+      *reinterpret_cast<uint2*>(ent + 4) = make_uint2(S[4], (lane_off / kBytesPerLane) | (m16 << 16));
     }
     q.tail += n;
   }
