@@ -158,7 +158,8 @@ def main():
     torch.cuda.synchronize()
 
     tables = yara_amd.Tables.from_npz(os.path.join(REPO, "tests", "golden", "tables",
-                                                   "%s.npz" % args.rules), device=dev.index)
+                                                   "%s.npz" % args.rules), device=dev.index,
+                                      strings=True)
     stream = torch.cuda.Stream(device=dev)
     scanner = yara_amd.Scanner(tables, stream=stream.cuda_stream)
     block = end - lo
@@ -204,6 +205,22 @@ def main():
 
     # parity spot check of this run's own output (rank 0): ascending and the
     # candidate count of config C at 4 GiB recorded from the reference run
+    # on-device pre-verification of the last step's candidates (SURVEY.md §8f
+    # rows 1 and 4; not part of the timed step): how many of the reference's
+    # verify calls can have an effect, and what it costs on the GPU
+    preverify = None
+    if rank == 0 and world == 1:
+        scanner.scan_device(buf.data_ptr(), block, halo, block)
+        scanner.device_result()
+        torch.cuda.synchronize()
+        scanner.verify_device(0)                    # workspace allocation
+        t0 = time.perf_counter()
+        _, n_rec = scanner.verify_device(0)
+        preverify = {"records": int(n_rec), "ms": round((time.perf_counter() - t0) * 1e3, 3),
+                     "what": "verify calls left for the host after on-device literal/hex "
+                             "pre-verification of the candidates (yr_amd_verify_device, "
+                             "synchronous, wall clock)"}
+
     check = None
     if rank == 0 and not args.no_check:
         if world == 1:
@@ -254,6 +271,7 @@ def main():
                          "kernel": "scan_segments_kernel", "kernel_ms_avg": round(k_avg, 4)},
             "cpu_baseline": cpu,
             "cpu_port_parallel": cpu_par,
+            "preverify": preverify,
             "check": check,
         }
         print(json.dumps(line), flush=True)
