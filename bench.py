@@ -52,6 +52,16 @@ def parse():
     return ap.parse_args()
 
 
+def cpu_model() -> str:
+    try:
+        for line in open("/proc/cpuinfo"):
+            if line.startswith("model name"):
+                return line.split(":", 1)[1].strip()
+    except OSError:
+        pass
+    return "unknown CPU"
+
+
 def cpu_baseline(rules: str, sample_mib: int, seed: int):
     """Stock reference libyara yr_rules_scan_mem on the host (kind "reference"),
     or the in-repo restatement of scanner.c:45-176 (kind "port") if the
@@ -91,7 +101,8 @@ def cpu_baseline(rules: str, sample_mib: int, seed: int):
         kind, what = "port", "in-repo restatement of scanner.c:45-176 (oracle/ac_oracle.c)"
     return {"value": round(n / dt / 1e9, 4), "unit": "GB/s", "cores": 1, "kind": kind,
             "sample": "%s, rule set %s, first %d MiB of the xorshift64 seed-%d input, 1 thread, "
-                      "%.1f s" % (what, rules, sample_mib, seed, dt)}
+                      "%.1f s, %s (nproc %d)" % (what, rules, sample_mib, seed, dt, cpu_model(),
+                                                 os.cpu_count() or 0)}
 
 
 def cpu_parallel(rules: str, sample_mib: int, seed: int, threads: int):
