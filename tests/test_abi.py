@@ -158,6 +158,30 @@ def test_rejects_cyclic_match_pool():
     assert e.value.code == _lib.INVALID_ARGUMENT
 
 
+def test_rejects_failure_links_that_do_not_shorten_and_rows_past_the_table():
+    """The walk follows T[state] >> 9 (scanner.c:124-141): a failure link to a
+    state that is not shallower could loop forever, a row past the end of T
+    would read out of bounds -- both are rejected at creation."""
+    T = np.zeros(1024, np.uint32)
+    M = np.zeros(1024, np.uint32)
+    T[0x41 + 1] = (512 << 9) | (0x41 + 1)   # root --'A'--> slot 512
+    M[512] = 1
+    _mk(T, M, nx=[0], bt=[1])                # failure of 512 = root: fine
+    T2 = T.copy()
+    T2[512] = 512 << 9                       # failure link to itself
+    with pytest.raises(yara_amd.YaraAmdError) as e:
+        _mk(T2, M, nx=[0], bt=[1])
+    assert e.value.code == _lib.INVALID_ARGUMENT
+    T3 = T.copy()
+    T3[512] = 5000 << 9                      # failure link outside T
+    with pytest.raises(yara_amd.YaraAmdError) as e:
+        _mk(T3, M, nx=[0], bt=[1])
+    assert e.value.code == _lib.INVALID_ARGUMENT
+    with pytest.raises(yara_amd.YaraAmdError) as e:   # state row 512..768 past n = 700
+        _mk(T[:700].copy(), M[:700].copy(), nx=[0], bt=[1])
+    assert e.value.code == _lib.INVALID_ARGUMENT
+
+
 def test_scanner_on_host_only_tables_is_invalid():
     t = yara_amd.Tables.from_npz(tables_npz("B"), device=-1)
     with pytest.raises(yara_amd.YaraAmdError) as e:

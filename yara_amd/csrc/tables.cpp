@@ -143,6 +143,21 @@ int flatten_tables(const uint32_t* T, const uint32_t* M, uint32_t n_slots,
       nodes.push_back(n);
     }
   }
+  // the walk (scanner.c:124-141, replayed by ac_step and the verify kernel)
+  // reads T[state + byte + 1] and follows failure links T[state] >> 9: every
+  // state's 256-slot row must lie inside T, and every failure link must lead
+  // to a shallower state, so the walk stays in bounds and terminates
+  {
+    std::vector<int16_t> depth_of(n_slots, -1);
+    for (const Node& n : nodes) depth_of[n.slot] = (int16_t)n.depth;
+    for (const Node& n : nodes) {
+      if ((uint64_t)n.slot + 256 >= n_slots) return YR_AMD_INVALID_ARGUMENT;
+      if (n.depth == 0) continue;
+      const uint32_t f = T[n.slot] >> 9;
+      if (f >= n_slots || depth_of[f] < 0 || (uint32_t)depth_of[f] >= n.depth)
+        return YR_AMD_INVALID_ARGUMENT;
+    }
+  }
   out.n_states = (uint32_t)nodes.size();
   for (const Node& n : nodes) {
     out.by_depth[n.depth]++;
