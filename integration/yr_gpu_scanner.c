@@ -56,6 +56,7 @@ struct YR_GPU_SCANNER
   yr_amd_pipeline* pipe; /* blocks in flight on the GPU (preverify path) */
   uint32_t depth;
   uint32_t inflight;
+  int direct;            /* single in-memory block (scan_mem): no staging copy */
 };
 
 /* Length (incl. MATCH) of a linear fast-exec program (the opcodes
@@ -389,6 +390,42 @@ static int _pipeline_block(
   return ERROR_SUCCESS;
 }
 
+/* A block the caller keeps valid and in memory for the whole scan (the one
+ * block of yr_gpu_scanner_scan_mem): no staging copy -- H2D straight from the
+ * caller's buffer, pre-verification, replay of the effective calls.  Reads of
+ * the block during the replay stay inside YR_TRYCATCH as in scanner.c:493-496. */
+static int _direct_block(
+    YR_SCANNER* scanner,
+    YR_GPU_SCANNER* gs,
+    const uint8_t* data,
+    YR_MEMORY_BLOCK* block)
+{
+  int result = ERROR_SUCCESS;
+  if (scanner->timeout > 0 &&
+      yr_stopwatch_elapsed_ns(&scanner->stopwatch) > scanner->timeout)
+    return ERROR_SCAN_TIMEOUT;
+  const yr_amd_verify_rec* recs = NULL;
+  uint64_t n = 0;
+  FAIL_ON_ERROR(yr_amd_scan_block_verified(gs->scanner, data, block->size, block->base, &recs, &n));
+  if (scanner->timeout > 0 &&
+      yr_stopwatch_elapsed_ns(&scanner->stopwatch) > scanner->timeout)
+    return ERROR_SCAN_TIMEOUT;
+  YR_TRYCATCH(
+      !(scanner->flags & SCAN_FLAGS_NO_TRYCATCH),
+      {
+        for (uint64_t c = 0; c < n && result == ERROR_SUCCESS; c++)
+          result = yr_scan_verify_match(
+              scanner,
+              &scanner->rules->ac_match_pool[recs[c].pool_index],
+              data,
+              block->size,
+              block->base,
+              (size_t) recs[c].offset);
+      },
+      { result = ERROR_COULD_NOT_MAP_FILE; });
+  return result;
+}
+
 /* _yr_scanner_clean_matches (scanner.c:178-203) is static: same memsets. */
 static void _clean_matches(YR_SCANNER* scanner)
 {
@@ -466,8 +503,12 @@ int yr_gpu_scanner_scan_mem_blocks(
           {});
     }
 
-    result = gs->preverify ? _pipeline_block(scanner, gs, data, block)
-                           : _yr_gpu_scan_mem_block(scanner, gs, data, block);
+    if (!gs->preverify)
+      result = _yr_gpu_scan_mem_block(scanner, gs, data, block);
+    else if (gs->direct)
+      result = _direct_block(scanner, gs, data, block);
+    else
+      result = _pipeline_block(scanner, gs, data, block);
     if (result != ERROR_SUCCESS) goto _exit;
     block = iterator->next(iterator);
   }
@@ -560,12 +601,12 @@ static const uint8_t* _fetch(YR_MEMORY_BLOCK* b)
   return (const uint8_t*) b->context;
 }
 
-/* yr_scanner_scan_mem (scanner.c:633-671) with the GPU driver. */
-int yr_gpu_scanner_scan_mem(
+static int _scan_mem(
     YR_SCANNER* scanner,
     YR_GPU_SCANNER* gs,
     const uint8_t* buffer,
-    size_t buffer_size)
+    size_t buffer_size,
+    int direct)
 {
   YR_MEMORY_BLOCK block;
   YR_MEMORY_BLOCK_ITERATOR iterator;
@@ -578,7 +619,22 @@ int yr_gpu_scanner_scan_mem(
   iterator.next = _next_block;
   iterator.file_size = _file_size;
   iterator.last_error = ERROR_SUCCESS;
-  return yr_gpu_scanner_scan_mem_blocks(scanner, gs, &iterator);
+  gs->direct = direct;
+  int result = yr_gpu_scanner_scan_mem_blocks(scanner, gs, &iterator);
+  gs->direct = 0;
+  return result;
+}
+
+/* yr_scanner_scan_mem (scanner.c:633-671) with the GPU driver: the caller's
+ * buffer is ordinary memory, valid for the whole call, so it is scanned in
+ * place (no staging copy). */
+int yr_gpu_scanner_scan_mem(
+    YR_SCANNER* scanner,
+    YR_GPU_SCANNER* gs,
+    const uint8_t* buffer,
+    size_t buffer_size)
+{
+  return _scan_mem(scanner, gs, buffer, buffer_size, 1);
 }
 
 /* yr_scanner_scan_file (scanner.c:674-688): map, scan, unmap. */
@@ -588,7 +644,7 @@ int yr_gpu_scanner_scan_file(YR_SCANNER* scanner, YR_GPU_SCANNER* gs, const char
   int result = yr_filemap_map(filename, &mfile);
   if (result == ERROR_SUCCESS)
   {
-    result = yr_gpu_scanner_scan_mem(scanner, gs, mfile.data, mfile.size);
+    result = _scan_mem(scanner, gs, mfile.data, mfile.size, 0);   /* mmap: copy under TRYCATCH */
     yr_filemap_unmap(&mfile);
   }
   return result;
@@ -601,7 +657,7 @@ int yr_gpu_scanner_scan_fd(YR_SCANNER* scanner, YR_GPU_SCANNER* gs, YR_FILE_DESC
   int result = yr_filemap_map_fd(fd, 0, 0, &mfile);
   if (result == ERROR_SUCCESS)
   {
-    result = yr_gpu_scanner_scan_mem(scanner, gs, mfile.data, mfile.size);
+    result = _scan_mem(scanner, gs, mfile.data, mfile.size, 0);
     yr_filemap_unmap_fd(&mfile);
   }
   return result;
