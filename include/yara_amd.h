@@ -246,10 +246,13 @@ int yr_amd_tables_set_strings(
  * pool entry k, forward code = code[fwd_off[k] .. + fwd_len[k]) (a copy of
  * rules->ac_match_pool[k].forward_code up to and including RE_OPCODE_MATCH),
  * backward code likewise (bwd_len[k] = 0: backward_code == NULL);
- * fwd_len[k] = 0: no program (the call is always kept).  Programs may only use
- * the opcodes yr_re_fast_exec executes (re.c:2150-2391): ANY, LITERAL,
- * NOT_LITERAL, MASKED_LITERAL, MASKED_NOT_LITERAL, REPEAT_ANY_UNGREEDY, MATCH;
- * YR_AMD_INVALID_ARGUMENT otherwise.  Requires yr_amd_tables_set_strings first.
+ * fwd_len[k] = 0: no program (the call is always kept).  For FAST_REGEXP
+ * strings the program must be linear in the opcodes yr_re_fast_exec executes
+ * (re.c:2150-2391): ANY, LITERAL, NOT_LITERAL, MASKED_LITERAL,
+ * MASKED_NOT_LITERAL, REPEAT_ANY_UNGREEDY, MATCH; for other regexp strings any
+ * well-formed yr_re_exec program (re.c:1693) whose reachable instructions span
+ * exactly the given length (yr_amd_re_code_extent).  YR_AMD_INVALID_ARGUMENT
+ * otherwise.  Requires yr_amd_tables_set_strings first.
  */
 int yr_amd_tables_set_re_code(
     yr_amd_tables* tables,
@@ -260,6 +263,15 @@ int yr_amd_tables_set_re_code(
     const uint32_t* bwd_len,
     const uint8_t* code,
     uint64_t code_len);
+
+/*
+ * Extent of a regexp program starting at `code` with `avail` readable bytes:
+ * the end of the furthest instruction reachable from its start through jumps,
+ * splits and repeat offsets (re.h:65-92 opcodes).  YR_AMD_INVALID_ARGUMENT if
+ * an unknown opcode or an out-of-range target is reachable.  Used to copy
+ * YR_AC_MATCH.forward_code / backward_code for yr_amd_tables_set_re_code.
+ */
+int yr_amd_re_code_extent(const uint8_t* code, uint64_t avail, uint32_t* extent);
 
 /*
  * One call of the replay that can have an effect: the host calls

@@ -79,14 +79,18 @@ static uint32_t _fast_code_len(const uint8_t* code)
   return 0;
 }
 
-/* Forward/backward fast-exec programs of the hex strings' pool entries for
- * yr_amd_tables_set_re_code (YR_AC_MATCH.forward_code / backward_code). */
+/* Forward/backward regexp programs of the pool entries for
+ * yr_amd_tables_set_re_code (YR_AC_MATCH.forward_code / backward_code): the
+ * linear fast-exec program of a hex string, or every reachable instruction of
+ * another regexp's yr_re_exec program (yr_amd_re_code_extent). */
 static int _attach_re_code(YR_RULES* rules, uint32_t n_pool, yr_amd_tables* t)
 {
   uint32_t* a = (uint32_t*) calloc(4 * (size_t) (n_pool ? n_pool : 1), sizeof(uint32_t));
   if (a == NULL) return ERROR_INSUFFICIENT_MEMORY;
   uint32_t *fo = a, *fl = a + n_pool, *bo = a + 2 * n_pool, *bl = a + 3 * n_pool;
   uint64_t total = 0;
+  const uint8_t* re_base = (const uint8_t*) yr_arena_get_ptr(rules->arena, YR_RE_CODE_SECTION, 0);
+  const size_t re_size = yr_arena_get_current_offset(rules->arena, YR_RE_CODE_SECTION);
   for (uint32_t pass = 0; pass < 2; pass++)
   {
     uint8_t* code = pass ? (uint8_t*) malloc(total ? total : 1) : NULL;
@@ -105,6 +109,20 @@ static int _attach_re_code(YR_RULES* rules, uint32_t n_pool, yr_amd_tables* t)
         f = _fast_code_len(m->forward_code);
         b = m->backward_code ? _fast_code_len(m->backward_code) : 0;
         if (f == 0 || (m->backward_code != NULL && b == 0)) f = b = 0;
+      }
+      else if (!(m->string->flags & STRING_FLAGS_LITERAL) && m->forward_code != NULL &&
+               m->forward_code >= re_base && m->forward_code < re_base + re_size)
+      {
+        /* yr_re_exec programs: copy every instruction reachable from the start */
+        int okf = yr_amd_re_code_extent(m->forward_code,
+                                        (uint64_t) (re_base + re_size - m->forward_code), &f);
+        int okb = ERROR_SUCCESS;
+        if (m->backward_code != NULL)
+          okb = m->backward_code >= re_base && m->backward_code < re_base + re_size
+                    ? yr_amd_re_code_extent(m->backward_code,
+                                            (uint64_t) (re_base + re_size - m->backward_code), &b)
+                    : ERROR_INVALID_ARGUMENT;
+        if (okf != ERROR_SUCCESS || okb != ERROR_SUCCESS) f = b = 0;
       }
       if (pass)
       {

@@ -344,6 +344,138 @@ static int fast_re_reachable(const uint8_t* code, uint32_t len, const uint8_t* i
 }
 
 /*
+ * yr_re_exec programs (re.c:1693-2072), same over-approximating question as
+ * the product's general_re_reachable (verify.hip) and the same search order,
+ * stack limit (16 open choices) and step budget (4096): exhausting either
+ * answers 1.  Exact character tests: LITERAL (case-folded with `lower` under
+ * NO_CASE), NOT/MASKED literals, CLASS (+ ASCII case swap under NO_CASE,
+ * negation), ANY (newline unless DOT_ALL); every consumed character needs
+ * bytes_matched < max_bytes_matched and, wide, a zero high byte.  SPLIT
+ * branches, REPEAT_START (min 0: skip) / REPEAT_END (loop or leave),
+ * REPEAT_ANY ranges, boundary/anchor assertions and \w\s\d are unconstrained.
+ */
+static int re_sz(uint8_t op)
+{
+  if (op == 0xA0 || (op >= 0xA7 && op <= 0xAD) || (op >= 0xB0 && op <= 0xB3)) return 1;
+  if (op == 0xA2 || op == 0xAE) return 2;
+  if (op == 0xA4 || op == 0xAF) return 3;
+  if (op == 0xA5) return 34;
+  if (op == 0xB4 || op == 0xB5) return 5;
+  if (op == 0xC0 || op == 0xC1) return 4;
+  if (op == 0xC2) return 3;
+  if (op >= 0xC3 && op <= 0xC6) return 9;
+  return 0;
+}
+
+static int general_reachable(const uint8_t* code, uint32_t len, const uint8_t* input,
+                             uint64_t avail, int backwards, int wide, int nocase, int dotall,
+                             const uint8_t* lower)
+{
+  struct { int32_t ip; int b, j, jmax, step; } st[16];
+  int sp = 0;
+  int cs = wide ? 2 : 1;
+  int maxb = (int) (avail < RE_SCAN_LIMIT ? avail : RE_SCAN_LIMIT);
+  maxb -= maxb % cs;
+  int32_t ip = 0;
+  int b = 0;
+  for (int steps = 0; steps < 4096; steps++)
+  {
+    if (ip < 0 || (uint32_t) ip >= len) return 1;
+    uint8_t op = code[ip];
+    int alive = 1;
+    if (op == 0xAD) return 1;
+    if (op == 0xC2) { ip += (int16_t) (code[ip + 1] | (code[ip + 2] << 8)); continue; }
+    if (op == 0xC0 || op == 0xC1)
+    {
+      if (sp == 16) return 1;
+      st[sp].ip = ip + (int16_t) (code[ip + 2] | (code[ip + 3] << 8));
+      st[sp].b = b; st[sp].j = 0; st[sp].jmax = 0; st[sp].step = 0; sp++;
+      ip += 4;
+      continue;
+    }
+    if (op >= 0xC3 && op <= 0xC6)
+    {
+      int32_t off = (int32_t) ((uint32_t) code[ip + 5] | ((uint32_t) code[ip + 6] << 8) |
+                               ((uint32_t) code[ip + 7] << 16) | ((uint32_t) code[ip + 8] << 24));
+      int is_start = op == 0xC3 || op == 0xC5;
+      int min0 = (code[ip + 1] | (code[ip + 2] << 8)) == 0;
+      if (!is_start || min0)
+      {
+        if (sp == 16) return 1;
+        st[sp].ip = ip + off; st[sp].b = b; st[sp].j = 0; st[sp].jmax = 0; st[sp].step = 0; sp++;
+      }
+      ip += 9;
+      continue;
+    }
+    if (op >= 0xB0 && op <= 0xB3) { ip += 1; continue; }
+    if (op == 0xB4 || op == 0xB5)
+    {
+      int mn = code[ip + 1] | (code[ip + 2] << 8), mx = code[ip + 3] | (code[ip + 4] << 8);
+      int jmax = (maxb - b) / cs;
+      if (mx < jmax) jmax = mx;
+      if (mn > jmax) alive = 0;
+      else
+      {
+        if (mn < jmax)
+        {
+          if (sp == 16) return 1;
+          st[sp].ip = ip + 5; st[sp].b = b; st[sp].j = mn + 1; st[sp].jmax = jmax; st[sp].step = cs;
+          sp++;
+        }
+        b += mn * cs;
+        ip += 5;
+        continue;
+      }
+    }
+    else
+    {
+      int sz = re_sz(op);
+      if (sz == 0) return 1;
+      if (b >= maxb) alive = 0;
+      else
+      {
+        const uint8_t* ch = backwards ? input - cs - b : input + b;
+        if (wide && ch[1] != 0) alive = 0;
+        else
+        {
+          uint8_t c = ch[0];
+          int ok = 1;
+          switch (op)
+          {
+          case 0xA0: ok = dotall || c != 0x0A; break;
+          case 0xA2: ok = nocase ? lower[c] == lower[code[ip + 1]] : c == code[ip + 1]; break;
+          case 0xAE: ok = c != code[ip + 1]; break;
+          case 0xA4: ok = (c & code[ip + 2]) == code[ip + 1]; break;
+          case 0xAF: ok = (c & code[ip + 2]) != code[ip + 1]; break;
+          case 0xA5:
+          {
+            const uint8_t* bm = code + ip + 2;
+            int in = (bm[c / 8] >> (c % 8)) & 1;
+            if (nocase)
+            {
+              uint8_t a = (c >= 'a' && c <= 'z') ? c - 32 : (c >= 'A' && c <= 'Z') ? c + 32 : c;
+              in = in || ((bm[a / 8] >> (a % 8)) & 1);
+            }
+            ok = code[ip + 1] ? !in : in;
+            break;
+          }
+          default: ok = 1; /* \w \W \s \S \d \D */
+          }
+          if (!ok) alive = 0;
+          else { b += cs; ip += sz; continue; }
+        }
+      }
+    }
+    if (alive) continue;
+    if (sp == 0) return 0;
+    ip = st[sp - 1].ip;
+    b = st[sp - 1].b + st[sp - 1].j * st[sp - 1].step;
+    if (++st[sp - 1].j > st[sp - 1].jmax) sp--;
+  }
+  return 1;
+}
+
+/*
  * Does the regex call (non-literal string, pool entry k at offset off) have a
  * possible effect?  _yr_scan_verify_re_match (scan.c:778-880): the forward
  * program from `off` must match (forward_matches != -1), then, if a backward
@@ -351,6 +483,25 @@ static int fast_re_reachable(const uint8_t* code, uint32_t len, const uint8_t* i
  * reach _yr_scan_match_callback); forward_matches == 0 without a backward
  * program returns early too.  Only FAST ascii hex strings are decided.
  */
+static int general_call_effect(uint32_t flags, const uint8_t* fwd, uint32_t fl, const uint8_t* bwd,
+                               uint32_t bl, const uint8_t* data, uint64_t size, uint64_t off,
+                               const uint8_t* lower)
+{
+  /* scan.c:817-848: ascii attempt for ASCII/base64 strings, wide attempt for
+   * WIDE non-base64 strings; the backward program with the matching flags */
+  int nocase = (flags & SF_NO_CASE) != 0, dotall = (flags & 0x20000u) != 0;
+  int try_ascii = (flags & (SF_ASCII | SF_BASE64_ANY)) != 0;
+  int try_wide = (flags & SF_WIDE) && !(flags & SF_BASE64_ANY);
+  for (int w = 0; w < 2; w++)
+  {
+    if (w == 0 ? !try_ascii : !try_wide) continue;
+    if (!general_reachable(fwd, fl, data + off, size - off, 0, w, nocase, dotall, lower)) continue;
+    if (bl == 0 || general_reachable(bwd, bl, data + off, off, 1, w, nocase, dotall, lower))
+      return 1;
+  }
+  return 0;
+}
+
 static int re_call_effect(uint32_t flags, const uint8_t* fwd, uint32_t fl, const uint8_t* bwd,
                           uint32_t bl, const uint8_t* data, uint64_t size, uint64_t off)
 {
@@ -410,10 +561,15 @@ int64_t oracle_literal_effect(
         }
       }
     }
-    else if (!(f & SF_LITERAL) && re_kind != NULL && re_kind[k])
+    else if (!(f & SF_LITERAL) && re_kind != NULL && re_kind[k] == 1)
     {
       fm = re_call_effect(f, re_code + re_fwd_off[k], re_fwd_len[k], re_code + re_bwd_off[k],
                           re_bwd_len[k], data, size, off);
+    }
+    else if (!(f & SF_LITERAL) && re_kind != NULL && re_kind[k] == 2)
+    {
+      fm = general_call_effect(f, re_code + re_fwd_off[k], re_fwd_len[k], re_code + re_bwd_off[k],
+                               re_bwd_len[k], data, size, off, lowercase);
     }
     out[c] = fm != 0;
     kept += fm != 0;

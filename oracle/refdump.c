@@ -108,6 +108,62 @@ static uint32_t fast_code_len(const uint8_t* code)
   return 0;
 }
 
+/* Size of one regexp instruction (re.h:65-92 opcodes, re.c:65-87 operands), 0 if unknown. */
+static uint32_t re_insn_size(uint8_t op)
+{
+  if (op == 0xA0 || (op >= 0xA7 && op <= 0xAD) || (op >= 0xB0 && op <= 0xB3)) return 1;
+  if (op == 0xA2 || op == 0xAE) return 2;
+  if (op == 0xA4 || op == 0xAF) return 3;
+  if (op == 0xA5) return 34;
+  if (op == 0xB4 || op == 0xB5) return 5;
+  if (op == 0xC0 || op == 0xC1) return 4;
+  if (op == 0xC2) return 3;
+  if (op >= 0xC3 && op <= 0xC6) return 9;
+  return 0;
+}
+
+/* Extent of a yr_re_exec program: furthest end of an instruction reachable
+ * from its start (jumps, splits, repeat back/forward offsets), 0 if invalid. */
+static uint32_t general_code_len(const uint8_t* code, size_t avail)
+{
+  if (avail == 0 || avail > (1u << 20)) avail = avail ? (1u << 20) : 0;
+  if (avail == 0) return 0;
+  uint8_t* seen = calloc(avail, 1);
+  int64_t* todo = malloc(sizeof(int64_t) * (avail + 1));
+  size_t nt = 0;
+  uint64_t end = 0;
+  int ok = 1;
+  todo[nt++] = 0;
+  while (nt > 0 && ok)
+  {
+    int64_t ip = todo[--nt];
+    for (;;)
+    {
+      if (ip < 0 || (uint64_t) ip >= avail) { ok = 0; break; }
+      if (seen[ip]) break;
+      seen[ip] = 1;
+      uint8_t op = code[ip];
+      uint32_t sz = re_insn_size(op);
+      if (sz == 0 || (uint64_t) ip + sz > avail) { ok = 0; break; }
+      if ((uint64_t) ip + sz > end) end = ip + sz;
+      if (op == 0xAD) break;
+      if (op == 0xC2) { ip += (int16_t) (code[ip + 1] | (code[ip + 2] << 8)); continue; }
+      if ((op == 0xC0 || op == 0xC1) && nt < avail)
+        todo[nt++] = ip + (int16_t) (code[ip + 2] | (code[ip + 3] << 8));
+      if (op >= 0xC3 && op <= 0xC6 && nt < avail)
+      {
+        int32_t off = (int32_t) ((uint32_t) code[ip + 5] | ((uint32_t) code[ip + 6] << 8) |
+                                 ((uint32_t) code[ip + 7] << 16) | ((uint32_t) code[ip + 8] << 24));
+        todo[nt++] = ip + off;
+      }
+      ip += sz;
+    }
+  }
+  free(seen);
+  free(todo);
+  return ok ? (uint32_t) end : 0;
+}
+
 static void w32(FILE* f, uint32_t v) { fwrite(&v, 4, 1, f); }
 static void w64(FILE* f, uint64_t v) { fwrite(&v, 8, 1, f); }
 
@@ -148,7 +204,10 @@ static int cmd_tables(const char* rules_path, const char* out)
   }
   /* v2: per pool entry {u32 kind, u32 fwd_len, u32 bwd_len, fwd, bwd, pad};
    * kind 1 = FAST_REGEXP string with linear forward (and, if bwd_len > 0,
-   * backward) programs; kind 0 = anything else (no code dumped). */
+   * backward) programs; kind 2 = other regexp string, every instruction of its
+   * yr_re_exec programs reachable from their start; kind 0 = anything else. */
+  const uint8_t* re_base = yr_arena_get_ptr(rules->arena, YR_RE_CODE_SECTION, 0);
+  size_t re_size = yr_arena_get_current_offset(rules->arena, YR_RE_CODE_SECTION);
   for (uint32_t k = 0; k < np; k++)
   {
     YR_AC_MATCH* m = &rules->ac_match_pool[k];
@@ -158,6 +217,18 @@ static int cmd_tables(const char* rules_path, const char* out)
       fl = fast_code_len(m->forward_code);
       bl = m->backward_code ? fast_code_len(m->backward_code) : 0;
       kind = fl > 0 && (m->backward_code == NULL || bl > 0);
+      if (!kind) fl = bl = 0;
+    }
+    else if (!(m->string->flags & STRING_FLAGS_LITERAL) && m->forward_code != NULL &&
+             m->forward_code >= re_base && m->forward_code < re_base + re_size)
+    {
+      fl = general_code_len(m->forward_code, re_base + re_size - m->forward_code);
+      bl = 0;
+      if (m->backward_code != NULL)
+        bl = m->backward_code >= re_base && m->backward_code < re_base + re_size
+                 ? general_code_len(m->backward_code, re_base + re_size - m->backward_code)
+                 : 0;
+      kind = fl > 0 && (m->backward_code == NULL || bl > 0) ? 2 : 0;
       if (!kind) fl = bl = 0;
     }
     w32(f, kind);

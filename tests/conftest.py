@@ -64,6 +64,8 @@ def case_data(rec):
         return planted.lit_buffer(oracle.xorshift, spec[2], spec[1])
     if kind == "hex":
         return planted.hex_buffer(oracle.xorshift, spec[2], spec[1])
+    if kind == "rx":
+        return planted.rx_buffer(oracle.xorshift, spec[2], spec[1])
     if kind == "file":
         return np.frombuffer(bytes.fromhex(rec["data_bytes_hex"]), dtype=np.uint8)
     raise ValueError(kind)

@@ -180,3 +180,37 @@ def hex_buffer(xorshift, size: int, seed: int = 17) -> np.ndarray:
     tail = H("4D5A01025045") + bytes(2) + H("11")           # truncated at the end
     buf[size - len(tail):] = np.frombuffer(tail, np.uint8)
     return buf
+
+
+# --- regexp buffer (tests/golden/rules/rx.yar) --------------------------------
+# Matches and near misses of yr_re_exec programs (re.c:1693): classes, optional
+# groups, alternation, bounded / unbounded repeats, word boundaries, nocase,
+# wide, dot-all, and hex strings with alternatives (not fast-exec programs).
+def rx_buffer(xorshift, size: int, seed: int = 19) -> np.ndarray:
+    buf = xorshift(size, seed).copy()
+    r = random.Random(seed)
+    H = bytes.fromhex
+    pieces = [b"http://abc.com", b"https://example12.com", b"http://ab.com", b"https://abc.org",
+              b"Content-Type: text/html", b"CONTENT-TYPE: Application/JSON", b"Content-Type: 1/2",
+              b"username=alice_01", b"username_id=bob42", b"username=ab", b"username_id=",
+              b" password ", b"xpassword ", b"(password)", b"passwords",
+              b"GET /index.php?id=42", b"GET /index.php?id=", b"GET /Index.php?id=1",
+              b"abcde12vwxyz", b"abcde\n\n\nvwxyz", b"abcde1vwxyz", b"abcde123456vwxyz",
+              b"cathouse", b"doghouse", b"birdhouse", b"cowhouse", b"Qx1234Zq!", b"Qx12\n4Zq!",
+              b"Qx1Zq!", b"Qx123456789Zq!"]
+    for w in (b" password ", b"password", b"xpasswordx"):
+        pieces.append(bytes(x for c in w for x in (c, 0)))
+    pieces += [H("4D5A9000030102FFFF"), H("4D5A5000030102030405FFFF"), H("4D5A9100030102FFFF"),
+               H("4D5A900003FFFF"), H("E8010203045BC3"), H("E8010203045DC3"), H("E8010203045CC3"),
+               H("1122334455BB"), H("112233446677BB"), H("112233448899AABB"),
+               H("112233446699BB")]
+    for p in pieces:
+        for _ in range(3):
+            pos = r.randrange(16, size - len(p) - 16)
+            buf[pos:pos + len(p)] = np.frombuffer(p, dtype=np.uint8)
+    # an atom right at the block start and a match cut by the block end
+    head = b"cathouse"
+    buf[0:len(head)] = np.frombuffer(head, np.uint8)
+    tail = b"https://abcd.co"
+    buf[size - len(tail):] = np.frombuffer(tail, np.uint8)
+    return buf

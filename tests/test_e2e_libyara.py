@@ -31,7 +31,7 @@ needs_check = pytest.mark.skipif(not os.path.exists(CHECK),
 
 def _rules_file(tmp_path, name):
     p = tmp_path / ("%s.yar" % name)
-    if name in ("short", "root", "lit", "hex"):
+    if name in ("short", "root", "lit", "hex", "rx"):
         p.write_text(open(os.path.join(GOLDEN, "rules", name + ".yar")).read())
     else:
         p.write_text(gen_rules.gen(name))
@@ -69,6 +69,9 @@ CASES = [
     ("hex", "hex", 1 << 20, 0, 0),
     ("hex", "hex", 1 << 20, 8192, 1024),
     ("hex", "hex", 4 << 20, 3000, 64),
+    ("rx", "rx", 1 << 20, 0, 0),
+    ("rx", "rx", 1 << 20, 8192, 1024),
+    ("rx", "rx", 4 << 20, 3000, 64),
 ]
 
 
@@ -83,6 +86,8 @@ def test_match_set_equals_stock_libyara(tmp_path, rules, kind, size, block, over
         spec = _data_file(tmp_path, planted.lit_buffer(oracle.xorshift, size, 13), "d.bin")
     elif kind == "hex":
         spec = _data_file(tmp_path, planted.hex_buffer(oracle.xorshift, size, 17), "d.bin")
+    elif kind == "rx":
+        spec = _data_file(tmp_path, planted.rx_buffer(oracle.xorshift, size, 19), "d.bin")
     elif kind == "planted":
         spec = _data_file(tmp_path, planted.planted_buffer(oracle.xorshift, gen_rules.gen(rules),
                                                            size, 3), "d.bin")
@@ -93,7 +98,7 @@ def test_match_set_equals_stock_libyara(tmp_path, rules, kind, size, block, over
     assert res["rc_stock"] == 0 and res["rc_gpu"] == 0, res
     assert res["same_matches"] and res["same_rule_reports"], res
     assert res["finished"] == [1, 1], res
-    if kind in ("planted", "lit", "hex"):
+    if kind in ("planted", "lit", "hex", "rx"):
         assert res["matches_stock"] > 0 and res["rules_matching"] > 0, res
     assert rc == 0
 

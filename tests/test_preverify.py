@@ -50,11 +50,23 @@ def test_oracle_keeps_every_reported_match(case):
     ps = z["pool_string"]
     kept = set(zip((base[keep] + off[keep]).tolist(), ps[idx[keep]].tolist()))
     flags = z["str_flags"]
-    for s, o in zip(arr["match_string"].tolist(), arr["match_offset"].tolist()):
+    by_string = {}
+    for o_, s_ in kept:
+        by_string.setdefault(s_, []).append(o_)
+    by_string = {k: np.sort(np.array(v, np.int64)) for k, v in by_string.items()}
+    for s, o, n in zip(arr["match_string"].tolist(), arr["match_offset"].tolist(),
+                       arr["match_len"].tolist()):
         if flags[s] & SF_LITERAL:
             assert (o, s) in kept, (case, s, o)
-    # the filter is not a no-op where literal near misses exist
-    if case.startswith("lit"):
+        else:
+            # regexp / hex: the atom lies inside the reported match, so some
+            # kept call of that string has its atom offset in [o, o + len]
+            v = by_string.get(s)
+            assert v is not None, (case, s, o)
+            j = np.searchsorted(v, o)
+            assert j < len(v) and v[j] <= o + n, (case, s, o, n)
+    # the filter is not a no-op where near misses exist
+    if case.startswith(("lit", "hex", "rx")):
         assert keep.sum() < len(keep)
 
 

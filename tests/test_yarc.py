@@ -18,7 +18,7 @@ import oracle
 import yara_amd
 from conftest import GOLDEN, case_arrays, case_data, golden, ref_tables, tables_npz
 
-SETS = ["B", "C", "E", "lit", "hex", "short", "root"]
+SETS = ["B", "C", "E", "lit", "hex", "rx", "short", "root"]
 CASES = golden()["cases"]
 
 
@@ -34,7 +34,7 @@ def test_yarc_tables_equal_compiler_tables(name):
     assert a == b
 
 
-@pytest.mark.parametrize("case", [c for c in ("B_64M", "short_1M", "lit_1M", "hex_1M",
+@pytest.mark.parametrize("case", [c for c in ("B_64M", "short_1M", "lit_1M", "hex_1M", "rx_1M",
                                                "root_4K", "short_3")])
 def test_yarc_tables_replay_reference_stream(case):
     rec = CASES[case]
@@ -83,7 +83,7 @@ def test_yarc_mutations_never_crash():
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("case", ["lit_1M", "hex_1M", "C_planted16M", "E_planted16M",
+@pytest.mark.parametrize("case", ["lit_1M", "hex_1M", "rx_1M", "C_planted16M", "E_planted16M",
                                   "short_1M", "B_planted4M_blocks"])
 def test_yarc_device_tables_preverify_like_compiler_tables(case):
     rec = CASES[case]

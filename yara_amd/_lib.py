@@ -82,6 +82,7 @@ PROTOTYPES = {
                                          ctypes.c_uint32, _u8p, ctypes.c_uint64, _u8p]),
     "yr_amd_tables_set_re_code": (_int, [_vp, ctypes.c_uint32, _u32p, _u32p, _u32p, _u32p, _u8p,
                                          ctypes.c_uint64]),
+    "yr_amd_re_code_extent": (_int, [_u8p, ctypes.c_uint64, ctypes.POINTER(ctypes.c_uint32)]),
     "yr_amd_verify_device": (_int, [_vp, ctypes.c_uint64, ctypes.POINTER(_vp),
                                     ctypes.POINTER(ctypes.c_uint64)]),
     "yr_amd_pipeline_create": (_int, [_vp, ctypes.c_uint32, ctypes.POINTER(_vp)]),

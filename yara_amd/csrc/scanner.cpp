@@ -17,6 +17,7 @@
 #include "../../include/yara_amd.h"
 #include "internal.h"
 #include "tables.h"
+#include "re_program.h"
 #include "verify.h"
 
 namespace yamd {
@@ -26,6 +27,49 @@ hipError_t launch_compact(const ScanParams& p, uint64_t* seg_offset, uint64_t* s
 hipError_t launch_xorshift(uint8_t* buf, uint64_t n, const uint64_t* states, uint32_t n_chunks,
                            uint32_t chunk, hipStream_t s);
 hipError_t configure_scan_kernel();
+}  // namespace yamd
+
+namespace yamd {
+// Length of a general regexp program (yr_re_exec, re.c:1693): every
+// instruction reachable from offset 0 through jumps, splits and repeat
+// offsets is a known opcode lying inside [0, avail); returns the end of the
+// furthest one, 0 if the program is malformed.
+uint32_t re_general_extent(const uint8_t* c, uint64_t avail) {
+  const uint64_t lim = std::min<uint64_t>(avail, 1u << 20);
+  if (lim == 0) return 0;
+  std::vector<uint8_t> seen(lim, 0);
+  std::vector<int64_t> work{0};
+  uint64_t end = 0;
+  while (!work.empty()) {
+    int64_t ip = work.back();
+    work.pop_back();
+    while (true) {
+      if (ip < 0 || (uint64_t)ip >= lim) return 0;
+      if (seen[ip]) break;
+      seen[ip] = 1;
+      const uint8_t op = c[ip];
+      const uint32_t sz = re_op_size(op);
+      if (sz == 0 || (uint64_t)ip + sz > lim) return 0;
+      end = std::max<uint64_t>(end, (uint64_t)ip + sz);
+      if (op == kOpMatch) break;
+      if (op == kOpJump) {
+        ip += re_i16(c + ip + 1);
+        continue;
+      }
+      if (op == kOpSplitA || op == kOpSplitB) work.push_back(ip + re_i16(c + ip + 2));
+      if (op == kOpRepeatStartGreedy || op == kOpRepeatStartUngreedy ||
+          op == kOpRepeatEndGreedy || op == kOpRepeatEndUngreedy) {
+        if (re_u16(c + ip + 1) > re_u16(c + ip + 3)) return 0;   // min > max
+        work.push_back(ip + re_i32(c + ip + 5));
+      }
+      if ((op == kOpRepeatAnyGreedy || op == kOpRepeatAnyUngreedy) &&
+          re_u16(c + ip + 1) > re_u16(c + ip + 3))
+        return 0;
+      ip += sz;
+    }
+  }
+  return (uint32_t)end;
+}
 }  // namespace yamd
 
 using namespace yamd;
@@ -49,6 +93,7 @@ struct yr_amd_tables {
   uint8_t* d_lowercase = nullptr;
   DevRe* d_re = nullptr;          // yr_amd_tables_set_re_code
   uint8_t* d_re_code = nullptr;
+  std::vector<uint32_t> h_str_flags, h_pool_string;   // host copies (validation)
 };
 
 struct yr_amd_scanner {
@@ -492,6 +537,9 @@ int yr_amd_tables_set_strings(yr_amd_tables* t, const uint32_t* pool_string, uin
   if (!r) r = upload(t->d_str_bytes, bytes, n_bytes);
   if (!r) r = upload(t->d_lowercase, lowercase, 256);
   if (r) return r;   // partial uploads are freed with the tables
+  t->h_pool_string.assign(pool_string, pool_string + n_pool);
+  t->h_str_flags.resize(n_strings);
+  for (uint32_t k = 0; k < n_strings; ++k) t->h_str_flags[k] = strings[k].flags;
   t->has_strings = true;
   return YR_AMD_SUCCESS;
 }
@@ -521,6 +569,13 @@ uint32_t fast_program_ok(const uint8_t* c, uint32_t len) {
 }
 }  // namespace
 
+int yr_amd_re_code_extent(const uint8_t* code, uint64_t avail, uint32_t* extent) {
+  using yamd::re_general_extent;
+  if (code == nullptr || extent == nullptr) return YR_AMD_INVALID_ARGUMENT;
+  *extent = re_general_extent(code, avail);
+  return *extent ? YR_AMD_SUCCESS : YR_AMD_INVALID_ARGUMENT;
+}
+
 int yr_amd_tables_set_re_code(yr_amd_tables* t, uint32_t n_pool, const uint32_t* fwd_off,
                               const uint32_t* fwd_len, const uint32_t* bwd_off,
                               const uint32_t* bwd_len, const uint8_t* code, uint64_t code_len) {
@@ -540,9 +595,15 @@ int yr_amd_tables_set_re_code(yr_amd_tables* t, uint32_t n_pool, const uint32_t*
     }
     if ((uint64_t)fwd_off[k] + fwd_len[k] > code_len || (uint64_t)bwd_off[k] + bwd_len[k] > code_len)
       return YR_AMD_INVALID_ARGUMENT;
-    if (!fast_program_ok(code + fwd_off[k], fwd_len[k])) return YR_AMD_INVALID_ARGUMENT;
-    if (bwd_len[k] > 0 && !fast_program_ok(code + bwd_off[k], bwd_len[k]))
-      return YR_AMD_INVALID_ARGUMENT;
+    // FAST_REGEXP strings run yr_re_fast_exec (a linear program), the others
+    // yr_re_exec (any well-formed program of exactly the given length)
+    const bool fast = t->h_str_flags[t->h_pool_string[k]] & kStrFastRegexp;
+    auto ok = [&](uint32_t off, uint32_t len) {
+      return fast ? fast_program_ok(code + off, len) == len
+                  : re_general_extent(code + off, len) == len;
+    };
+    if (!ok(fwd_off[k], fwd_len[k])) return YR_AMD_INVALID_ARGUMENT;
+    if (bwd_len[k] > 0 && !ok(bwd_off[k], bwd_len[k])) return YR_AMD_INVALID_ARGUMENT;
   }
   HIP_TRY(hipSetDevice(t->device));
   int r = upload(t->d_re_code, code, (size_t)code_len);

@@ -19,6 +19,7 @@ constexpr uint32_t kStrXor = 0x80000;
 constexpr uint32_t kStrUnmodelled = 0x200000 | 0x400000;
 
 constexpr uint32_t kStrFastRegexp = 0x40;
+constexpr uint32_t kStrDotAll = 0x20000;
 constexpr uint32_t kStrBase64Any = 0x200000 | 0x400000;
 
 // Fast-exec RE programs (hex strings) of one pool entry: forward code at

@@ -24,6 +24,7 @@
 // C): this is latency-bound pointer chasing in L2, microseconds per block, so
 // the kernels are simple two-pass (count, exclusive scan, write).
 #include "internal.h"
+#include "re_program.h"
 #include "verify.h"
 
 namespace yamd {
@@ -146,6 +147,137 @@ __device__ bool fast_re_reachable(const uint8_t* __restrict__ code, uint32_t len
   return true;
 }
 
+// yr_re_exec (re.c:1693-2072) as a reachability question, over-approximated:
+// can some path from the program's start reach RE_OPCODE_MATCH?  Character
+// tests are exact where they are locale-free (LITERAL with the host's case
+// folding, NOT/MASKED literals, CLASS, ANY with DOT_ALL), every character
+// consumes character_size bytes subject to the prolog (bytes_matched <
+// max_bytes_matched, and for wide input a zero high byte, re.c:1727-1735);
+// everything else is allowed: both branches of SPLIT, every iteration count
+// of REPEAT_START/END loops and REPEAT_ANY ranges, word-boundary and anchor
+// assertions, the \w \s \d classes.  A reference fiber's path is therefore
+// always one of these paths, and "unreachable" proves forward_matches == -1.
+// Depth-first with an explicit choice stack; stack or step budget exhausted
+// -> true (keep the call).
+__device__ bool general_re_reachable(const uint8_t* __restrict__ code, uint32_t len,
+                                     const uint8_t* __restrict__ input, uint64_t avail,
+                                     bool backwards, bool wide, bool nocase, bool dotall,
+                                     const uint8_t* __restrict__ lower) {
+  constexpr int kMaxChoices = 16;
+  struct Choice {
+    int32_t ip;
+    int b, j, jmax, step;
+  } st[kMaxChoices];
+  int sp = 0;
+  const int cs = wide ? 2 : 1;
+  int maxb = (int)min<uint64_t>(avail, (uint64_t)kReScanLimit);
+  maxb -= maxb % cs;
+  int32_t ip = 0;
+  int b = 0;
+  for (int budget = 0; budget < 4096; ++budget) {
+    if (ip < 0 || (uint32_t)ip >= len) return true;
+    const uint8_t op = code[ip];
+    bool dead = false;
+    switch (op) {
+      case kOpMatch:
+        return true;
+      case kOpJump:
+        ip += re_i16(code + ip + 1);
+        continue;
+      case kOpSplitA:
+      case kOpSplitB:
+        if (sp == kMaxChoices) return true;
+        st[sp++] = Choice{ip + re_i16(code + ip + 2), b, 0, 0, 0};
+        ip += 4;
+        continue;
+      case kOpRepeatStartGreedy:
+      case kOpRepeatStartUngreedy:
+        if (re_u16(code + ip + 1) == 0) {   // min == 0: the body may be skipped
+          if (sp == kMaxChoices) return true;
+          st[sp++] = Choice{ip + re_i32(code + ip + 5), b, 0, 0, 0};
+        }
+        ip += 9;
+        continue;
+      case kOpRepeatEndGreedy:
+      case kOpRepeatEndUngreedy:   // loop back or leave, any number of times
+        if (sp == kMaxChoices) return true;
+        st[sp++] = Choice{ip + re_i32(code + ip + 5), b, 0, 0, 0};
+        ip += 9;
+        continue;
+      case kOpWordBoundary:
+      case kOpNonWordBoundary:
+      case kOpMatchAtStart:
+      case kOpMatchAtEnd:
+        ip += 1;
+        continue;
+      case kOpRepeatAnyGreedy:
+      case kOpRepeatAnyUngreedy: {
+        const int mn = re_u16(code + ip + 1), mx = re_u16(code + ip + 3);
+        const int jmax = min(mx, (maxb - b) / cs);   // every repetition passes the prolog
+        if (mn > jmax) {
+          dead = true;
+          break;
+        }
+        if (mn < jmax) {
+          if (sp == kMaxChoices) return true;
+          st[sp++] = Choice{ip + 5, b, mn + 1, jmax, cs};
+        }
+        b += mn * cs;
+        ip += 5;
+        continue;
+      }
+      default: {
+        const uint32_t sz = re_op_size(op);
+        if (sz == 0) return true;   // not a program this analysis knows
+        if (b >= maxb) {
+          dead = true;
+          break;
+        }
+        const uint8_t* ch = backwards ? input - cs - b : input + b;
+        if (wide && ch[1] != 0) {
+          dead = true;
+          break;
+        }
+        const uint8_t c = ch[0];
+        bool ok = true;
+        if (op == kOpAny) {
+          ok = dotall || c != 0x0A;
+        } else if (op == kOpLiteral) {
+          ok = nocase ? lower[c] == lower[code[ip + 1]] : c == code[ip + 1];
+        } else if (op == kOpNotLiteral) {
+          ok = c != code[ip + 1];
+        } else if (op == kOpMaskedLiteral) {
+          ok = (c & code[ip + 2]) == code[ip + 1];
+        } else if (op == kOpMaskedNotLiteral) {
+          ok = (c & code[ip + 2]) != code[ip + 1];
+        } else if (op == kOpClass) {
+          const uint8_t* bm = code + ip + 2;
+          bool in = (bm[c >> 3] >> (c & 7)) & 1;
+          if (nocase) {   // yr_altercase (libyara.c:249-256): ASCII case swap
+            const uint8_t a = (c >= 'a' && c <= 'z') ? c - 32 : (c >= 'A' && c <= 'Z') ? c + 32 : c;
+            in = in || ((bm[a >> 3] >> (a & 7)) & 1);
+          }
+          ok = code[ip + 1] ? !in : in;
+        }   // \w \W \s \S \d \D: allowed (locale-dependent in the reference)
+        if (!ok) {
+          dead = true;
+          break;
+        }
+        b += cs;
+        ip += (int32_t)sz;
+        continue;
+      }
+    }
+    if (!dead) continue;
+    if (sp == 0) return false;
+    Choice& t = st[sp - 1];
+    ip = t.ip;
+    b = t.b + t.j * t.step;
+    if (++t.j > t.jmax) --sp;
+  }
+  return true;
+}
+
 // _yr_scan_verify_re_match (scan.c:778-880) for FAST ascii hex strings: the
 // forward program from `offset` must reach MATCH (else forward_matches == -1:
 // return), a zero-length forward match needs a backward program, and with a
@@ -153,17 +285,36 @@ __device__ bool fast_re_reachable(const uint8_t* __restrict__ code, uint32_t len
 __device__ bool re_call_matters(const VerifyParams& p, uint32_t k, uint32_t flags,
                                 uint64_t offset) {
   if (p.re == nullptr) return true;
-  if (!(flags & kStrFastRegexp) || !(flags & kStrAscii) || (flags & (kStrWide | kStrBase64Any)))
-    return true;
   const DevRe r = p.re[k];
   if (r.fwd_len == 0) return true;
   const uint8_t* d = p.data + offset;
-  if (r.fwd_len == 1)   // forward program = MATCH: forward_matches = 0
-    return r.bwd_len > 0 && fast_re_reachable(p.re_code + r.bwd_off, r.bwd_len, d, offset, true);
-  if (!fast_re_reachable(p.re_code + r.fwd_off, r.fwd_len, d, p.size - offset, false)) return false;
-  if (r.bwd_len > 0 && !fast_re_reachable(p.re_code + r.bwd_off, r.bwd_len, d, offset, true))
-    return false;
-  return true;
+  const uint8_t* fwd = p.re_code + r.fwd_off;
+  const uint8_t* bwd = p.re_code + r.bwd_off;
+  if (flags & kStrFastRegexp) {
+    if (!(flags & kStrAscii) || (flags & (kStrWide | kStrBase64Any))) return true;
+    if (r.fwd_len == 1)   // forward program = MATCH: forward_matches = 0
+      return r.bwd_len > 0 && fast_re_reachable(bwd, r.bwd_len, d, offset, true);
+    if (!fast_re_reachable(fwd, r.fwd_len, d, p.size - offset, false)) return false;
+    if (r.bwd_len > 0 && !fast_re_reachable(bwd, r.bwd_len, d, offset, true)) return false;
+    return true;
+  }
+  // yr_re_exec strings: the ascii attempt runs for ASCII / base64 strings, the
+  // wide one (flags | RE_FLAGS_WIDE) for WIDE non-base64 strings when the
+  // ascii one found nothing; the backward program runs with the flags of the
+  // attempt that matched.  Keep iff some attempt can match both ways.
+  const bool nocase = flags & kStrNoCase, dotall = flags & kStrDotAll;
+  const bool try_ascii = flags & (kStrAscii | kStrBase64Any);
+  const bool try_wide = (flags & kStrWide) && !(flags & kStrBase64Any);
+  for (int w = 0; w < 2; ++w) {
+    if (w == 0 ? !try_ascii : !try_wide) continue;
+    if (!general_re_reachable(fwd, r.fwd_len, d, p.size - offset, false, w == 1, nocase, dotall,
+                              p.lowercase))
+      continue;
+    if (r.bwd_len == 0 ||
+        general_re_reachable(bwd, r.bwd_len, d, offset, true, w == 1, nocase, dotall, p.lowercase))
+      return true;
+  }
+  return false;
 }
 
 // Does yr_scan_verify_match(ctx, &pool[k], data, size, base, offset) possibly

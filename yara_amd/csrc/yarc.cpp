@@ -30,6 +30,7 @@
 #include <vector>
 
 #include "../../include/yara_amd.h"
+#include "re_program.h"
 
 namespace {
 
@@ -37,7 +38,7 @@ constexpr uint32_t kArenaVersion = 19;
 constexpr uint32_t kStringsTable = 3, kSzPool = 5, kReCode = 7, kAcTransition = 8,
                    kAcMatchTable = 9, kAcMatchPool = 10, kSummary = 11;
 constexpr uint32_t kStringSize = 56, kMatchSize = 40;
-constexpr uint32_t kFastRegexp = 0x40;
+constexpr uint32_t kFastRegexp = 0x40, kLiteral = 0x400;
 
 struct Ref {
   uint32_t buffer, offset;
@@ -168,14 +169,21 @@ extern "C" int yr_amd_tables_load_yarc(const uint8_t* file, size_t file_size, in
     }
     bt[k] = rd<uint16_t>(a.data[kAcMatchPool] + base + 32);
     fo[k] = fl[k] = bo[k] = bl[k] = 0;
-    if ((sflags[ps[k]] & kFastRegexp) && !rf.null() && rf.buffer == kReCode &&
-        rf.offset < a.size[kReCode]) {
-      const uint32_t f = fast_len(a.data[kReCode] + rf.offset, a.size[kReCode] - rf.offset);
+    const uint32_t sf = sflags[ps[k]];
+    if (!(sf & kLiteral) && !rf.null() && rf.buffer == kReCode && rf.offset < a.size[kReCode]) {
+      // FAST_REGEXP (hex) strings: linear fast-exec programs; other regexps:
+      // every instruction reachable from the start (yr_re_exec)
+      auto len_of = [&](uint32_t off) {
+        const uint8_t* p = a.data[kReCode] + off;
+        const uint64_t avail = a.size[kReCode] - off;
+        return (sf & kFastRegexp) ? fast_len(p, avail) : yamd::re_general_extent(p, avail);
+      };
+      const uint32_t f = len_of(rf.offset);
       uint32_t b = 0;
       bool ok = f > 0;
       if (ok && !rb.null()) {
         ok = rb.buffer == kReCode && rb.offset < a.size[kReCode];
-        if (ok) b = fast_len(a.data[kReCode] + rb.offset, a.size[kReCode] - rb.offset);
+        if (ok) b = len_of(rb.offset);
         ok = ok && b > 0;
       }
       if (ok) {
