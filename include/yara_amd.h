@@ -96,7 +96,7 @@ int yr_amd_tables_destroy(yr_amd_tables* tables);
  * The same tables straight from a compiled rules file (SURVEY.md section 8f,
  * row 3): the bytes of a .yarc written by yarac / yr_rules_save (arena format
  * version 19, arena.c:543-700, sections compiler.h:58-69), parsed without
- * libyara.  With device >= 0 the string records and the hex strings' regex
+ * libyara.  With device >= 0 the string records and the strings' regex
  * programs are attached too (yr_amd_tables_set_strings with C-locale case
  * folding, yr_amd_tables_set_re_code), so pre-verification works directly.
  * YR_AMD_INVALID_ARGUMENT for anything that is not a well-formed v19 arena.
@@ -241,8 +241,9 @@ int yr_amd_tables_set_strings(
     const uint8_t* lowercase);
 
 /*
- * Attach the fast-exec regex programs so that
- * calls on hex strings (STRING_FLAGS_FAST_REGEXP) are pre-verified too.  For
+ * Attach the regexp programs so that calls on
+ * hex strings (STRING_FLAGS_FAST_REGEXP) and other regexp strings are
+ * pre-verified too.  For
  * pool entry k, forward code = code[fwd_off[k] .. + fwd_len[k]) (a copy of
  * rules->ac_match_pool[k].forward_code up to and including RE_OPCODE_MATCH),
  * backward code likewise (bwd_len[k] = 0: backward_code == NULL);

@@ -346,8 +346,10 @@ static int fast_re_reachable(const uint8_t* code, uint32_t len, const uint8_t* i
 /*
  * yr_re_exec programs (re.c:1693-2072), same over-approximating question as
  * the product's general_re_reachable (verify.hip) and the same search order,
- * stack limit (16 open choices) and step budget (4096): exhausting either
- * answers 1.  Exact character tests: LITERAL (case-folded with `lower` under
+ * stack limit (16 open choices) and step budget (1000 < RE_MAX_FIBERS, so an
+ * exec that would fail with ERROR_TOO_MANY_RE_FIBERS, re.c:1228, always runs
+ * out): exhausting either, or unknown code, answers 2 = keep the call.
+ * 0 = no path reaches MATCH, 1 = some path does.  Exact character tests: LITERAL (case-folded with `lower` under
  * NO_CASE), NOT/MASKED literals, CLASS (+ ASCII case swap under NO_CASE,
  * negation), ANY (newline unless DOT_ALL); every consumed character needs
  * bytes_matched < max_bytes_matched and, wide, a zero high byte.  SPLIT
@@ -378,16 +380,16 @@ static int general_reachable(const uint8_t* code, uint32_t len, const uint8_t* i
   maxb -= maxb % cs;
   int32_t ip = 0;
   int b = 0;
-  for (int steps = 0; steps < 4096; steps++)
+  for (int steps = 0; steps < 1000; steps++)
   {
-    if (ip < 0 || (uint32_t) ip >= len) return 1;
+    if (ip < 0 || (uint32_t) ip >= len) return 2;
     uint8_t op = code[ip];
     int alive = 1;
     if (op == 0xAD) return 1;
     if (op == 0xC2) { ip += (int16_t) (code[ip + 1] | (code[ip + 2] << 8)); continue; }
     if (op == 0xC0 || op == 0xC1)
     {
-      if (sp == 16) return 1;
+      if (sp == 16) return 2;
       st[sp].ip = ip + (int16_t) (code[ip + 2] | (code[ip + 3] << 8));
       st[sp].b = b; st[sp].j = 0; st[sp].jmax = 0; st[sp].step = 0; sp++;
       ip += 4;
@@ -401,7 +403,7 @@ static int general_reachable(const uint8_t* code, uint32_t len, const uint8_t* i
       int min0 = (code[ip + 1] | (code[ip + 2] << 8)) == 0;
       if (!is_start || min0)
       {
-        if (sp == 16) return 1;
+        if (sp == 16) return 2;
         st[sp].ip = ip + off; st[sp].b = b; st[sp].j = 0; st[sp].jmax = 0; st[sp].step = 0; sp++;
       }
       ip += 9;
@@ -418,7 +420,7 @@ static int general_reachable(const uint8_t* code, uint32_t len, const uint8_t* i
       {
         if (mn < jmax)
         {
-          if (sp == 16) return 1;
+          if (sp == 16) return 2;
           st[sp].ip = ip + 5; st[sp].b = b; st[sp].j = mn + 1; st[sp].jmax = jmax; st[sp].step = cs;
           sp++;
         }
@@ -430,7 +432,7 @@ static int general_reachable(const uint8_t* code, uint32_t len, const uint8_t* i
     else
     {
       int sz = re_sz(op);
-      if (sz == 0) return 1;
+      if (sz == 0) return 2;
       if (b >= maxb) alive = 0;
       else
       {
@@ -472,16 +474,16 @@ static int general_reachable(const uint8_t* code, uint32_t len, const uint8_t* i
     b = st[sp - 1].b + st[sp - 1].j * st[sp - 1].step;
     if (++st[sp - 1].j > st[sp - 1].jmax) sp--;
   }
-  return 1;
+  return 2;
 }
 
 /*
- * Does the regex call (non-literal string, pool entry k at offset off) have a
- * possible effect?  _yr_scan_verify_re_match (scan.c:778-880): the forward
- * program from `off` must match (forward_matches != -1), then, if a backward
- * program exists, it must match backwards from `off` (its MATCHes are what
- * reach _yr_scan_match_callback); forward_matches == 0 without a backward
- * program returns early too.  Only FAST ascii hex strings are decided.
+ * Does a yr_re_exec regex call have a possible effect?  _yr_scan_verify_re_match
+ * (scan.c:817-848): the ascii attempt runs for ASCII / base64 strings, the wide
+ * one for WIDE non-base64 strings when the ascii one found nothing, the
+ * backward program with the flags of the attempt that matched.  Since a "1"
+ * forward answer may be a reference miss, every attempt is tried; an answer of
+ * 2 (search exhausted) keeps the call.
  */
 static int general_call_effect(uint32_t flags, const uint8_t* fwd, uint32_t fl, const uint8_t* bwd,
                                uint32_t bl, const uint8_t* data, uint64_t size, uint64_t off,
@@ -495,13 +497,22 @@ static int general_call_effect(uint32_t flags, const uint8_t* fwd, uint32_t fl, 
   for (int w = 0; w < 2; w++)
   {
     if (w == 0 ? !try_ascii : !try_wide) continue;
-    if (!general_reachable(fwd, fl, data + off, size - off, 0, w, nocase, dotall, lower)) continue;
-    if (bl == 0 || general_reachable(bwd, bl, data + off, off, 1, w, nocase, dotall, lower))
+    int f = general_reachable(fwd, fl, data + off, size - off, 0, w, nocase, dotall, lower);
+    if (f == 2) return 1;
+    if (f == 0) continue;
+    if (bl == 0 || general_reachable(bwd, bl, data + off, off, 1, w, nocase, dotall, lower) != 0)
       return 1;
   }
   return 0;
 }
 
+/*
+ * FAST (hex) strings, _yr_scan_verify_re_match (scan.c:778-880) with
+ * yr_re_fast_exec: the forward program from `off` must match
+ * (forward_matches != -1); with a backward program its MATCHes are what reach
+ * _yr_scan_match_callback; forward_matches == 0 without one returns early.
+ * Only ascii hex strings are decided.
+ */
 static int re_call_effect(uint32_t flags, const uint8_t* fwd, uint32_t fl, const uint8_t* bwd,
                           uint32_t bl, const uint8_t* data, uint64_t size, uint64_t off)
 {

@@ -149,3 +149,21 @@ def test_fast_mode_abort_and_too_many_matches(tmp_path, preverify):
     assert res["rc_stock"] == 0 and res["rc_gpu"] == 0, res
     assert res["too_many"][0] > 0 and res["too_many"] == [res["too_many"][0]] * 2, res
     assert res["same_matches"] and res["same_rule_reports"], res
+
+
+@needs_check
+@pytest.mark.parametrize("preverify", [True, False], ids=["preverify", "full-replay"])
+def test_regexp_fiber_limit_error_is_preserved(tmp_path, preverify):
+    """A yr_re_exec call that fails with ERROR_TOO_MANY_RE_FIBERS (re.c:1228,
+    RE_MAX_FIBERS = 1024) fails the stock scan even though it matches nothing;
+    pre-verification must keep that call (its search budget is below the fiber
+    limit), so the shim reports the same error."""
+    rf = tmp_path / "fib.yar"
+    rf.write_text('rule fib { strings: $a = /x(a{1,40}){1,40}b/ condition: $a }\n'
+                  'rule other { strings: $b = "needle" condition: $b }\n')
+    d = np.zeros(64 << 10, np.uint8)
+    d[100:106] = np.frombuffer(b"needle", np.uint8)
+    run = b"x" + b"a" * 3000 + b"c"
+    d[4096:4096 + len(run)] = np.frombuffer(run, np.uint8)
+    rc, res = _run(str(rf), _data_file(tmp_path, d, "d.bin"), preverify=preverify)
+    assert res["rc_stock"] == 46 and res["rc_gpu"] == 46, res   # ERROR_TOO_MANY_RE_FIBERS

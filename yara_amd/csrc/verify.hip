@@ -157,9 +157,15 @@ __device__ bool fast_re_reachable(const uint8_t* __restrict__ code, uint32_t len
 // of REPEAT_START/END loops and REPEAT_ANY ranges, word-boundary and anchor
 // assertions, the \w \s \d classes.  A reference fiber's path is therefore
 // always one of these paths, and "unreachable" proves forward_matches == -1.
-// Depth-first with an explicit choice stack; stack or step budget exhausted
-// -> true (keep the call).
-__device__ bool general_re_reachable(const uint8_t* __restrict__ code, uint32_t len,
+// Depth-first with an explicit choice stack.  Stack or step budget exhausted,
+// or code this analysis does not know -> kPathUnknown, and the caller keeps the
+// call outright.  The budget (1000 steps) is below RE_MAX_FIBERS (1024,
+// limits.h:168): every live reference fiber is a distinct node of this search
+// tree, so an exec that would fail with ERROR_TOO_MANY_RE_FIBERS
+// (re.c:1228-1229, a scan error the host must still see) always exhausts it.
+constexpr int kPathDead = 0, kPathMatch = 1, kPathUnknown = 2;
+constexpr int kReGeneralBudget = 1000;
+__device__ int general_re_reachable(const uint8_t* __restrict__ code, uint32_t len,
                                      const uint8_t* __restrict__ input, uint64_t avail,
                                      bool backwards, bool wide, bool nocase, bool dotall,
                                      const uint8_t* __restrict__ lower) {
@@ -174,33 +180,33 @@ __device__ bool general_re_reachable(const uint8_t* __restrict__ code, uint32_t 
   maxb -= maxb % cs;
   int32_t ip = 0;
   int b = 0;
-  for (int budget = 0; budget < 4096; ++budget) {
-    if (ip < 0 || (uint32_t)ip >= len) return true;
+  for (int budget = 0; budget < kReGeneralBudget; ++budget) {
+    if (ip < 0 || (uint32_t)ip >= len) return kPathUnknown;
     const uint8_t op = code[ip];
     bool dead = false;
     switch (op) {
       case kOpMatch:
-        return true;
+        return kPathMatch;
       case kOpJump:
         ip += re_i16(code + ip + 1);
         continue;
       case kOpSplitA:
       case kOpSplitB:
-        if (sp == kMaxChoices) return true;
+        if (sp == kMaxChoices) return kPathUnknown;
         st[sp++] = Choice{ip + re_i16(code + ip + 2), b, 0, 0, 0};
         ip += 4;
         continue;
       case kOpRepeatStartGreedy:
       case kOpRepeatStartUngreedy:
         if (re_u16(code + ip + 1) == 0) {   // min == 0: the body may be skipped
-          if (sp == kMaxChoices) return true;
+          if (sp == kMaxChoices) return kPathUnknown;
           st[sp++] = Choice{ip + re_i32(code + ip + 5), b, 0, 0, 0};
         }
         ip += 9;
         continue;
       case kOpRepeatEndGreedy:
       case kOpRepeatEndUngreedy:   // loop back or leave, any number of times
-        if (sp == kMaxChoices) return true;
+        if (sp == kMaxChoices) return kPathUnknown;
         st[sp++] = Choice{ip + re_i32(code + ip + 5), b, 0, 0, 0};
         ip += 9;
         continue;
@@ -219,7 +225,7 @@ __device__ bool general_re_reachable(const uint8_t* __restrict__ code, uint32_t 
           break;
         }
         if (mn < jmax) {
-          if (sp == kMaxChoices) return true;
+          if (sp == kMaxChoices) return kPathUnknown;
           st[sp++] = Choice{ip + 5, b, mn + 1, jmax, cs};
         }
         b += mn * cs;
@@ -228,7 +234,7 @@ __device__ bool general_re_reachable(const uint8_t* __restrict__ code, uint32_t 
       }
       default: {
         const uint32_t sz = re_op_size(op);
-        if (sz == 0) return true;   // not a program this analysis knows
+        if (sz == 0) return kPathUnknown;   // not a program this analysis knows
         if (b >= maxb) {
           dead = true;
           break;
@@ -269,13 +275,13 @@ __device__ bool general_re_reachable(const uint8_t* __restrict__ code, uint32_t 
       }
     }
     if (!dead) continue;
-    if (sp == 0) return false;
+    if (sp == 0) return kPathDead;
     Choice& t = st[sp - 1];
     ip = t.ip;
     b = t.b + t.j * t.step;
     if (++t.j > t.jmax) --sp;
   }
-  return true;
+  return kPathUnknown;
 }
 
 // _yr_scan_verify_re_match (scan.c:778-880) for FAST ascii hex strings: the
@@ -305,14 +311,18 @@ __device__ bool re_call_matters(const VerifyParams& p, uint32_t k, uint32_t flag
   const bool nocase = flags & kStrNoCase, dotall = flags & kStrDotAll;
   const bool try_ascii = flags & (kStrAscii | kStrBase64Any);
   const bool try_wide = (flags & kStrWide) && !(flags & kStrBase64Any);
+  // A forward "match" here may be a reference miss, after which the wide
+  // attempt runs: both branches are covered by trying every attempt.
   for (int w = 0; w < 2; ++w) {
     if (w == 0 ? !try_ascii : !try_wide) continue;
-    if (!general_re_reachable(fwd, r.fwd_len, d, p.size - offset, false, w == 1, nocase, dotall,
-                              p.lowercase))
-      continue;
-    if (r.bwd_len == 0 ||
-        general_re_reachable(bwd, r.bwd_len, d, offset, true, w == 1, nocase, dotall, p.lowercase))
-      return true;
+    const int f = general_re_reachable(fwd, r.fwd_len, d, p.size - offset, false, w == 1, nocase,
+                                       dotall, p.lowercase);
+    if (f == kPathUnknown) return true;
+    if (f == kPathDead) continue;
+    if (r.bwd_len == 0) return true;
+    const int b = general_re_reachable(bwd, r.bwd_len, d, offset, true, w == 1, nocase, dotall,
+                                       p.lowercase);
+    if (b != kPathDead) return true;
   }
   return false;
 }
