@@ -28,33 +28,42 @@ constexpr int kFilterLog2Bits = 20;
 constexpr uint32_t kFilterWords = 1u << (kFilterLog2Bits - 5);   // 32768
 constexpr uint32_t kFilterBytes = kFilterWords * 4;              // 131072
 
-// Per-wave LDS ring of filter hits awaiting the exact check: one 32-byte entry
-// per (tile, lane) with hits = the lane's 20 bytes of window context + mask.
+// Per-wave LDS ring of filter hits awaiting the exact check: one 24-byte entry
+// per (tile, lane) with hits = the lane's 20 bytes of window context + mask;
+// then per wave a pending list of 64 {window, offset} pairs (kernels.hip).
 constexpr uint32_t kQueueCap = 64;
-constexpr uint32_t kQueueEntryWords = 8;
-constexpr uint32_t kQueueBytes = kWavesPerWG * kQueueCap * kQueueEntryWords * 4;   // 32 KiB
-constexpr uint32_t kScanLdsBytes = kFilterBytes + kQueueBytes;                   // 160 KiB
+constexpr uint32_t kQueueEntryWords = 6;
+constexpr uint32_t kQueueBytes = kWavesPerWG * kQueueCap * kQueueEntryWords * 4;   // 24 KiB
+constexpr uint32_t kPendBytes = kWavesPerWG * kWave * 8;                          // 8 KiB
+constexpr uint32_t kScanLdsBytes = kFilterBytes + kQueueBytes + kPendBytes;       // 160 KiB
 
-// Split-block Bloom filter probe of a 3-byte window x = a | b << 8 | c << 16
-// (a = oldest byte).  The filter is 2^14 blocks of two 32-bit words (lo, hi);
-// a key sets one bit in each word of its block, and a position passes when
-// both are set: one ds_read_b64 and the same VOP2 shift/and work per position
-// as a single-word block with k = 2, but each bit now lives in a 32-position
-// space of its own, so a block holding one key passes 1/1024 of random
-// windows instead of 1/256 (config C: 0.15% false positives vs 0.24%).  The
-// three fields are disjoint and cover the window exactly:
-//   block = x[10..23]   device byte address: (x >> 7) & 0x1FFF8
-//   b_lo  = x[0..4]     device: the shifter reads only bits 0..4 of x
-//   b_hi  = x[5..9]     device: x >> 5, same
-// Bits 24..31 of a window register are never read, so it may carry a
-// neighbouring byte there.
+// Pair filter over 3-byte windows: one 8-byte block serves the windows ending
+// at two adjacent positions.  With a | b << 8 | c << 16 | d << 24 the four
+// bytes around a pair (positions of c and d), both windows (a,b,c) and
+// (b,c,d) contain b and c, and the block is chosen by b[2..7] and c alone;
+// each window then tests one bit of the block's low word and one of its high
+// word, picked by the bits of that window not in the block index (10 each):
+//   block = x[10..23]           device byte address (x >> 7) & 0x1FFF8
+//   left  (a,b,c): lo x[0..4]  = a[0..4],  hi x[5..9]  = a[5..7] b[0..1]
+//   right (b,c,d): lo x[24..28] = d[0..4], hi d[5..7] b[0..1]
+// Every key window is inserted in both roles (a window may end at either
+// position of a pair), so a block holds ~2x the keys of a one-window block
+// (config C: 0.39% of random positions pass instead of 0.15%), but one
+// ds_read_b64 now serves two positions: the LDS bank conflicts of these
+// random reads were the kernel's bound.
 struct FilterProbe {
   uint32_t block;  // index into the kFilterWords / 2 blocks; words 2*block, 2*block+1
   uint32_t b_lo, b_hi;
 };
-__host__ __device__ inline FilterProbe filter_probe(uint32_t w3) {
+// window w3 = p | q << 8 | r << 16 in the left role (p, q, r) = (a, b, c)
+__host__ __device__ inline FilterProbe filter_probe_left(uint32_t w3) {
   const uint32_t x = w3 & 0xFFFFFFu;
   return FilterProbe{x >> 10, x & 31u, (x >> 5) & 31u};
+}
+// the same window in the right role (p, q, r) = (b, c, d)
+__host__ __device__ inline FilterProbe filter_probe_right(uint32_t w3) {
+  const uint32_t x = w3 & 0xFFFFFFu;
+  return FilterProbe{x >> 2 & 0x3FFFu, (x >> 16) & 31u, ((x >> 21) & 7u) | ((x & 3u) << 3)};
 }
 
 // Exact key sets (second stage), one uint32 array in HBM:
@@ -66,10 +75,23 @@ __host__ __device__ inline FilterProbe filter_probe(uint32_t w3) {
 //                 chains).  t3 stores key | 1 << 24, t4 stores the key; 0 marks
 //                 an empty slot (a 4-byte key of 0 is kept in a flag).
 // Keys are little endian: the first byte of the key in bits 0..7.
+//   [2056, +32768) first-level word filter of the 3- and 4-byte keys (below)
 constexpr uint32_t kExactBm1 = 0;
 constexpr uint32_t kExactBm2 = 8;
-constexpr uint32_t kExactHeadWords = 8 + 2048;
+constexpr uint32_t kExactFl = 8 + 2048;
+constexpr uint32_t kExactFlWords = 1u << 15;
+constexpr uint32_t kExactHeadWords = kExactFl + kExactFlWords;
 constexpr uint32_t kExactZero4 = 1u;   // flag: the 4-byte key 0x00000000 exists
+
+// First level of the exact check (one dword = one cache line per filter hit
+// instead of four 16-byte buckets): the word is chosen by the last 3 bytes of
+// the position's window; a 3-byte key sets one of its bits 0..15 (picked by
+// the same 3 bytes), a 4-byte key one of bits 16..31 (picked by all 4).  A
+// clear bit proves "no 3-/4-byte key ends here"; a set one sends the position
+// to the bucket tables.  w4 = the 4 bytes ending at the position.
+__host__ __device__ inline uint32_t fl_word(uint32_t w4) { return ((w4 >> 8) * 0x9E3779B1u) >> 17; }
+__host__ __device__ inline uint32_t fl_bit3(uint32_t w4) { return ((w4 >> 8) * 0x85EBCA77u) >> 28; }
+__host__ __device__ inline uint32_t fl_bit4(uint32_t w4) { return 16u + ((w4 * 0xC2B2AE35u) >> 28); }
 
 __host__ __device__ inline uint32_t bucket_hash1(uint32_t key) {
   uint32_t h = key * 0x9E3779B1u;

@@ -11,10 +11,10 @@
 // That makes every position independent of every other: no sequential state
 // chain, just a window test.
 //
-//   stage 1 (every byte, LDS):  a split-block Bloom filter (2^20 bits) over
-//             the 3-byte window ending at the byte (internal.h filter_probe).
-//             128 KiB, staged once per workgroup; one ds_read_b64 per input
-//             byte.  Superset of the keys (config C: 0.15% of positions pass).
+//   stage 1 (every byte, LDS):  a pair filter (2^20 bits) over the 3-byte
+//             window ending at each byte (internal.h filter_probe_left/right).
+//             128 KiB, staged once per workgroup; one ds_read_b64 per two
+//             input bytes.  Superset of the keys (config C: 0.39% pass).
 //   stage 2 (filter hits):  hits are appended in position order to a per-wave
 //             LDS ring; full batches of 64 are checked exactly against the key
 //             sets (bitmaps / bucketed cuckoo tables in HBM/L2), and survivors
@@ -43,71 +43,136 @@ __device__ __forceinline__ uint32_t wave_inclusive_scan(uint32_t v) {
   return v;
 }
 
+// Does some of the 8 bucket slots hold `k`?  (min over slot ^ k == 0: two
+// v_min3 and one v_min instead of a compare/select chain.)
+__device__ __forceinline__ bool bucket_pair_has(const uint4& a, const uint4& b, uint32_t k) {
+  const uint32_t x = min(min(a.x ^ k, a.y ^ k), a.z ^ k);
+  const uint32_t y = min(min(a.w ^ k, b.x ^ k), b.y ^ k);
+  const uint32_t z = min(min(b.z ^ k, b.w ^ k), min(x, y));
+  return z == 0u;
+}
+
 // Exact test of one position `pos` of the block: does a key of length
 // L <= min(4, pos) equal the last L bytes before it?  w4 = those 4 bytes,
 // little endian (oldest lowest; zeros before the block start).  Every load
-// (bitmap words, both candidate buckets of each table) is independent: one
-// round trip.
+// (bitmap words, both candidate buckets of each table) is issued before any
+// result is used -- one round trip -- and the branches are wave-uniform (the
+// key-length set `len_mask`); tables that are not in use are never read.
+template <bool kLoads = true>
 __device__ __forceinline__ bool exact_check(uint32_t w4, uint64_t pos, const ScanParams& p) {
   const uint32_t* __restrict__ ex = p.exact;
-  bool hit = false;
   const uint32_t lm = p.len_mask;
-  if ((lm & 2u) && pos >= 1) {
-    const uint32_t k = w4 >> 24;
-    hit |= (ex[kExactBm1 + (k >> 5)] >> (k & 31)) & 1u;
-  }
-  if ((lm & 4u) && pos >= 2) {
-    const uint32_t k = w4 >> 16;
-    hit |= (ex[kExactBm2 + (k >> 5)] >> (k & 31)) & 1u;
-  }
-  if ((lm & 8u) && pos >= 3) {
-    const uint32_t k = (w4 >> 8) | (1u << 24);
-    const uint4 a = *reinterpret_cast<const uint4*>(ex + p.t3_off + (bucket_hash1(k) & p.t3_mask) * 4);
-    const uint4 b = *reinterpret_cast<const uint4*>(ex + p.t3_off + (bucket_hash2(k) & p.t3_mask) * 4);
-    hit |= a.x == k || a.y == k || a.z == k || a.w == k || b.x == k || b.y == k || b.z == k || b.w == k;
-  }
-  if ((lm & 16u) && pos >= 4) {
-    const uint32_t k = w4;
-    if (k == 0) {
-      hit |= (p.exact_flags & kExactZero4) != 0;
-    } else {
-      const uint4 a = *reinterpret_cast<const uint4*>(ex + p.t4_off + (bucket_hash1(k) & p.t4_mask) * 4);
-      const uint4 b = *reinterpret_cast<const uint4*>(ex + p.t4_off + (bucket_hash2(k) & p.t4_mask) * 4);
-      hit |= a.x == k || a.y == k || a.z == k || a.w == k || b.x == k || b.y == k || b.z == k || b.w == k;
+  const uint32_t k1 = w4 >> 24, k2 = w4 >> 16, k3 = (w4 >> 8) | (1u << 24), k4 = w4;
+  uint32_t v1 = 0, v2 = 0;
+  uint4 a3 = make_uint4(0, 0, 0, 0), b3 = a3, a4 = a3, b4 = a3;
+  if (lm & 2u) v1 = ex[kExactBm1 + (k1 >> 5)];
+  if (lm & 4u) v2 = ex[kExactBm2 + (k2 >> 5)];
+  if constexpr (!kLoads) {   // ablation: the same VALU, no memory round trip
+    const uint32_t h3 = bucket_hash1(k3) & p.t3_mask, g3 = bucket_hash2(k3) & p.t3_mask;
+    const uint32_t h4 = bucket_hash1(k4) & p.t4_mask, g4 = bucket_hash2(k4) & p.t4_mask;
+    a3 = make_uint4(h3, h3 + 1, h3 + 2, h3 + 3);
+    b3 = make_uint4(g3, g3 + 1, g3 + 2, g3 + 3);
+    a4 = make_uint4(h4, h4 + 1, h4 + 2, h4 + 3);
+    b4 = make_uint4(g4, g4 + 1, g4 + 2, g4 + 3);
+  } else {
+    if (lm & 8u) {
+      a3 = *reinterpret_cast<const uint4*>(ex + p.t3_off + (bucket_hash1(k3) & p.t3_mask) * 4);
+      b3 = *reinterpret_cast<const uint4*>(ex + p.t3_off + (bucket_hash2(k3) & p.t3_mask) * 4);
+    }
+    if (lm & 16u) {
+      a4 = *reinterpret_cast<const uint4*>(ex + p.t4_off + (bucket_hash1(k4) & p.t4_mask) * 4);
+      b4 = *reinterpret_cast<const uint4*>(ex + p.t4_off + (bucket_hash2(k4) & p.t4_mask) * 4);
     }
   }
+  bool hit = false;
+  if (lm & 2u) hit |= pos >= 1 && ((v1 >> (k1 & 31)) & 1u);
+  if (lm & 4u) hit |= pos >= 2 && ((v2 >> (k2 & 31)) & 1u);
+  if (lm & 8u) hit |= pos >= 3 && bucket_pair_has(a3, b3, k3);   // k3 != 0: empty slots never match
+  if (lm & 16u)
+    hit |= pos >= 4 && (k4 == 0 ? (p.exact_flags & kExactZero4) != 0 : bucket_pair_has(a4, b4, k4));
   return hit;
 }
 
-// The 4 bytes ending at lane byte j (0..15) from the lane's window context
-// C[0] = the 4 bytes before the lane, C[1..4] = its 16 bytes.
-__device__ __forceinline__ uint32_t window4(const uint32_t (&C)[5], uint32_t j) {
+// First level (internal.h fl_word): false proves that no key ends at the
+// position; true sends it to exact_check.  Rule sets with 1- or 2-byte keys
+// skip this level (every hit goes to exact_check).
+__device__ __forceinline__ bool first_level(uint32_t w4, const ScanParams& p) {
+  if (p.len_mask & 6u) return true;
+  const uint32_t d = p.exact[kExactFl + fl_word(w4)];
+  return ((d >> fl_bit3(w4)) | (d >> fl_bit4(w4))) & 1u;
+}
+
+// The 4 bytes ending at lane byte j (0..15) of a ring entry whose dwords 0..4
+// are the lane's window context (the 4 bytes before the lane, then its 16):
+// entry bytes j+1 .. j+4, from two aligned LDS dwords.
+__device__ __forceinline__ uint32_t window4(const uint32_t* ent, uint32_t j) {
   const uint32_t o = j + 1, i = o >> 2;
-  uint32_t lo = C[0], hi = C[1];
-  if (i == 1) { lo = C[1]; hi = C[2]; }
-  if (i == 2) { lo = C[2]; hi = C[3]; }
-  if (i == 3) { lo = C[3]; hi = C[4]; }
-  if (i == 4) { lo = C[4]; hi = 0u; }
-  return __builtin_amdgcn_alignbyte(hi, lo, o & 3u);
+  return __builtin_amdgcn_alignbyte(ent[i + 1], ent[i], o & 3u);
 }
 
 // Lane byte (0..15) of bit b of a tile hit mask: bit 8n + r <=> byte 4n + r.
 __device__ __forceinline__ uint32_t mask_position(uint32_t b) { return ((b >> 3) << 2) | (b & 3u); }
 
-// Per-wave LDS ring of filter hits awaiting the exact check.  One entry (32-byte
-// slot, 24 bytes written) per (tile, lane) with at least one hit: the lane's
-// window context (4 bytes before it + its 16 bytes) and (lane byte offset in
-// segment / 16) | (16-bit hit mask, bit j = lane byte j) << 16.  Entries are appended in lane order, so ring order
-// is ascending position order.  The exact check then needs no global load
-// of the input, only the hash-table probes.
+// Per-wave LDS ring of filter hits awaiting the exact check.  One entry (24
+// bytes) per (tile, lane) with at least one hit: the lane's window context (4
+// bytes before it + its 16 bytes) and (lane byte offset in segment / 16) |
+// (16-bit hit mask, bit j = lane byte j) << 16.  Entries are appended in lane
+// order, so ring order is ascending position order.  The exact check then
+// needs no global load of the input, only table probes.
+//
+// Drains run the first level of the exact check (internal.h fl_word: one
+// dword per hit) over 64 entries; the few hits that pass it go, in order, to
+// a per-wave pending list of (window, offset) pairs, and the bucket probes
+// run once that list holds a wave's worth -- one lane per hit, one round
+// trip per 64 hits instead of one per drain.
 struct WaveQueue {
   uint32_t* ring;   // kQueueCap entries of kQueueEntryWords dwords
   uint32_t head;    // wave-uniform counters (monotonic)
   uint32_t tail;
+  uint32_t* pend;   // kWave pairs {w4, segment offset}
+  uint32_t pend_n;  // wave-uniform
 };
 
-// Exact-check the hits of up to 64 ring entries and append the survivors, in
-// order, to the segment's output.
+// Bucket-probe every pending hit (one lane each) and append the survivors,
+// in order, to the segment's output.
+__device__ __forceinline__ void flush_pending(const ScanParams& p, WaveQueue& q, uint32_t lane,
+                                              uint64_t seg_start, uint32_t* out, uint32_t& found) {
+  __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+  bool keep = false;
+  uint32_t off = 0;
+  if (lane < q.pend_n) {
+    const uint2 e = *reinterpret_cast<const uint2*>(q.pend + 2 * lane);
+    off = e.y;
+    keep = exact_check(e.x, seg_start + off + 1, p);
+  }
+  const uint64_t b = __ballot(keep);
+  if (keep) {
+    const uint32_t idx = found + __builtin_amdgcn_mbcnt_hi((uint32_t)(b >> 32),
+                                                           __builtin_amdgcn_mbcnt_lo((uint32_t)b, 0u));
+    if (idx < p.seg_cap) out[idx] = off;
+  }
+  found += (uint32_t)__popcll(b);
+  q.pend_n = 0;
+}
+
+// Append hits (bit j of `keep` = lane byte j at segment offset off0 + j) to
+// the segment's output in order.  incl = inclusive scan of popcount(keep).
+__device__ __forceinline__ void append_hits(const ScanParams& p, uint32_t keep, uint32_t c,
+                                            uint32_t incl, uint32_t off0, uint32_t* out,
+                                            uint32_t& found) {
+  uint32_t idx = found + incl - c;
+  while (keep) {
+    const uint32_t j = (uint32_t)__builtin_ctz(keep);
+    keep &= keep - 1;
+    if (idx < p.seg_cap) out[idx] = off0 + j;
+    ++idx;
+  }
+  found += __builtin_amdgcn_readlane(incl, kWave - 1);
+}
+
+// First-level check of the hits of up to 64 ring entries; survivors go to
+// the pending list (or, if a drain alone yields more than 64 of them, are
+// bucket-probed in place).
 template <int MODE>
 __device__ __forceinline__ void drain(const ScanParams& p, WaveQueue& q, uint32_t lane,
                                       uint64_t seg_start, uint32_t* out, uint32_t& found) {
@@ -120,33 +185,58 @@ __device__ __forceinline__ void drain(const ScanParams& p, WaveQueue& q, uint32_
     __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "workgroup");   // ring in global memory
   else
     __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
-  uint32_t keep = 0, off0 = 0;
+  uint32_t maybe = 0, off0 = 0;
+  const uint32_t* ent = q.ring + ((q.head + lane) % kQueueCap) * kQueueEntryWords;
   if (lane < n) {
-    const uint32_t* ent = q.ring + ((q.head + lane) % kQueueCap) * kQueueEntryWords;
-    const uint4 a = *reinterpret_cast<const uint4*>(ent);
-    const uint2 b = *reinterpret_cast<const uint2*>(ent + 4);
-    const uint32_t C[5] = {a.x, a.y, a.z, a.w, b.x};
-    off0 = (b.y & 0xFFFFu) * kBytesPerLane;
-    uint32_t m = b.y >> 16;   // 16-bit mask, bit j = lane byte j
+    const uint32_t packed = ent[5];
+    off0 = (packed & 0xFFFFu) * kBytesPerLane;
+    uint32_t m = packed >> 16;   // 16-bit mask, bit j = lane byte j
     while (m) {
       const uint32_t j = (uint32_t)__builtin_ctz(m);
       m &= m - 1;
-      const bool hit = MODE == 1 ? ((off0 + j) & 1023u) == 7u
-                                 : exact_check(window4(C, j), seg_start + off0 + j + 1, p);
-      keep |= (uint32_t)hit << j;
+      bool hit;
+      if constexpr (MODE == 1) {
+        hit = ((off0 + j) & 1023u) == 7u;
+      } else if constexpr (MODE == 9) {   // one L2 dword per hit, minimal VALU
+        hit = (p.exact[kExactBm2 + (window4(ent, j) & 2047u)] >> 31) != 0u;
+      } else if constexpr (MODE == 10) {
+        hit = exact_check<false>(window4(ent, j), seg_start + off0 + j + 1, p);
+      } else {
+        hit = first_level(window4(ent, j), p);
+      }
+      maybe |= (uint32_t)hit << j;
     }
   }
-  const uint32_t c = __popc(keep);
-  const uint32_t incl = wave_inclusive_scan(c);
-  uint32_t idx = found + incl - c;
-  while (keep) {
-    const uint32_t j = (uint32_t)__builtin_ctz(keep);
-    keep &= keep - 1;
-    if (idx < p.seg_cap) out[idx] = off0 + j;
-    ++idx;
-  }
-  found += __builtin_amdgcn_readlane(incl, kWave - 1);
   q.head += n;
+  const uint32_t c = __popc(maybe);
+  const uint32_t incl = wave_inclusive_scan(c);
+  if constexpr (MODE == 1 || MODE == 9 || MODE == 10) {   // ablations: output as is
+    append_hits(p, maybe, c, incl, off0, out, found);
+    return;
+  }
+  const uint32_t total = __builtin_amdgcn_readlane(incl, kWave - 1);
+  if (total == 0) return;
+  if (q.pend_n + total > kWave) flush_pending(p, q, lane, seg_start, out, found);
+  if (total <= kWave) {
+    uint32_t idx = q.pend_n + incl - c;
+    while (maybe) {
+      const uint32_t j = (uint32_t)__builtin_ctz(maybe);
+      maybe &= maybe - 1;
+      *reinterpret_cast<uint2*>(q.pend + 2 * idx) = make_uint2(window4(ent, j), off0 + j);
+      ++idx;
+    }
+    q.pend_n += total;
+    return;
+  }
+  // more than a wave's worth from one drain (dense true hits): probe in place
+  uint32_t keep = 0;
+  while (maybe) {
+    const uint32_t j = (uint32_t)__builtin_ctz(maybe);
+    maybe &= maybe - 1;
+    keep |= (uint32_t)exact_check(window4(ent, j), seg_start + off0 + j + 1, p) << j;
+  }
+  const uint32_t kc = __popc(keep);
+  append_hits(p, keep, kc, wave_inclusive_scan(kc), off0, out, found);
 }
 
 // A tile entirely inside the block: one 16-byte non-temporal load per lane
@@ -203,58 +293,68 @@ __device__ __forceinline__ void tile_step(const ScanParams& p, WaveQueue& q, Seg
   st.carry = __builtin_amdgcn_readlane(cur.w, kWave - 1);
   const uint32_t S[6] = {S0, cur.x, cur.y, cur.z, cur.w, 0u};
 
-  // Phase A: the 16 windows of this lane and their 16 filter-block reads.
-  uint32_t xs[kBytesPerLane];
-  uint2 ws[kBytesPerLane];
+  // Phase A: the lane's 8 position pairs and their 8 filter-block reads.
+  // Pair j covers lane bytes k = 2j and k + 1; xs[j] = bytes k-2 .. k+1
+  // (stream offset k + 2: even, so an aligned dword or one alignbyte).
+  constexpr int kPairs = kBytesPerLane / 2;
+  uint32_t xs[kPairs];
+  uint2 ws[kPairs];
 #pragma unroll
-  for (int k = 0; k < kBytesPerLane; ++k) {
-    // low 24 bits = bytes k-2, k-1, k of this lane (stream offset k + 2)
-    const int o = k + 2;
-    xs[k] = (o & 3) == 0   ? S[o >> 2]
-            : (o & 3) == 1 ? S[o >> 2] >> 8
-                           : __builtin_amdgcn_alignbyte(S[(o >> 2) + 1], S[o >> 2], o & 3);
+  for (int j = 0; j < kPairs; ++j) {
+    const int o = 2 * j + 2;
+    xs[j] = (o & 3) == 0 ? S[o >> 2] : __builtin_amdgcn_alignbyte(S[(o >> 2) + 1], S[o >> 2], 2);
     if constexpr (MODE != 3) {
-      const uint32_t x = xs[k];
+      const uint32_t x = xs[j];
       uint32_t addr = (x >> 7) & (kFilterBytes - 8);   // block x[10..23], 8 B each
-      if constexpr (MODE == 4) addr = ((lane & 31u) * 8u + (uint32_t)k * 256u) & (kFilterBytes - 8);
+      if constexpr (MODE == 4) addr = ((lane & 31u) * 8u + (uint32_t)j * 256u) & (kFilterBytes - 8);
       if constexpr (MODE == 5) {
-        ws[k] = make_uint2(addr ^ x, addr + x);
+        ws[j] = make_uint2(addr ^ x, addr + x);
       } else {
         typedef uint32_t u32x2 __attribute__((ext_vector_type(2)));
         const u32x2 v = *reinterpret_cast<const __attribute__((address_space(3))) u32x2*>(
             (uintptr_t)addr);   // filter sits at LDS offset 0: no base add
-        ws[k] = make_uint2(v.x, v.y);
+        ws[j] = make_uint2(v.x, v.y);
       }
     }
   }
-  // Phase B: split-block test, bit x[0..4] of the lo word and bit x[5..9] of
-  // the hi word (the shifter reads only the low 5 bits of the amount).  The
-  // AND of the two shifted words is written by one SDWA v_and straight into
-  // byte n of accumulator r (k = 4n + r), so bit 0 of that byte is position
-  // k's result and no separate accumulate instruction is needed; bits 1..7
-  // of each byte are don't-care and masked off once per tile below.
+  // Phase B: the two windows of each pair against their block (internal.h
+  // filter_probe_left / _right): left (position k) bit x[0..4] of the lo word
+  // and x[5..9] of the hi word; right (position k + 1) the same fields of
+  // y = d | b << 8 (one v_perm).  The shifter reads only the low 5 bits of the
+  // amount.  The AND of the two shifted words is written by one SDWA v_and
+  // straight into byte n of accumulator r (position 4n + r), so bit 0 of that
+  // byte is the position's result and no separate accumulate instruction is
+  // needed; bits 1..7 of each byte are don't-care and masked off below.
   uint32_t acc[4];   // every byte is written below: no initial value needed
+  if constexpr (MODE == 3 || MODE == 6) acc[0] = acc[1] = acc[2] = acc[3] = 0u;
+#define YAMD_SDWA_AND(K, U, V)                                                                   \
+  switch ((K) >> 2) {                                                                            \
+    case 0: asm("v_and_b32_sdwa %0, %1, %2 dst_sel:BYTE_0 dst_unused:UNUSED_PRESERVE src0_sel:DWORD src1_sel:DWORD" \
+                : "+v"(acc[(K) & 3]) : "v"(U), "v"(V)); break;                                   \
+    case 1: asm("v_and_b32_sdwa %0, %1, %2 dst_sel:BYTE_1 dst_unused:UNUSED_PRESERVE src0_sel:DWORD src1_sel:DWORD" \
+                : "+v"(acc[(K) & 3]) : "v"(U), "v"(V)); break;                                   \
+    case 2: asm("v_and_b32_sdwa %0, %1, %2 dst_sel:BYTE_2 dst_unused:UNUSED_PRESERVE src0_sel:DWORD src1_sel:DWORD" \
+                : "+v"(acc[(K) & 3]) : "v"(U), "v"(V)); break;                                   \
+    default: asm("v_and_b32_sdwa %0, %1, %2 dst_sel:BYTE_3 dst_unused:UNUSED_PRESERVE src0_sel:DWORD src1_sel:DWORD" \
+                 : "+v"(acc[(K) & 3]) : "v"(U), "v"(V)); break;                                  \
+  }
 #pragma unroll
-  for (int k = 0; k < kBytesPerLane; ++k) {
+  for (int j = 0; j < kPairs; ++j) {
+    const int k = 2 * j;
     if constexpr (MODE == 3) {
-      acc[k & 3] ^= xs[k];
+      acc[k & 3] ^= xs[j];
     } else if constexpr (MODE == 6) {
-      acc[k & 3] ^= ws[k].x ^ ws[k].y;
+      acc[k & 3] ^= ws[j].x ^ ws[j].y;
     } else {
-      const uint32_t x = xs[k];
-      const uint32_t u = ws[k].x >> (x & 31u), v = ws[k].y >> ((x >> 5) & 31u);
-      switch (k >> 2) {
-        case 0: asm("v_and_b32_sdwa %0, %1, %2 dst_sel:BYTE_0 dst_unused:UNUSED_PRESERVE src0_sel:DWORD src1_sel:DWORD"
-                    : "+v"(acc[k & 3]) : "v"(u), "v"(v)); break;
-        case 1: asm("v_and_b32_sdwa %0, %1, %2 dst_sel:BYTE_1 dst_unused:UNUSED_PRESERVE src0_sel:DWORD src1_sel:DWORD"
-                    : "+v"(acc[k & 3]) : "v"(u), "v"(v)); break;
-        case 2: asm("v_and_b32_sdwa %0, %1, %2 dst_sel:BYTE_2 dst_unused:UNUSED_PRESERVE src0_sel:DWORD src1_sel:DWORD"
-                    : "+v"(acc[k & 3]) : "v"(u), "v"(v)); break;
-        default: asm("v_and_b32_sdwa %0, %1, %2 dst_sel:BYTE_3 dst_unused:UNUSED_PRESERVE src0_sel:DWORD src1_sel:DWORD"
-                     : "+v"(acc[k & 3]) : "v"(u), "v"(v)); break;
-      }
+      const uint32_t x = xs[j];
+      const uint32_t ul = ws[j].x >> (x & 31u), vl = ws[j].y >> ((x >> 5) & 31u);
+      YAMD_SDWA_AND(k, ul, vl);
+      const uint32_t y = __builtin_amdgcn_perm(0u, x, 0x0c0c0103u);   // d | b << 8
+      const uint32_t ur = ws[j].x >> (y & 31u), vr = ws[j].y >> ((y >> 5) & 31u);
+      YAMD_SDWA_AND(k + 1, ur, vr);
     }
   }
+#undef YAMD_SDWA_AND
   if constexpr (MODE >= 2 && MODE <= 6) {
     asm volatile("" ::"v"(acc[0] ^ acc[1] ^ acc[2] ^ acc[3]));
     return;
@@ -284,7 +384,8 @@ __device__ __forceinline__ void tile_step(const ScanParams& p, WaveQueue& q, Seg
       // nibbles (bit 8n + r) are packed: t = m | m >> 4 has them in bytes 0, 2
       const uint32_t t = mask | (mask >> 4);
       const uint32_t m16 = __builtin_amdgcn_perm(0u, t, 0x0c0c0200u);   // bytes 0, 2
-      *reinterpret_cast<uint4*>(ent) = make_uint4(S[0], S[1], S[2], S[3]);
+      *reinterpret_cast<uint2*>(ent) = make_uint2(S[0], S[1]);
+      *reinterpret_cast<uint2*>(ent + 2) = make_uint2(S[2], S[3]);
       *reinterpret_cast<uint2*>(ent + 4) = make_uint2(S[4], (lane_off / kBytesPerLane) | (m16 << 16));
     }
     q.tail += n;
@@ -300,7 +401,8 @@ __device__ __forceinline__ void tile_step(const ScanParams& p, WaveQueue& q, Seg
 // bank-conflict-free LDS addresses, 5 = stage 1 VALU without the LDS reads,
 // 6 = stage 1 addresses + LDS reads without the bit tests, 7 = stage 1 +
 // ring appends, drains drop the entries, 8 = product with the hit rings in
-// global memory (L2) instead of LDS.
+// global memory (L2) instead of LDS, 9 = exact check replaced by one L2 dword
+// load per hit, 10 = exact-check VALU with the bucket loads replaced by values.
 template <int MODE>
 __device__ void scan_segment(const ScanParams& p, WaveQueue& q, uint32_t seg, uint32_t lane) {
   SegState st;
@@ -315,6 +417,7 @@ __device__ void scan_segment(const ScanParams& p, WaveQueue& q, uint32_t seg, ui
   // 4 bytes before the segment (warm-up halo); zeros before the block start.
   st.carry = st.seg_start >= 4 ? *reinterpret_cast<const uint32_t*>(base - 4) : 0u;
   q.head = q.tail = 0;
+  q.pend_n = 0;
 
   const uint32_t n_full = st.seg_len / kTile;            // tiles needing no mask / bounds
   const uint32_t n_all = (st.seg_len + kTile - 1) / kTile;
@@ -331,6 +434,7 @@ __device__ void scan_segment(const ScanParams& p, WaveQueue& q, uint32_t seg, ui
   }
   if (n_all > n_full) tile_step<MODE, true>(p, q, st, cur, n_full * kTile, lane);
   while (q.tail != q.head) drain<MODE>(p, q, lane, st.seg_start, st.out, st.found);
+  if (q.pend_n != 0) flush_pending(p, q, lane, st.seg_start, st.out, st.found);
   if (lane == 0) p.seg_count[seg] = st.found;
 }
 
@@ -353,6 +457,7 @@ __global__ __launch_bounds__(kWGThreads, 1) void scan_segments_kernel(ScanParams
     q.ring = p.gring + ((size_t)blockIdx.x * kWavesPerWG + wid) * kQueueCap * kQueueEntryWords;
   else
     q.ring = lds + kFilterWords + wid * kQueueCap * kQueueEntryWords;
+  q.pend = lds + kFilterWords + kWavesPerWG * kQueueCap * kQueueEntryWords + wid * 2 * kWave;
   const uint32_t total_waves = gridDim.x * kWavesPerWG;
   for (uint32_t seg = blockIdx.x * kWavesPerWG + wid; seg < p.n_segments; seg += total_waves) {
     scan_segment<MODE>(p, q, seg, lane);
@@ -467,6 +572,8 @@ hipError_t launch_scan(const ScanParams& p, int grid, hipStream_t s, int mode) {
     case 6: hipLaunchKernelGGL(scan_segments_kernel<6>, dim3(grid), dim3(kWGThreads), lds, s, p); break;
     case 7: hipLaunchKernelGGL(scan_segments_kernel<7>, dim3(grid), dim3(kWGThreads), lds, s, p); break;
     case 8: hipLaunchKernelGGL(scan_segments_kernel<8>, dim3(grid), dim3(kWGThreads), kFilterBytes, s, p); break;
+    case 9: hipLaunchKernelGGL(scan_segments_kernel<9>, dim3(grid), dim3(kWGThreads), lds, s, p); break;
+    case 10: hipLaunchKernelGGL(scan_segments_kernel<10>, dim3(grid), dim3(kWGThreads), lds, s, p); break;
     default: hipLaunchKernelGGL(scan_segments_kernel<0>, dim3(grid), dim3(kWGThreads), lds, s, p); break;
   }
   return hipGetLastError();
@@ -499,7 +606,8 @@ hipError_t configure_scan_kernel() {
                         (const void*)scan_segments_kernel<2>, (const void*)scan_segments_kernel<3>,
                         (const void*)scan_segments_kernel<4>, (const void*)scan_segments_kernel<5>,
                         (const void*)scan_segments_kernel<6>, (const void*)scan_segments_kernel<7>,
-                        (const void*)scan_segments_kernel<8>}) {
+                        (const void*)scan_segments_kernel<8>, (const void*)scan_segments_kernel<9>,
+                        (const void*)scan_segments_kernel<10>}) {
     hipError_t r = hipFuncSetAttribute(k, hipFuncAttributeMaxDynamicSharedMemorySize, lds);
     if (r != hipSuccess) e = r;
   }

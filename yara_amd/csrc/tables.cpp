@@ -39,9 +39,10 @@ struct Node {
 inline uint64_t node_key(uint32_t bytes, uint32_t depth) { return ((uint64_t)depth << 32) | bytes; }
 
 void filter_set(std::vector<uint32_t>& f, uint32_t w3) {
-  const FilterProbe fp = filter_probe(w3);
-  f[2 * fp.block] |= 1u << fp.b_lo;
-  f[2 * fp.block + 1] |= 1u << fp.b_hi;
+  for (const FilterProbe fp : {filter_probe_left(w3), filter_probe_right(w3)}) {
+    f[2 * fp.block] |= 1u << fp.b_lo;
+    f[2 * fp.block + 1] |= 1u << fp.b_hi;
+  }
 }
 
 // Two-choice, 4-way bucketed cuckoo table of non-zero keys.  Load <= 1/2 to
@@ -212,10 +213,14 @@ int flatten_tables(const uint32_t* T, const uint32_t* M, uint32_t n_slots,
     switch (k.len) {
       case 1: out.exact[kExactBm1 + (k.bytes >> 5)] |= 1u << (k.bytes & 31); break;
       case 2: out.exact[kExactBm2 + (k.bytes >> 5)] |= 1u << (k.bytes & 31); break;
-      case 3: k3.push_back(k.bytes | (1u << 24)); break;
+      case 3:
+        k3.push_back(k.bytes | (1u << 24));
+        out.exact[kExactFl + fl_word(k.bytes << 8)] |= 1u << fl_bit3(k.bytes << 8);
+        break;
       case 4:
         if (k.bytes == 0) out.exact_flags |= kExactZero4;
         else k4.push_back(k.bytes);
+        out.exact[kExactFl + fl_word(k.bytes)] |= 1u << fl_bit4(k.bytes);
         break;
     }
   }
