@@ -30,6 +30,16 @@ __global__ __launch_bounds__(1024) void k(uint32_t* out, uint32_t iters, uint32_
         if constexpr (OP == 11)  // v_lshrrev_b32_sdwa, amount = byte 1 of a register
           asm("v_lshrrev_b32_sdwa %0, %1, %0 dst_sel:DWORD dst_unused:UNUSED_PAD src0_sel:BYTE_1 src1_sel:DWORD"
               : "+v"(a[i]) : "v"(a[(i + 1) & 7]));
+        if constexpr (OP == 12)  // packed 16-bit shift: two shifts per lane
+          asm("v_pk_lshrrev_b16 %0, %1, %0" : "+v"(a[i]) : "v"(a[(i + 1) & 7]));
+        if constexpr (OP == 13)  // v_and_or_b32
+          asm("v_and_or_b32 %0, %1, %2, %0" : "+v"(a[i]) : "v"(a[(i + 1) & 7]), "v"(a[(i + 2) & 7]));
+        if constexpr (OP == 14)  // v_bitop3_b32 (a & b) | c
+          asm("v_bitop3_b32 %0, %1, %2, %0 bitop3:0xec" : "+v"(a[i]) : "v"(a[(i + 1) & 7]), "v"(a[(i + 2) & 7]));
+        if constexpr (OP == 15)  // v_lshl_or_b32 with a register shift amount
+          asm("v_lshl_or_b32 %0, %1, %2, %0" : "+v"(a[i]) : "v"(a[(i + 1) & 7]), "v"(a[(i + 2) & 7]));
+        if constexpr (OP == 16)  // v_lshrrev_b32 (VOP2) alone
+          asm("v_lshrrev_b32 %0, %1, %0" : "+v"(a[i]) : "v"(a[(i + 1) & 7]));
       }
     }
   }
@@ -55,15 +65,18 @@ int main() {
   uint32_t* out; hipMalloc(&out, 4);
   int cus; hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, 0);
   const uint32_t iters = 4096;
-  const char* names[] = {"alignbit", "mul_u24+xor", "mul_hi_u24+add", "lshr+xor", "add", "alignbyte", "perm", "bfe+xor", "lshr,lshl,bitop3", "lshl_or", "and_sdwa_byte", "lshr_sdwa_src"};
+  const char* names[] = {"alignbit", "mul_u24+xor", "mul_hi_u24+add", "lshr+xor", "add", "alignbyte", "perm", "bfe+xor", "lshr,lshl,bitop3", "lshl_or", "and_sdwa_byte", "lshr_sdwa_src",
+                         "pk_lshrrev_b16", "and_or", "bitop3", "lshl_or_vvv", "lshrrev_vop2"};
   for (int g : {cus, 2 * cus}) {
-    double ms[12] = {run<0>(out, g, iters), run<1>(out, g, iters), run<2>(out, g, iters),
+    double ms[17] = {run<0>(out, g, iters), run<1>(out, g, iters), run<2>(out, g, iters),
                     run<3>(out, g, iters), run<4>(out, g, iters), run<5>(out, g, iters),
                     run<6>(out, g, iters), run<7>(out, g, iters), run<8>(out, g, iters),
-                    run<9>(out, g, iters), run<10>(out, g, iters), run<11>(out, g, iters)};
-    for (int o = 0; o < 12; ++o) {
+                    run<9>(out, g, iters), run<10>(out, g, iters), run<11>(out, g, iters),
+                    run<12>(out, g, iters), run<13>(out, g, iters), run<14>(out, g, iters),
+                    run<15>(out, g, iters), run<16>(out, g, iters)};
+    for (int o = 0; o < 17; ++o) {
       // wave-instructions executed per chain-step
-      const double nops[12] = {1, 2, 2, 2, 1, 1, 1, 2, 3, 1, 1, 1};
+      const double nops[17] = {1, 2, 2, 2, 1, 1, 1, 2, 3, 1, 1, 1, 1, 1, 1, 1, 1};
       double ops = nops[o];
       double winstr = (double)g * 16 * iters * 64 * ops;
       printf("grid %d  %-15s %8.3f ms  %.3f wave-instr/clk/CU @2.4GHz  (%.1f G lane-op/s/CU)\n", g,

@@ -170,12 +170,16 @@ __device__ __forceinline__ void append_hits(const ScanParams& p, uint32_t keep, 
   found += __builtin_amdgcn_readlane(incl, kWave - 1);
 }
 
+template <int MODE, bool kAny>
+__device__ __forceinline__ uint32_t stage1(const uint32_t (&S)[6], uint32_t lane);
+
 // First-level check of the hits of up to 64 ring entries; survivors go to
 // the pending list (or, if a drain alone yields more than 64 of them, are
 // bucket-probed in place).
 template <int MODE>
 __device__ __forceinline__ void drain(const ScanParams& p, WaveQueue& q, uint32_t lane,
-                                      uint64_t seg_start, uint32_t* out, uint32_t& found) {
+                                      uint64_t seg_start, uint32_t seg_len, uint32_t* out,
+                                      uint32_t& found) {
   const uint32_t n = min(q.tail - q.head, (uint32_t)kWave);
   if constexpr (MODE == 7) {   // ablation: ring appends only, entries dropped
     q.head += n;
@@ -188,9 +192,22 @@ __device__ __forceinline__ void drain(const ScanParams& p, WaveQueue& q, uint32_
   uint32_t maybe = 0, off0 = 0;
   const uint32_t* ent = q.ring + ((q.head + lane) % kQueueCap) * kQueueEntryWords;
   if (lane < n) {
-    const uint32_t packed = ent[5];
-    off0 = (packed & 0xFFFFu) * kBytesPerLane;
-    uint32_t m = packed >> 16;   // 16-bit mask, bit j = lane byte j
+    // the entry's 16 positions again, now with a per-position result
+    const uint2 e0 = *reinterpret_cast<const uint2*>(ent);
+    const uint2 e1 = *reinterpret_cast<const uint2*>(ent + 2);
+    const uint2 e2 = *reinterpret_cast<const uint2*>(ent + 4);
+    const uint32_t S[6] = {e0.x, e0.y, e1.x, e1.y, e2.x, 0u};
+    off0 = e2.y * kBytesPerLane;
+    uint32_t mk = stage1<MODE, false>(S, lane);   // bit 8n + r <=> lane byte 4n + r
+    if (off0 + kBytesPerLane > seg_len) {        // the segment's partial last tile
+      const uint32_t lim = off0 >= seg_len ? 0u : seg_len - off0;
+      uint32_t keep_bits = 0;
+      for (uint32_t j = 0; j < lim; ++j) keep_bits |= 1u << (((j >> 2) << 3) | (j & 3u));
+      mk &= keep_bits;
+    }
+    // 16-bit mask, bit j = lane byte j: t = mk | mk >> 4 has the nibbles in bytes 0, 2
+    const uint32_t t = mk | (mk >> 4);
+    uint32_t m = __builtin_amdgcn_perm(0u, t, 0x0c0c0200u);
     while (m) {
       const uint32_t j = (uint32_t)__builtin_ctz(m);
       m &= m - 1;
@@ -282,17 +299,11 @@ struct SegState {
   uint32_t carry;   // the 4 bytes before the current tile (lane 0's window head)
 };
 
-// One 1 KiB tile: stage-1 filter over its 1024 byte positions, then the ordered
-// append of the hits to the wave ring.  TAIL: the segment's last, partial tile
-// (positions past seg_len are masked off).
-template <int MODE, bool TAIL>
-__device__ __forceinline__ void tile_step(const ScanParams& p, WaveQueue& q, SegState& st,
-                                          uint4 cur, uint32_t tile_off, uint32_t lane) {
-  // previous lane's last dword (lane 0: the previous tile's / the halo)
-  const uint32_t S0 = __builtin_amdgcn_update_dpp(st.carry, cur.w, 0x138, 0xF, 0xF, false);  // wave_shr:1
-  st.carry = __builtin_amdgcn_readlane(cur.w, kWave - 1);
-  const uint32_t S[6] = {S0, cur.x, cur.y, cur.z, cur.w, 0u};
-
+// Stage 1 of one 1 KiB tile: the filter over its 1024 byte positions.  Returns
+// the lane's hit mask (bit 8n + r <=> lane byte 4n + r), or with kAny only
+// whether any of the lane's 16 positions passes.
+template <int MODE, bool kAny>
+__device__ __forceinline__ uint32_t stage1(const uint32_t (&S)[6], uint32_t lane) {
   // Phase A: the lane's 8 position pairs and their 8 filter-block reads.
   // Pair j covers lane bytes k = 2j and k + 1; xs[j] = bytes k-2 .. k+1
   // (stream offset k + 2: even, so an aligned dword or one alignbyte).
@@ -317,6 +328,7 @@ __device__ __forceinline__ void tile_step(const ScanParams& p, WaveQueue& q, Seg
       }
     }
   }
+  if constexpr (MODE == 11) __builtin_amdgcn_sched_barrier(0);   // ablation: all 8 reads first
   // Phase B: the two windows of each pair against their block (internal.h
   // filter_probe_left / _right): left (position k) bit x[0..4] of the lo word
   // and x[5..9] of the hi word; right (position k + 1) the same fields of
@@ -325,12 +337,38 @@ __device__ __forceinline__ void tile_step(const ScanParams& p, WaveQueue& q, Seg
   // straight into byte n of accumulator r (position 4n + r), so bit 0 of that
   // byte is the position's result and no separate accumulate instruction is
   // needed; bits 1..7 of each byte are don't-care and masked off below.
-  uint32_t acc[4];   // every byte is written below: no initial value needed
+  if constexpr (kAny && MODE != 3 && MODE != 6) {
+    // the main loop only needs "does any position of this lane pass?": OR the
+    // shifted-word ANDs together (v_bitop3: full rate, unlike SDWA) and keep
+    // bit 0; the drain recomputes the per-position results of the few lanes
+    // that do
+    uint32_t a0, a1;
+#pragma unroll
+    for (int j = 0; j < kPairs; ++j) {
+      const uint32_t x = xs[j];
+      const uint32_t ul = ws[j].x >> (x & 31u), vl = ws[j].y >> ((x >> 5) & 31u);
+      const uint32_t y = __builtin_amdgcn_perm(0u, x, 0x0c0c0103u);   // d | b << 8
+      const uint32_t ur = ws[j].x >> (y & 31u), vr = ws[j].y >> ((y >> 5) & 31u);
+      if (j == 0) {
+        a0 = ul & vl;
+        a1 = ur & vr;
+      } else {   // acc |= u & v in one v_bitop3 (S0 = u, S1 = v, S2 = acc: 0xF0 & 0xCC | 0xAA)
+        asm("v_bitop3_b32 %0, %1, %2, %0 bitop3:0xea" : "+v"(a0) : "v"(ul), "v"(vl));
+        asm("v_bitop3_b32 %0, %1, %2, %0 bitop3:0xea" : "+v"(a1) : "v"(ur), "v"(vr));
+      }
+    }
+    if constexpr (MODE == 2 || MODE == 4 || MODE == 5) {   // ablations: no ring
+      asm volatile("" ::"v"(a0 | a1));
+      return 0u;
+    }
+    return (a0 | a1) & 1u;
+  }
+  uint32_t acc[4];   // byte 0 written first (zero-padding the rest), then bytes 1..3
   if constexpr (MODE == 3 || MODE == 6) acc[0] = acc[1] = acc[2] = acc[3] = 0u;
 #define YAMD_SDWA_AND(K, U, V)                                                                   \
   switch ((K) >> 2) {                                                                            \
-    case 0: asm("v_and_b32_sdwa %0, %1, %2 dst_sel:BYTE_0 dst_unused:UNUSED_PRESERVE src0_sel:DWORD src1_sel:DWORD" \
-                : "+v"(acc[(K) & 3]) : "v"(U), "v"(V)); break;                                   \
+    case 0: asm("v_and_b32_sdwa %0, %1, %2 dst_sel:BYTE_0 dst_unused:UNUSED_PAD src0_sel:DWORD src1_sel:DWORD" \
+                : "=v"(acc[(K) & 3]) : "v"(U), "v"(V)); break;                                   \
     case 1: asm("v_and_b32_sdwa %0, %1, %2 dst_sel:BYTE_1 dst_unused:UNUSED_PRESERVE src0_sel:DWORD src1_sel:DWORD" \
                 : "+v"(acc[(K) & 3]) : "v"(U), "v"(V)); break;                                   \
     case 2: asm("v_and_b32_sdwa %0, %1, %2 dst_sel:BYTE_2 dst_unused:UNUSED_PRESERVE src0_sel:DWORD src1_sel:DWORD" \
@@ -357,39 +395,63 @@ __device__ __forceinline__ void tile_step(const ScanParams& p, WaveQueue& q, Seg
 #undef YAMD_SDWA_AND
   if constexpr (MODE >= 2 && MODE <= 6) {
     asm volatile("" ::"v"(acc[0] ^ acc[1] ^ acc[2] ^ acc[3]));
-    return;
+    return 0u;
   }
   // hit mask: bit 8n + r <=> position 4n + r of the lane (mask_position())
-  uint32_t mask = (acc[0] & 0x01010101u) | ((acc[1] & 0x01010101u) << 1) |
-                  ((acc[2] & 0x01010101u) << 2) | ((acc[3] & 0x01010101u) << 3);
+  return (acc[0] & 0x01010101u) | ((acc[1] & 0x01010101u) << 1) |
+         ((acc[2] & 0x01010101u) << 2) | ((acc[3] & 0x01010101u) << 3);
+}
+
+// The ordered append of a tile's hits to the wave ring.  TAIL: the segment's
+// last, partial tile (positions past seg_len are masked off).
+template <int MODE, bool TAIL>
+__device__ __forceinline__ void ring_append(const ScanParams& p, WaveQueue& q, SegState& st,
+                                            const uint32_t (&S)[6], uint32_t any,
+                                            uint32_t tile_off, uint32_t lane) {
+  if constexpr (MODE >= 2 && MODE <= 6) return;
   const uint32_t lane_off = tile_off + lane * kBytesPerLane;
   if constexpr (TAIL) {
-    if (lane_off + kBytesPerLane > st.seg_len) {
-      const uint32_t lim = lane_off >= st.seg_len ? 0u : st.seg_len - lane_off;
-      uint32_t keep = 0;
-      for (uint32_t j = 0; j < lim; ++j) keep |= 1u << (((j >> 2) << 3) | (j & 3u));
-      mask &= keep;
-    }
+    if (lane_off >= st.seg_len) any = 0u;   // lanes wholly past the segment end
   }
-  const uint64_t any = __ballot(mask != 0);
-  if (any != 0) {
-    const uint32_t n = (uint32_t)__popcll(any);
-    if (q.tail - q.head + n > kQueueCap) drain<MODE>(p, q, lane, st.seg_start, st.out, st.found);
-    if (mask != 0) {
-      const uint32_t below = __builtin_amdgcn_mbcnt_hi((uint32_t)(any >> 32),
-                                                       __builtin_amdgcn_mbcnt_lo((uint32_t)any, 0u));
+  const uint64_t lanes = __ballot(any != 0);
+  if (lanes != 0) {
+    const uint32_t n = (uint32_t)__popcll(lanes);
+    if (q.tail - q.head + n > kQueueCap)
+      drain<MODE>(p, q, lane, st.seg_start, st.seg_len, st.out, st.found);
+    if (any != 0) {
+      const uint32_t below = __builtin_amdgcn_mbcnt_hi((uint32_t)(lanes >> 32),
+                                                       __builtin_amdgcn_mbcnt_lo((uint32_t)lanes, 0u));
       uint32_t* ent = q.ring + ((q.tail + below) % kQueueCap) * kQueueEntryWords;
-      // 24-byte entry (b128 + b64: 19 LDS transfer cycles instead of 26):
-      // context, then (lane index in segment) | (16-bit mask) << 16; the mask's
-      // nibbles (bit 8n + r) are packed: t = m | m >> 4 has them in bytes 0, 2
-      const uint32_t t = mask | (mask >> 4);
-      const uint32_t m16 = __builtin_amdgcn_perm(0u, t, 0x0c0c0200u);   // bytes 0, 2
+      // 24-byte entry: the window context, then the lane index in the segment
       *reinterpret_cast<uint2*>(ent) = make_uint2(S[0], S[1]);
       *reinterpret_cast<uint2*>(ent + 2) = make_uint2(S[2], S[3]);
-      *reinterpret_cast<uint2*>(ent + 4) = make_uint2(S[4], (lane_off / kBytesPerLane) | (m16 << 16));
+      *reinterpret_cast<uint2*>(ent + 4) = make_uint2(S[4], lane_off / kBytesPerLane);
     }
     q.tail += n;
   }
+}
+
+// The lane's window context: the previous lane's last dword (lane 0: the
+// previous tile's, or the halo), then its own 16 bytes.
+__device__ __forceinline__ void tile_context(SegState& st, const uint4& cur, uint32_t (&S)[6]) {
+  S[0] = __builtin_amdgcn_update_dpp(st.carry, cur.w, 0x138, 0xF, 0xF, false);  // wave_shr:1
+  st.carry = __builtin_amdgcn_readlane(cur.w, kWave - 1);
+  S[1] = cur.x;
+  S[2] = cur.y;
+  S[3] = cur.z;
+  S[4] = cur.w;
+  S[5] = 0u;
+}
+
+// One 1 KiB tile: stage-1 filter over its 1024 byte positions, then the ordered
+// append of the hits to the wave ring.
+template <int MODE, bool TAIL>
+__device__ __forceinline__ void tile_step(const ScanParams& p, WaveQueue& q, SegState& st,
+                                          uint4 cur, uint32_t tile_off, uint32_t lane) {
+  uint32_t S[6];
+  tile_context(st, cur, S);
+  const uint32_t any = stage1<MODE, true>(S, lane);
+  ring_append<MODE, TAIL>(p, q, st, S, any, tile_off, lane);
 }
 
 // Stream one segment [seg_start, seg_start + seg_len) of the block: full tiles
@@ -402,7 +464,8 @@ __device__ __forceinline__ void tile_step(const ScanParams& p, WaveQueue& q, Seg
 // 6 = stage 1 addresses + LDS reads without the bit tests, 7 = stage 1 +
 // ring appends, drains drop the entries, 8 = product with the hit rings in
 // global memory (L2) instead of LDS, 9 = exact check replaced by one L2 dword
-// load per hit, 10 = exact-check VALU with the bucket loads replaced by values.
+// load per hit, 10 = exact-check VALU with the bucket loads replaced by values,
+// 11 = product with all 8 filter reads of a tile issued before any test.
 template <int MODE>
 __device__ void scan_segment(const ScanParams& p, WaveQueue& q, uint32_t seg, uint32_t lane) {
   SegState st;
@@ -427,13 +490,14 @@ __device__ void scan_segment(const ScanParams& p, WaveQueue& q, uint32_t seg, ui
                       : (t < n_all ? load_tile(base, t * kTile, lane, avail) : make_uint4(0, 0, 0, 0));
   };
   uint4 cur = fetch(0);
-  for (uint32_t t = 0; t < n_full; ++t) {
+  uint32_t t = 0;
+  for (; t < n_full; ++t) {
     const uint4 nxt = fetch(t + 1);
     tile_step<MODE, false>(p, q, st, cur, t * kTile, lane);
     cur = nxt;
   }
   if (n_all > n_full) tile_step<MODE, true>(p, q, st, cur, n_full * kTile, lane);
-  while (q.tail != q.head) drain<MODE>(p, q, lane, st.seg_start, st.out, st.found);
+  while (q.tail != q.head) drain<MODE>(p, q, lane, st.seg_start, st.seg_len, st.out, st.found);
   if (q.pend_n != 0) flush_pending(p, q, lane, st.seg_start, st.out, st.found);
   if (lane == 0) p.seg_count[seg] = st.found;
 }
@@ -574,6 +638,7 @@ hipError_t launch_scan(const ScanParams& p, int grid, hipStream_t s, int mode) {
     case 8: hipLaunchKernelGGL(scan_segments_kernel<8>, dim3(grid), dim3(kWGThreads), kFilterBytes, s, p); break;
     case 9: hipLaunchKernelGGL(scan_segments_kernel<9>, dim3(grid), dim3(kWGThreads), lds, s, p); break;
     case 10: hipLaunchKernelGGL(scan_segments_kernel<10>, dim3(grid), dim3(kWGThreads), lds, s, p); break;
+    case 11: hipLaunchKernelGGL(scan_segments_kernel<11>, dim3(grid), dim3(kWGThreads), lds, s, p); break;
     default: hipLaunchKernelGGL(scan_segments_kernel<0>, dim3(grid), dim3(kWGThreads), lds, s, p); break;
   }
   return hipGetLastError();
@@ -607,7 +672,7 @@ hipError_t configure_scan_kernel() {
                         (const void*)scan_segments_kernel<4>, (const void*)scan_segments_kernel<5>,
                         (const void*)scan_segments_kernel<6>, (const void*)scan_segments_kernel<7>,
                         (const void*)scan_segments_kernel<8>, (const void*)scan_segments_kernel<9>,
-                        (const void*)scan_segments_kernel<10>}) {
+                        (const void*)scan_segments_kernel<10>, (const void*)scan_segments_kernel<11>}) {
     hipError_t r = hipFuncSetAttribute(k, hipFuncAttributeMaxDynamicSharedMemorySize, lds);
     if (r != hipSuccess) e = r;
   }
