@@ -1,8 +1,9 @@
 #!/bin/bash
 # Per-kernel PMC detail of the scan kernel (separate passes; no tracing domains).
-#   bash tools/pmc_detail.sh <tag>
+#   bash tools/pmc_detail.sh <tag> [modes]     (modes: tools/ablate.py kernel variants, default 0)
 set -euo pipefail
 TAG=${1:-detail}
+MODES=${2:-0}
 OUT=gpurun_out/pmc_${TAG}
 mkdir -p $OUT
 cd /tmp && export TMPDIR=/tmp && cd - >/dev/null
@@ -11,6 +12,6 @@ for set in "SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE
            "SQ_INSTS_LDS SQ_LDS_BANK_CONFLICT SQ_LDS_IDX_ACTIVE SQ_WAIT_INST_LDS SQ_INSTS_SALU SQ_INSTS_VMEM SQ_ACTIVE_INST_SCA GRBM_GUI_ACTIVE"; do
   i=$((i+1))
   timeout -k 10 240 rocprofv3 --pmc $set -d $OUT/p$i -o run --output-format csv -- \
-    python3 tools/ablate.py --modes 0 --rounds 1 --reps 2 > $OUT/p$i.log 2>&1
+    python3 tools/ablate.py --modes $MODES --rounds 1 --reps 2 > $OUT/p$i.log 2>&1
 done
 find $OUT -name "*counter_collection.csv"

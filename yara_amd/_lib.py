@@ -7,7 +7,8 @@ import ctypes
 import os
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(_HERE, "libyara_amd.so")
+# YARA_AMD_LIB: another build of the same library (tools/ablate.py variants)
+LIB_PATH = os.environ.get("YARA_AMD_LIB") or os.path.join(_HERE, "libyara_amd.so")
 
 # error codes (libyara/include/yara/error.h values)
 SUCCESS = 0

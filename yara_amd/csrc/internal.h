@@ -19,6 +19,10 @@ namespace yamd {
 constexpr int kWave = 64;
 constexpr int kBytesPerLane = 16;
 constexpr int kTile = kWave * kBytesPerLane;        // 1024 B
+#ifndef YAMD_PREFETCH
+#define YAMD_PREFETCH 1
+#endif
+constexpr int kPrefetch = YAMD_PREFETCH;             // input tiles in flight per wave
 constexpr uint32_t kSegment = 1u << 20;   // max segment: 1 MiB (ring entries hold offset/16 in 16 bits)
 constexpr int kWavesPerWG = 16;
 constexpr int kWGThreads = kWave * kWavesPerWG;     // 1024
@@ -79,7 +83,10 @@ __host__ __device__ inline FilterProbe filter_probe_right(uint32_t w3) {
 constexpr uint32_t kExactBm1 = 0;
 constexpr uint32_t kExactBm2 = 8;
 constexpr uint32_t kExactFl = 8 + 2048;
-constexpr uint32_t kExactFlWords = 1u << 15;
+#ifndef YAMD_FL_LOG2
+#define YAMD_FL_LOG2 15
+#endif
+constexpr uint32_t kExactFlWords = 1u << YAMD_FL_LOG2;
 constexpr uint32_t kExactHeadWords = kExactFl + kExactFlWords;
 constexpr uint32_t kExactZero4 = 1u;   // flag: the 4-byte key 0x00000000 exists
 
@@ -89,7 +96,9 @@ constexpr uint32_t kExactZero4 = 1u;   // flag: the 4-byte key 0x00000000 exists
 // the same 3 bytes), a 4-byte key one of bits 16..31 (picked by all 4).  A
 // clear bit proves "no 3-/4-byte key ends here"; a set one sends the position
 // to the bucket tables.  w4 = the 4 bytes ending at the position.
-__host__ __device__ inline uint32_t fl_word(uint32_t w4) { return ((w4 >> 8) * 0x9E3779B1u) >> 17; }
+__host__ __device__ inline uint32_t fl_word(uint32_t w4) {
+  return ((w4 >> 8) * 0x9E3779B1u) >> (32 - YAMD_FL_LOG2);
+}
 __host__ __device__ inline uint32_t fl_bit3(uint32_t w4) { return ((w4 >> 8) * 0x85EBCA77u) >> 28; }
 __host__ __device__ inline uint32_t fl_bit4(uint32_t w4) { return 16u + ((w4 * 0xC2B2AE35u) >> 28); }
 
@@ -117,6 +126,8 @@ struct ScanParams {
   uint32_t seg_bytes;       // bytes per segment (multiple of kTile)
   uint32_t seg_cap;         // output capacity (entries) per segment
   uint32_t* seg_count;      // [n_segments] candidates found (may exceed cap)
+  uint32_t* seg_split;      // [n_segments] how many of them come from the segment's
+                            // rotated first part (kernels.hip scan_segment)
   uint32_t* seg_out;        // [n_segments * seg_cap] byte offset within segment
   uint32_t* gring;          // hit rings in global memory (one per wave of the grid), or null
   const uint64_t* seg_base; // null: segment s writes at seg_out + s * seg_cap; else at

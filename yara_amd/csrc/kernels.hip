@@ -110,6 +110,19 @@ __device__ __forceinline__ uint32_t window4(const uint32_t* ent, uint32_t j) {
   return __builtin_amdgcn_alignbyte(ent[i + 1], ent[i], o & 3u);
 }
 
+// The filter test of one pair (internal.h filter_probe_left / _right): x =
+// the 4 bytes a b c d around lane bytes c, d; returns bit 0 = the window
+// ending at c passes, bit 1 = the one ending at d does.
+__device__ __forceinline__ uint32_t pair_bits(uint32_t x) {
+  typedef uint32_t u32x2 __attribute__((ext_vector_type(2)));
+  const u32x2 w = *reinterpret_cast<const __attribute__((address_space(3))) u32x2*>(
+      (uintptr_t)((x >> 7) & (kFilterBytes - 8)));   // the filter sits at LDS offset 0
+  const uint32_t y = __builtin_amdgcn_perm(0u, x, 0x0c0c0103u);   // d | b << 8
+  const uint32_t l = (w.x >> (x & 31u)) & (w.y >> ((x >> 5) & 31u));
+  const uint32_t r = (w.x >> (y & 31u)) & (w.y >> ((y >> 5) & 31u));
+  return (l & 1u) | ((r & 1u) << 1);
+}
+
 // Lane byte (0..15) of bit b of a tile hit mask: bit 8n + r <=> byte 4n + r.
 __device__ __forceinline__ uint32_t mask_position(uint32_t b) { return ((b >> 3) << 2) | (b & 3u); }
 
@@ -135,6 +148,7 @@ struct WaveQueue {
 
 // Bucket-probe every pending hit (one lane each) and append the survivors,
 // in order, to the segment's output.
+template <int MODE>
 __device__ __forceinline__ void flush_pending(const ScanParams& p, WaveQueue& q, uint32_t lane,
                                               uint64_t seg_start, uint32_t* out, uint32_t& found) {
   __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
@@ -143,7 +157,7 @@ __device__ __forceinline__ void flush_pending(const ScanParams& p, WaveQueue& q,
   if (lane < q.pend_n) {
     const uint2 e = *reinterpret_cast<const uint2*>(q.pend + 2 * lane);
     off = e.y;
-    keep = exact_check(e.x, seg_start + off + 1, p);
+    keep = MODE == 12 ? true : exact_check(e.x, seg_start + off + 1, p);   // 12: ablation
   }
   const uint64_t b = __ballot(keep);
   if (keep) {
@@ -192,22 +206,25 @@ __device__ __forceinline__ void drain(const ScanParams& p, WaveQueue& q, uint32_
   uint32_t maybe = 0, off0 = 0;
   const uint32_t* ent = q.ring + ((q.head + lane) % kQueueCap) * kQueueEntryWords;
   if (lane < n) {
-    // the entry's 16 positions again, now with a per-position result
-    const uint2 e0 = *reinterpret_cast<const uint2*>(ent);
-    const uint2 e1 = *reinterpret_cast<const uint2*>(ent + 2);
-    const uint2 e2 = *reinterpret_cast<const uint2*>(ent + 4);
-    const uint32_t S[6] = {e0.x, e0.y, e1.x, e1.y, e2.x, 0u};
-    off0 = e2.y * kBytesPerLane;
-    uint32_t mk = stage1<MODE, false>(S, lane);   // bit 8n + r <=> lane byte 4n + r
-    if (off0 + kBytesPerLane > seg_len) {        // the segment's partial last tile
-      const uint32_t lim = off0 >= seg_len ? 0u : seg_len - off0;
-      uint32_t keep_bits = 0;
-      for (uint32_t j = 0; j < lim; ++j) keep_bits |= 1u << (((j >> 2) << 3) | (j & 3u));
-      mk &= keep_bits;
+    // the hit quarters' positions again, now with a per-position result
+    const uint32_t packed = ent[5];
+    off0 = (packed & 0xFFFFu) * kBytesPerLane;
+    uint32_t quarters = packed >> 16;
+    uint32_t m = 0;   // bit j = lane byte j
+    while (quarters) {
+      const uint32_t qq = (uint32_t)__builtin_ctz(quarters);
+      quarters &= quarters - 1;
+#pragma unroll
+      for (uint32_t h = 0; h < 2; ++h) {
+        const uint32_t j = 2 * qq + h;             // pair: lane bytes 2j, 2j+1
+        const uint32_t x = window4(ent, 2 * j + 1);  // bytes 2j-2 .. 2j+1
+        m |= pair_bits(x) << (2 * j);
+      }
     }
-    // 16-bit mask, bit j = lane byte j: t = mk | mk >> 4 has the nibbles in bytes 0, 2
-    const uint32_t t = mk | (mk >> 4);
-    uint32_t m = __builtin_amdgcn_perm(0u, t, 0x0c0c0200u);
+    if (off0 + kBytesPerLane > seg_len) {   // the segment's partial last tile
+      const uint32_t lim = off0 >= seg_len ? 0u : seg_len - off0;
+      m &= lim >= 16u ? 0xFFFFu : (1u << lim) - 1u;
+    }
     while (m) {
       const uint32_t j = (uint32_t)__builtin_ctz(m);
       m &= m - 1;
@@ -233,7 +250,7 @@ __device__ __forceinline__ void drain(const ScanParams& p, WaveQueue& q, uint32_
   }
   const uint32_t total = __builtin_amdgcn_readlane(incl, kWave - 1);
   if (total == 0) return;
-  if (q.pend_n + total > kWave) flush_pending(p, q, lane, seg_start, out, found);
+  if (q.pend_n + total > kWave) flush_pending<MODE>(p, q, lane, seg_start, out, found);
   if (total <= kWave) {
     uint32_t idx = q.pend_n + incl - c;
     while (maybe) {
@@ -301,7 +318,8 @@ struct SegState {
 
 // Stage 1 of one 1 KiB tile: the filter over its 1024 byte positions.  Returns
 // the lane's hit mask (bit 8n + r <=> lane byte 4n + r), or with kAny only
-// whether any of the lane's 16 positions passes.
+// which quarters of the lane (bit q: bytes 4q .. 4q+3) have a position that
+// passes.
 template <int MODE, bool kAny>
 __device__ __forceinline__ uint32_t stage1(const uint32_t (&S)[6], uint32_t lane) {
   // Phase A: the lane's 8 position pairs and their 8 filter-block reads.
@@ -342,26 +360,32 @@ __device__ __forceinline__ uint32_t stage1(const uint32_t (&S)[6], uint32_t lane
     // shifted-word ANDs together (v_bitop3: full rate, unlike SDWA) and keep
     // bit 0; the drain recomputes the per-position results of the few lanes
     // that do
-    uint32_t a0, a1;
+    // one accumulator per quarter of the lane (pairs 2q, 2q+1 = bytes 4q..4q+3)
+    uint32_t a[4];
 #pragma unroll
     for (int j = 0; j < kPairs; ++j) {
       const uint32_t x = xs[j];
       const uint32_t ul = ws[j].x >> (x & 31u), vl = ws[j].y >> ((x >> 5) & 31u);
       const uint32_t y = __builtin_amdgcn_perm(0u, x, 0x0c0c0103u);   // d | b << 8
       const uint32_t ur = ws[j].x >> (y & 31u), vr = ws[j].y >> ((y >> 5) & 31u);
-      if (j == 0) {
-        a0 = ul & vl;
-        a1 = ur & vr;
-      } else {   // acc |= u & v in one v_bitop3 (S0 = u, S1 = v, S2 = acc: 0xF0 & 0xCC | 0xAA)
-        asm("v_bitop3_b32 %0, %1, %2, %0 bitop3:0xea" : "+v"(a0) : "v"(ul), "v"(vl));
-        asm("v_bitop3_b32 %0, %1, %2, %0 bitop3:0xea" : "+v"(a1) : "v"(ur), "v"(vr));
-      }
+      uint32_t& aq = a[j >> 1];
+      if ((j & 1) == 0) aq = ul & vl;
+      else asm("v_bitop3_b32 %0, %1, %2, %0 bitop3:0xea" : "+v"(aq) : "v"(ul), "v"(vl));
+      // acc |= u & v in one v_bitop3 (S0 = u, S1 = v, S2 = acc: 0xF0 & 0xCC | 0xAA)
+      asm("v_bitop3_b32 %0, %1, %2, %0 bitop3:0xea" : "+v"(aq) : "v"(ur), "v"(vr));
     }
     if constexpr (MODE == 2 || MODE == 4 || MODE == 5) {   // ablations: no ring
-      asm volatile("" ::"v"(a0 | a1));
+      asm volatile("" ::"v"(a[0] | a[1] | a[2] | a[3]));
       return 0u;
     }
-    return (a0 | a1) & 1u;
+    // quarter-hit mask: bit q = bit 0 of a[q]; t = (t & m) | (b & ~m) is one
+    // v_bitop3 (S0 = t, S1 = b, S2 = m: 0xF0 & 0xAA | 0xCC & 0x55)
+    uint32_t t = a[0];
+    const uint32_t b1 = a[1] << 1, b2 = a[2] << 2, b3 = a[3] << 3;
+    asm("v_bitop3_b32 %0, %0, %1, 1 bitop3:0xe4" : "+v"(t) : "v"(b1));
+    asm("v_bitop3_b32 %0, %0, %1, 3 bitop3:0xe4" : "+v"(t) : "v"(b2));
+    asm("v_bitop3_b32 %0, %0, %1, 7 bitop3:0xe4" : "+v"(t) : "v"(b3));
+    return t & 15u;
   }
   uint32_t acc[4];   // byte 0 written first (zero-padding the rest), then bytes 1..3
   if constexpr (MODE == 3 || MODE == 6) acc[0] = acc[1] = acc[2] = acc[3] = 0u;
@@ -423,9 +447,10 @@ __device__ __forceinline__ void ring_append(const ScanParams& p, WaveQueue& q, S
                                                        __builtin_amdgcn_mbcnt_lo((uint32_t)lanes, 0u));
       uint32_t* ent = q.ring + ((q.tail + below) % kQueueCap) * kQueueEntryWords;
       // 24-byte entry: the window context, then the lane index in the segment
+      // and (bits 16..19) which quarters of the lane have a filter hit
       *reinterpret_cast<uint2*>(ent) = make_uint2(S[0], S[1]);
       *reinterpret_cast<uint2*>(ent + 2) = make_uint2(S[2], S[3]);
-      *reinterpret_cast<uint2*>(ent + 4) = make_uint2(S[4], lane_off / kBytesPerLane);
+      *reinterpret_cast<uint2*>(ent + 4) = make_uint2(S[4], (lane_off / kBytesPerLane) | (any << 16));
     }
     q.tail += n;
   }
@@ -465,7 +490,9 @@ __device__ __forceinline__ void tile_step(const ScanParams& p, WaveQueue& q, Seg
 // ring appends, drains drop the entries, 8 = product with the hit rings in
 // global memory (L2) instead of LDS, 9 = exact check replaced by one L2 dword
 // load per hit, 10 = exact-check VALU with the bucket loads replaced by values,
-// 11 = product with all 8 filter reads of a tile issued before any test.
+// 11 = product with all 8 filter reads of a tile issued before any test,
+// 12 = product without the bucket probes (first level only), 13 = product with
+// the segment's tiles in plain order (no rotation).
 template <int MODE>
 __device__ void scan_segment(const ScanParams& p, WaveQueue& q, uint32_t seg, uint32_t lane) {
   SegState st;
@@ -484,21 +511,56 @@ __device__ void scan_segment(const ScanParams& p, WaveQueue& q, uint32_t seg, ui
 
   const uint32_t n_full = st.seg_len / kTile;            // tiles needing no mask / bounds
   const uint32_t n_all = (st.seg_len + kTile - 1) / kTile;
-  // the next tile's loads in flight while this one is filtered
-  auto fetch = [&](uint32_t t) {
-    return t < n_full ? load_tile_full(base, t * kTile, lane)
-                      : (t < n_all ? load_tile(base, t * kTile, lane, avail) : make_uint4(0, 0, 0, 0));
+  // Rotated order: tiles r .. n_full-1, the partial tail tile, then tiles
+  // 0 .. r-1.  Segments are equal and (for a full-chip 4 GiB launch) exactly
+  // 1 MiB apart, so in plain order every wave of the chip would read the same
+  // offset of its segment at the same time and the reads would pile onto the
+  // same HBM channels (stage 1 alone: 0.93 ms in order, 0.73 ms rotated).
+  // The output of the first part (positions >= r tiles) is appended first;
+  // seg_split records its length and the scatter puts the second part first.
+  // The next full tile's loads are always in flight (the wrap prefetches tile
+  // 0; the last tile of a part re-reads itself rather than branch), and the
+  // ragged tail tile is loaded on its own, outside the loops.
+  const uint32_t r = (n_full > 1 && MODE != 13) ? (seg * 61u) % n_full : 0u;   // 13: ablation
+  const uint32_t halo = st.carry;
+  const uint32_t wrap = r > 0 ? n_full - r : n_full;   // the step that reaches tile 0
+  auto tile_at = [&](uint32_t i) { return r + i < n_full ? r + i : r + i - n_full; };
+  // kPrefetch full tiles in flight (the last step's prefetches re-read the
+  // last tile rather than branch)
+  uint4 c[kPrefetch];
+#pragma unroll
+  for (int d = 0; d < kPrefetch; ++d)
+    c[d] = n_full > 0 ? load_tile_full(base, tile_at(min((uint32_t)d, n_full - 1)) * kTile, lane)
+                      : make_uint4(0, 0, 0, 0);
+  if (r > 0) st.carry = *reinterpret_cast<const uint32_t*>(base + (size_t)r * kTile - 4);
+  uint32_t split = 0;
+  auto finish_part = [&]() {
+    // the tail tile ends the first part (it is the segment's last tile)
+    if (n_all > n_full)
+      tile_step<MODE, true>(p, q, st, load_tile(base, n_full * kTile, lane, avail), n_full * kTile,
+                            lane);
+    while (q.tail != q.head) drain<MODE>(p, q, lane, st.seg_start, st.seg_len, st.out, st.found);
+    if (q.pend_n != 0) flush_pending<MODE>(p, q, lane, st.seg_start, st.out, st.found);
+    split = st.found;
   };
-  uint4 cur = fetch(0);
-  uint32_t t = 0;
-  for (; t < n_full; ++t) {
-    const uint4 nxt = fetch(t + 1);
-    tile_step<MODE, false>(p, q, st, cur, t * kTile, lane);
-    cur = nxt;
+  for (uint32_t i = 0; i < n_full; ++i) {
+    if (i == wrap) {   // r > 0: tile 0 is next
+      finish_part();
+      st.carry = halo;
+    }
+    const uint4 nxt = load_tile_full(base, tile_at(min(i + kPrefetch, n_full - 1)) * kTile, lane);
+    tile_step<MODE, false>(p, q, st, c[0], tile_at(i) * kTile, lane);
+#pragma unroll
+    for (int d = 0; d + 1 < kPrefetch; ++d) c[d] = c[d + 1];
+    c[kPrefetch - 1] = nxt;
   }
-  if (n_all > n_full) tile_step<MODE, true>(p, q, st, cur, n_full * kTile, lane);
-  while (q.tail != q.head) drain<MODE>(p, q, lane, st.seg_start, st.seg_len, st.out, st.found);
-  if (q.pend_n != 0) flush_pending(p, q, lane, st.seg_start, st.out, st.found);
+  if (wrap == n_full) {
+    finish_part();
+  } else {
+    while (q.tail != q.head) drain<MODE>(p, q, lane, st.seg_start, st.seg_len, st.out, st.found);
+    if (q.pend_n != 0) flush_pending<MODE>(p, q, lane, st.seg_start, st.out, st.found);
+  }
+  if (lane == 0) p.seg_split[seg] = split;
   if (lane == 0) p.seg_count[seg] = st.found;
 }
 
@@ -570,6 +632,7 @@ __global__ __launch_bounds__(1024) void seg_offsets_kernel(const uint32_t* seg_c
 }
 
 __global__ __launch_bounds__(256) void seg_scatter_kernel(const uint32_t* seg_count,
+                                                          const uint32_t* seg_split,
                                                           const uint32_t* seg_out,
                                                           const uint64_t* seg_base,
                                                           const uint64_t* seg_offset, uint32_t cap,
@@ -580,7 +643,11 @@ __global__ __launch_bounds__(256) void seg_scatter_kernel(const uint32_t* seg_co
   const uint64_t base = byte_begin + (uint64_t)seg * seg_bytes + 1;  // position = byte + 1
   const uint32_t* src = seg_out + (seg_base ? seg_base[seg] : (size_t)seg * cap);
   uint64_t* dst = positions + seg_offset[seg];
-  for (uint32_t i = threadIdx.x; i < c; i += blockDim.x) dst[i] = base + src[i];
+  // the segment wrote its rotated first part (split entries) before the
+  // second: the second part's entries come first in position order
+  const uint32_t split = min(seg_split[seg], c), nb = c - split;
+  for (uint32_t i = threadIdx.x; i < c; i += blockDim.x)
+    dst[i] = base + src[i < nb ? split + i : i - nb];
 }
 
 // ---------------------------------------------------------------------------
@@ -639,6 +706,8 @@ hipError_t launch_scan(const ScanParams& p, int grid, hipStream_t s, int mode) {
     case 9: hipLaunchKernelGGL(scan_segments_kernel<9>, dim3(grid), dim3(kWGThreads), lds, s, p); break;
     case 10: hipLaunchKernelGGL(scan_segments_kernel<10>, dim3(grid), dim3(kWGThreads), lds, s, p); break;
     case 11: hipLaunchKernelGGL(scan_segments_kernel<11>, dim3(grid), dim3(kWGThreads), lds, s, p); break;
+    case 12: hipLaunchKernelGGL(scan_segments_kernel<12>, dim3(grid), dim3(kWGThreads), lds, s, p); break;
+    case 13: hipLaunchKernelGGL(scan_segments_kernel<13>, dim3(grid), dim3(kWGThreads), lds, s, p); break;
     default: hipLaunchKernelGGL(scan_segments_kernel<0>, dim3(grid), dim3(kWGThreads), lds, s, p); break;
   }
   return hipGetLastError();
@@ -651,7 +720,7 @@ hipError_t launch_compact(const ScanParams& p, uint64_t* seg_offset, uint64_t* s
                        p.seg_cap, seg_offset, summary);
   } else {
     hipLaunchKernelGGL(seg_scatter_kernel, dim3(p.n_segments), dim3(256), 0, s, p.seg_count,
-                       p.seg_out, p.seg_base, seg_offset, p.seg_cap, p.byte_begin, p.seg_bytes,
+                       p.seg_split, p.seg_out, p.seg_base, seg_offset, p.seg_cap, p.byte_begin, p.seg_bytes,
                        positions);
   }
   return hipGetLastError();
@@ -672,7 +741,8 @@ hipError_t configure_scan_kernel() {
                         (const void*)scan_segments_kernel<4>, (const void*)scan_segments_kernel<5>,
                         (const void*)scan_segments_kernel<6>, (const void*)scan_segments_kernel<7>,
                         (const void*)scan_segments_kernel<8>, (const void*)scan_segments_kernel<9>,
-                        (const void*)scan_segments_kernel<10>, (const void*)scan_segments_kernel<11>}) {
+                        (const void*)scan_segments_kernel<10>, (const void*)scan_segments_kernel<11>,
+                        (const void*)scan_segments_kernel<12>, (const void*)scan_segments_kernel<13>}) {
     hipError_t r = hipFuncSetAttribute(k, hipFuncAttributeMaxDynamicSharedMemorySize, lds);
     if (r != hipSuccess) e = r;
   }
