@@ -15,6 +15,13 @@
 # upstream, so no bison/flex/autotools are needed.
 
 REF ?= /root/reference
+
+# The checked-in parsers must never be regenerated (no yacc/lex here, and a
+# fresh checkout may give grammar.y a later mtime than grammar.c).
+MAKEFLAGS += -r
+.SUFFIXES:
+%.c: %.y
+%.c: %.l
 OUT := oracle/_ref
 OBJ := $(OUT)/obj
 
