@@ -17,7 +17,7 @@ NAMES = {0: "product", 1: "no-exact-check", 2: "stage1-only", 3: "stream-only",
          4: "stage1-conflict-free-lds", 5: "stage1-valu-no-lds",
          6: "stage1-lds-no-test", 7: "stage1+appends-no-drain", 8: "product-global-ring",
          9: "drain-one-l2-load", 10: "drain-exact-valu-no-loads", 11: "product-reads-first",
-         12: "first-level-only", 13: "product-no-rotation"}
+         12: "first-level-only"}
 
 
 def main():
@@ -56,7 +56,7 @@ def main():
     out = {}
     for m in modes:
         med = statistics.median(res[m])
-        out[NAMES[m]] = {"median_ms": round(med, 4), "min_ms": round(min(res[m]), 4),
+        out[NAMES.get(m, "mode%d" % m)] = {"median_ms": round(med, 4), "min_ms": round(min(res[m]), 4),
                          "GB/s": round(n / (med * 1e-3) / 1e9, 1), "candidates": counts[m]}
     print(json.dumps({"rules": a.rules, "bytes": n, "modes": out}, indent=1))
 

@@ -19,10 +19,6 @@ namespace yamd {
 constexpr int kWave = 64;
 constexpr int kBytesPerLane = 16;
 constexpr int kTile = kWave * kBytesPerLane;        // 1024 B
-#ifndef YAMD_PREFETCH
-#define YAMD_PREFETCH 1
-#endif
-constexpr int kPrefetch = YAMD_PREFETCH;             // input tiles in flight per wave
 constexpr uint32_t kSegment = 1u << 20;   // max segment: 1 MiB (ring entries hold offset/16 in 16 bits)
 constexpr int kWavesPerWG = 16;
 constexpr int kWGThreads = kWave * kWavesPerWG;     // 1024

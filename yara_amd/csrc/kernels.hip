@@ -96,10 +96,12 @@ __device__ __forceinline__ bool exact_check(uint32_t w4, uint64_t pos, const Sca
 // First level (internal.h fl_word): false proves that no key ends at the
 // position; true sends it to exact_check.  Rule sets with 1- or 2-byte keys
 // skip this level (every hit goes to exact_check).
+__device__ __forceinline__ bool first_level_test(uint32_t d, uint32_t w4) {
+  return ((d >> fl_bit3(w4)) | (d >> fl_bit4(w4))) & 1u;
+}
 __device__ __forceinline__ bool first_level(uint32_t w4, const ScanParams& p) {
   if (p.len_mask & 6u) return true;
-  const uint32_t d = p.exact[kExactFl + fl_word(w4)];
-  return ((d >> fl_bit3(w4)) | (d >> fl_bit4(w4))) & 1u;
+  return first_level_test(p.exact[kExactFl + fl_word(w4)], w4);
 }
 
 // The 4 bytes ending at lane byte j (0..15) of a ring entry whose dwords 0..4
@@ -126,25 +128,50 @@ __device__ __forceinline__ uint32_t pair_bits(uint32_t x) {
 // Lane byte (0..15) of bit b of a tile hit mask: bit 8n + r <=> byte 4n + r.
 __device__ __forceinline__ uint32_t mask_position(uint32_t b) { return ((b >> 3) << 2) | (b & 3u); }
 
+// The 4 bytes around pair j (lane bytes 2j, 2j+1) of a window context S
+// (S[0] = the 4 bytes before the lane, S[1..4] its 16 bytes): lane bytes
+// 2j-2 .. 2j+1 = context bytes 2j+2 .. 2j+5 (an aligned dword or one alignbyte).
+__device__ __forceinline__ uint32_t pair_window(const uint32_t (&S)[6], uint32_t j) {
+  const uint32_t o = 2 * j + 2;
+  return (o & 3) == 0 ? S[o >> 2] : __builtin_amdgcn_alignbyte(S[(o >> 2) + 1], S[o >> 2], 2);
+}
+
 // Per-wave LDS ring of filter hits awaiting the exact check.  One entry (24
 // bytes) per (tile, lane) with at least one hit: the lane's window context (4
-// bytes before it + its 16 bytes) and (lane byte offset in segment / 16) |
-// (16-bit hit mask, bit j = lane byte j) << 16.  Entries are appended in lane
-// order, so ring order is ascending position order.  The exact check then
-// needs no global load of the input, only table probes.
+// bytes before it + its 16 bytes) and the lane byte offset in the segment / 16.
+// Entries are appended in lane order, so ring order is ascending position
+// order.  A drain takes the whole ring (one entry per lane), recomputes the
+// filter per position from the context, and needs no global load of the
+// input, only table probes.
 //
 // Drains run the first level of the exact check (internal.h fl_word: one
 // dword per hit) over 64 entries; the few hits that pass it go, in order, to
 // a per-wave pending list of (window, offset) pairs, and the bucket probes
 // run once that list holds a wave's worth -- one lane per hit, one round
 // trip per 64 hits instead of one per drain.
+//
+// The first-level loads of a drain are not waited for in the drain: the
+// drain leaves each lane's (at most two) hit windows and the dword indices
+// to probe in the queue, every tile step issues exactly two first-level
+// loads at one program point (index 0, a harmless word, when nothing is
+// deferred), and the next tile step consumes them after its stage 1 -- the
+// L2 round trip overlaps a tile of filtering.  Issuing the loads
+// unconditionally keeps the vmcnt bookkeeping identical on every path, so
+// waiting for the next input tile never waits for them (loads complete in
+// order; a conditional load would make the compiler's merged wait cover it).
 struct WaveQueue {
   uint32_t* ring;   // kQueueCap entries of kQueueEntryWords dwords
-  uint32_t head;    // wave-uniform counters (monotonic)
-  uint32_t tail;
+  uint32_t count;   // wave-uniform: entries in the ring (a drain takes all of them)
   uint32_t* pend;   // kWave pairs {w4, segment offset}
   uint32_t pend_n;  // wave-uniform
+  bool defer;       // wave-uniform: wa/wb/oa/ob await their first-level words
+  uint32_t wa, wb;  // per lane: windows of the lane's first and second hit
+  uint32_t oa, ob;  // their segment offsets, kNoHit = none
+  uint32_t ia, ib;  // byte offsets into exact[] the next tile step loads (0 = none)
+  uint32_t da, db;  // the loaded words
 };
+constexpr uint32_t kNoHit = 0xFFFFFFFFu;
+static_assert(kQueueCap == kWave, "a drain takes the whole ring, one entry per lane");
 
 // Bucket-probe every pending hit (one lane each) and append the survivors,
 // in order, to the segment's output.
@@ -187,44 +214,103 @@ __device__ __forceinline__ void append_hits(const ScanParams& p, uint32_t keep, 
 template <int MODE, bool kAny>
 __device__ __forceinline__ uint32_t stage1(const uint32_t (&S)[6], uint32_t lane);
 
+// Kernel variants whose drains defer their first-level loads (WaveQueue).
+template <int MODE>
+constexpr bool kDeferFl = MODE == 0 || MODE == 12;
+
+// Consume a deferred drain's first-level words: the lanes' hits that pass go,
+// in order, to the pending list (or, if they are more than a wave's worth,
+// are bucket-probed in place).
+template <int MODE>
+__device__ __forceinline__ void drain_complete(const ScanParams& p, WaveQueue& q, uint32_t lane,
+                                               uint64_t seg_start, uint32_t* out, uint32_t& found) {
+  const bool ha = q.oa != kNoHit && first_level_test(q.da, q.wa);
+  const bool hb = q.ob != kNoHit && first_level_test(q.db, q.wb);
+  q.defer = false;
+  q.ia = q.ib = 0u;
+  const uint32_t c = (uint32_t)ha + (uint32_t)hb;
+  const uint32_t incl = wave_inclusive_scan(c);
+  const uint32_t total = __builtin_amdgcn_readlane(incl, kWave - 1);
+  if (total == 0) return;
+  if (q.pend_n + total > kWave) flush_pending<MODE>(p, q, lane, seg_start, out, found);
+  if (total <= kWave) {
+    uint32_t idx = q.pend_n + incl - c;
+    if (ha) *reinterpret_cast<uint2*>(q.pend + 2 * idx++) = make_uint2(q.wa, q.oa);
+    if (hb) *reinterpret_cast<uint2*>(q.pend + 2 * idx) = make_uint2(q.wb, q.ob);
+    q.pend_n += total;
+    return;
+  }
+  const bool ka = ha && (MODE == 12 || exact_check(q.wa, seg_start + q.oa + 1, p));
+  const bool kb = hb && (MODE == 12 || exact_check(q.wb, seg_start + q.ob + 1, p));
+  const uint32_t kc = (uint32_t)ka + (uint32_t)kb;
+  const uint32_t kincl = wave_inclusive_scan(kc);
+  uint32_t idx = found + kincl - kc;
+  if (ka) {
+    if (idx < p.seg_cap) out[idx] = q.oa;
+    ++idx;
+  }
+  if (kb && idx < p.seg_cap) out[idx] = q.ob;
+  found += __builtin_amdgcn_readlane(kincl, kWave - 1);
+}
+
 // First-level check of the hits of up to 64 ring entries; survivors go to
 // the pending list (or, if a drain alone yields more than 64 of them, are
-// bucket-probed in place).
-template <int MODE>
+// bucket-probed in place).  kAsync (drains inside a tile step): when no lane
+// has more than two hits, only compute the first-level indices and leave the
+// loads to the tile step (WaveQueue).
+template <int MODE, bool kAsync = false>
 __device__ __forceinline__ void drain(const ScanParams& p, WaveQueue& q, uint32_t lane,
                                       uint64_t seg_start, uint32_t seg_len, uint32_t* out,
                                       uint32_t& found) {
-  const uint32_t n = min(q.tail - q.head, (uint32_t)kWave);
-  if constexpr (MODE == 7) {   // ablation: ring appends only, entries dropped
-    q.head += n;
-    return;
-  }
+  if constexpr (kDeferFl<MODE>)
+    if (q.defer) drain_complete<MODE>(p, q, lane, seg_start, out, found);
+  const uint32_t n = q.count;   // <= kQueueCap = kWave
+  q.count = 0;
+  if constexpr (MODE == 7) return;   // ablation: ring appends only, entries dropped
   if constexpr (MODE == 8)
     __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "workgroup");   // ring in global memory
   else
     __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
-  uint32_t maybe = 0, off0 = 0;
-  const uint32_t* ent = q.ring + ((q.head + lane) % kQueueCap) * kQueueEntryWords;
+  uint32_t maybe = 0, off0 = 0, m = 0;   // m: bit j = lane byte j passes the filter
+  const uint32_t* ent = q.ring + lane * kQueueEntryWords;
   if (lane < n) {
-    // the hit quarters' positions again, now with a per-position result
-    const uint32_t packed = ent[5];
-    off0 = (packed & 0xFFFFu) * kBytesPerLane;
-    uint32_t quarters = packed >> 16;
-    uint32_t m = 0;   // bit j = lane byte j
-    while (quarters) {
-      const uint32_t qq = (uint32_t)__builtin_ctz(quarters);
-      quarters &= quarters - 1;
+    // the entry's 16 positions again, now with a per-position result: the
+    // same pair tests as stage 1 over the entry's window context
+    const uint2 e01 = *reinterpret_cast<const uint2*>(ent);
+    const uint2 e23 = *reinterpret_cast<const uint2*>(ent + 2);
+    const uint2 e45 = *reinterpret_cast<const uint2*>(ent + 4);
+    const uint32_t S[6] = {e01.x, e01.y, e23.x, e23.y, e45.x, 0u};
+    off0 = (e45.y & 0xFFFFu) * kBytesPerLane;
 #pragma unroll
-      for (uint32_t h = 0; h < 2; ++h) {
-        const uint32_t j = 2 * qq + h;             // pair: lane bytes 2j, 2j+1
-        const uint32_t x = window4(ent, 2 * j + 1);  // bytes 2j-2 .. 2j+1
-        m |= pair_bits(x) << (2 * j);
-      }
-    }
+    for (uint32_t j = 0; j < kBytesPerLane / 2; ++j) m |= pair_bits(pair_window(S, j)) << (2 * j);
     if (off0 + kBytesPerLane > seg_len) {   // the segment's partial last tile
       const uint32_t lim = off0 >= seg_len ? 0u : seg_len - off0;
       m &= lim >= 16u ? 0xFFFFu : (1u << lim) - 1u;
     }
+  }
+  if constexpr (kDeferFl<MODE> && kAsync) {
+    const uint32_t m2 = m & (m - 1u);
+    if ((p.len_mask & 6u) == 0u && __ballot((m2 & (m2 - 1u)) != 0u) == 0) {
+      q.oa = q.ob = kNoHit;
+      q.wa = q.wb = 0u;
+      q.ia = q.ib = 0u;
+      if (m != 0u) {
+        const uint32_t j = (uint32_t)__builtin_ctz(m);
+        q.wa = window4(ent, j);
+        q.oa = off0 + j;
+        q.ia = (kExactFl + fl_word(q.wa)) * 4u;
+      }
+      if (m2 != 0u) {
+        const uint32_t j = (uint32_t)__builtin_ctz(m2);
+        q.wb = window4(ent, j);
+        q.ob = off0 + j;
+        q.ib = (kExactFl + fl_word(q.wb)) * 4u;
+      }
+      q.defer = true;
+      return;
+    }
+  }
+  {
     while (m) {
       const uint32_t j = (uint32_t)__builtin_ctz(m);
       m &= m - 1;
@@ -241,7 +327,6 @@ __device__ __forceinline__ void drain(const ScanParams& p, WaveQueue& q, uint32_
       maybe |= (uint32_t)hit << j;
     }
   }
-  q.head += n;
   const uint32_t c = __popc(maybe);
   const uint32_t incl = wave_inclusive_scan(c);
   if constexpr (MODE == 1 || MODE == 9 || MODE == 10) {   // ablations: output as is
@@ -318,8 +403,7 @@ struct SegState {
 
 // Stage 1 of one 1 KiB tile: the filter over its 1024 byte positions.  Returns
 // the lane's hit mask (bit 8n + r <=> lane byte 4n + r), or with kAny only
-// which quarters of the lane (bit q: bytes 4q .. 4q+3) have a position that
-// passes.
+// whether some position of the lane passes (bit 0).
 template <int MODE, bool kAny>
 __device__ __forceinline__ uint32_t stage1(const uint32_t (&S)[6], uint32_t lane) {
   // Phase A: the lane's 8 position pairs and their 8 filter-block reads.
@@ -330,8 +414,7 @@ __device__ __forceinline__ uint32_t stage1(const uint32_t (&S)[6], uint32_t lane
   uint2 ws[kPairs];
 #pragma unroll
   for (int j = 0; j < kPairs; ++j) {
-    const int o = 2 * j + 2;
-    xs[j] = (o & 3) == 0 ? S[o >> 2] : __builtin_amdgcn_alignbyte(S[(o >> 2) + 1], S[o >> 2], 2);
+    xs[j] = pair_window(S, j);
     if constexpr (MODE != 3) {
       const uint32_t x = xs[j];
       uint32_t addr = (x >> 7) & (kFilterBytes - 8);   // block x[10..23], 8 B each
@@ -359,33 +442,28 @@ __device__ __forceinline__ uint32_t stage1(const uint32_t (&S)[6], uint32_t lane
     // the main loop only needs "does any position of this lane pass?": OR the
     // shifted-word ANDs together (v_bitop3: full rate, unlike SDWA) and keep
     // bit 0; the drain recomputes the per-position results of the few lanes
-    // that do
-    // one accumulator per quarter of the lane (pairs 2q, 2q+1 = bytes 4q..4q+3)
-    uint32_t a[4];
+    // that do.  Two accumulators (pairs 0-3, 4-7) for some ILP.
+    uint32_t a[2];
 #pragma unroll
     for (int j = 0; j < kPairs; ++j) {
       const uint32_t x = xs[j];
       const uint32_t ul = ws[j].x >> (x & 31u), vl = ws[j].y >> ((x >> 5) & 31u);
       const uint32_t y = __builtin_amdgcn_perm(0u, x, 0x0c0c0103u);   // d | b << 8
       const uint32_t ur = ws[j].x >> (y & 31u), vr = ws[j].y >> ((y >> 5) & 31u);
-      uint32_t& aq = a[j >> 1];
-      if ((j & 1) == 0) aq = ul & vl;
-      else asm("v_bitop3_b32 %0, %1, %2, %0 bitop3:0xea" : "+v"(aq) : "v"(ul), "v"(vl));
+      uint32_t& aq = a[j >> 2];
+      if ((j & 3) == 0) aq = ul & vl;
       // acc |= u & v in one v_bitop3 (S0 = u, S1 = v, S2 = acc: 0xF0 & 0xCC | 0xAA)
+      else asm("v_bitop3_b32 %0, %1, %2, %0 bitop3:0xea" : "+v"(aq) : "v"(ul), "v"(vl));
       asm("v_bitop3_b32 %0, %1, %2, %0 bitop3:0xea" : "+v"(aq) : "v"(ur), "v"(vr));
     }
     if constexpr (MODE == 2 || MODE == 4 || MODE == 5) {   // ablations: no ring
-      asm volatile("" ::"v"(a[0] | a[1] | a[2] | a[3]));
+      asm volatile("" ::"v"(a[0] | a[1]));
       return 0u;
     }
-    // quarter-hit mask: bit q = bit 0 of a[q]; t = (t & m) | (b & ~m) is one
-    // v_bitop3 (S0 = t, S1 = b, S2 = m: 0xF0 & 0xAA | 0xCC & 0x55)
-    uint32_t t = a[0];
-    const uint32_t b1 = a[1] << 1, b2 = a[2] << 2, b3 = a[3] << 3;
-    asm("v_bitop3_b32 %0, %0, %1, 1 bitop3:0xe4" : "+v"(t) : "v"(b1));
-    asm("v_bitop3_b32 %0, %0, %1, 3 bitop3:0xe4" : "+v"(t) : "v"(b2));
-    asm("v_bitop3_b32 %0, %0, %1, 7 bitop3:0xe4" : "+v"(t) : "v"(b3));
-    return t & 15u;
+    // (a0 | a1) & 1 in one v_bitop3 (S0 = a0, S1 = a1, S2 = 1: (0xF0 | 0xCC) & 0xAA)
+    uint32_t t;
+    asm("v_bitop3_b32 %0, %1, %2, 1 bitop3:0xa8" : "=v"(t) : "v"(a[0]), "v"(a[1]));
+    return t;
   }
   uint32_t acc[4];   // byte 0 written first (zero-padding the rest), then bytes 1..3
   if constexpr (MODE == 3 || MODE == 6) acc[0] = acc[1] = acc[2] = acc[3] = 0u;
@@ -440,19 +518,18 @@ __device__ __forceinline__ void ring_append(const ScanParams& p, WaveQueue& q, S
   const uint64_t lanes = __ballot(any != 0);
   if (lanes != 0) {
     const uint32_t n = (uint32_t)__popcll(lanes);
-    if (q.tail - q.head + n > kQueueCap)
-      drain<MODE>(p, q, lane, st.seg_start, st.seg_len, st.out, st.found);
+    if (q.count + n > kQueueCap)
+      drain<MODE, true>(p, q, lane, st.seg_start, st.seg_len, st.out, st.found);
     if (any != 0) {
       const uint32_t below = __builtin_amdgcn_mbcnt_hi((uint32_t)(lanes >> 32),
                                                        __builtin_amdgcn_mbcnt_lo((uint32_t)lanes, 0u));
-      uint32_t* ent = q.ring + ((q.tail + below) % kQueueCap) * kQueueEntryWords;
+      uint32_t* ent = q.ring + (q.count + below) * kQueueEntryWords;
       // 24-byte entry: the window context, then the lane index in the segment
-      // and (bits 16..19) which quarters of the lane have a filter hit
       *reinterpret_cast<uint2*>(ent) = make_uint2(S[0], S[1]);
       *reinterpret_cast<uint2*>(ent + 2) = make_uint2(S[2], S[3]);
-      *reinterpret_cast<uint2*>(ent + 4) = make_uint2(S[4], (lane_off / kBytesPerLane) | (any << 16));
+      *reinterpret_cast<uint2*>(ent + 4) = make_uint2(S[4], lane_off / kBytesPerLane);
     }
-    q.tail += n;
+    q.count += n;
   }
 }
 
@@ -476,12 +553,27 @@ __device__ __forceinline__ void tile_step(const ScanParams& p, WaveQueue& q, Seg
   uint32_t S[6];
   tile_context(st, cur, S);
   const uint32_t any = stage1<MODE, true>(S, lane);
+  if constexpr (kDeferFl<MODE>)
+    if (q.defer) drain_complete<MODE>(p, q, lane, st.seg_start, st.out, st.found);
   ring_append<MODE, TAIL>(p, q, st, S, any, tile_off, lane);
+  if constexpr (kDeferFl<MODE>) {
+    // every tile step: the two first-level loads of a drain it deferred, or
+    // of word 0 (see WaveQueue)
+    // (relaxed wavefront-scope atomic loads: plain global_load_dword, but
+    // "ordered", so the compiler cannot sink them into the consumer's
+    // conditional block -- they must issue here)
+    const char* ex = reinterpret_cast<const char*>(p.exact);
+    q.da = __hip_atomic_load(reinterpret_cast<const uint32_t*>(ex + q.ia), __ATOMIC_RELAXED,
+                             __HIP_MEMORY_SCOPE_WAVEFRONT);
+    q.db = __hip_atomic_load(reinterpret_cast<const uint32_t*>(ex + q.ib), __ATOMIC_RELAXED,
+                             __HIP_MEMORY_SCOPE_WAVEFRONT);
+  }
 }
 
 // Stream one segment [seg_start, seg_start + seg_len) of the block: full tiles
-// in the main loop (unmasked, the next tile's loads in flight), then the
-// partial tail tile if any.
+// in the main loop (unmasked; the next tile's loads in flight, two tile
+// registers used alternately so no copy waits for a load), then the partial
+// tail tile if any.
 // MODE: 0 = the product kernel.  Others are profiling ablations only (their
 // output is wrong by construction): 1 = no exact check, 2 = stage 1 only
 // (no queue), 3 = input streaming only (no filter), 4 = stage 1 with
@@ -491,10 +583,14 @@ __device__ __forceinline__ void tile_step(const ScanParams& p, WaveQueue& q, Seg
 // global memory (L2) instead of LDS, 9 = exact check replaced by one L2 dword
 // load per hit, 10 = exact-check VALU with the bucket loads replaced by values,
 // 11 = product with all 8 filter reads of a tile issued before any test,
-// 12 = product without the bucket probes (first level only), 13 = product with
-// the segment's tiles in plain order (no rotation).
+// 12 = product without the bucket probes (first level only).
+//
+// (An earlier version rotated each segment's tile order so that the waves of
+// the chip would not read the same offsets of their equal segments at the
+// same time; it helped the filter alone but made the product kernel 2-4 %
+// slower -- the waves' drains de-synchronise them anyway.)
 template <int MODE>
-__device__ void scan_segment(const ScanParams& p, WaveQueue& q, uint32_t seg, uint32_t lane) {
+__device__ __forceinline__ void scan_segment(const ScanParams& p, WaveQueue& q, uint32_t seg, uint32_t lane) {
   SegState st;
   st.seg_start = p.byte_begin + (uint64_t)seg * p.seg_bytes;
   const uint64_t seg_end = min(st.seg_start + p.seg_bytes, p.byte_end);
@@ -505,62 +601,45 @@ __device__ void scan_segment(const ScanParams& p, WaveQueue& q, uint32_t seg, ui
   const uint8_t* base = p.data + st.seg_start;
 
   // 4 bytes before the segment (warm-up halo); zeros before the block start.
-  st.carry = st.seg_start >= 4 ? *reinterpret_cast<const uint32_t*>(base - 4) : 0u;
-  q.head = q.tail = 0;
+  // (readfirstlane: waited for here, so no load is pending on the carry's
+  // register when the tile loop starts -- see WaveQueue on vmcnt)
+  st.carry = __builtin_amdgcn_readfirstlane(
+      st.seg_start >= 4 ? *reinterpret_cast<const uint32_t*>(base - 4) : 0u);
+  q.count = 0;
   q.pend_n = 0;
+  q.defer = false;
+  q.ia = q.ib = 0u;
+  q.da = q.db = 0u;
+  q.wa = q.wb = 0u;
+  q.oa = q.ob = kNoHit;
 
   const uint32_t n_full = st.seg_len / kTile;            // tiles needing no mask / bounds
-  const uint32_t n_all = (st.seg_len + kTile - 1) / kTile;
-  // Rotated order: tiles r .. n_full-1, the partial tail tile, then tiles
-  // 0 .. r-1.  Segments are equal and (for a full-chip 4 GiB launch) exactly
-  // 1 MiB apart, so in plain order every wave of the chip would read the same
-  // offset of its segment at the same time and the reads would pile onto the
-  // same HBM channels (stage 1 alone: 0.93 ms in order, 0.73 ms rotated).
-  // The output of the first part (positions >= r tiles) is appended first;
-  // seg_split records its length and the scatter puts the second part first.
-  // The next full tile's loads are always in flight (the wrap prefetches tile
-  // 0; the last tile of a part re-reads itself rather than branch), and the
-  // ragged tail tile is loaded on its own, outside the loops.
-  const uint32_t r = (n_full > 1 && MODE != 13) ? (seg * 61u) % n_full : 0u;   // 13: ablation
-  const uint32_t halo = st.carry;
-  const uint32_t wrap = r > 0 ? n_full - r : n_full;   // the step that reaches tile 0
-  auto tile_at = [&](uint32_t i) { return r + i < n_full ? r + i : r + i - n_full; };
-  // kPrefetch full tiles in flight (the last step's prefetches re-read the
-  // last tile rather than branch)
-  uint4 c[kPrefetch];
-#pragma unroll
-  for (int d = 0; d < kPrefetch; ++d)
-    c[d] = n_full > 0 ? load_tile_full(base, tile_at(min((uint32_t)d, n_full - 1)) * kTile, lane)
-                      : make_uint4(0, 0, 0, 0);
-  if (r > 0) st.carry = *reinterpret_cast<const uint32_t*>(base + (size_t)r * kTile - 4);
-  uint32_t split = 0;
-  auto finish_part = [&]() {
-    // the tail tile ends the first part (it is the segment's last tile)
-    if (n_all > n_full)
-      tile_step<MODE, true>(p, q, st, load_tile(base, n_full * kTile, lane, avail), n_full * kTile,
-                            lane);
-    while (q.tail != q.head) drain<MODE>(p, q, lane, st.seg_start, st.seg_len, st.out, st.found);
-    if (q.pend_n != 0) flush_pending<MODE>(p, q, lane, st.seg_start, st.out, st.found);
-    split = st.found;
-  };
-  for (uint32_t i = 0; i < n_full; ++i) {
-    if (i == wrap) {   // r > 0: tile 0 is next
-      finish_part();
-      st.carry = halo;
+  if (n_full > 0) {
+    const uint32_t last = (n_full - 1) * kTile;
+    uint4 a = load_tile_full(base, 0, lane), b;
+    // waited for before the loop, so that no path into the loop arrives with
+    // a load pending on a (the loop's wait for its input tile would
+    // otherwise cover the deferred first-level loads too)
+    asm volatile("" : "+v"(a.x), "+v"(a.y), "+v"(a.z), "+v"(a.w));
+    uint32_t i = 0;
+    // the last step's prefetch re-reads the last tile rather than branch
+    for (; i + 2 <= n_full; i += 2) {
+      b = load_tile_full(base, (i + 1) * kTile, lane);
+      tile_step<MODE, false>(p, q, st, a, i * kTile, lane);
+      a = load_tile_full(base, min((i + 2) * kTile, last), lane);
+      tile_step<MODE, false>(p, q, st, b, (i + 1) * kTile, lane);
     }
-    const uint4 nxt = load_tile_full(base, tile_at(min(i + kPrefetch, n_full - 1)) * kTile, lane);
-    tile_step<MODE, false>(p, q, st, c[0], tile_at(i) * kTile, lane);
-#pragma unroll
-    for (int d = 0; d + 1 < kPrefetch; ++d) c[d] = c[d + 1];
-    c[kPrefetch - 1] = nxt;
+    if (i < n_full) tile_step<MODE, false>(p, q, st, a, i * kTile, lane);
   }
-  if (wrap == n_full) {
-    finish_part();
-  } else {
-    while (q.tail != q.head) drain<MODE>(p, q, lane, st.seg_start, st.seg_len, st.out, st.found);
-    if (q.pend_n != 0) flush_pending<MODE>(p, q, lane, st.seg_start, st.out, st.found);
-  }
-  if (lane == 0) p.seg_split[seg] = split;
+  if (st.seg_len % kTile != 0)   // the ragged tail tile
+    tile_step<MODE, true>(p, q, st, load_tile(base, n_full * kTile, lane, avail), n_full * kTile,
+                          lane);
+  // everything queued to the segment's output, in order
+  if (q.count != 0) drain<MODE>(p, q, lane, st.seg_start, st.seg_len, st.out, st.found);
+  if constexpr (kDeferFl<MODE>)
+    if (q.defer) drain_complete<MODE>(p, q, lane, st.seg_start, st.out, st.found);
+  if (q.pend_n != 0) flush_pending<MODE>(p, q, lane, st.seg_start, st.out, st.found);
+  if (lane == 0) p.seg_split[seg] = 0;
   if (lane == 0) p.seg_count[seg] = st.found;
 }
 
@@ -707,7 +786,6 @@ hipError_t launch_scan(const ScanParams& p, int grid, hipStream_t s, int mode) {
     case 10: hipLaunchKernelGGL(scan_segments_kernel<10>, dim3(grid), dim3(kWGThreads), lds, s, p); break;
     case 11: hipLaunchKernelGGL(scan_segments_kernel<11>, dim3(grid), dim3(kWGThreads), lds, s, p); break;
     case 12: hipLaunchKernelGGL(scan_segments_kernel<12>, dim3(grid), dim3(kWGThreads), lds, s, p); break;
-    case 13: hipLaunchKernelGGL(scan_segments_kernel<13>, dim3(grid), dim3(kWGThreads), lds, s, p); break;
     default: hipLaunchKernelGGL(scan_segments_kernel<0>, dim3(grid), dim3(kWGThreads), lds, s, p); break;
   }
   return hipGetLastError();
@@ -742,7 +820,7 @@ hipError_t configure_scan_kernel() {
                         (const void*)scan_segments_kernel<6>, (const void*)scan_segments_kernel<7>,
                         (const void*)scan_segments_kernel<8>, (const void*)scan_segments_kernel<9>,
                         (const void*)scan_segments_kernel<10>, (const void*)scan_segments_kernel<11>,
-                        (const void*)scan_segments_kernel<12>, (const void*)scan_segments_kernel<13>}) {
+                        (const void*)scan_segments_kernel<12>}) {
     hipError_t r = hipFuncSetAttribute(k, hipFuncAttributeMaxDynamicSharedMemorySize, lds);
     if (r != hipSuccess) e = r;
   }
