@@ -31,6 +31,21 @@ __device__ __forceinline__ uint32_t lane_id() {
   return __builtin_amdgcn_mbcnt_hi(~0u, __builtin_amdgcn_mbcnt_lo(~0u, 0u));
 }
 
+// LDS accesses by 32-bit byte address (the ring, pending list and filter are
+// at fixed offsets of the dynamic LDS block, which starts at address 0):
+// keeps the address arithmetic in 32-bit VALU ops.
+typedef uint32_t u32x2 __attribute__((ext_vector_type(2)));
+template <typename T>
+__device__ __forceinline__ T lds_load(uint32_t addr) {
+  return *reinterpret_cast<const __attribute__((address_space(3))) T*>((uintptr_t)addr);
+}
+__device__ __forceinline__ void lds_store2(uint32_t addr, uint32_t x, uint32_t y) {
+  u32x2 v;
+  v.x = x;
+  v.y = y;
+  *reinterpret_cast<__attribute__((address_space(3))) u32x2*>((uintptr_t)addr) = v;
+}
+
 // Inclusive prefix sum over the 64 lanes with DPP (no LDS traffic):
 // Hillis-Steele inside each 16-lane row, then row_bcast:15 / row_bcast:31.
 __device__ __forceinline__ uint32_t wave_inclusive_scan(uint32_t v) {
@@ -104,21 +119,20 @@ __device__ __forceinline__ bool first_level(uint32_t w4, const ScanParams& p) {
   return first_level_test(p.exact[kExactFl + fl_word(w4)], w4);
 }
 
-// The 4 bytes ending at lane byte j (0..15) of a ring entry whose dwords 0..4
-// are the lane's window context (the 4 bytes before the lane, then its 16):
-// entry bytes j+1 .. j+4, from two aligned LDS dwords.
-__device__ __forceinline__ uint32_t window4(const uint32_t* ent, uint32_t j) {
-  const uint32_t o = j + 1, i = o >> 2;
-  return __builtin_amdgcn_alignbyte(ent[i + 1], ent[i], o & 3u);
+// The 4 bytes ending at lane byte j (0..15) of a ring entry (bytes 0..15 =
+// the lane's 16 bytes, 16..19 = the 4 bytes before the lane), from two LDS
+// dwords: lane bytes j-3 .. j.
+__device__ __forceinline__ uint32_t window4(uint32_t ent, uint32_t j) {
+  const uint32_t o = j - 3, lo = j >= 3 ? ent + (o & ~3u) : ent + 16;
+  const uint32_t hi = j >= 3 ? lo + 4 : ent, sh = j >= 3 ? (o & 3u) : j + 1;
+  return __builtin_amdgcn_alignbyte(lds_load<uint32_t>(hi), lds_load<uint32_t>(lo), sh);
 }
 
 // The filter test of one pair (internal.h filter_probe_left / _right): x =
 // the 4 bytes a b c d around lane bytes c, d; returns bit 0 = the window
 // ending at c passes, bit 1 = the one ending at d does.
 __device__ __forceinline__ uint32_t pair_bits(uint32_t x) {
-  typedef uint32_t u32x2 __attribute__((ext_vector_type(2)));
-  const u32x2 w = *reinterpret_cast<const __attribute__((address_space(3))) u32x2*>(
-      (uintptr_t)((x >> 7) & (kFilterBytes - 8)));   // the filter sits at LDS offset 0
+  const u32x2 w = lds_load<u32x2>((x >> 7) & (kFilterBytes - 8));   // the filter sits at LDS 0
   const uint32_t y = __builtin_amdgcn_perm(0u, x, 0x0c0c0103u);   // d | b << 8
   const uint32_t l = (w.x >> (x & 31u)) & (w.y >> ((x >> 5) & 31u));
   const uint32_t r = (w.x >> (y & 31u)) & (w.y >> ((y >> 5) & 31u));
@@ -160,15 +174,16 @@ __device__ __forceinline__ uint32_t pair_window(const uint32_t (&S)[6], uint32_t
 // waiting for the next input tile never waits for them (loads complete in
 // order; a conditional load would make the compiler's merged wait cover it).
 struct WaveQueue {
-  uint32_t* ring;   // kQueueCap entries of kQueueEntryWords dwords
+  uint32_t ring;    // LDS address: kQueueCap entries of kQueueEntryWords dwords
   uint32_t count;   // wave-uniform: entries in the ring (a drain takes all of them)
-  uint32_t* pend;   // kWave pairs {w4, segment offset}
+  uint32_t pend;    // LDS address: kWave pairs {w4, segment offset}
   uint32_t pend_n;  // wave-uniform
-  bool defer;       // wave-uniform: wa/wb/oa/ob await their first-level words
-  uint32_t wa, wb;  // per lane: windows of the lane's first and second hit
-  uint32_t oa, ob;  // their segment offsets, kNoHit = none
-  uint32_t ia, ib;  // byte offsets into exact[] the next tile step loads (0 = none)
-  uint32_t da, db;  // the loaded words
+  bool defer;       // wave-uniform: the per-lane hits below await their words
+  // per lane, the first (a) and second (b) deferred hit: window, segment
+  // offset (kNoHit = none), byte offset into exact[] that the next tile step
+  // loads (0 = none), the loaded word
+  uint32_t wa, oa, ia, da;
+  uint32_t wb, ob, ib, db;
 };
 constexpr uint32_t kNoHit = 0xFFFFFFFFu;
 static_assert(kQueueCap == kWave, "a drain takes the whole ring, one entry per lane");
@@ -182,7 +197,7 @@ __device__ __forceinline__ void flush_pending(const ScanParams& p, WaveQueue& q,
   bool keep = false;
   uint32_t off = 0;
   if (lane < q.pend_n) {
-    const uint2 e = *reinterpret_cast<const uint2*>(q.pend + 2 * lane);
+    const u32x2 e = lds_load<u32x2>(q.pend + 8 * lane);
     off = e.y;
     keep = MODE == 12 ? true : exact_check(e.x, seg_start + off + 1, p);   // 12: ablation
   }
@@ -235,8 +250,8 @@ __device__ __forceinline__ void drain_complete(const ScanParams& p, WaveQueue& q
   if (q.pend_n + total > kWave) flush_pending<MODE>(p, q, lane, seg_start, out, found);
   if (total <= kWave) {
     uint32_t idx = q.pend_n + incl - c;
-    if (ha) *reinterpret_cast<uint2*>(q.pend + 2 * idx++) = make_uint2(q.wa, q.oa);
-    if (hb) *reinterpret_cast<uint2*>(q.pend + 2 * idx) = make_uint2(q.wb, q.ob);
+    if (ha) lds_store2(q.pend + 8 * idx++, q.wa, q.oa);
+    if (hb) lds_store2(q.pend + 8 * idx, q.wb, q.ob);
     q.pend_n += total;
     return;
   }
@@ -267,19 +282,16 @@ __device__ __forceinline__ void drain(const ScanParams& p, WaveQueue& q, uint32_
   const uint32_t n = q.count;   // <= kQueueCap = kWave
   q.count = 0;
   if constexpr (MODE == 7) return;   // ablation: ring appends only, entries dropped
-  if constexpr (MODE == 8)
-    __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "workgroup");   // ring in global memory
-  else
-    __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+  __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
   uint32_t maybe = 0, off0 = 0, m = 0;   // m: bit j = lane byte j passes the filter
-  const uint32_t* ent = q.ring + lane * kQueueEntryWords;
+  const uint32_t ent = q.ring + lane * (kQueueEntryWords * 4);
   if (lane < n) {
     // the entry's 16 positions again, now with a per-position result: the
     // same pair tests as stage 1 over the entry's window context
-    const uint2 e01 = *reinterpret_cast<const uint2*>(ent);
-    const uint2 e23 = *reinterpret_cast<const uint2*>(ent + 2);
-    const uint2 e45 = *reinterpret_cast<const uint2*>(ent + 4);
-    const uint32_t S[6] = {e01.x, e01.y, e23.x, e23.y, e45.x, 0u};
+    const u32x2 e01 = lds_load<u32x2>(ent);
+    const u32x2 e23 = lds_load<u32x2>(ent + 8);
+    const u32x2 e45 = lds_load<u32x2>(ent + 16);
+    const uint32_t S[6] = {e45.x, e01.x, e01.y, e23.x, e23.y, 0u};
     off0 = (e45.y & 0xFFFFu) * kBytesPerLane;
 #pragma unroll
     for (uint32_t j = 0; j < kBytesPerLane / 2; ++j) m |= pair_bits(pair_window(S, j)) << (2 * j);
@@ -341,7 +353,7 @@ __device__ __forceinline__ void drain(const ScanParams& p, WaveQueue& q, uint32_
     while (maybe) {
       const uint32_t j = (uint32_t)__builtin_ctz(maybe);
       maybe &= maybe - 1;
-      *reinterpret_cast<uint2*>(q.pend + 2 * idx) = make_uint2(window4(ent, j), off0 + j);
+      lds_store2(q.pend + 8 * idx, window4(ent, j), off0 + j);
       ++idx;
     }
     q.pend_n += total;
@@ -360,10 +372,17 @@ __device__ __forceinline__ void drain(const ScanParams& p, WaveQueue& q, uint32_
 
 // A tile entirely inside the block: one 16-byte non-temporal load per lane
 // (read-once stream; keeps the exact tables' L2 lines).
-__device__ __forceinline__ uint4 load_tile_full(const uint8_t* base, uint32_t tile_off, uint32_t lane) {
+// Buffer load: the resource (segment base) and the tile offset live in SGPRs,
+// the lane's 16-byte offset is a loop-invariant VGPR -- no per-tile address
+// VALU.  aux 2 = nt (gfx950 cache policy).
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t segment_rsrc(const uint8_t* base) {
+  return __builtin_amdgcn_make_buffer_rsrc(const_cast<uint8_t*>(base), (short)0, 0x7FFFFFFF,
+                                           0x00020000);
+}
+__device__ __forceinline__ uint4 load_tile_full(__amdgpu_buffer_rsrc_t rsrc, uint32_t tile_off,
+                                                uint32_t lane16) {
   typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
-  const u32x4 v = __builtin_nontemporal_load(
-      reinterpret_cast<const u32x4*>(base + tile_off + lane * kBytesPerLane));
+  const u32x4 v = __builtin_amdgcn_raw_buffer_load_b128(rsrc, lane16, tile_off, 2);
   return make_uint4(v.x, v.y, v.z, v.w);
 }
 
@@ -521,13 +540,15 @@ __device__ __forceinline__ void ring_append(const ScanParams& p, WaveQueue& q, S
     if (q.count + n > kQueueCap)
       drain<MODE, true>(p, q, lane, st.seg_start, st.seg_len, st.out, st.found);
     if (any != 0) {
-      const uint32_t below = __builtin_amdgcn_mbcnt_hi((uint32_t)(lanes >> 32),
-                                                       __builtin_amdgcn_mbcnt_lo((uint32_t)lanes, 0u));
-      uint32_t* ent = q.ring + (q.count + below) * kQueueEntryWords;
-      // 24-byte entry: the window context, then the lane index in the segment
-      *reinterpret_cast<uint2*>(ent) = make_uint2(S[0], S[1]);
-      *reinterpret_cast<uint2*>(ent + 2) = make_uint2(S[2], S[3]);
-      *reinterpret_cast<uint2*>(ent + 4) = make_uint2(S[4], lane_off / kBytesPerLane);
+      // slot = count + the appending lanes below this one
+      const uint32_t slot = __builtin_amdgcn_mbcnt_hi(
+          (uint32_t)(lanes >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)lanes, q.count));
+      const uint32_t ent = q.ring + __umul24(slot, kQueueEntryWords * 4);
+      // 24-byte entry: the lane's 16 bytes (as loaded: no register moves),
+      // the 4 bytes before them, the lane index in the segment
+      lds_store2(ent, S[1], S[2]);
+      lds_store2(ent + 8, S[3], S[4]);
+      lds_store2(ent + 16, S[0], (tile_off >> 4) + lane);
     }
     q.count += n;
   }
@@ -579,8 +600,7 @@ __device__ __forceinline__ void tile_step(const ScanParams& p, WaveQueue& q, Seg
 // (no queue), 3 = input streaming only (no filter), 4 = stage 1 with
 // bank-conflict-free LDS addresses, 5 = stage 1 VALU without the LDS reads,
 // 6 = stage 1 addresses + LDS reads without the bit tests, 7 = stage 1 +
-// ring appends, drains drop the entries, 8 = product with the hit rings in
-// global memory (L2) instead of LDS, 9 = exact check replaced by one L2 dword
+// ring appends, drains drop the entries, 8 = (unused), 9 = exact check replaced by one L2 dword
 // load per hit, 10 = exact-check VALU with the bucket loads replaced by values,
 // 11 = product with all 8 filter reads of a tile issued before any test,
 // 12 = product without the bucket probes (first level only).
@@ -616,7 +636,9 @@ __device__ __forceinline__ void scan_segment(const ScanParams& p, WaveQueue& q, 
   const uint32_t n_full = st.seg_len / kTile;            // tiles needing no mask / bounds
   if (n_full > 0) {
     const uint32_t last = (n_full - 1) * kTile;
-    uint4 a = load_tile_full(base, 0, lane), b;
+    const __amdgpu_buffer_rsrc_t rsrc = segment_rsrc(base);
+    const uint32_t lane16 = lane * kBytesPerLane;
+    uint4 a = load_tile_full(rsrc, 0, lane16), b;
     // waited for before the loop, so that no path into the loop arrives with
     // a load pending on a (the loop's wait for its input tile would
     // otherwise cover the deferred first-level loads too)
@@ -624,9 +646,9 @@ __device__ __forceinline__ void scan_segment(const ScanParams& p, WaveQueue& q, 
     uint32_t i = 0;
     // the last step's prefetch re-reads the last tile rather than branch
     for (; i + 2 <= n_full; i += 2) {
-      b = load_tile_full(base, (i + 1) * kTile, lane);
+      b = load_tile_full(rsrc, (i + 1) * kTile, lane16);
       tile_step<MODE, false>(p, q, st, a, i * kTile, lane);
-      a = load_tile_full(base, min((i + 2) * kTile, last), lane);
+      a = load_tile_full(rsrc, min((i + 2) * kTile, last), lane16);
       tile_step<MODE, false>(p, q, st, b, (i + 1) * kTile, lane);
     }
     if (i < n_full) tile_step<MODE, false>(p, q, st, a, i * kTile, lane);
@@ -657,14 +679,11 @@ __global__ __launch_bounds__(kWGThreads, 1) void scan_segments_kernel(ScanParams
   // wave index, provably wave-uniform: everything derived from it (segment
   // bounds, loop counts, ring base) stays in SGPRs with scalar branches
   const uint32_t wid = __builtin_amdgcn_readfirstlane(threadIdx.x / kWave);
-  WaveQueue q;
-  if constexpr (MODE == 8)
-    q.ring = p.gring + ((size_t)blockIdx.x * kWavesPerWG + wid) * kQueueCap * kQueueEntryWords;
-  else
-    q.ring = lds + kFilterWords + wid * kQueueCap * kQueueEntryWords;
-  q.pend = lds + kFilterWords + kWavesPerWG * kQueueCap * kQueueEntryWords + wid * 2 * kWave;
   const uint32_t total_waves = gridDim.x * kWavesPerWG;
   for (uint32_t seg = blockIdx.x * kWavesPerWG + wid; seg < p.n_segments; seg += total_waves) {
+    WaveQueue q;   // (per segment: its per-lane state then stays in registers)
+    q.ring = kFilterBytes + wid * (kQueueCap * kQueueEntryWords * 4);
+    q.pend = kFilterBytes + kQueueBytes + wid * (kWave * 8);
     scan_segment<MODE>(p, q, seg, lane);
   }
 }
@@ -781,7 +800,6 @@ hipError_t launch_scan(const ScanParams& p, int grid, hipStream_t s, int mode) {
     case 5: hipLaunchKernelGGL(scan_segments_kernel<5>, dim3(grid), dim3(kWGThreads), lds, s, p); break;
     case 6: hipLaunchKernelGGL(scan_segments_kernel<6>, dim3(grid), dim3(kWGThreads), lds, s, p); break;
     case 7: hipLaunchKernelGGL(scan_segments_kernel<7>, dim3(grid), dim3(kWGThreads), lds, s, p); break;
-    case 8: hipLaunchKernelGGL(scan_segments_kernel<8>, dim3(grid), dim3(kWGThreads), kFilterBytes, s, p); break;
     case 9: hipLaunchKernelGGL(scan_segments_kernel<9>, dim3(grid), dim3(kWGThreads), lds, s, p); break;
     case 10: hipLaunchKernelGGL(scan_segments_kernel<10>, dim3(grid), dim3(kWGThreads), lds, s, p); break;
     case 11: hipLaunchKernelGGL(scan_segments_kernel<11>, dim3(grid), dim3(kWGThreads), lds, s, p); break;

@@ -130,8 +130,6 @@ struct yr_amd_scanner {
   bool ev_valid = false;
 
   int diag_mode = 0;   // profiling ablation of the scan kernel (0 = product)
-  uint32_t* d_gring = nullptr;   // global-memory hit rings (diag mode 8)
-  size_t gring_cap = 0;
   uint64_t* d_seg_base = nullptr; // exact per-segment output offsets (overflow rerun)
   size_t seg_base_cap = 0;
   uint64_t rerun_total = 0;
@@ -329,7 +327,7 @@ int yr_amd_scanner_destroy(yr_amd_scanner* s) {
                   (void*)s->d_seg_offset,
                   (void*)s->d_seg_out, (void*)s->d_positions, (void*)s->d_summary,
                   (void*)s->d_vcount, (void*)s->d_voffset, (void*)s->d_vchunk, (void*)s->d_vrec,
-                  (void*)s->d_gring, (void*)s->d_seg_base})
+                  (void*)s->d_seg_base})
     if (p) (void)hipFree(p);
   if (s->h_summary) (void)hipHostFree(s->h_summary);
   if (s->ev_begin) (void)hipEventDestroy(s->ev_begin);
@@ -412,14 +410,7 @@ int yr_amd_scan_device(yr_amd_scanner* s, const uint8_t* d_data, uint64_t block_
   p.seg_count = s->d_seg_count;
   p.seg_split = s->d_seg_split;
   p.seg_out = s->d_seg_out;
-  p.gring = nullptr;
   p.seg_base = nullptr;
-  if (s->diag_mode == 8) {
-    r = grow(s->d_gring, s->gring_cap,
-             (size_t)t->num_cus * kWavesPerWG * kQueueCap * kQueueEntryWords);
-    if (r) return r;
-    p.gring = s->d_gring;
-  }
   s->last_grid = (int)std::min<uint64_t>((n_segments + kWavesPerWG - 1) / kWavesPerWG,
                                          (uint64_t)t->num_cus);
   return run_scan(s);
