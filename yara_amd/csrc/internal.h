@@ -92,11 +92,19 @@ constexpr uint32_t kExactZero4 = 1u;   // flag: the 4-byte key 0x00000000 exists
 // the same 3 bytes), a 4-byte key one of bits 16..31 (picked by all 4).  A
 // clear bit proves "no 3-/4-byte key ends here"; a set one sends the position
 // to the bucket tables.  w4 = the 4 bytes ending at the position.
-__host__ __device__ inline uint32_t fl_word(uint32_t w4) {
-  return ((w4 >> 8) * 0x9E3779B1u) >> (32 - YAMD_FL_LOG2);
+// The hashes are 24 x 24-bit products (low 32 bits), so the device uses the
+// full-rate v_mul_u32_u24 rather than the quarter-rate v_mul_lo_u32; the
+// 4-byte bit folds the window's first byte into the top byte of the other 3.
+__host__ __device__ inline uint32_t fl_mul24(uint32_t a, uint32_t b) {
+  return (a & 0xFFFFFFu) * (b & 0xFFFFFFu);
 }
-__host__ __device__ inline uint32_t fl_bit3(uint32_t w4) { return ((w4 >> 8) * 0x85EBCA77u) >> 28; }
-__host__ __device__ inline uint32_t fl_bit4(uint32_t w4) { return 16u + ((w4 * 0xC2B2AE35u) >> 28); }
+__host__ __device__ inline uint32_t fl_word(uint32_t w4) {
+  return fl_mul24(w4 >> 8, 0x9E3779u) >> (32 - YAMD_FL_LOG2);
+}
+__host__ __device__ inline uint32_t fl_bit3(uint32_t w4) { return fl_mul24(w4 >> 8, 0xEBCA77u) >> 28; }
+__host__ __device__ inline uint32_t fl_bit4(uint32_t w4) {
+  return 16u + (fl_mul24((w4 >> 8) ^ (w4 << 16), 0xB2AE35u) >> 28);
+}
 
 __host__ __device__ inline uint32_t bucket_hash1(uint32_t key) {
   uint32_t h = key * 0x9E3779B1u;

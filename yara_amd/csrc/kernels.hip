@@ -230,8 +230,11 @@ template <int MODE, bool kAny>
 __device__ __forceinline__ uint32_t stage1(const uint32_t (&S)[6], uint32_t lane);
 
 // Kernel variants whose drains defer their first-level loads (WaveQueue).
+#ifndef YAMD_DEFER_FL
+#define YAMD_DEFER_FL 1
+#endif
 template <int MODE>
-constexpr bool kDeferFl = MODE == 0 || MODE == 12;
+constexpr bool kDeferFl = YAMD_DEFER_FL && (MODE == 0 || MODE == 12);
 
 // Consume a deferred drain's first-level words: the lanes' hits that pass go,
 // in order, to the pending list (or, if they are more than a wave's worth,
@@ -540,10 +543,13 @@ __device__ __forceinline__ void ring_append(const ScanParams& p, WaveQueue& q, S
     if (q.count + n > kQueueCap)
       drain<MODE, true>(p, q, lane, st.seg_start, st.seg_len, st.out, st.found);
     if (any != 0) {
-      // slot = count + the appending lanes below this one
-      const uint32_t slot = __builtin_amdgcn_mbcnt_hi(
-          (uint32_t)(lanes >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)lanes, q.count));
-      const uint32_t ent = q.ring + __umul24(slot, kQueueEntryWords * 4);
+      // slot = count (scalar, folded into the base) + the appending lanes below
+      const uint32_t below = __builtin_amdgcn_mbcnt_hi(
+          (uint32_t)(lanes >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)lanes, 0u));
+      static_assert(kQueueEntryWords * 4 == 24, "entry size is the asm's inline constant");
+      const uint32_t base = q.ring + q.count * (kQueueEntryWords * 4);   // scalar
+      uint32_t ent;   // (asm: the compiler would re-associate into a 64-bit mad)
+      asm("v_mad_u32_u24 %0, %1, 24, %2" : "=v"(ent) : "v"(below), "s"(base));
       // 24-byte entry: the lane's 16 bytes (as loaded: no register moves),
       // the 4 bytes before them, the lane index in the segment
       lds_store2(ent, S[1], S[2]);
