@@ -128,17 +128,6 @@ __device__ __forceinline__ uint32_t window4(uint32_t ent, uint32_t j) {
   return __builtin_amdgcn_alignbyte(lds_load<uint32_t>(hi), lds_load<uint32_t>(lo), sh);
 }
 
-// The filter test of one pair (internal.h filter_probe_left / _right): x =
-// the 4 bytes a b c d around lane bytes c, d; returns bit 0 = the window
-// ending at c passes, bit 1 = the one ending at d does.
-__device__ __forceinline__ uint32_t pair_bits(uint32_t x) {
-  const u32x2 w = lds_load<u32x2>((x >> 7) & (kFilterBytes - 8));   // the filter sits at LDS 0
-  const uint32_t y = __builtin_amdgcn_perm(0u, x, 0x0c0c0103u);   // d | b << 8
-  const uint32_t l = (w.x >> (x & 31u)) & (w.y >> ((x >> 5) & 31u));
-  const uint32_t r = (w.x >> (y & 31u)) & (w.y >> ((y >> 5) & 31u));
-  return (l & 1u) | ((r & 1u) << 1);
-}
-
 // Lane byte (0..15) of bit b of a tile hit mask: bit 8n + r <=> byte 4n + r.
 __device__ __forceinline__ uint32_t mask_position(uint32_t b) { return ((b >> 3) << 2) | (b & 3u); }
 
@@ -229,6 +218,13 @@ __device__ __forceinline__ void append_hits(const ScanParams& p, uint32_t keep, 
 template <int MODE, bool kAny>
 __device__ __forceinline__ uint32_t stage1(const uint32_t (&S)[6], uint32_t lane);
 
+// stage1's per-position mask (bit 8n + r <=> lane byte 4n + r) -> bit j <=> byte j.
+__device__ __forceinline__ uint32_t dense_mask(uint32_t h) {
+  h &= 0x0F0F0F0Fu;
+  h = (h | (h >> 4)) & 0x00FF00FFu;
+  return (h | (h >> 8)) & 0xFFFFu;
+}
+
 // Kernel variants whose drains defer their first-level loads (WaveQueue).
 #ifndef YAMD_DEFER_FL
 #define YAMD_DEFER_FL 1
@@ -296,8 +292,7 @@ __device__ __forceinline__ void drain(const ScanParams& p, WaveQueue& q, uint32_
     const u32x2 e45 = lds_load<u32x2>(ent + 16);
     const uint32_t S[6] = {e45.x, e01.x, e01.y, e23.x, e23.y, 0u};
     off0 = (e45.y & 0xFFFFu) * kBytesPerLane;
-#pragma unroll
-    for (uint32_t j = 0; j < kBytesPerLane / 2; ++j) m |= pair_bits(pair_window(S, j)) << (2 * j);
+    m = dense_mask(stage1<0, false>(S, lane));
     if (off0 + kBytesPerLane > seg_len) {   // the segment's partial last tile
       const uint32_t lim = off0 >= seg_len ? 0u : seg_len - off0;
       m &= lim >= 16u ? 0xFFFFu : (1u << lim) - 1u;
