@@ -567,6 +567,21 @@ __device__ __forceinline__ void tile_context(SegState& st, const uint4& cur, uin
   S[5] = 0u;
 }
 
+// Every tile step: the two first-level loads of a drain it deferred, or of
+// word 0 (see WaveQueue).  (Relaxed wavefront-scope atomic loads: plain
+// global_load_dword, but "ordered", so the compiler cannot sink them into the
+// consumer's conditional block -- they must issue here.)
+template <int MODE>
+__device__ __forceinline__ void issue_first_level(const ScanParams& p, WaveQueue& q) {
+  if constexpr (kDeferFl<MODE>) {
+    const char* ex = reinterpret_cast<const char*>(p.exact);
+    q.da = __hip_atomic_load(reinterpret_cast<const uint32_t*>(ex + q.ia), __ATOMIC_RELAXED,
+                             __HIP_MEMORY_SCOPE_WAVEFRONT);
+    q.db = __hip_atomic_load(reinterpret_cast<const uint32_t*>(ex + q.ib), __ATOMIC_RELAXED,
+                             __HIP_MEMORY_SCOPE_WAVEFRONT);
+  }
+}
+
 // One 1 KiB tile: stage-1 filter over its 1024 byte positions, then the ordered
 // append of the hits to the wave ring.
 template <int MODE, bool TAIL>
@@ -578,18 +593,7 @@ __device__ __forceinline__ void tile_step(const ScanParams& p, WaveQueue& q, Seg
   if constexpr (kDeferFl<MODE>)
     if (q.defer) drain_complete<MODE>(p, q, lane, st.seg_start, st.out, st.found);
   ring_append<MODE, TAIL>(p, q, st, S, any, tile_off, lane);
-  if constexpr (kDeferFl<MODE>) {
-    // every tile step: the two first-level loads of a drain it deferred, or
-    // of word 0 (see WaveQueue)
-    // (relaxed wavefront-scope atomic loads: plain global_load_dword, but
-    // "ordered", so the compiler cannot sink them into the consumer's
-    // conditional block -- they must issue here)
-    const char* ex = reinterpret_cast<const char*>(p.exact);
-    q.da = __hip_atomic_load(reinterpret_cast<const uint32_t*>(ex + q.ia), __ATOMIC_RELAXED,
-                             __HIP_MEMORY_SCOPE_WAVEFRONT);
-    q.db = __hip_atomic_load(reinterpret_cast<const uint32_t*>(ex + q.ib), __ATOMIC_RELAXED,
-                             __HIP_MEMORY_SCOPE_WAVEFRONT);
-  }
+  issue_first_level<MODE>(p, q);
 }
 
 // Stream one segment [seg_start, seg_start + seg_len) of the block: full tiles
