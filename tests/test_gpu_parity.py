@@ -135,6 +135,32 @@ def test_atoms_ending_on_slice_boundaries(period):
     np.testing.assert_array_equal(pos, ref)
 
 
+@pytest.mark.parametrize("stride", [3, 4, 5, 8, 12, 16, 24, 40])
+def test_dense_hits_per_lane(stride):
+    """4-byte atoms of config C planted every `stride` bytes (period 16 = the
+    lane width): lanes with 1, 2 and >2 hits exercise the kernel's deferred
+    first-level path (<= 2 hits per lane, incl. more than a wave's worth of
+    survivors in one drain) and its synchronous fallback (> 2 hits in a lane).
+    Bursts alternate with random stretches so both regimes meet in one drain."""
+    import planted
+    import gen_rules
+    tab = ref_tables("C")
+    atoms = [b[:4] for b, _ in planted.string_instances(gen_rules.gen("C")) if len(b) >= 4][:997]
+    size = 4 << 20
+    data = oracle.xorshift(size, 41).copy()
+    k = 0
+    for burst in range(0, size, 96 << 10):          # 64 KiB dense, 32 KiB random
+        for off in range(burst, min(burst + (64 << 10), size) - 4, stride):
+            data[off:off + 4] = np.frombuffer(atoms[k % len(atoms)], np.uint8)
+            k += 1
+    sc = yara_amd.Scanner(dev_tables("C"))
+    pos, _ = sc.candidates(data)
+    ref = oracle.candidates(tab, data)
+    if stride >= 4:                                 # (stride 3: atoms overwrite each other)
+        assert len(ref) > k // 4                    # (not every string's first 4 bytes are a key)
+    np.testing.assert_array_equal(pos, ref)
+
+
 def test_periodic_data_deep_chains():
     """'aaaa...' keeps the automaton in depth-3/4 states (failure chains)."""
     tab = ref_tables("short")
