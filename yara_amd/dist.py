@@ -47,12 +47,16 @@ def gather_positions(local: torch.Tensor, group=None, dst: int = 0):
     if dist.get_backend(group) == "gloo":
         local = local.cpu()                  # gloo collectives run on host tensors
     n = torch.tensor([local.numel()], dtype=torch.int64, device=local.device)
-    counts = [torch.zeros_like(n) for _ in range(world)]
-    dist.all_gather(counts, n, group=group)
-    counts = [int(c.item()) for c in counts]
+    counts_t = torch.empty(world, dtype=torch.int64, device=local.device)
+    dist.all_gather_into_tensor(counts_t, n, group=group)
+    counts = counts_t.tolist()               # one host sync for all ranks' counts
     width = max(max(counts), 1)
-    padded = torch.full((width,), -1, dtype=torch.int64, device=local.device)
-    padded[:local.numel()] = local
+    if local.numel() == width:
+        padded = local.contiguous()
+    else:
+        padded = torch.empty((width,), dtype=torch.int64, device=local.device)
+        padded[:local.numel()] = local
+        padded[local.numel():] = -1
     bufs = [torch.empty_like(padded) for _ in range(world)] if rank == dst else None
     dist.gather(padded, bufs, dst=dst, group=group)
     if rank != dst:
