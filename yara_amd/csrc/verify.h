@@ -66,6 +66,10 @@ struct VerifyParams {
   const DevRe* re;            // per pool entry, or null (no regex decisions)
   const uint8_t* re_code;
   uint32_t* counts;           // [count] records per candidate (pass 0)
+  uint32_t* keep;             // [count] pass 0's decisions for pass 1: bit t = the t-th
+                              // entry of the candidate's list is kept (t < 31); bit 31 =
+                              // the list is longer, pass 1 decides again
+  uint32_t* states;           // [count] the candidate's AC state (pass 0)
   const uint64_t* offsets;    // [count] exclusive scan of counts (pass 1)
   VerifyRec* out;             // records (pass 1)
 };

@@ -359,31 +359,52 @@ __device__ bool call_matters(const VerifyParams& p, uint32_t k, uint64_t offset)
   return false;
 }
 
-// PASS 0: count the records of each candidate; PASS 1: write them.
+// PASS 0: decide every call of each candidate, count the records, keep the
+// decisions (keep mask + state); PASS 1: write the records -- from the keep
+// mask, without deciding again (most candidates have none: they return at
+// once), except for lists longer than 31 entries.
+constexpr uint32_t kKeepOverflow = 1u << 31;
 template <int PASS>
 __global__ __launch_bounds__(256) void verify_kernel(VerifyParams p) {
   const uint64_t c = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (c >= p.count) return;
+  uint32_t keep = 0, state = 0;
+  if (PASS) {
+    keep = p.keep[c];
+    if (keep == 0) return;
+    state = p.states[c];
+  }
   const uint64_t i = p.all ? p.all_first + c : p.positions[c];
-  uint32_t state = 0;
-  for (uint64_t j = i > 4 ? i - 4 : 0; j < i; ++j) state = dev_ac_step(p.T, state, p.data[j]);
-  uint32_t n = 0;
+  if (!PASS)
+    for (uint64_t j = i > 4 ? i - 4 : 0; j < i; ++j) state = dev_ac_step(p.T, state, p.data[j]);
+  const bool decide = !PASS || (keep & kKeepOverflow);
+  uint32_t n = 0, t = 0, mask = 0;
   uint64_t o = PASS ? p.offsets[c] : 0;
   // scanner.c:105-121: the list of state_i in pool order
-  for (uint32_t k = p.M[state]; k != 0; k = p.pool_next[k - 1]) {
+  for (uint32_t k = p.M[state]; k != 0; k = p.pool_next[k - 1], ++t) {
     const uint32_t bt = p.pool_backtrack[k - 1];
-    if (bt > i) continue;
-    if (!call_matters(p, k - 1, i - bt)) continue;
+    bool kept;
+    if (decide)
+      kept = bt <= i && call_matters(p, k - 1, i - bt);
+    else
+      kept = t < 31 && ((keep >> t) & 1u);
+    if (!kept) continue;
     if (PASS) {
       VerifyRec r;
       r.offset = i - bt;
       r.pool_index = k - 1;
       r.candidate = (uint32_t)c;
       p.out[o++] = r;
+    } else if (t < 31) {
+      mask |= 1u << t;
     }
     ++n;
   }
-  if (!PASS) p.counts[c] = n;
+  if (!PASS) {
+    p.counts[c] = n;
+    p.keep[c] = n == 0 ? 0u : (t > 31 ? kKeepOverflow : mask);
+    p.states[c] = state;
+  }
 }
 
 // Exclusive scan of n uint32 counts into uint64 offsets, three launches:
