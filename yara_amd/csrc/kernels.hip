@@ -15,14 +15,19 @@
 //             window ending at each byte (internal.h filter_probe_left/right).
 //             128 KiB, staged once per workgroup; one ds_read_b64 per two
 //             input bytes.  Superset of the keys (config C: 0.39% pass).
-//   stage 2 (filter hits):  hits are appended in position order to a per-wave
-//             LDS ring; full batches of 64 are checked exactly against the key
-//             sets (bitmaps / bucketed cuckoo tables in HBM/L2), and survivors
-//             are compacted with a wave ballot + mbcnt into the segment's output.
+//             The main loop only asks "does some position of the lane pass".
+//   stage 2 (filter hits):  lanes that pass append their 20 bytes of window
+//             context, in position order, to a per-wave LDS ring; a drain
+//             (one entry per lane) re-tests the 16 positions, sends each hit
+//             through a first-level word filter (L2, loads deferred to the
+//             next tile step) and the survivors through bucketed two-choice
+//             tables (L2); exact hits are compacted in order (ballot + mbcnt /
+//             DPP prefix sums) into the segment's output.
 //
-// Memory: the input is streamed once, 16 B per lane (1 KiB per wave per step),
-// tile t+1 in flight while tile t is filtered.  Roofline: HBM read bandwidth
-// (1 algorithmic byte per input byte).
+// Memory: the input is streamed once, 16 B per lane (1 KiB per wave per step,
+// buffer loads), tile t+1 in flight while tile t is filtered.  Roofline: HBM
+// read bandwidth (1 algorithmic byte per input byte); in practice the kernel
+// is VALU-issue bound.
 #include "internal.h"
 
 namespace yamd {
@@ -140,8 +145,8 @@ __device__ __forceinline__ uint32_t pair_window(const uint32_t (&S)[6], uint32_t
 }
 
 // Per-wave LDS ring of filter hits awaiting the exact check.  One entry (24
-// bytes) per (tile, lane) with at least one hit: the lane's window context (4
-// bytes before it + its 16 bytes) and the lane byte offset in the segment / 16.
+// bytes) per (tile, lane) with at least one hit: the lane's 16 bytes, the 4
+// bytes before them, and the lane byte offset in the segment / 16.
 // Entries are appended in lane order, so ring order is ascending position
 // order.  A drain takes the whole ring (one entry per lane), recomputes the
 // filter per position from the context, and needs no global load of the
