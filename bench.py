@@ -172,13 +172,22 @@ def main():
                                                    "%s.npz" % args.rules), device=dev.index,
                                       strings=True)
     stream = torch.cuda.Stream(device=dev)
-    scanner = yara_amd.Scanner(tables, stream=stream.cuda_stream)
+    # two scanners on ONE stream, used alternately: step k+1's scan is queued
+    # before the host waits for step k's result (yr_amd_scan_device_result
+    # waits on the scan's own event), so the GPU does not idle while the host
+    # turns a result around; the kernels still run one after another, so the
+    # per-kernel timing is unaffected
+    scanners = [yara_amd.Scanner(tables, stream=stream.cuda_stream) for _ in range(2)]
+    scanner = scanners[0]
     block = end - lo
 
-    def step(timed_kernel=False):
-        scanner.scan_device(buf.data_ptr(), block, halo, block)
-        ptr, cnt, _ = scanner.device_result()       # ascending positions in HBM
-        kms = scanner.kernel_ms() if timed_kernel else None
+    def launch(k):
+        scanners[k % 2].scan_device(buf.data_ptr(), block, halo, block)
+
+    def finish(k, timed_kernel=False):
+        sc = scanners[k % 2]
+        ptr, cnt, _ = sc.device_result()            # ascending positions in HBM
+        kms = sc.kernel_ms() if timed_kernel else None
         if world == 1:                              # lo == 0: already global
             return (ptr, cnt), kms
         pos = torch.empty(max(cnt, 1), dtype=torch.int64, device=dev)
@@ -187,22 +196,32 @@ def main():
         pos = ydist.gather_positions(pos)           # RCCL: counts + padded gather
         return pos, kms
 
-    for _ in range(args.warmup):
-        step()
-    scanner.set_timing(True)
+    def run(steps, timed_kernel=False):
+        out, kms = None, []
+        for k in range(steps):
+            launch(k)
+            if k > 0:
+                out, t = finish(k - 1, timed_kernel)
+                kms.append(t)
+        if steps > 0:
+            out, t = finish(steps - 1, timed_kernel)
+            kms.append(t)
+        return out, kms
+
+    run(args.warmup)
+    for sc in scanners:
+        sc.set_timing(True)
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize()
     t0 = time.perf_counter()
-    kernel_ms = []
-    for _ in range(args.steps):
-        pos, kms = step(True)
-        kernel_ms.append(kms)
+    pos, kernel_ms = run(args.steps, True)
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
     elapsed = time.perf_counter() - t0
-    scanner.set_timing(False)
+    for sc in scanners:
+        sc.set_timing(False)
     if world > 1:
         t = torch.tensor([elapsed], dtype=torch.float64,
                          device=dev if args.backend == "nccl" else "cpu")

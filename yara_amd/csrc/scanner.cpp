@@ -127,6 +127,9 @@ struct yr_amd_scanner {
   // optional kernel timing (HIP events on the scan stream)
   bool timing = false;
   hipEvent_t ev_begin = nullptr, ev_end = nullptr;
+  // recorded behind a scan's result copy: yr_amd_scan_device_result waits for
+  // this scan only, so scanners sharing a stream can have the next scan queued
+  hipEvent_t ev_done = nullptr;
   bool ev_valid = false;
 
   int diag_mode = 0;   // profiling ablation of the scan kernel (0 = product)
@@ -218,6 +221,7 @@ int run_scan(yr_amd_scanner* s) {
   HIP_TRY(launch_compact(p, s->d_seg_offset, s->d_summary, s->d_positions, true, s->stream));
   HIP_TRY(hipMemcpyAsync(s->h_summary, s->d_summary, 2 * sizeof(uint64_t), hipMemcpyDeviceToHost,
                          s->stream));
+  HIP_TRY(hipEventRecord(s->ev_done, s->stream));
   return YR_AMD_SUCCESS;
 }
 
@@ -314,7 +318,8 @@ int yr_amd_scanner_create(yr_amd_tables* tables, void* stream, yr_amd_scanner** 
   }
   if (hipHostMalloc((void**)&s->h_summary, 2 * sizeof(uint64_t), hipHostMallocDefault) !=
           hipSuccess ||
-      hipMalloc((void**)&s->d_summary, 2 * sizeof(uint64_t)) != hipSuccess) {
+      hipMalloc((void**)&s->d_summary, 2 * sizeof(uint64_t)) != hipSuccess ||
+      hipEventCreateWithFlags(&s->ev_done, hipEventDisableTiming) != hipSuccess) {
     yr_amd_scanner_destroy(s);
     return YR_AMD_INTERNAL_FATAL_ERROR;
   }
@@ -334,6 +339,7 @@ int yr_amd_scanner_destroy(yr_amd_scanner* s) {
   if (s->h_summary) (void)hipHostFree(s->h_summary);
   if (s->ev_begin) (void)hipEventDestroy(s->ev_begin);
   if (s->ev_end) (void)hipEventDestroy(s->ev_end);
+  if (s->ev_done) (void)hipEventDestroy(s->ev_done);
   if (s->own_stream && s->stream) (void)hipStreamDestroy(s->stream);
   delete s;
   return YR_AMD_SUCCESS;
@@ -428,7 +434,7 @@ int yr_amd_scan_device_result(yr_amd_scanner* s, const uint64_t** d_positions, u
     if (count) *count = 0;
     return YR_AMD_SUCCESS;
   }
-  HIP_TRY(hipStreamSynchronize(s->stream));
+  HIP_TRY(hipEventSynchronize(s->ev_done));
   uint64_t total = s->h_summary[0];
   const uint64_t maxc = s->h_summary[1];
   if (maxc > s->last.seg_cap) {
