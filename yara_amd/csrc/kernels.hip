@@ -705,10 +705,12 @@ __global__ __launch_bounds__(kWGThreads, 1) void scan_segments_kernel(ScanParams
 __global__ __launch_bounds__(1024) void seg_offsets_kernel(const uint32_t* seg_count, uint32_t n,
                                                            uint32_t cap, uint64_t* seg_offset,
                                                            uint64_t* summary) {
-  __shared__ uint64_t part[1024];
-  __shared__ uint32_t pmax[1024];
-  const uint32_t t = threadIdx.x;
-  const uint32_t per = (n + 1023) / 1024;
+  // each thread a contiguous run of segments; wave scans by shuffles, then
+  // one wave scans the 16 wave totals (two barriers in all)
+  __shared__ uint64_t wsum[kWGThreads / kWave];
+  __shared__ uint32_t wmax[kWGThreads / kWave];
+  const uint32_t t = threadIdx.x, lane = t % kWave, w = t / kWave;
+  const uint32_t per = (n + kWGThreads - 1) / kWGThreads;
   const uint32_t lo = min(t * per, n), hi = min(lo + per, n);
   uint64_t s = 0;
   uint32_t mx = 0;
@@ -717,25 +719,37 @@ __global__ __launch_bounds__(1024) void seg_offsets_kernel(const uint32_t* seg_c
     s += min(c, cap);
     mx = max(mx, c);
   }
-  part[t] = s;
-  pmax[t] = mx;
-  __syncthreads();
-  for (uint32_t d = 1; d < 1024; d <<= 1) {
-    uint64_t v = t >= d ? part[t - d] : 0;
-    uint32_t m = t >= d ? pmax[t - d] : 0;
-    __syncthreads();
-    part[t] += v;
-    pmax[t] = max(pmax[t], m);
-    __syncthreads();
+  uint64_t incl = s;
+  for (int d = 1; d < kWave; d <<= 1) {
+    const uint64_t v = __shfl_up(incl, d, kWave);
+    if (lane >= (uint32_t)d) incl += v;
   }
-  uint64_t run = part[t] - s;
+  for (int d = kWave / 2; d >= 1; d >>= 1) mx = max(mx, (uint32_t)__shfl_xor(mx, d, kWave));
+  if (lane == kWave - 1) wsum[w] = incl;
+  if (lane == 0) wmax[w] = mx;
+  __syncthreads();
+  if (w == 0) {
+    constexpr uint32_t kWaves = kWGThreads / kWave;
+    const uint64_t v = lane < kWaves ? wsum[lane] : 0;
+    uint32_t m = lane < kWaves ? wmax[lane] : 0;
+    uint64_t inc = v;
+    for (int d = 1; d < kWave; d <<= 1) {
+      const uint64_t u = __shfl_up(inc, d, kWave);
+      if (lane >= (uint32_t)d) inc += u;
+    }
+    for (int d = kWave / 2; d >= 1; d >>= 1) m = max(m, (uint32_t)__shfl_xor(m, d, kWave));
+    if (lane < kWaves) wsum[lane] = inc - v;   // exclusive
+    if (lane == kWaves - 1) {
+      // (host-mapped coherent memory: system-scope stores)
+      __hip_atomic_store(&summary[0], inc, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+      __hip_atomic_store(&summary[1], (uint64_t)m, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+    }
+  }
+  __syncthreads();
+  uint64_t run = wsum[w] + incl - s;
   for (uint32_t i = lo; i < hi; ++i) {
     seg_offset[i] = run;
     run += min(seg_count[i], cap);
-  }
-  if (t == 1023) {
-    summary[0] = part[1023];   // total entries written
-    summary[1] = pmax[1023];   // max per-segment count (overflow if > cap)
   }
 }
 

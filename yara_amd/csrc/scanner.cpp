@@ -111,7 +111,9 @@ struct yr_amd_scanner {
   size_t seg_out_cap = 0;               // entries
   uint64_t* d_positions = nullptr;
   size_t positions_cap = 0;             // entries
-  uint64_t* h_summary = nullptr;        // pinned: {total, max per segment}
+  uint64_t* h_summary = nullptr;        // pinned, coherent: {total, max per segment}
+  uint64_t* d_hsum = nullptr;           // h_summary mapped for the device: the offsets
+                                        // kernel writes it directly (no copy launch)
   uint64_t* d_summary = nullptr;
 
   std::vector<uint64_t> h_positions;
@@ -217,10 +219,8 @@ int run_scan(yr_amd_scanner* s) {
     HIP_TRY(hipEventRecord(s->ev_end, s->stream));
     s->ev_valid = true;
   }
-  HIP_TRY(launch_compact(p, s->d_seg_offset, s->d_summary, nullptr, false, s->stream));
-  HIP_TRY(launch_compact(p, s->d_seg_offset, s->d_summary, s->d_positions, true, s->stream));
-  HIP_TRY(hipMemcpyAsync(s->h_summary, s->d_summary, 2 * sizeof(uint64_t), hipMemcpyDeviceToHost,
-                         s->stream));
+  HIP_TRY(launch_compact(p, s->d_seg_offset, s->d_hsum, nullptr, false, s->stream));
+  HIP_TRY(launch_compact(p, s->d_seg_offset, s->d_hsum, s->d_positions, true, s->stream));
   HIP_TRY(hipEventRecord(s->ev_done, s->stream));
   return YR_AMD_SUCCESS;
 }
@@ -316,8 +316,9 @@ int yr_amd_scanner_create(yr_amd_tables* tables, void* stream, yr_amd_scanner** 
     }
     s->own_stream = true;
   }
-  if (hipHostMalloc((void**)&s->h_summary, 2 * sizeof(uint64_t), hipHostMallocDefault) !=
+  if (hipHostMalloc((void**)&s->h_summary, 2 * sizeof(uint64_t), hipHostMallocCoherent) !=
           hipSuccess ||
+      hipHostGetDevicePointer((void**)&s->d_hsum, s->h_summary, 0) != hipSuccess ||
       hipMalloc((void**)&s->d_summary, 2 * sizeof(uint64_t)) != hipSuccess ||
       hipEventCreateWithFlags(&s->ev_done, hipEventDisableTiming) != hipSuccess) {
     yr_amd_scanner_destroy(s);
@@ -443,9 +444,7 @@ int yr_amd_scan_device_result(yr_amd_scanner* s, const uint64_t** d_positions, u
     // workspace is exactly the candidate count however skewed the segments
     ScanParams exact = s->last;
     exact.seg_cap = 0xFFFFFFFFu;
-    HIP_TRY(launch_compact(exact, s->d_seg_offset, s->d_summary, nullptr, false, s->stream));
-    HIP_TRY(hipMemcpyAsync(s->h_summary, s->d_summary, 2 * sizeof(uint64_t),
-                           hipMemcpyDeviceToHost, s->stream));
+    HIP_TRY(launch_compact(exact, s->d_seg_offset, s->d_hsum, nullptr, false, s->stream));
     HIP_TRY(hipStreamSynchronize(s->stream));
     total = s->h_summary[0];
     int r = grow(s->d_seg_out, s->seg_out_cap, std::max<uint64_t>(total, 1));
