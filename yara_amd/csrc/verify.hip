@@ -284,12 +284,17 @@ __device__ int general_re_reachable(const uint8_t* __restrict__ code, uint32_t l
   return kPathUnknown;
 }
 
+#ifndef YAMD_VERIFY_DIAG
+#define YAMD_VERIFY_DIAG 0   // profiling builds only: 1 = decide nothing, 2 = no regex decisions
+#endif
+
 // _yr_scan_verify_re_match (scan.c:778-880) for FAST ascii hex strings: the
 // forward program from `offset` must reach MATCH (else forward_matches == -1:
 // return), a zero-length forward match needs a backward program, and with a
 // backward program its MATCHes are the only way to _yr_scan_match_callback.
 __device__ bool re_call_matters(const VerifyParams& p, uint32_t k, uint32_t flags,
                                 uint64_t offset) {
+  if (YAMD_VERIFY_DIAG == 2) return true;
   if (p.re == nullptr) return true;
   const DevRe r = p.re[k];
   if (r.fwd_len == 0) return true;
@@ -331,6 +336,7 @@ __device__ bool re_call_matters(const VerifyParams& p, uint32_t k, uint32_t flag
 // have an effect?  false only where the reference provably returns without
 // touching the context.
 __device__ bool call_matters(const VerifyParams& p, uint32_t k, uint64_t offset) {
+  if (YAMD_VERIFY_DIAG == 1) return false;
   // scan.c:1013: data_size - offset <= 0 (size_t) <=> offset == size
   if (offset >= p.size) return false;
   const DevString st = p.strings[p.pool_string[k]];
