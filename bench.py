@@ -48,6 +48,7 @@ def parse():
     ap.add_argument("--cpu-sample-mib", type=int, default=3072)
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--no-check", action="store_true")
+    ap.add_argument("--no-other", action="store_true", help="skip the B / E kernel timings")
     ap.add_argument("--backend", default="nccl", help="nccl (= RCCL) or gloo (rehearsal)")
     return ap.parse_args()
 
@@ -238,6 +239,31 @@ def main():
     # on-device pre-verification of the last step's candidates (SURVEY.md §8f
     # rows 1 and 4; not part of the timed step): how many of the reference's
     # verify calls can have an effect, and what it costs on the GPU
+    # the same input under the other rule sets of SURVEY.md §8d (kernel time only,
+    # not the bench value): B = 1,000 4-byte hex atoms, E = 2,000 nocase/masked
+    other = None
+    if rank == 0 and world == 1 and not args.no_other and args.rules == "C":
+        other = {}
+        for name in ("B", "E"):
+            t_o = yara_amd.Tables.from_npz(os.path.join(REPO, "tests", "golden", "tables",
+                                                        "%s.npz" % name), device=dev.index)
+            s_o = yara_amd.Scanner(t_o, stream=stream.cuda_stream)
+            for _ in range(20):
+                s_o.scan_device(buf.data_ptr(), block, halo, block)
+                s_o.device_result()
+            s_o.set_timing(True)
+            ks = []
+            for _ in range(20):
+                s_o.scan_device(buf.data_ptr(), block, halo, block)
+                _, c_o, _ = s_o.device_result()
+                ks.append(s_o.kernel_ms())
+            k_o = sum(ks) / len(ks)
+            other[name] = {"kernel_ms": round(k_o, 4),
+                           "GB/s": round(shard / (k_o * 1e-3) / 1e9, 1),
+                           "frac": round(shard / (k_o * 1e-3) / 1e9 / HBM_PEAK_GBS, 4),
+                           "candidates": int(c_o)}
+            del s_o, t_o
+
     preverify = None
     if rank == 0 and world == 1:
         scanner.scan_device(buf.data_ptr(), block, halo, block)
@@ -303,6 +329,7 @@ def main():
             "cpu_port_parallel": cpu_par,
             "preverify": preverify,
             "check": check,
+            "other_rule_sets": other,
         }
         print(json.dumps(line), flush=True)
     if world > 1:
