@@ -25,10 +25,12 @@ def _shard_candidates(tab, data, begin, end):
     return keep.astype(np.int64) + lo
 
 
-def _worker(rank, world, port, n, period, q):
+def _worker(rank, world, port, n, period, q, no_gather=False):
     os.environ["MASTER_ADDR"] = "127.0.0.1"
     os.environ["MASTER_PORT"] = str(port)
     dist.init_process_group("gloo", rank=rank, world_size=world)
+    if no_gather:                      # the all_gather fallback of gather_positions
+        ydist._GATHER_OK = False
     try:
         import planted
         import gen_rules
@@ -45,13 +47,14 @@ def _worker(rank, world, port, n, period, q):
         dist.destroy_process_group()
 
 
-@pytest.mark.parametrize("world", [2, 3])
-def test_sharded_scan_gathers_full_stream(world):
+@pytest.mark.parametrize("world,no_gather", [(2, False), (3, False), (2, True)])
+def test_sharded_scan_gathers_full_stream(world, no_gather):
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
-    port = 29400 + world
+    port = 29400 + world + (10 if no_gather else 0)
     n, period = (3 << 20) + 77, 1 << 16
-    ps = [ctx.Process(target=_worker, args=(r, world, port, n, period, q)) for r in range(world)]
+    ps = [ctx.Process(target=_worker, args=(r, world, port, n, period, q, no_gather))
+          for r in range(world)]
     for p in ps:
         p.start()
     ok = q.get(timeout=300)

@@ -57,8 +57,20 @@ def gather_positions(local: torch.Tensor, group=None, dst: int = 0):
         padded = torch.empty((width,), dtype=torch.int64, device=local.device)
         padded[:local.numel()] = local
         padded[local.numel():] = -1
-    bufs = [torch.empty_like(padded) for _ in range(world)] if rank == dst else None
-    dist.gather(padded, bufs, dst=dst, group=group)
+    global _GATHER_OK
+    if _GATHER_OK:
+        bufs = [torch.empty_like(padded) for _ in range(world)] if rank == dst else None
+        try:
+            dist.gather(padded, bufs, dst=dst, group=group)
+        except RuntimeError:   # a backend without gather: every rank takes the same branch
+            _GATHER_OK = False
+    if not _GATHER_OK:
+        flat = torch.empty(world * width, dtype=torch.int64, device=local.device)
+        dist.all_gather_into_tensor(flat, padded, group=group)
+        bufs = list(flat.view(world, width))
     if rank != dst:
         return None
     return torch.cat([b[:c] for b, c in zip(bufs, counts)])
+
+
+_GATHER_OK = True
