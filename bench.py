@@ -173,20 +173,22 @@ def main():
                                                    "%s.npz" % args.rules), device=dev.index,
                                       strings=True)
     stream = torch.cuda.Stream(device=dev)
-    # two scanners on ONE stream, used alternately: step k+1's scan is queued
-    # before the host waits for step k's result (yr_amd_scan_device_result
-    # waits on the scan's own event), so the GPU does not idle while the host
-    # turns a result around; the kernels still run one after another, so the
+    # DEPTH scanners on ONE stream, used in turn: the scans of steps k+1 ..
+    # k+DEPTH-1 are queued before the host collects step k's result
+    # (yr_amd_scan_device_result waits on the scan's own event), so the GPU does
+    # not idle while the host -- or, with N > 1, the RCCL gather -- turns a
+    # result around; the kernels still run one after another, so the
     # per-kernel timing is unaffected
-    scanners = [yara_amd.Scanner(tables, stream=stream.cuda_stream) for _ in range(2)]
+    depth = 3
+    scanners = [yara_amd.Scanner(tables, stream=stream.cuda_stream) for _ in range(depth)]
     scanner = scanners[0]
     block = end - lo
 
     def launch(k):
-        scanners[k % 2].scan_device(buf.data_ptr(), block, halo, block)
+        scanners[k % depth].scan_device(buf.data_ptr(), block, halo, block)
 
     def finish(k, timed_kernel=False):
-        sc = scanners[k % 2]
+        sc = scanners[k % depth]
         ptr, cnt, _ = sc.device_result()            # ascending positions in HBM
         kms = sc.kernel_ms() if timed_kernel else None
         if world == 1:                              # lo == 0: already global
@@ -201,11 +203,11 @@ def main():
         out, kms = None, []
         for k in range(steps):
             launch(k)
-            if k > 0:
-                out, t = finish(k - 1, timed_kernel)
+            if k >= depth - 1:
+                out, t = finish(k - depth + 1, timed_kernel)
                 kms.append(t)
-        if steps > 0:
-            out, t = finish(steps - 1, timed_kernel)
+        for k in range(max(0, steps - depth + 1), steps):
+            out, t = finish(k, timed_kernel)
             kms.append(t)
         return out, kms
 
