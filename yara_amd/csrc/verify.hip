@@ -93,9 +93,41 @@ __device__ bool cmp_xor(const uint8_t* d, uint64_t avail, const uint8_t* s, uint
 // requiring b < max_bytes_matched.  "Exists a path" semantics, i.e. a superset
 // of what the reference's de-duplicating list reaches; out of stack or step
 // budget -> true (keep the call).
+// The input bytes a fast program can touch first, staged in LDS: the search
+// reads them one at a time, each read depending on the previous one's outcome,
+// so reading them from HBM would cost one memory round trip per byte.  One
+// window per lane: 48 bytes from three aligned 16-byte loads (issued together),
+// covering the 32 bytes after (forward) or before (backward) the start; reads
+// outside it, or any read when the window would leave the block, go to memory.
+constexpr int kWinBytes = 48;
+struct ByteWindow {
+  const uint8_t* lo;   // block address of window byte 0 (null: no window)
+  uint32_t lds;        // LDS byte address of this lane's window
+};
+__device__ __forceinline__ ByteWindow stage_window(const VerifyParams& p, const uint8_t* start,
+                                                   bool backwards, uint32_t lds) {
+  const uint8_t* s = backwards ? start - 32 : start;
+  const uint8_t* lo = reinterpret_cast<const uint8_t*>((uintptr_t)s & ~(uintptr_t)15);
+  if (lds == 0xFFFFFFFFu || lo < p.data || lo + kWinBytes > p.data + p.size) return {nullptr, lds};
+  typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
+  const u32x4* g = reinterpret_cast<const u32x4*>(lo);
+  const u32x4 a = g[0], b = g[1], c = g[2];
+  typedef __attribute__((address_space(3))) u32x4 lds_u4;
+  reinterpret_cast<lds_u4*>((uintptr_t)lds)[0] = a;
+  reinterpret_cast<lds_u4*>((uintptr_t)lds)[1] = b;
+  reinterpret_cast<lds_u4*>((uintptr_t)lds)[2] = c;
+  return {lo, lds};
+}
+__device__ __forceinline__ uint8_t window_byte(const ByteWindow& w, const uint8_t* at) {
+  if (w.lo != nullptr && at >= w.lo && at < w.lo + kWinBytes)
+    return *reinterpret_cast<const __attribute__((address_space(3))) uint8_t*>(
+        (uintptr_t)(w.lds + (uint32_t)(at - w.lo)));
+  return *at;
+}
+
 __device__ bool fast_re_reachable(const uint8_t* __restrict__ code, uint32_t len,
                                   const uint8_t* __restrict__ input, uint64_t avail,
-                                  bool backwards) {
+                                  bool backwards, const ByteWindow& win) {
   constexpr int kMaxChoices = 8;
   struct Choice {
     uint32_t ip;
@@ -111,7 +143,7 @@ __device__ bool fast_re_reachable(const uint8_t* __restrict__ code, uint32_t len
     if (op == kReMatch) return true;
     bool ok = false;
     if (b < maxb) {
-      const uint8_t c = backwards ? input[-1 - (int64_t)b] : input[b];
+      const uint8_t c = window_byte(win, backwards ? input - 1 - b : input + b);
       switch (op) {
         case kReAny: ok = true; ip += 1; break;
         case kReLiteral: ok = c == code[ip + 1]; ip += 2; break;
@@ -293,7 +325,7 @@ __device__ int general_re_reachable(const uint8_t* __restrict__ code, uint32_t l
 // return), a zero-length forward match needs a backward program, and with a
 // backward program its MATCHes are the only way to _yr_scan_match_callback.
 __device__ bool re_call_matters(const VerifyParams& p, uint32_t k, uint32_t flags,
-                                uint64_t offset) {
+                                uint64_t offset, uint32_t lds) {
   if (YAMD_VERIFY_DIAG == 2) return true;
   if (p.re == nullptr) return true;
   const DevRe r = p.re[k];
@@ -304,9 +336,14 @@ __device__ bool re_call_matters(const VerifyParams& p, uint32_t k, uint32_t flag
   if (flags & kStrFastRegexp) {
     if (!(flags & kStrAscii) || (flags & (kStrWide | kStrBase64Any))) return true;
     if (r.fwd_len == 1)   // forward program = MATCH: forward_matches = 0
-      return r.bwd_len > 0 && fast_re_reachable(bwd, r.bwd_len, d, offset, true);
-    if (!fast_re_reachable(fwd, r.fwd_len, d, p.size - offset, false)) return false;
-    if (r.bwd_len > 0 && !fast_re_reachable(bwd, r.bwd_len, d, offset, true)) return false;
+      return r.bwd_len > 0 &&
+             fast_re_reachable(bwd, r.bwd_len, d, offset, true, stage_window(p, d, true, lds));
+    if (!fast_re_reachable(fwd, r.fwd_len, d, p.size - offset, false,
+                           stage_window(p, d, false, lds)))
+      return false;
+    if (r.bwd_len > 0 &&
+        !fast_re_reachable(bwd, r.bwd_len, d, offset, true, stage_window(p, d, true, lds)))
+      return false;
     return true;
   }
   // yr_re_exec strings: the ascii attempt runs for ASCII / base64 strings, the
@@ -335,7 +372,7 @@ __device__ bool re_call_matters(const VerifyParams& p, uint32_t k, uint32_t flag
 // Does yr_scan_verify_match(ctx, &pool[k], data, size, base, offset) possibly
 // have an effect?  false only where the reference provably returns without
 // touching the context.
-__device__ bool call_matters(const VerifyParams& p, uint32_t k, uint64_t offset) {
+__device__ bool call_matters(const VerifyParams& p, uint32_t k, uint64_t offset, uint32_t lds) {
   if (YAMD_VERIFY_DIAG == 1) return false;
   // scan.c:1013: data_size - offset <= 0 (size_t) <=> offset == size
   if (offset >= p.size) return false;
@@ -343,7 +380,7 @@ __device__ bool call_matters(const VerifyParams& p, uint32_t k, uint64_t offset)
   // scan.c:1023-1025
   if ((st.flags & kStrFixedOffset) && st.fixed_offset != (int64_t)(p.data_base + offset))
     return false;
-  if (!(st.flags & kStrLiteral)) return re_call_matters(p, k, st.flags, offset);
+  if (!(st.flags & kStrLiteral)) return re_call_matters(p, k, st.flags, offset, lds);
   if (st.flags & kStrUnmodelled) return true;            // conservative
   // _yr_scan_verify_literal_match, scan.c:907-972
   if (st.flags & kStrFitsInAtom) return p.pool_backtrack[k] != 0;
@@ -372,6 +409,9 @@ __device__ bool call_matters(const VerifyParams& p, uint32_t k, uint64_t offset)
 constexpr uint32_t kKeepOverflow = 1u << 31;
 template <int PASS>
 __global__ __launch_bounds__(256) void verify_kernel(VerifyParams p) {
+  __shared__ __attribute__((aligned(16))) uint8_t win[256 * kWinBytes];
+  // (the low 32 bits of a flat LDS address are the LDS offset)
+  const uint32_t lds = (uint32_t)(uintptr_t)(win + threadIdx.x * kWinBytes);
   const uint64_t c = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (c >= p.count) return;
   uint32_t keep = 0, state = 0;
@@ -391,7 +431,7 @@ __global__ __launch_bounds__(256) void verify_kernel(VerifyParams p) {
     const uint32_t bt = p.pool_backtrack[k - 1];
     bool kept;
     if (decide)
-      kept = bt <= i && call_matters(p, k - 1, i - bt);
+      kept = bt <= i && call_matters(p, k - 1, i - bt, lds);
     else
       kept = t < 31 && ((keep >> t) & 1u);
     if (!kept) continue;
