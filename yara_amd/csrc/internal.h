@@ -130,8 +130,6 @@ struct ScanParams {
   uint32_t seg_bytes;       // bytes per segment (multiple of kTile)
   uint32_t seg_cap;         // output capacity (entries) per segment
   uint32_t* seg_count;      // [n_segments] candidates found (may exceed cap)
-  uint32_t* seg_split;      // [n_segments] how many of them come from the segment's
-                            // rotated first part (kernels.hip scan_segment)
   uint32_t* seg_out;        // [n_segments * seg_cap] byte offset within segment
   const uint64_t* seg_base; // null: segment s writes at seg_out + s * seg_cap; else at
                             // seg_out + seg_base[s] (exact-size rerun after an overflow)

@@ -671,7 +671,6 @@ __device__ __forceinline__ void scan_segment(const ScanParams& p, WaveQueue& q, 
   if constexpr (kDeferFl<MODE>)
     if (q.defer) drain_complete<MODE>(p, q, lane, st.seg_start, st.out, st.found);
   if (q.pend_n != 0) flush_pending<MODE>(p, q, lane, st.seg_start, st.out, st.found);
-  if (lane == 0) p.seg_split[seg] = 0;
   if (lane == 0) p.seg_count[seg] = st.found;
 }
 
@@ -754,7 +753,6 @@ __global__ __launch_bounds__(1024) void seg_offsets_kernel(const uint32_t* seg_c
 }
 
 __global__ __launch_bounds__(256) void seg_scatter_kernel(const uint32_t* seg_count,
-                                                          const uint32_t* seg_split,
                                                           const uint32_t* seg_out,
                                                           const uint64_t* seg_base,
                                                           const uint64_t* seg_offset, uint32_t cap,
@@ -765,11 +763,7 @@ __global__ __launch_bounds__(256) void seg_scatter_kernel(const uint32_t* seg_co
   const uint64_t base = byte_begin + (uint64_t)seg * seg_bytes + 1;  // position = byte + 1
   const uint32_t* src = seg_out + (seg_base ? seg_base[seg] : (size_t)seg * cap);
   uint64_t* dst = positions + seg_offset[seg];
-  // the segment wrote its rotated first part (split entries) before the
-  // second: the second part's entries come first in position order
-  const uint32_t split = min(seg_split[seg], c), nb = c - split;
-  for (uint32_t i = threadIdx.x; i < c; i += blockDim.x)
-    dst[i] = base + src[i < nb ? split + i : i - nb];
+  for (uint32_t i = threadIdx.x; i < c; i += blockDim.x) dst[i] = base + src[i];
 }
 
 // ---------------------------------------------------------------------------
@@ -840,7 +834,7 @@ hipError_t launch_compact(const ScanParams& p, uint64_t* seg_offset, uint64_t* s
                        p.seg_cap, seg_offset, summary);
   } else {
     hipLaunchKernelGGL(seg_scatter_kernel, dim3(p.n_segments), dim3(256), 0, s, p.seg_count,
-                       p.seg_split, p.seg_out, p.seg_base, seg_offset, p.seg_cap, p.byte_begin, p.seg_bytes,
+                       p.seg_out, p.seg_base, seg_offset, p.seg_cap, p.byte_begin, p.seg_bytes,
                        positions);
   }
   return hipGetLastError();

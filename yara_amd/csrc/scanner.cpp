@@ -104,7 +104,6 @@ struct yr_amd_scanner {
   uint8_t* d_block = nullptr;           // staging for host blocks
   size_t d_block_cap = 0;
   uint32_t* d_seg_count = nullptr;
-  uint32_t* d_seg_split = nullptr;
   uint64_t* d_seg_offset = nullptr;
   uint32_t seg_alloc = 0;               // segments the count/offset arrays hold
   uint32_t* d_seg_out = nullptr;
@@ -181,15 +180,11 @@ int ensure_segments(yr_amd_scanner* s, uint32_t n_segments, uint32_t seg_cap) {
   if (n_segments > s->seg_alloc) {
     size_t c = 0;
     if (s->d_seg_count) (void)hipFree(s->d_seg_count);
-    if (s->d_seg_split) (void)hipFree(s->d_seg_split);
     if (s->d_seg_offset) (void)hipFree(s->d_seg_offset);
     s->d_seg_count = nullptr;
-    s->d_seg_split = nullptr;
     s->d_seg_offset = nullptr;
     s->seg_alloc = 0;
     if (grow(s->d_seg_count, c, n_segments)) return YR_AMD_INSUFFICIENT_MEMORY;
-    c = 0;
-    if (grow(s->d_seg_split, c, n_segments)) return YR_AMD_INSUFFICIENT_MEMORY;
     c = 0;
     if (grow(s->d_seg_offset, c, n_segments)) return YR_AMD_INSUFFICIENT_MEMORY;
     s->seg_alloc = n_segments;
@@ -331,7 +326,7 @@ int yr_amd_scanner_create(yr_amd_tables* tables, void* stream, yr_amd_scanner** 
 int yr_amd_scanner_destroy(yr_amd_scanner* s) {
   if (s == nullptr) return YR_AMD_SUCCESS;
   if (s->stream) (void)hipStreamSynchronize(s->stream);
-  for (void* p : {(void*)s->d_block, (void*)s->d_seg_count, (void*)s->d_seg_split,
+  for (void* p : {(void*)s->d_block, (void*)s->d_seg_count,
                   (void*)s->d_seg_offset,
                   (void*)s->d_seg_out, (void*)s->d_positions, (void*)s->d_summary,
                   (void*)s->d_vcount, (void*)s->d_vkeep, (void*)s->d_voffset, (void*)s->d_vchunk, (void*)s->d_vrec,
@@ -417,7 +412,6 @@ int yr_amd_scan_device(yr_amd_scanner* s, const uint8_t* d_data, uint64_t block_
   p.seg_bytes = seg_bytes;
   p.seg_cap = seg_cap;
   p.seg_count = s->d_seg_count;
-  p.seg_split = s->d_seg_split;
   p.seg_out = s->d_seg_out;
   p.seg_base = nullptr;
   s->last_grid = (int)std::min<uint64_t>((n_segments + kWavesPerWG - 1) / kWavesPerWG,
