@@ -179,6 +179,85 @@ __device__ bool fast_re_reachable(const uint8_t* __restrict__ code, uint32_t len
   return true;
 }
 
+// The same question in the oracle's set form (oracle/ac_oracle.c
+// fast_re_reachable): the set of bytes_matched values reachable before each
+// opcode, kept as a 64-bit window m over [base, base + 64).  A consuming
+// opcode tests the bytes of every live element (b < max_bytes_matched) --
+// independent LDS reads, no choice stack -- and a REPEAT_ANY {min, max} maps
+// b -> b + min and b + j (min < j <= max, b + j < max_bytes_matched).
+// Returns 0 = no path reaches MATCH, 1 = some path does, 2 = the set would
+// leave the window or come near YR_RE_SCAN_LIMIT, or an opcode outside the
+// fast set: the caller then runs the depth-first search, whose answer this
+// form equals wherever it answers.
+__device__ int fast_re_set(const uint8_t* __restrict__ code, uint32_t len,
+                           const uint8_t* __restrict__ input, uint64_t avail, bool backwards,
+                           const ByteWindow& win) {
+  const int maxb = (int)min<uint64_t>(avail, (uint64_t)kReScanLimit);
+  int base = 0;
+  uint64_t m = 1;
+  uint32_t ip = 0;
+  while (ip < len) {
+    const uint8_t op = code[ip];
+    if (op == kReMatch) return m != 0 ? 1 : 0;
+    const int lim = maxb - base;   // bits i < lim are live (b < max_bytes_matched)
+    const uint64_t live = lim >= 64 ? m : (lim <= 0 ? 0ull : m & ((1ull << lim) - 1));
+    if (live == 0) return 0;
+    if (op == kReRepeatAnyUngreedy) {
+      const int mn = code[ip + 1] | (code[ip + 2] << 8);
+      const int mx = code[ip + 3] | (code[ip + 4] << 8);
+      const int lo = __builtin_ctzll(live), hi = 63 - __builtin_clzll(live);
+      const int span = hi - lo + (mx - mn);
+      const int nb = base + lo + mn;
+      if (span > 63 || nb + span >= kReScanLimit) return 2;
+      const uint64_t t = live >> lo;
+      uint64_t more = 0;
+      for (int k = 1; k <= mx - mn; ++k) more |= t << k;
+      const int lim2 = maxb - nb;
+      more &= lim2 >= 64 ? ~0ull : (lim2 <= 0 ? 0ull : (1ull << lim2) - 1);
+      m = t | more;
+      base = nb;
+      ip += 5;
+      continue;
+    }
+    uint32_t sz;
+    switch (op) {
+      case kReAny: sz = 1; break;
+      case kReLiteral: case kReNotLiteral: sz = 2; break;
+      case kReMaskedLiteral: case kReMaskedNotLiteral: sz = 3; break;
+      default: return 2;
+    }
+    const uint8_t a1 = sz > 1 ? code[ip + 1] : 0, a2 = sz > 2 ? code[ip + 2] : 0;
+    uint64_t r = 0, x = live;
+    while (x) {
+      const int i = __builtin_ctzll(x);
+      x &= x - 1;
+      const int b = base + i;
+      const uint8_t c = window_byte(win, backwards ? input - 1 - b : input + b);
+      bool pass;
+      switch (op) {
+        case kReAny: pass = true; break;
+        case kReLiteral: pass = c == a1; break;
+        case kReNotLiteral: pass = c != a1; break;
+        case kReMaskedLiteral: pass = (c & a2) == a1; break;
+        default: pass = (c & a2) != a1; break;
+      }
+      if (pass) r |= 1ull << i;
+    }
+    if (r == 0) return 0;
+    m = r;
+    base += 1;
+    ip += sz;
+  }
+  return 1;
+}
+
+__device__ __forceinline__ bool fast_re_decide(const uint8_t* code, uint32_t len,
+                                               const uint8_t* input, uint64_t avail,
+                                               bool backwards, const ByteWindow& win) {
+  const int v = fast_re_set(code, len, input, avail, backwards, win);
+  return v == 2 ? fast_re_reachable(code, len, input, avail, backwards, win) : v == 1;
+}
+
 // yr_re_exec (re.c:1693-2072) as a reachability question, over-approximated:
 // can some path from the program's start reach RE_OPCODE_MATCH?  Character
 // tests are exact where they are locale-free (LITERAL with the host's case
@@ -337,12 +416,12 @@ __device__ bool re_call_matters(const VerifyParams& p, uint32_t k, uint32_t flag
     if (!(flags & kStrAscii) || (flags & (kStrWide | kStrBase64Any))) return true;
     if (r.fwd_len == 1)   // forward program = MATCH: forward_matches = 0
       return r.bwd_len > 0 &&
-             fast_re_reachable(bwd, r.bwd_len, d, offset, true, stage_window(p, d, true, lds));
-    if (!fast_re_reachable(fwd, r.fwd_len, d, p.size - offset, false,
-                           stage_window(p, d, false, lds)))
+             fast_re_decide(bwd, r.bwd_len, d, offset, true, stage_window(p, d, true, lds));
+    if (!fast_re_decide(fwd, r.fwd_len, d, p.size - offset, false,
+                        stage_window(p, d, false, lds)))
       return false;
     if (r.bwd_len > 0 &&
-        !fast_re_reachable(bwd, r.bwd_len, d, offset, true, stage_window(p, d, true, lds)))
+        !fast_re_decide(bwd, r.bwd_len, d, offset, true, stage_window(p, d, true, lds)))
       return false;
     return true;
   }
