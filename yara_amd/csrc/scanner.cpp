@@ -143,10 +143,8 @@ struct yr_amd_scanner {
   size_t vcount_cap = 0;
   uint32_t* d_vkeep = nullptr;    // pre-verification keep masks + states (2 x count)
   size_t vkeep_cap = 0;
-  uint64_t* d_voffset = nullptr;
-  size_t voffset_cap = 0;
-  uint64_t* d_vchunk = nullptr;
-  size_t vchunk_cap = 0;
+  uint64_t* d_vblock = nullptr;   // per-256-candidate record counts -> offsets
+  size_t vblock_cap = 0;
   VerifyRec* d_vrec = nullptr;
   size_t vrec_cap = 0;
   std::vector<yr_amd_verify_rec> h_vrec;
@@ -329,7 +327,7 @@ int yr_amd_scanner_destroy(yr_amd_scanner* s) {
   for (void* p : {(void*)s->d_block, (void*)s->d_seg_count,
                   (void*)s->d_seg_offset,
                   (void*)s->d_seg_out, (void*)s->d_positions, (void*)s->d_summary,
-                  (void*)s->d_vcount, (void*)s->d_vkeep, (void*)s->d_voffset, (void*)s->d_vchunk, (void*)s->d_vrec,
+                  (void*)s->d_vcount, (void*)s->d_vkeep, (void*)s->d_vblock, (void*)s->d_vrec,
                   (void*)s->d_seg_base})
     if (p) (void)hipFree(p);
   if (s->h_summary) (void)hipHostFree(s->h_summary);
@@ -645,18 +643,15 @@ int yr_amd_verify_device(yr_amd_scanner* s, uint64_t data_base, const yr_amd_ver
     if (v.data == nullptr) return YR_AMD_INVALID_ARGUMENT;
     int r = grow(s->d_vcount, s->vcount_cap, v.count);
     if (!r) r = grow(s->d_vkeep, s->vkeep_cap, 2 * v.count);
-    if (!r) r = grow(s->d_voffset, s->voffset_cap, v.count);
-    if (!r) r = grow(s->d_vchunk, s->vchunk_cap, exclusive_scan_chunks(v.count));
+    if (!r) r = grow(s->d_vblock, s->vblock_cap, verify_blocks(v.count));
     if (r) return r;
     v.counts = s->d_vcount;
     v.keep = s->d_vkeep;
     v.states = s->d_vkeep + v.count;
-    v.offsets = s->d_voffset;
+    v.block_off = s->d_vblock;
+    // count pass -> block offsets (total straight into the host-mapped summary)
     HIP_TRY(launch_verify(v, 0, s->stream));
-    HIP_TRY(launch_exclusive_scan(s->d_vcount, v.count, s->d_vchunk, s->d_voffset, s->d_summary,
-                                  s->stream));
-    HIP_TRY(hipMemcpyAsync(s->h_summary, s->d_summary, sizeof(uint64_t), hipMemcpyDeviceToHost,
-                           s->stream));
+    HIP_TRY(launch_block_offsets(s->d_vblock, v.count, s->d_hsum, s->stream));
     HIP_TRY(hipStreamSynchronize(s->stream));
     total = s->h_summary[0];
     r = grow(s->d_vrec, s->vrec_cap, total);

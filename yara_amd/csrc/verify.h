@@ -70,13 +70,14 @@ struct VerifyParams {
                               // entry of the candidate's list is kept (t < 31); bit 31 =
                               // the list is longer, pass 1 decides again
   uint32_t* states;           // [count] the candidate's AC state (pass 0)
-  const uint64_t* offsets;    // [count] exclusive scan of counts (pass 1)
+  uint64_t* block_off;        // [verify_blocks(count)] pass 0: records per 256-candidate
+                              // block; then (launch_block_offsets) exclusive offsets
   VerifyRec* out;             // records (pass 1)
 };
 
 hipError_t launch_verify(const VerifyParams& p, int pass, hipStream_t s);
-hipError_t launch_exclusive_scan(const uint32_t* counts, uint64_t n, uint64_t* chunk_sum,
-                                 uint64_t* offsets, uint64_t* total, hipStream_t s);
-uint64_t exclusive_scan_chunks(uint64_t n);
+hipError_t launch_block_offsets(uint64_t* block_off, uint64_t count, uint64_t* total,
+                                hipStream_t s);
+uint64_t verify_blocks(uint64_t count);
 
 }  // namespace yamd

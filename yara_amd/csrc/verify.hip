@@ -481,30 +481,20 @@ __device__ bool call_matters(const VerifyParams& p, uint32_t k, uint64_t offset,
   return false;
 }
 
-// PASS 0: decide every call of each candidate, count the records, keep the
-// decisions (keep mask + state); PASS 1: write the records -- from the keep
-// mask, without deciding again (most candidates have none: they return at
-// once), except for lists longer than 31 entries.
+// One candidate: PASS 0 decides every call of its list, counts the records and
+// keeps the decisions (keep mask + state); PASS 1 writes the records from `o`
+// on -- from the keep mask, without deciding again, except for lists longer
+// than 31 entries.
 constexpr uint32_t kKeepOverflow = 1u << 31;
 template <int PASS>
-__global__ __launch_bounds__(256) void verify_kernel(VerifyParams p) {
-  __shared__ __attribute__((aligned(16))) uint8_t win[256 * kWinBytes];
-  // (the low 32 bits of a flat LDS address are the LDS offset)
-  const uint32_t lds = (uint32_t)(uintptr_t)(win + threadIdx.x * kWinBytes);
-  const uint64_t c = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (c >= p.count) return;
-  uint32_t keep = 0, state = 0;
-  if (PASS) {
-    keep = p.keep[c];
-    if (keep == 0) return;
-    state = p.states[c];
-  }
+__device__ __forceinline__ void verify_one(const VerifyParams& p, uint64_t c, uint32_t lds,
+                                           uint32_t keep, uint32_t state, uint64_t o,
+                                           uint32_t& count) {
   const uint64_t i = p.all ? p.all_first + c : p.positions[c];
   if (!PASS)
     for (uint64_t j = i > 4 ? i - 4 : 0; j < i; ++j) state = dev_ac_step(p.T, state, p.data[j]);
   const bool decide = !PASS || (keep & kKeepOverflow);
   uint32_t n = 0, t = 0, mask = 0;
-  uint64_t o = PASS ? p.offsets[c] : 0;
   // scanner.c:105-121: the list of state_i in pool order
   for (uint32_t k = p.M[state]; k != 0; k = p.pool_next[k - 1], ++t) {
     const uint32_t bt = p.pool_backtrack[k - 1];
@@ -530,36 +520,68 @@ __global__ __launch_bounds__(256) void verify_kernel(VerifyParams p) {
     p.keep[c] = n == 0 ? 0u : (t > 31 ? kKeepOverflow : mask);
     p.states[c] = state;
   }
+  count = n;
 }
 
-// Exclusive scan of n uint32 counts into uint64 offsets, three launches:
-// per-chunk sums, one-workgroup scan of the chunk sums (+ total), chunk scans.
-constexpr uint32_t kScanChunk = 4096;   // 256 threads x 16
-
-__global__ __launch_bounds__(256) void chunk_sum_kernel(const uint32_t* counts, uint64_t n,
-                                                        uint64_t* chunk_sum) {
-  __shared__ uint64_t red[256];
-  const uint64_t base = (uint64_t)blockIdx.x * kScanChunk;
-  uint64_t s = 0;
-  for (uint32_t j = threadIdx.x; j < kScanChunk; j += 256)
-    if (base + j < n) s += counts[base + j];
-  red[threadIdx.x] = s;
-  __syncthreads();
-  for (uint32_t d = 128; d > 0; d >>= 1) {
-    if (threadIdx.x < d) red[threadIdx.x] += red[threadIdx.x + d];
-    __syncthreads();
+// Exclusive scan of one value per thread over a 256-thread block (wave
+// shuffles, one barrier); `total` = the block's sum.
+__device__ __forceinline__ uint32_t block_exclusive_scan(uint32_t v, uint32_t* wsum,
+                                                         uint32_t& total) {
+  const uint32_t lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  uint32_t inc = v;
+  for (int d = 1; d < 64; d <<= 1) {
+    const uint32_t u = __shfl_up(inc, d, 64);
+    if (lane >= (uint32_t)d) inc += u;
   }
-  if (threadIdx.x == 0) chunk_sum[blockIdx.x] = red[0];
+  if (lane == 63) wsum[w] = inc;
+  __syncthreads();
+  uint32_t before = 0;
+  total = 0;
+#pragma unroll
+  for (uint32_t k = 0; k < 4; ++k) {
+    const uint32_t x = wsum[k];
+    if (k < w) before += x;
+    total += x;
+  }
+  return before + inc - v;
 }
 
-__global__ __launch_bounds__(1024) void chunk_offsets_kernel(uint64_t* chunk_sum, uint64_t n_chunks,
+// PASS 0: every candidate of the block is decided; the block's record count
+// goes to block_off[block].  (launch_block_offsets turns those into exclusive
+// offsets.)  PASS 1: each block scans its candidates' counts, adds its block
+// offset and writes the records; candidates without records return at once.
+template <int PASS>
+__global__ __launch_bounds__(256) void verify_kernel(VerifyParams p) {
+  __shared__ __attribute__((aligned(16))) uint8_t win[256 * kWinBytes];
+  __shared__ uint32_t wsum[4];
+  // (the low 32 bits of a flat LDS address are the LDS offset)
+  const uint32_t lds = (uint32_t)(uintptr_t)(win + threadIdx.x * kWinBytes);
+  const uint64_t c = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  const bool in = c < p.count;
+  uint32_t n = 0, total = 0;
+  if (!PASS) {
+    if (in) verify_one<0>(p, c, lds, 0, 0, 0, n);
+    (void)block_exclusive_scan(n, wsum, total);
+    if (threadIdx.x == 0) p.block_off[blockIdx.x] = total;
+    return;
+  }
+  const uint32_t keep = in ? p.keep[c] : 0u;
+  n = keep == 0 ? 0u : p.counts[c];
+  const uint32_t pre = block_exclusive_scan(n, wsum, total);
+  if (total == 0 || keep == 0) return;
+  verify_one<1>(p, c, lds, keep, p.states[c], p.block_off[blockIdx.x] + pre, n);
+}
+
+// Exclusive scan, in place, of the per-block record counts (one workgroup),
+// and their total.
+__global__ __launch_bounds__(1024) void block_offsets_kernel(uint64_t* block_off, uint64_t n_blocks,
                                                              uint64_t* total) {
   __shared__ uint64_t part[1024];
   const uint32_t t = threadIdx.x;
-  const uint64_t per = (n_chunks + 1023) / 1024;
-  const uint64_t lo = min(t * per, n_chunks), hi = min(lo + per, n_chunks);
+  const uint64_t per = (n_blocks + 1023) / 1024;
+  const uint64_t lo = min(t * per, n_blocks), hi = min(lo + per, n_blocks);
   uint64_t s = 0;
-  for (uint64_t i = lo; i < hi; ++i) s += chunk_sum[i];
+  for (uint64_t i = lo; i < hi; ++i) s += block_off[i];
   part[t] = s;
   __syncthreads();
   for (uint32_t d = 1; d < 1024; d <<= 1) {
@@ -570,39 +592,11 @@ __global__ __launch_bounds__(1024) void chunk_offsets_kernel(uint64_t* chunk_sum
   }
   uint64_t run = part[t] - s;
   for (uint64_t i = lo; i < hi; ++i) {
-    const uint64_t c = chunk_sum[i];
-    chunk_sum[i] = run;
+    const uint64_t c = block_off[i];
+    block_off[i] = run;
     run += c;
   }
   if (t == 1023) *total = part[1023];
-}
-
-__global__ __launch_bounds__(256) void chunk_scan_kernel(const uint32_t* counts, uint64_t n,
-                                                         const uint64_t* chunk_off,
-                                                         uint64_t* offsets) {
-  __shared__ uint64_t part[256];
-  const uint64_t base = (uint64_t)blockIdx.x * kScanChunk + (uint64_t)threadIdx.x * 16;
-  uint32_t v[16];
-  uint64_t s = 0;
-#pragma unroll
-  for (int j = 0; j < 16; ++j) {
-    v[j] = base + j < n ? counts[base + j] : 0u;
-    s += v[j];
-  }
-  part[threadIdx.x] = s;
-  __syncthreads();
-  for (uint32_t d = 1; d < 256; d <<= 1) {
-    const uint64_t x = threadIdx.x >= d ? part[threadIdx.x - d] : 0;
-    __syncthreads();
-    part[threadIdx.x] += x;
-    __syncthreads();
-  }
-  uint64_t run = chunk_off[blockIdx.x] + part[threadIdx.x] - s;
-#pragma unroll
-  for (int j = 0; j < 16; ++j) {
-    if (base + j < n) offsets[base + j] = run;
-    run += v[j];
-  }
 }
 
 hipError_t launch_verify(const VerifyParams& p, int pass, hipStream_t s) {
@@ -615,17 +609,14 @@ hipError_t launch_verify(const VerifyParams& p, int pass, hipStream_t s) {
   return hipGetLastError();
 }
 
-hipError_t launch_exclusive_scan(const uint32_t* counts, uint64_t n, uint64_t* chunk_sum,
-                                 uint64_t* offsets, uint64_t* total, hipStream_t s) {
-  const uint64_t chunks = (n + kScanChunk - 1) / kScanChunk;
-  if (chunks == 0) return hipMemsetAsync(total, 0, sizeof(uint64_t), s);
-  hipLaunchKernelGGL(chunk_sum_kernel, dim3((uint32_t)chunks), dim3(256), 0, s, counts, n, chunk_sum);
-  hipLaunchKernelGGL(chunk_offsets_kernel, dim3(1), dim3(1024), 0, s, chunk_sum, chunks, total);
-  hipLaunchKernelGGL(chunk_scan_kernel, dim3((uint32_t)chunks), dim3(256), 0, s, counts, n, chunk_sum,
-                     offsets);
+hipError_t launch_block_offsets(uint64_t* block_off, uint64_t count, uint64_t* total,
+                                hipStream_t s) {
+  const uint64_t blocks = verify_blocks(count);
+  if (blocks == 0) return hipMemsetAsync(total, 0, sizeof(uint64_t), s);
+  hipLaunchKernelGGL(block_offsets_kernel, dim3(1), dim3(1024), 0, s, block_off, blocks, total);
   return hipGetLastError();
 }
 
-uint64_t exclusive_scan_chunks(uint64_t n) { return (n + kScanChunk - 1) / kScanChunk; }
+uint64_t verify_blocks(uint64_t count) { return (count + 255) / 256; }
 
 }  // namespace yamd
