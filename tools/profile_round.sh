@@ -9,7 +9,7 @@ OUT=gpurun_out/prof_${TAG}
 mkdir -p $OUT
 cd /tmp && export TMPDIR=/tmp && cd - >/dev/null
 timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $OUT/trace -o run --output-format csv -- \
-  python3 bench.py --no-cpu > $OUT/bench_under_trace.log 2>&1
+  python3 bench.py --no-cpu --no-other > $OUT/bench_under_trace.log 2>&1
 timeout -k 10 300 rocprofv3 --pmc FETCH_SIZE -d $OUT/pmc -o run --output-format csv -- \
-  python3 bench.py --steps 5 --warmup 20 --no-cpu > $OUT/bench_under_pmc.log 2>&1
+  python3 bench.py --steps 5 --warmup 20 --no-cpu --no-other > $OUT/bench_under_pmc.log 2>&1
 find $OUT -name "*.csv" | head -20
