@@ -57,6 +57,9 @@ def case_data(rec):
         return oracle.xorshift(spec[2], spec[1])
     if kind == "planted":
         return planted.planted_buffer(oracle.xorshift, gen_rules.gen(spec[1]), spec[3], spec[2])
+    if kind == "fuzz":
+        import fuzz_rules
+        return fuzz_rules.buffer(oracle.xorshift, spec[1], spec[2])
     if kind == "alpha":
         x = oracle.xorshift(spec[2], spec[1])
         return np.frombuffer(ALPHA, dtype=np.uint8)[x % len(ALPHA)]

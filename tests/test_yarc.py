@@ -18,7 +18,7 @@ import oracle
 import yara_amd
 from conftest import GOLDEN, case_arrays, case_data, golden, ref_tables, tables_npz
 
-SETS = ["B", "C", "E", "lit", "hex", "rx", "short", "root"]
+SETS = ["B", "C", "E", "lit", "hex", "rx", "short", "root"] + ["fuzz%d" % s for s in range(12)]
 CASES = golden()["cases"]
 
 
