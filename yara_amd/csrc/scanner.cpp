@@ -644,20 +644,30 @@ int yr_amd_verify_device(yr_amd_scanner* s, uint64_t data_base, const yr_amd_ver
     int r = grow(s->d_vcount, s->vcount_cap, v.count);
     if (!r) r = grow(s->d_vkeep, s->vkeep_cap, 2 * v.count);
     if (!r) r = grow(s->d_vblock, s->vblock_cap, verify_blocks(v.count));
+    // record space before the count is known (one per 16 candidates, capped;
+    // the buffer is kept, so mostly a scanner's first calls outgrow it): the
+    // write pass is queued behind the count pass with no host round trip in
+    // between, and re-run into a larger buffer only when the records did not fit
+    if (!r) r = grow(s->d_vrec, s->vrec_cap, std::min<uint64_t>(v.count / 16 + 1, 1u << 20));
     if (r) return r;
     v.counts = s->d_vcount;
     v.keep = s->d_vkeep;
     v.states = s->d_vkeep + v.count;
     v.block_off = s->d_vblock;
-    // count pass -> block offsets (total straight into the host-mapped summary)
+    v.out = s->d_vrec;
+    v.out_cap = s->vrec_cap;
+    // count pass -> block offsets (total straight into the host-mapped
+    // summary) -> write pass, then one wait
     HIP_TRY(launch_verify(v, 0, s->stream));
     HIP_TRY(launch_block_offsets(s->d_vblock, v.count, s->d_hsum, s->stream));
+    HIP_TRY(launch_verify(v, 1, s->stream));
     HIP_TRY(hipStreamSynchronize(s->stream));
     total = s->h_summary[0];
-    r = grow(s->d_vrec, s->vrec_cap, total);
-    if (r) return r;
-    if (total > 0) {
+    if (total > v.out_cap) {
+      r = grow(s->d_vrec, s->vrec_cap, total);
+      if (r) return r;
       v.out = s->d_vrec;
+      v.out_cap = s->vrec_cap;
       HIP_TRY(launch_verify(v, 1, s->stream));
       HIP_TRY(hipStreamSynchronize(s->stream));
     }

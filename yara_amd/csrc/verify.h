@@ -73,6 +73,8 @@ struct VerifyParams {
   uint64_t* block_off;        // [verify_blocks(count)] pass 0: records per 256-candidate
                               // block; then (launch_block_offsets) exclusive offsets
   VerifyRec* out;             // records (pass 1)
+  uint64_t out_cap;           // records that fit in out; pass 1 drops the rest (the
+                              // host re-runs it when the total turns out larger)
 };
 
 hipError_t launch_verify(const VerifyParams& p, int pass, hipStream_t s);

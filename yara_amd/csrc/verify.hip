@@ -509,7 +509,8 @@ __device__ __forceinline__ void verify_one(const VerifyParams& p, uint64_t c, ui
       r.offset = i - bt;
       r.pool_index = k - 1;
       r.candidate = (uint32_t)c;
-      p.out[o++] = r;
+      if (o < p.out_cap) p.out[o] = r;
+      ++o;
     } else if (t < 31) {
       mask |= 1u << t;
     }
