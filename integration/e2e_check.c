@@ -18,12 +18,25 @@
  *   E2E_REPEAT = N: time N more runs of each side, report the minimum.
  *   E2E_FAST=1: SCAN_FLAGS_FAST_MODE; E2E_ABORT=n: the callback returns
  *   CALLBACK_ABORT on the n-th matching rule (scanner.c:540-548).
+ *   E2E_TIMEOUT=s: yr_scanner_set_timeout(s); E2E_SLEEP_TOO_MANY=ms: the
+ *   callback sleeps on CALLBACK_MSG_TOO_MANY_MATCHES (a deterministic way to
+ *   exceed the timeout in the middle of a block, scanner.c:74-81).
+ *   E2E_MODE=truncmap: both sides scan_mem an mmap of the data file whose
+ *   file was truncated to half its size (the tail faults: scanner.c:493-496
+ *   maps that to ERROR_COULD_NOT_MAP_FILE).
+ *   E2E_THREADS=n: afterwards n threads, each with its own YR_SCANNER and
+ *   YR_GPU_SCANNER on the one shared YR_GPU_RULES, scan the data
+ *   E2E_THREAD_REPS times concurrently; every result must equal stock's
+ *   (docs/capi.rst:330-347, cli/yara.c:1564-1608).
  */
 #include <stdint.h>
 #include <stdio.h>
 #include <stdlib.h>
 #include <string.h>
+#include <fcntl.h>
+#include <pthread.h>
 #include <signal.h>
+#include <sys/mman.h>
 #include <sys/wait.h>
 #include <time.h>
 #include <unistd.h>
@@ -87,6 +100,8 @@ static int cb(YR_SCAN_CONTEXT* ctx, int msg, void* data, void* user)
   else if (msg == CALLBACK_MSG_TOO_MANY_MATCHES)
   {
     c->too_many++;
+    const char* sl = getenv("E2E_SLEEP_TOO_MANY");
+    if (sl != NULL) usleep(1000 * atoi(sl));
   }
   if (msg == CALLBACK_MSG_RULE_MATCHING && c->abort_after > 0 &&
       ++c->n_matching >= c->abort_after)
@@ -192,6 +207,7 @@ static int run(YR_RULES* rules, YR_GPU_SCANNER* gs, const uint8_t* data, size_t 
   int flags = SCAN_FLAGS_REPORT_RULES_MATCHING | SCAN_FLAGS_REPORT_RULES_NOT_MATCHING;
   if (getenv("E2E_FAST") && strcmp(getenv("E2E_FAST"), "1") == 0) flags |= SCAN_FLAGS_FAST_MODE;
   yr_scanner_set_flags(sc, flags);
+  if (getenv("E2E_TIMEOUT")) yr_scanner_set_timeout(sc, atoi(getenv("E2E_TIMEOUT")));
   c->abort_after = getenv("E2E_ABORT") ? atoi(getenv("E2E_ABORT")) : 0;
   yr_scanner_set_callback(sc, cb, c);
   double t0 = now();
@@ -224,6 +240,42 @@ static int run(YR_RULES* rules, YR_GPU_SCANNER* gs, const uint8_t* data, size_t 
   return r;
 }
 
+typedef struct
+{
+  YR_RULES* rules;
+  YR_GPU_RULES* gr;
+  const uint8_t* data;
+  size_t n, bsize, overlap;
+  const collect* want;
+  int reps;
+  int ok;
+} thread_job;
+
+static void* thread_main(void* arg)
+{
+  thread_job* j = (thread_job*) arg;
+  YR_GPU_SCANNER* gs;
+  j->ok = 0;
+  if (yr_gpu_scanner_create(j->gr, &gs) != 0) return NULL;
+  int good = 1;
+  for (int k = 0; k < j->reps && good; k++)
+  {
+    collect x = {j->rules};
+    x.rule_msg = (uint8_t*) calloc(j->rules->num_rules + 1, 1);
+    double t;
+    int r = run(j->rules, gs, j->data, j->n, j->bsize, j->overlap, &x, &t);
+    qsort(x.r, x.n, sizeof(rec), cmp_rec);
+    good = r == 0 && x.n == j->want->n &&
+           (x.n == 0 || memcmp(x.r, j->want->r, x.n * sizeof(rec)) == 0) &&
+           memcmp(x.rule_msg, j->want->rule_msg, j->rules->num_rules) == 0;
+    free(x.r);
+    free(x.rule_msg);
+  }
+  yr_gpu_scanner_destroy(gs);
+  j->ok = good;
+  return NULL;
+}
+
 int main(int argc, char** argv)
 {
   if (argc < 3)
@@ -252,7 +304,19 @@ int main(int argc, char** argv)
   }
   if (getenv("E2E_MODE")) g_mode = getenv("E2E_MODE");
   char tmpl[] = "/tmp/e2e_check_XXXXXX";
-  if (strcmp(g_mode, "file") == 0 || strcmp(g_mode, "fd") == 0)
+  const uint8_t* scan_data = data;
+  if (strcmp(g_mode, "truncmap") == 0)
+  {
+    int fd = mkstemp(tmpl);
+    if (fd < 0 || write(fd, data, n) != (ssize_t) n) return 2;
+    void* m = mmap(NULL, n, PROT_READ, MAP_PRIVATE, fd, 0);
+    if (m == MAP_FAILED || ftruncate(fd, n / 2) != 0) return 2;
+    close(fd);
+    g_path = tmpl;
+    scan_data = (const uint8_t*) m;
+    g_mode = "mem";
+  }
+  else if (strcmp(g_mode, "file") == 0 || strcmp(g_mode, "fd") == 0)
   {
     int fd = mkstemp(tmpl);
     if (fd < 0 || write(fd, data, n) != (ssize_t) n) return 2;
@@ -298,7 +362,7 @@ int main(int argc, char** argv)
   g_mode = "mem";
   run(rules, gs, data, n < 4096 ? n : 4096, 0, 0, &warm, &tw); /* GPU warm-up */
   g_mode = mode;
-  const uint8_t* d_arg = scan_whole ? NULL : data;
+  const uint8_t* d_arg = scan_whole ? NULL : scan_data;
   int rs = run(rules, NULL, d_arg, n, bsize, overlap, &a, &ts);
   int rg = run(rules, gs, d_arg, n, bsize, overlap, &b, &tg);
   /* E2E_REPEAT=N: N more timed runs of each side (steady state: warm caches,
@@ -320,6 +384,28 @@ int main(int argc, char** argv)
     free(x.r);
     free(x.rule_msg);
   }
+  int threads = getenv("E2E_THREADS") ? atoi(getenv("E2E_THREADS")) : 0;
+  int threads_ok = 1;
+  if (threads > 0)
+  {
+    thread_job jobs[32];
+    pthread_t tid[32];
+    if (threads > 32) threads = 32;
+    collect want = a;
+    qsort(want.r, want.n, sizeof(rec), cmp_rec);
+    for (int k = 0; k < threads; k++)
+    {
+      thread_job j = {rules, gr, d_arg, n, bsize, overlap, &want,
+                      getenv("E2E_THREAD_REPS") ? atoi(getenv("E2E_THREAD_REPS")) : 4, 0};
+      jobs[k] = j;
+      pthread_create(&tid[k], NULL, thread_main, &jobs[k]);
+    }
+    for (int k = 0; k < threads; k++)
+    {
+      pthread_join(tid[k], NULL);
+      threads_ok &= jobs[k].ok;
+    }
+  }
   if (g_pid > 0)
   {
     kill(g_pid, SIGKILL);
@@ -335,13 +421,15 @@ int main(int argc, char** argv)
   printf("{\"mode\": \"%s\", \"size\": %zu, \"block\": %zu, \"rc_stock\": %d, \"rc_gpu\": %d, "
          "\"matches_stock\": %zu, \"matches_gpu\": %zu, \"rules_matching\": %d, "
          "\"same_matches\": %s, \"same_rule_reports\": %s, \"finished\": [%d, %d], "
-         "\"stock_s\": %.4f, \"gpu_s\": %.4f, \"too_many\": [%d, %d]}\n",
+         "\"stock_s\": %.4f, \"gpu_s\": %.4f, \"too_many\": [%d, %d], \"threads\": %d, "
+         "\"threads_ok\": %s}\n",
          g_mode, n, bsize, rs, rg, a.n, b.n, n_match_rules, same_matches ? "true" : "false",
-         same_rules ? "true" : "false", a.finished, b.finished, ts, tg, a.too_many, b.too_many);
+         same_rules ? "true" : "false", a.finished, b.finished, ts, tg, a.too_many, b.too_many,
+         threads, threads_ok ? "true" : "false");
   yr_gpu_scanner_destroy(gs);
   yr_gpu_rules_destroy(gr);
   yr_rules_destroy(rules);
   yr_compiler_destroy(comp);
   yr_finalize();
-  return (rs == rg && same_matches && same_rules) ? 0 : 1;
+  return (rs == rg && same_matches && same_rules && threads_ok) ? 0 : 1;
 }

@@ -279,25 +279,60 @@ void yr_gpu_scanner_destroy(YR_GPU_SCANNER* s)
   free(s);
 }
 
+/* Timeout checks at the block positions the reference walk checks them
+ * (scanner.c:74-81): at the top of the loop for every i < size with
+ * i % 4096 == 0, i.e. before the verify calls dispatched at i.  The GPU path
+ * reaches position `pos` of the block when it replays the first call
+ * dispatched at a position >= pos; every check of the reference up to pos that
+ * has not been made yet is made then (one clock read: the clock is monotonic,
+ * so a later read fires whenever an earlier one would have).  *next is the
+ * first position not yet checked. */
+static int _timeout_upto(YR_SCANNER* scanner, uint64_t* next, uint64_t pos, size_t size)
+{
+  if (scanner->timeout <= 0 || size == 0) return ERROR_SUCCESS;
+  if (pos > size - 1) pos = size - 1;
+  if (*next > pos) return ERROR_SUCCESS;
+  *next = (pos / 4096 + 1) * 4096;
+  if (yr_stopwatch_elapsed_ns(&scanner->stopwatch) > scanner->timeout)
+    return ERROR_SCAN_TIMEOUT;
+  return ERROR_SUCCESS;
+}
+
 typedef struct
 {
   YR_SCANNER* scanner;
   const uint8_t* data;
   size_t size;
   uint64_t base;
+  uint64_t next_check; /* _timeout_upto */
 } verify_ctx;
 
-/* The reference's own call, scanner.c:111-117 / :153-159. */
+/* The reference's own call, scanner.c:111-117 / :153-159, after the timeout
+ * checks the walk makes before reaching the call's position. */
 static int _verify(void* user, uint32_t pool_index, uint64_t offset)
 {
   verify_ctx* c = (verify_ctx*) user;
-  return yr_scan_verify_match(
-      c->scanner,
-      &c->scanner->rules->ac_match_pool[pool_index],
-      c->data,
-      c->size,
-      c->base,
-      (size_t) offset);
+  YR_AC_MATCH* m = &c->scanner->rules->ac_match_pool[pool_index];
+  FAIL_ON_ERROR(_timeout_upto(c->scanner, &c->next_check, offset + m->backtrack, c->size));
+  return yr_scan_verify_match(c->scanner, m, c->data, c->size, c->base, (size_t) offset);
+}
+
+/* The effective verify calls of one block (pre-verification records), in the
+ * reference's order, with the walk's timeout checks (_timeout_upto). */
+static int _replay_records(
+    YR_SCANNER* scanner,
+    const yr_amd_verify_rec* recs,
+    uint64_t n,
+    const uint8_t* data,
+    size_t size,
+    uint64_t base,
+    uint64_t next_check)
+{
+  verify_ctx ctx = {scanner, data, size, base, next_check};
+  for (uint64_t c = 0; c < n; c++)
+    FAIL_ON_ERROR(_verify(&ctx, recs[c].pool_index, recs[c].offset));
+  /* the checks the walk makes after its last dispatch, up to size - 1 */
+  return _timeout_upto(scanner, &ctx.next_check, size, size);
 }
 
 /* Replacement of _yr_scanner_scan_mem_block (scanner.c:45-176). */
@@ -308,12 +343,10 @@ static int _yr_gpu_scan_mem_block(
     YR_MEMORY_BLOCK* block)
 {
   int result = ERROR_SUCCESS;
+  uint64_t next_check = 0;
 
-  /* The reference checks the timeout every 4096 bytes (scanner.c:74-81); the
-   * GPU path checks before and after the whole-block candidate pass. */
-  if (scanner->timeout > 0 &&
-      yr_stopwatch_elapsed_ns(&scanner->stopwatch) > scanner->timeout)
-    return ERROR_SCAN_TIMEOUT;
+  /* the walk's first timeout check, position 0 (scanner.c:74-81) */
+  FAIL_ON_ERROR(_timeout_upto(scanner, &next_check, 0, block->size));
 
   /* Block bytes may live in an mmap (filemap.c:56): copy them in the scanning
    * thread inside the trycatch so a SIGBUS/SIGSEGV maps to
@@ -342,12 +375,8 @@ static int _yr_gpu_scan_mem_block(
       &count,
       &all_positions));
 
-  if (scanner->timeout > 0 &&
-      yr_stopwatch_elapsed_ns(&scanner->stopwatch) > scanner->timeout)
-    return ERROR_SCAN_TIMEOUT;
-
-  verify_ctx ctx = {scanner, gs->staging, block->size, block->base};
-  return yr_amd_replay(
+  verify_ctx ctx = {scanner, gs->staging, block->size, block->base, next_check};
+  FAIL_ON_ERROR(yr_amd_replay(
       gs->gpu_rules->tables,
       gs->staging,
       block->size,
@@ -355,7 +384,8 @@ static int _yr_gpu_scan_mem_block(
       count,
       all_positions,
       _verify,
-      &ctx);
+      &ctx));
+  return _timeout_upto(scanner, &ctx.next_check, block->size, block->size);
 }
 
 /* Replay the oldest block of the pipeline: its effective verify calls, in the
@@ -371,18 +401,10 @@ static int _replay_next(YR_SCANNER* scanner, YR_GPU_SCANNER* gs)
   int result = yr_amd_pipeline_next(gs->pipe, &recs, &n, &data, &size, &base);
   gs->inflight--;
   if (result != ERROR_SUCCESS) return result;
-  if (scanner->timeout > 0 &&
-      yr_stopwatch_elapsed_ns(&scanner->stopwatch) > scanner->timeout)
-    return ERROR_SCAN_TIMEOUT;
-  for (uint64_t c = 0; c < n; c++)
-    FAIL_ON_ERROR(yr_scan_verify_match(
-        scanner,
-        &scanner->rules->ac_match_pool[recs[c].pool_index],
-        data,
-        size,
-        base,
-        (size_t) recs[c].offset));
-  return ERROR_SUCCESS;
+  /* the walk of this block starts here: its position-0 timeout check */
+  uint64_t next_check = 0;
+  FAIL_ON_ERROR(_timeout_upto(scanner, &next_check, 0, size));
+  return _replay_records(scanner, recs, n, data, size, base, next_check);
 }
 
 /* One block into the pipeline; replays the oldest when `depth` are in flight. */
@@ -393,9 +415,6 @@ static int _pipeline_block(
     YR_MEMORY_BLOCK* block)
 {
   int result = ERROR_SUCCESS;
-  if (scanner->timeout > 0 &&
-      yr_stopwatch_elapsed_ns(&scanner->stopwatch) > scanner->timeout)
-    return ERROR_SCAN_TIMEOUT;
   /* the block copy may fault on an mmap: same mapping to
    * ERROR_COULD_NOT_MAP_FILE as scanner.c:493-496 */
   YR_TRYCATCH(
@@ -419,27 +438,29 @@ static int _direct_block(
     YR_MEMORY_BLOCK* block)
 {
   int result = ERROR_SUCCESS;
-  if (scanner->timeout > 0 &&
-      yr_stopwatch_elapsed_ns(&scanner->stopwatch) > scanner->timeout)
-    return ERROR_SCAN_TIMEOUT;
-  const yr_amd_verify_rec* recs = NULL;
-  uint64_t n = 0;
-  FAIL_ON_ERROR(yr_amd_scan_block_verified(gs->scanner, data, block->size, block->base, &recs, &n));
-  if (scanner->timeout > 0 &&
-      yr_stopwatch_elapsed_ns(&scanner->stopwatch) > scanner->timeout)
-    return ERROR_SCAN_TIMEOUT;
+  uint64_t next_check = 0;
+  FAIL_ON_ERROR(_timeout_upto(scanner, &next_check, 0, block->size));
+  /* The H2D below reads the caller's buffer inside the HIP runtime, where a
+   * fault cannot be unwound.  Touch every page of it first, inside the
+   * trycatch, so a buffer that faults (a truncated file mapping, an unmapped
+   * range) yields ERROR_COULD_NOT_MAP_FILE as scanner.c:493-496 does; ~3 ms
+   * per GiB of resident memory. */
   YR_TRYCATCH(
       !(scanner->flags & SCAN_FLAGS_NO_TRYCATCH),
       {
-        for (uint64_t c = 0; c < n && result == ERROR_SUCCESS; c++)
-          result = yr_scan_verify_match(
-              scanner,
-              &scanner->rules->ac_match_pool[recs[c].pool_index],
-              data,
-              block->size,
-              block->base,
-              (size_t) recs[c].offset);
+        volatile uint8_t sink = 0;
+        for (size_t o = 0; o < block->size; o += 4096) sink ^= data[o];
+        if (block->size > 0) sink ^= data[block->size - 1];
+        (void) sink;
       },
+      { result = ERROR_COULD_NOT_MAP_FILE; });
+  if (result != ERROR_SUCCESS) return result;
+  const yr_amd_verify_rec* recs = NULL;
+  uint64_t n = 0;
+  FAIL_ON_ERROR(yr_amd_scan_block_verified(gs->scanner, data, block->size, block->base, &recs, &n));
+  YR_TRYCATCH(
+      !(scanner->flags & SCAN_FLAGS_NO_TRYCATCH),
+      { result = _replay_records(scanner, recs, n, data, block->size, block->base, next_check); },
       { result = ERROR_COULD_NOT_MAP_FILE; });
   return result;
 }

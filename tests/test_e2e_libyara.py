@@ -167,3 +167,71 @@ def test_regexp_fiber_limit_error_is_preserved(tmp_path, preverify):
     d[4096:4096 + len(run)] = np.frombuffer(run, np.uint8)
     rc, res = _run(str(rf), _data_file(tmp_path, d, "d.bin"), preverify=preverify)
     assert res["rc_stock"] == 46 and res["rc_gpu"] == 46, res   # ERROR_TOO_MANY_RE_FIBERS
+
+
+def _alpha_file(tmp_path, size, name="a.bin"):
+    x = oracle.xorshift(size, 5)
+    return _data_file(tmp_path, np.frombuffer(ALPHA, np.uint8)[x % len(ALPHA)], name)
+
+
+@needs_check
+@pytest.mark.parametrize("preverify", [True, False], ids=["preverify", "full-replay"])
+@pytest.mark.parametrize("block", [0, 1 << 20], ids=["one-block", "pipeline"])
+def test_scan_timeout_inside_a_block(tmp_path, preverify, block):
+    """ERROR_SCAN_TIMEOUT from the walk's own checks (scanner.c:74-81: every
+    4096 positions of a block).  The callback sleeps past the 1 s timeout when
+    CALLBACK_MSG_TOO_MANY_MATCHES arrives (inside yr_scan_verify_match, in the
+    middle of the 16 MiB buffer); the next check of the reference walk fires,
+    and the GPU replay must make that check too (before this round it checked
+    only around the GPU pass, so it returned ERROR_SUCCESS)."""
+    short = _rules_file(tmp_path, "short")
+    spec = _alpha_file(tmp_path, 16 << 20)
+    rc, res = _run(short, spec, block, 0 if not block else 64, preverify,
+                   E2E_TIMEOUT="1", E2E_SLEEP_TOO_MANY="1200")
+    assert res["too_many"][0] >= 1 and res["too_many"][1] >= 1, res
+    assert res["rc_stock"] == 26 and res["rc_gpu"] == 26, res   # ERROR_SCAN_TIMEOUT
+
+
+@needs_check
+def test_no_timeout_without_sleep(tmp_path):
+    """Same scan, same 1 s timeout, no sleep: both finish (the timeout checks
+    themselves change nothing)."""
+    short = _rules_file(tmp_path, "short")
+    spec = _alpha_file(tmp_path, 16 << 20)
+    rc, res = _run(short, spec, E2E_TIMEOUT="5")
+    assert res["rc_stock"] == 0 and res["rc_gpu"] == 0, res
+    assert res["same_matches"] and res["same_rule_reports"], res
+
+
+@needs_check
+@pytest.mark.parametrize("preverify", [True, False], ids=["preverify", "full-replay"])
+def test_scan_mem_of_truncated_mapping(tmp_path, preverify):
+    """yr_scanner_scan_mem over an mmap whose file was truncated underneath:
+    the stock walk faults inside YR_TRYCATCH -> ERROR_COULD_NOT_MAP_FILE
+    (scanner.c:493-496).  The shim's in-place scan_mem touches the caller's
+    pages inside the trycatch before its H2D, so it returns the same code
+    instead of faulting inside the HIP runtime."""
+    lit = _rules_file(tmp_path, "lit")
+    spec = _data_file(tmp_path, planted.lit_buffer(oracle.xorshift, 4 << 20, 13), "d.bin")
+    rc, res = _run(lit, spec, preverify=preverify, mode="truncmap")
+    assert res["rc_stock"] == 4 and res["rc_gpu"] == 4, res   # ERROR_COULD_NOT_MAP_FILE
+    assert res["finished"] == [0, 0], res
+
+
+@needs_check
+@pytest.mark.parametrize("rules,block", [("C", 0), ("lit", 65536)])
+def test_threads_share_one_gpu_rules(tmp_path, rules, block):
+    """N threads, each with its own YR_SCANNER and YR_GPU_SCANNER, scanning
+    concurrently on ONE shared YR_GPU_RULES (as N scanners share one YR_RULES,
+    docs/capi.rst:330-347, cli/yara.c:1564-1608): every scan's match set and
+    rule reports equal stock."""
+    rf = _rules_file(tmp_path, rules)
+    if rules == "lit":
+        buf = planted.lit_buffer(oracle.xorshift, 4 << 20, 13)
+    else:
+        buf = planted.planted_buffer(oracle.xorshift, gen_rules.gen("C"), 4 << 20, 3)
+    spec = _data_file(tmp_path, buf, "d.bin")
+    rc, res = _run(rf, spec, block, 100 if block else 0, E2E_THREADS="6", E2E_THREAD_REPS="3")
+    assert res["threads"] == 6 and res["threads_ok"], res
+    assert res["same_matches"] and res["matches_stock"] > 0, res
+    assert rc == 0

@@ -88,6 +88,6 @@ def test_reference_suite_through_gpu(suite, preverify, topdir):
     assert int(m.group(1)) > 0 and int(m.group(2)) > 0 and m.group(3) == preverify
     if suite == "test-rules":
         assert "--- PASS 3 ---" in p.stdout
-        # every assert_*_rule of the three passes scans (thousands of scans)
-        assert int(m.group(1)) > 3000, m.group(0)
+        # ~650 assert_*_rule scans per pass, three passes
+        assert int(m.group(1)) > 1500, m.group(0)
     print(m.group(0))
