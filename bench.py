@@ -8,8 +8,11 @@ of the canonical xorshift64 input per GPU, resident in HBM before timing.
 A step = one pass of the hot path over the batch: the scan kernel over the
 whole shard, candidate compaction into one ascending position array, and for
 N > 1 the RCCL gather of every rank's candidate list to rank 0 (config D:
-one logical 4N GiB buffer, rank r owns bytes [4r, 4r+4) GiB plus a 16-byte
-warm-up halo; weak scaling).
+one logical 4N GiB buffer, rank r owns bytes [4r, 4r+4) GiB and holds them
+plus the rule set's verify halos, yara_amd/dist.py; weak scaling).  The
+line's "verified_step" times the verification-complete step separately: the
+same plus on-device pre-verification per rank and, for N > 1, the gather of
+the pre-verified {offset, pool index} records.
 
     python bench.py [--gpus N] [--steps K] [--warmup W]
 
@@ -124,17 +127,24 @@ def cpu_parallel(rules: str, sample_mib: int, seed: int, threads: int):
 
 
 def load_traffic(kernel_bytes):
-    """HBM bytes per scan-kernel launch from the committed PMC pass (profiles/)."""
+    """HBM bytes per scan-kernel launch from the committed PMC pass: a
+    separate `rocprofv3 --pmc FETCH_SIZE` run of this bench (tools/
+    profile_round.sh -> tools/pmc_summary.py -> profiles/pmc_traffic.json;
+    counters cannot be collected inside the timed run).  Returns (bytes,
+    source) -- the source names the file and the round/commit it was measured
+    at, so a stale profile is visible as such -- or (None, reason)."""
     p = os.path.join(REPO, "profiles", "pmc_traffic.json")
     if not os.path.exists(p):
-        return None
+        return None, "no PMC pass committed (profiles/pmc_traffic.json)"
     try:
         d = json.load(open(p))
         if int(d.get("input_bytes", -1)) == kernel_bytes:
-            return int(d["hbm_bytes_per_launch"])
+            return (int(d["hbm_bytes_per_launch"]),
+                    "profiles/pmc_traffic.json: rocprofv3 --pmc FETCH_SIZE (x2 gfx950 "
+                    "correction), %s" % d.get("measured", "round r01"))
     except Exception:
         pass
-    return None
+    return None, "profiles/pmc_traffic.json is for another input size"
 
 
 def main():
@@ -161,17 +171,21 @@ def main():
             dist.init_process_group(args.backend)
 
     from yara_amd import dist as ydist
-    shard = int(args.gib_per_gpu * GiB)
-    total = shard * world                           # one logical block, sharded
-    begin, end = ydist.shard_bounds(total, world, rank)
-    lo, halo = ydist.local_window(begin, end)       # >= 4-byte warm-up, 16-B aligned
-    buf = torch.empty(end - lo + 16, dtype=torch.uint8, device=dev)
-    yara_amd.fill_xorshift64(buf.data_ptr(), end - lo, args.seed, lo)
-    torch.cuda.synchronize()
-
     tables = yara_amd.Tables.from_npz(os.path.join(REPO, "tests", "golden", "tables",
                                                    "%s.npz" % args.rules), device=dev.index,
                                       strings=True)
+    shard = int(args.gib_per_gpu * GiB)
+    total = shard * world                           # one logical block, sharded
+    begin, end = ydist.shard_bounds(total, world, rank)
+    # the rank's window of the block: its shard plus the tables' verify halos
+    # (yr_amd_tables_info), so on-device pre-verification of its own candidates
+    # is exactly the whole block's (dist.py); N = 1: the whole block
+    halo_before, halo_after = ydist.tables_halos(tables)
+    lo, hi = ydist.shard_window(total, begin, end, halo_before, halo_after)
+    buf = torch.empty(hi - lo + 16, dtype=torch.uint8, device=dev)
+    yara_amd.fill_xorshift64(buf.data_ptr(), hi - lo, args.seed, lo)
+    torch.cuda.synchronize()
+
     stream = torch.cuda.Stream(device=dev)
     # DEPTH scanners on ONE stream, used in turn: the scans of steps k+1 ..
     # k+DEPTH-1 are queued before the host collects step k's result
@@ -182,21 +196,19 @@ def main():
     depth = 3
     scanners = [yara_amd.Scanner(tables, stream=stream.cuda_stream) for _ in range(depth)]
     scanner = scanners[0]
-    block = end - lo
 
     def launch(k):
-        scanners[k % depth].scan_device(buf.data_ptr(), block, halo, block)
+        scanners[k % depth].scan_window(buf.data_ptr(), lo, hi, total, begin, end)
 
     def finish(k, timed_kernel=False):
         sc = scanners[k % depth]
-        ptr, cnt, _ = sc.device_result()            # ascending positions in HBM
+        ptr, cnt, _ = sc.device_result()            # ascending block positions in HBM
         kms = sc.kernel_ms() if timed_kernel else None
-        if world == 1:                              # lo == 0: already global
+        if world == 1:
             return (ptr, cnt), kms
         pos = torch.empty(max(cnt, 1), dtype=torch.int64, device=dev)
         memcpy(pos.data_ptr(), ptr, cnt * 8, 3)
-        pos = pos[:cnt] + lo                        # global positions
-        pos = ydist.gather_positions(pos)           # RCCL: counts + padded gather
+        pos = ydist.gather_positions(pos[:cnt])     # RCCL: counts + padded gather
         return pos, kms
 
     def run(steps, timed_kernel=False):
@@ -236,6 +248,42 @@ def main():
     k_avg = sum(kernel_ms) / len(kernel_ms)
     achieved = shard / (k_avg * 1e-3) / 1e9
 
+    # The verification-complete step, timed separately over the same number of
+    # steps (not the bench value): scan + compaction + on-device
+    # pre-verification of the rank's candidates (yr_amd_verify_device) and, for
+    # N > 1, the RCCL gather of the {offset, pool index} records to rank 0 --
+    # i.e. everything the host's yr_scan_verify_match still has to see.
+    def verified_step():
+        scanner.scan_window(buf.data_ptr(), lo, hi, total, begin, end)
+        scanner.device_result()
+        ptr, n_rec = scanner.verify_device(0)
+        if world > 1:
+            return ydist.gather_rows(ydist.records_to_rows(ptr, n_rec, dev))
+        return n_rec
+    for _ in range(max(args.warmup, 3)):
+        verified_step()
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        v_out = verified_step()
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    v_elapsed = time.perf_counter() - t0
+    if world > 1:
+        t = torch.tensor([v_elapsed], dtype=torch.float64,
+                         device=dev if args.backend == "nccl" else "cpu")
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        v_elapsed = float(t.item())
+    verified = {"ms_per_step": round(v_elapsed / args.steps * 1e3, 4),
+                "value": round(total * args.steps / v_elapsed / 1e9, 3), "unit": "GB/s",
+                "records": int(v_out if world == 1 else (v_out.shape[0] if v_out is not None else -1)),
+                "what": "scan + compaction + on-device pre-verification (yr_amd_verify_device)"
+                        + ("" if world == 1 else " of each rank's window + RCCL gather of the "
+                           "{offset, pool index} records to rank 0")}
+
     # parity spot check of this run's own output (rank 0): ascending and the
     # candidate count of config C at 4 GiB recorded from the reference run
     # on-device pre-verification of the last step's candidates (SURVEY.md §8f
@@ -251,12 +299,12 @@ def main():
                                                         "%s.npz" % name), device=dev.index)
             s_o = yara_amd.Scanner(t_o, stream=stream.cuda_stream)
             for _ in range(20):
-                s_o.scan_device(buf.data_ptr(), block, halo, block)
+                s_o.scan_device(buf.data_ptr(), total)
                 s_o.device_result()
             s_o.set_timing(True)
             ks = []
             for _ in range(20):
-                s_o.scan_device(buf.data_ptr(), block, halo, block)
+                s_o.scan_device(buf.data_ptr(), total)
                 _, c_o, _ = s_o.device_result()
                 ks.append(s_o.kernel_ms())
             k_o = sum(ks) / len(ks)
@@ -268,7 +316,7 @@ def main():
 
     preverify = None
     if rank == 0 and world == 1:
-        scanner.scan_device(buf.data_ptr(), block, halo, block)
+        scanner.scan_device(buf.data_ptr(), total)
         scanner.device_result()
         torch.cuda.synchronize()
         scanner.verify_device(0)                    # workspace allocation
@@ -298,6 +346,7 @@ def main():
                                      oracle.positions_sha(p) == rec["candidate_sha"])
 
     if rank == 0:
+        traffic, traffic_src = load_traffic(shard)
         cpu = cpu_par = None
         if world == 1 and not args.no_cpu:
             cpu = cpu_baseline(args.rules, args.cpu_sample_mib, args.seed)
@@ -320,16 +369,19 @@ def main():
                                    "%.0f GiB per GPU%s" % (
                                        args.rules, {"B": 1000, "C": 10000, "E": 2000}.get(args.rules, 0),
                                        args.gib_per_gpu,
-                                       "" if world == 1 else ", one %d GiB buffer sharded, RCCL "
-                                       "gather of candidate lists" % (args.gib_per_gpu * world)),
+                                       "" if world == 1 else ", one %d GiB buffer sharded "
+                                       "(shard + verify halos per GPU), RCCL gather of candidate "
+                                       "lists" % (args.gib_per_gpu * world)),
                        "bytes_per_gpu": shard, "parallelism": "shard%d" % world},
             "roofline": {"bound": "hbm", "achieved": round(achieved, 2), "peak": HBM_PEAK_GBS,
                          "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4),
-                         "traffic": load_traffic(shard),
+                         "traffic": traffic,
+                         "traffic_source": traffic_src,
                          "kernel": "scan_segments_kernel", "kernel_ms_avg": round(k_avg, 4)},
             "cpu_baseline": cpu,
             "cpu_port_parallel": cpu_par,
             "preverify": preverify,
+            "verified_step": verified,
             "check": check,
             "other_rule_sets": other,
         }

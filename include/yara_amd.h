@@ -120,6 +120,14 @@ typedef struct
   uint32_t filter_bits;        /* log2 of the LDS window-filter size in bits */
   uint32_t filter_set_bits;    /* populated bits of that filter */
   uint32_t exact_slots;        /* slots of the HBM exact-suffix hash table */
+  uint32_t max_backtrack;      /* max YR_AC_MATCH.backtrack of the pool */
+  /* Bytes a shard must hold before / after the positions it owns for
+   * yr_amd_verify_device to decide every call exactly as on the whole block
+   * (yr_amd_scan_window): max_backtrack + YR_RE_SCAN_LIMIT (limits.h:163)
+   * before, max(YR_RE_SCAN_LIMIT, 2 * longest string) after.  Without string
+   * records (candidates only): the 4-byte warm-up before, 0 after. */
+  uint64_t verify_halo_before;
+  uint64_t verify_halo_after;
 } yr_amd_tables_info;
 
 int yr_amd_tables_get_info(const yr_amd_tables* tables, yr_amd_tables_info* info);
@@ -167,6 +175,29 @@ int yr_amd_scan_block(
 int yr_amd_scan_device(
     yr_amd_scanner* scanner,
     const uint8_t* d_data,
+    uint64_t block_size,
+    uint64_t byte_begin,
+    uint64_t byte_end);
+
+/*
+ * The same scan when the device holds only a WINDOW of the block: d_window
+ * holds bytes [window_begin, window_end) of a block of block_size bytes
+ * (multi-GPU shards, SURVEY.md section 8e: each GPU owns a byte range and
+ * holds it plus a halo).  Scans [byte_begin, byte_end) and reads only
+ * [byte_begin - min(4, byte_begin), byte_end), which must lie in the window.
+ * Positions, offsets and data_base semantics are those of the whole block, so
+ * the candidate stream (and yr_amd_verify_device's records, when the window
+ * includes yr_amd_tables_info's verify halos) equal the whole block's restricted
+ * to (byte_begin, byte_end].
+ * Requirements: d_window 16-byte aligned, window_begin and byte_begin
+ * multiples of 16.  yr_amd_scan_device(s, d, n, b, e) is
+ * yr_amd_scan_window(s, d, 0, n, n, b, e).
+ */
+int yr_amd_scan_window(
+    yr_amd_scanner* scanner,
+    const uint8_t* d_window,
+    uint64_t window_begin,
+    uint64_t window_end,
     uint64_t block_size,
     uint64_t byte_begin,
     uint64_t byte_end);
@@ -296,11 +327,21 @@ typedef struct
  * (_yr_scan_verify_literal_match returns before _yr_scan_match_callback,
  * scan.c:974-975), a FIXED_OFFSET string at another offset (scan.c:1023),
  * offset == size (scan.c:1013), and -- with yr_amd_tables_set_re_code -- a
- * hex string whose forward or backward fast-exec program cannot reach MATCH
- * (_yr_scan_verify_re_match, scan.c:778-880).  Other non-literal strings are
- * always kept (their verification is re.c's, on the host).  data_base = YR_MEMORY_BLOCK.base.
+ * regexp string whose program provably cannot match from the call's offset
+ * (_yr_scan_verify_re_match, scan.c:778-880): hex strings' fast-exec programs
+ * (yr_re_fast_exec, re.c:2150-2391) are decided exactly as a reachability
+ * question; other regexps' yr_re_exec programs (re.c:1693-2072) over an
+ * over-approximation (locale-dependent classes, assertions and repeat counts
+ * unconstrained) with a 1000-step search budget below RE_MAX_FIBERS, so calls
+ * that could fail with ERROR_TOO_MANY_RE_FIBERS are always kept.  Base64
+ * strings are always kept.  Kept calls are verified by re.c / scan.c on the
+ * host.  data_base = YR_MEMORY_BLOCK.base.  After yr_amd_scan_window, a call
+ * whose bytes are not all in the window is kept (never decided on missing
+ * bytes).
  * On success *d_records is a DEVICE pointer owned by the scanner (valid until
- * its next verify) to *count records.  Synchronous.
+ * its next verify) to *count records.  Synchronous.  The record's candidate
+ * field is a 32-bit index: a candidate stream of 2^32 or more (root-accepting
+ * rules on a block >= 4 GiB) returns YR_AMD_INVALID_ARGUMENT.
  * Requires yr_amd_tables_set_strings; YR_AMD_INVALID_ARGUMENT otherwise.
  */
 int yr_amd_verify_device(

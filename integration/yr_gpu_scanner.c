@@ -542,7 +542,18 @@ int yr_gpu_scanner_scan_mem_blocks(
           {});
     }
 
-    if (!gs->preverify)
+    /* Pre-verification takes candidate streams below 2^32 (yr_amd_verify_device):
+     * a root-accepting rule set on a block of 4 GiB or more makes every
+     * position a candidate, so that block is replayed from the GPU scan's
+     * stream instead -- after the blocks still in flight, in order. */
+    int replay_block = !gs->preverify ||
+                       (scanner->rules->ac_match_table[0] != 0 && block->size >= 0xFFFFFFFFull);
+    while (replay_block && gs->inflight > 0)
+    {
+      result = _replay_next(scanner, gs);
+      if (result != ERROR_SUCCESS) goto _exit;
+    }
+    if (replay_block)
       result = _yr_gpu_scan_mem_block(scanner, gs, data, block);
     else if (gs->direct)
       result = _direct_block(scanner, gs, data, block);

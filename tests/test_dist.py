@@ -19,18 +19,17 @@ from yara_amd import dist as ydist
 
 
 def _shard_candidates(tab, data, begin, end):
-    lo, halo = ydist.local_window(begin, end)
-    cand = oracle.candidates(tab, data[lo:end])
-    keep = cand[cand > halo] if begin > 0 else cand   # position 0 only on rank 0
-    return keep.astype(np.int64) + lo
+    lo, _ = ydist.shard_window(len(data), begin, end)
+    cand = oracle.candidates(tab, data[lo:end]).astype(np.int64) + lo
+    return cand[cand > begin] if begin > 0 else cand   # position 0 only on rank 0
 
 
 def _worker(rank, world, port, n, period, q, no_gather=False):
     os.environ["MASTER_ADDR"] = "127.0.0.1"
     os.environ["MASTER_PORT"] = str(port)
     dist.init_process_group("gloo", rank=rank, world_size=world)
-    if no_gather:                      # the all_gather fallback of gather_positions
-        ydist._GATHER_OK = False
+    if no_gather:                      # the all_gather path of gather_rows
+        ydist._gather_backend = lambda group: "all_gather"
     try:
         import planted
         import gen_rules
@@ -40,9 +39,15 @@ def _worker(rank, world, port, n, period, q, no_gather=False):
         b, e = ydist.shard_bounds(n, world, rank, align=period)
         local = torch.from_numpy(_shard_candidates(tab, data, b, e))
         out = ydist.gather_positions(local)
+        # two-column rows (the records path: {offset, pool index})
+        rows = torch.stack([local, local * 3 + rank], 1)
+        out2 = ydist.gather_rows(rows)
         if rank == 0:
             full = oracle.candidates(tab, data).astype(np.int64)
-            q.put(bool(np.array_equal(out.numpy(), full)) and out.numel() > 0)
+            ok = bool(np.array_equal(out.numpy(), full)) and out.numel() > 0
+            ok &= tuple(out2.shape) == (full.size, 2)
+            ok &= bool(np.array_equal(out2[:, 0].numpy(), full))
+            q.put(ok)
     finally:
         dist.destroy_process_group()
 
@@ -72,3 +77,16 @@ def test_shard_bounds_cover_block():
                 assert b == prev and b % 16 == 0 and e >= b
                 prev = e
             assert prev == n
+
+
+def test_shard_window_halos():
+    n = 10 << 20
+    # candidates only: 4-byte warm-up, 16-aligned
+    assert ydist.shard_window(n, 0, 1 << 20) == (0, 1 << 20)
+    assert ydist.shard_window(n, 1 << 20, 2 << 20) == ((1 << 20) - 16, 2 << 20)
+    # verification-complete: halos before/after, clipped to the block
+    lo, hi = ydist.shard_window(n, 1 << 20, 2 << 20, 4096 + 16, 4096)
+    assert lo % 16 == 0 and lo <= (1 << 20) - 4096 - 16 and hi == (2 << 20) + 4096
+    assert ydist.shard_window(n, 9 << 20, n, 5000, 5000) == (((9 << 20) - 5000) // 16 * 16, n)
+    with pytest.raises(ValueError):
+        ydist.shard_window(n, 5, 4)

@@ -236,3 +236,57 @@ def test_full_size_against_reference(case):
     assert yara_amd.replay(dev_tables(rec["rules"]), host, pos, allp, verify) == 0
     assert len(P) == rec["verify_count"]
     assert oracle.verify_stream_sha(np.array(P, np.uint64), np.array(K, np.uint32)) == rec["verify_sha"]
+
+
+def test_scan_window_holds_only_the_window():
+    """yr_amd_scan_window: the device holds just [lo, hi) of the block (a
+    shard + halo, the multi-GPU layout); candidates equal the whole block's in
+    (begin, end], and pre-verification records equal the whole block's for the
+    same candidates when the window includes the tables' verify halos."""
+    torch = _torch()
+    from yara_amd import dist as ydist
+    rec = CASES["lit_1M"]
+    data = case_data(rec)
+    n = data.size
+    t = yara_amd.Tables.from_npz(tables_npz("lit"), device=0, strings=True)
+    full = yara_amd.Scanner(t).verify_calls(data)
+    full_pos, _ = yara_amd.Scanner(t).candidates(data)
+    before, after = ydist.tables_halos(t)
+    assert before >= 4096 and after >= 4096
+    sc = yara_amd.Scanner(t)
+    for begin, end in [(0, 300000), (300000, 700000), (700000, n), (123456 // 16 * 16, 123456 // 16 * 16)]:
+        for halo in ((4, 0), (before, after)):
+            lo, hi = ydist.shard_window(n, begin, end, *halo)
+            win = torch.empty(max(hi - lo, 16), dtype=torch.uint8, device="cuda")
+            win[:hi - lo] = torch.from_numpy(data[lo:hi].copy()).cuda()
+            torch.cuda.synchronize()
+            sc.scan_window(win.data_ptr(), lo, hi, n, begin, end)
+            ptr, cnt, _ = sc.device_result()
+            pos = _d2h(torch, ptr, cnt)
+            sel = (full_pos > begin) & (full_pos <= end) if begin else (full_pos <= end)
+            np.testing.assert_array_equal(pos, full_pos[sel])
+            if halo[0] == before:
+                p, c = sc.verify_device(0)
+                got = np.zeros(c, dtype=yara_amd._lib.VERIFY_REC_DTYPE)
+                if c:
+                    from yara_amd._hip import memcpy
+                    memcpy(got.ctypes.data, p, c * 16, 2)
+                i = full["offset"] + t._bt[full["pool_index"]]
+                fsel = (i > begin) & (i <= end) if begin else (i <= end)
+                np.testing.assert_array_equal(got["offset"], full["offset"][fsel])
+                np.testing.assert_array_equal(got["pool_index"], full["pool_index"][fsel])
+
+
+def test_scan_window_rejects_bad_windows():
+    torch = _torch()
+    t = dev_tables("C")
+    sc = yara_amd.Scanner(t)
+    d = torch.zeros(1 << 16, dtype=torch.uint8, device="cuda")
+    bad = [(16, 1 << 16, 1 << 20, 16, 1024),      # warm-up before byte 16 not held
+           (0, 1 << 16, 1 << 20, 0, (1 << 16) + 16),  # scan past the window
+           (8, 1 << 16, 1 << 20, 32, 64),          # window_begin not 16-aligned
+           (0, 1 << 21, 1 << 20, 0, 64)]           # window past the block
+    for args in bad:
+        with pytest.raises(yara_amd.YaraAmdError) as e:
+            sc.scan_window(d.data_ptr(), *args)
+        assert e.value.code == yara_amd.INVALID_ARGUMENT

@@ -263,6 +263,14 @@ class Scanner:
                    _lib.lib().yr_amd_scan_device(self._h, ctypes.c_void_p(d_ptr), block_size,
                                                  byte_begin, byte_end))
 
+    def scan_window(self, d_ptr: int, window_begin: int, window_end: int, block_size: int,
+                    byte_begin: int, byte_end: int):
+        """Scan [byte_begin, byte_end) of a block of which the device holds only
+        bytes [window_begin, window_end) at d_ptr (yr_amd_scan_window: shards)."""
+        _lib.check("yr_amd_scan_window",
+                   _lib.lib().yr_amd_scan_window(self._h, ctypes.c_void_p(d_ptr), window_begin,
+                                                 window_end, block_size, byte_begin, byte_end))
+
     def device_result(self):
         """(device pointer to uint64 positions, count, all_positions)."""
         p = ctypes.c_void_p()

@@ -42,6 +42,9 @@ class TablesInfo(ctypes.Structure):
         ("filter_bits", ctypes.c_uint32),
         ("filter_set_bits", ctypes.c_uint32),
         ("exact_slots", ctypes.c_uint32),
+        ("max_backtrack", ctypes.c_uint32),
+        ("verify_halo_before", ctypes.c_uint64),
+        ("verify_halo_after", ctypes.c_uint64),
     ]
 
 
@@ -71,6 +74,8 @@ PROTOTYPES = {
     "yr_amd_scan_block": (_int, [_vp, _u8p, ctypes.c_size_t, ctypes.POINTER(_u64p),
                                  ctypes.POINTER(ctypes.c_uint64), ctypes.POINTER(_int)]),
     "yr_amd_scan_device": (_int, [_vp, _vp, ctypes.c_uint64, ctypes.c_uint64, ctypes.c_uint64]),
+    "yr_amd_scan_window": (_int, [_vp, _vp, ctypes.c_uint64, ctypes.c_uint64, ctypes.c_uint64,
+                                  ctypes.c_uint64, ctypes.c_uint64]),
     "yr_amd_scan_device_result": (_int, [_vp, ctypes.POINTER(_vp), ctypes.POINTER(ctypes.c_uint64),
                                          ctypes.POINTER(_int)]),
     "yr_amd_replay": (_int, [_vp, _u8p, ctypes.c_size_t, _u64p, ctypes.c_uint64, _int, VERIFY_FN,

@@ -627,7 +627,9 @@ __device__ __forceinline__ void scan_segment(const ScanParams& p, WaveQueue& q, 
   st.seg_len = (uint32_t)(seg_end - st.seg_start);
   st.out = p.seg_out + (p.seg_base ? p.seg_base[seg] : (size_t)seg * p.seg_cap);
   st.found = 0;
-  const uint64_t avail = p.block_size - st.seg_start;
+  // bytes read: [seg_start - 4, seg_end) only -- never past byte_end, so a
+  // shard that holds just its window of the block is never read beyond it
+  const uint64_t avail = p.byte_end - st.seg_start;
   const uint8_t* base = p.data + st.seg_start;
 
   // 4 bytes before the segment (warm-up halo); zeros before the block start.

@@ -94,6 +94,7 @@ struct yr_amd_tables {
   DevRe* d_re = nullptr;          // yr_amd_tables_set_re_code
   uint8_t* d_re_code = nullptr;
   std::vector<uint32_t> h_str_flags, h_pool_string;   // host copies (validation)
+  uint64_t max_str_bytes = 0;     // max over strings of the bytes a comparison reads
 };
 
 struct yr_amd_scanner {
@@ -117,8 +118,9 @@ struct yr_amd_scanner {
 
   std::vector<uint64_t> h_positions;
 
-  // state of the last yr_amd_scan_device
+  // state of the last yr_amd_scan_window / yr_amd_scan_device
   ScanParams last{};
+  uint64_t win_lo = 0, win_hi = 0;      // bytes of the block present in HBM
   int last_grid = 0;
   bool last_all = false;
   bool last_empty = false;
@@ -287,6 +289,17 @@ int yr_amd_tables_get_info(const yr_amd_tables* t, yr_amd_tables_info* info) {
   info->filter_bits = kFilterLog2Bits;
   info->filter_set_bits = f.filter_set_bits;
   info->exact_slots = 4 * (f.t3_mask + 1 + f.t4_mask + 1);
+  uint32_t mb = 0;
+  for (uint16_t b : f.pool_backtrack) mb = std::max<uint32_t>(mb, b);
+  info->max_backtrack = mb;
+  // a shard's verify window (yr_amd_scan_window + yr_amd_verify_device):
+  // candidates i in (begin, end] make calls at offsets >= begin + 1 - max
+  // backtrack whose reads reach YR_RE_SCAN_LIMIT further back, and at offsets
+  // <= end whose reads reach max(YR_RE_SCAN_LIMIT, 2 * string length) forward
+  // (verify.hip call_matters); without strings only the 4-byte warm-up
+  info->verify_halo_before = t->has_strings ? mb + (uint64_t)kReScanLimit : YR_AMD_MAX_ATOM_LENGTH;
+  info->verify_halo_after =
+      t->has_strings ? std::max<uint64_t>((uint64_t)kReScanLimit, t->max_str_bytes) : 0;
   return YR_AMD_SUCCESS;
 }
 
@@ -368,12 +381,31 @@ int yr_amd_scanner_kernel_ms(yr_amd_scanner* s, float* ms) {
 
 int yr_amd_scan_device(yr_amd_scanner* s, const uint8_t* d_data, uint64_t block_size,
                        uint64_t byte_begin, uint64_t byte_end) {
-  if (s == nullptr || byte_begin > byte_end || byte_end > block_size) return YR_AMD_INVALID_ARGUMENT;
-  if ((byte_begin & 15) != 0 || (((uintptr_t)d_data) & 15) != 0) return YR_AMD_INVALID_ARGUMENT;
+  return yr_amd_scan_window(s, d_data, 0, block_size, block_size, byte_begin, byte_end);
+}
+
+int yr_amd_scan_window(yr_amd_scanner* s, const uint8_t* d_window, uint64_t window_begin,
+                       uint64_t window_end, uint64_t block_size, uint64_t byte_begin,
+                       uint64_t byte_end) {
+  if (s == nullptr || byte_begin > byte_end || byte_end > window_end ||
+      window_begin > window_end || window_end > block_size)
+    return YR_AMD_INVALID_ARGUMENT;
+  // the 4-byte warm-up before byte_begin must be in the window
+  if (byte_begin - std::min<uint64_t>(byte_begin, YR_AMD_MAX_ATOM_LENGTH) < window_begin)
+    return YR_AMD_INVALID_ARGUMENT;
+  if ((byte_begin & 15) != 0 || (window_begin & 15) != 0 || (((uintptr_t)d_window) & 15) != 0)
+    return YR_AMD_INVALID_ARGUMENT;
   const yr_amd_tables* t = s->tables;
   s->pending = true;
   s->last_count = 0;
   s->ev_valid = false;
+  s->win_lo = window_begin;
+  s->win_hi = window_end;
+  // the kernels address the block by its own positions: position p of the
+  // block is d_window[p - window_begin] (only [window_begin, window_end) is
+  // ever read, kernels.hip scan_segment / verify.hip call_matters)
+  const uint8_t* d_data =
+      d_window == nullptr ? nullptr : (const uint8_t*)((uintptr_t)d_window - (uintptr_t)window_begin);
   s->last.data = d_data;
   s->last.block_size = block_size;
   s->last.byte_begin = byte_begin;
@@ -381,7 +413,7 @@ int yr_amd_scan_device(yr_amd_scanner* s, const uint8_t* d_data, uint64_t block_
   s->last_all = t->flat.root_accepting;
   s->last_empty = s->last_all || byte_end == byte_begin;
   if (s->last_empty) return YR_AMD_SUCCESS;
-  if (d_data == nullptr) return YR_AMD_INVALID_ARGUMENT;
+  if (d_window == nullptr) return YR_AMD_INVALID_ARGUMENT;
   HIP_TRY(hipSetDevice(t->device));
 
   const uint64_t nbytes = byte_end - byte_begin;
@@ -536,7 +568,10 @@ int yr_amd_tables_set_strings(yr_amd_tables* t, const uint32_t* pool_string, uin
   if (r) return r;   // partial uploads are freed with the tables
   t->h_pool_string.assign(pool_string, pool_string + n_pool);
   t->h_str_flags.resize(n_strings);
-  for (uint32_t k = 0; k < n_strings; ++k) t->h_str_flags[k] = strings[k].flags;
+  for (uint32_t k = 0; k < n_strings; ++k) {
+    t->h_str_flags[k] = strings[k].flags;
+    t->max_str_bytes = std::max<uint64_t>(t->max_str_bytes, 2ull * strings[k].length);
+  }
   t->has_strings = true;
   return YR_AMD_SUCCESS;
 }
@@ -617,6 +652,8 @@ int yr_amd_verify_device(yr_amd_scanner* s, uint64_t data_base, const yr_amd_ver
   VerifyParams v{};
   v.data = L.data;
   v.size = L.block_size;
+  v.win_lo = s->win_lo;
+  v.win_hi = s->win_hi;
   v.data_base = data_base;
   v.all = s->last_all ? 1 : 0;
   if (v.all) {
@@ -639,6 +676,11 @@ int yr_amd_verify_device(yr_amd_scanner* s, uint64_t data_base, const yr_amd_ver
   v.re = t->d_re;
   v.re_code = t->d_re_code;
   uint64_t total = 0;
+  // records carry a 32-bit candidate index, and the launch is one thread per
+  // candidate: a candidate stream of 2^32 or more (a root-accepting rule set
+  // on a block of 4 GiB or more) is refused -- replay it on the host
+  // (yr_amd_scan_block + yr_amd_replay) instead
+  if (v.count >= 0xFFFFFFFFull) return YR_AMD_INVALID_ARGUMENT;
   if (v.count > 0) {
     if (v.data == nullptr) return YR_AMD_INVALID_ARGUMENT;
     int r = grow(s->d_vcount, s->vcount_cap, v.count);
@@ -664,7 +706,9 @@ int yr_amd_verify_device(yr_amd_scanner* s, uint64_t data_base, const yr_amd_ver
     HIP_TRY(hipStreamSynchronize(s->stream));
     total = s->h_summary[0];
     if (total > v.out_cap) {
-      r = grow(s->d_vrec, s->vrec_cap, total);
+      // geometric growth: a scanner whose record counts creep upward re-runs
+      // the write pass O(log) times, not once per call
+      r = grow(s->d_vrec, s->vrec_cap, std::max<uint64_t>(total, 2 * s->vrec_cap));
       if (r) return r;
       v.out = s->d_vrec;
       v.out_cap = s->vrec_cap;

@@ -48,8 +48,9 @@ struct VerifyRec {
 };
 
 struct VerifyParams {
-  const uint8_t* data;        // block in HBM
+  const uint8_t* data;        // block in HBM (position 0; only [win_lo, win_hi) is read)
   uint64_t size;              // block size
+  uint64_t win_lo, win_hi;    // the bytes of the block present in HBM (yr_amd_scan_window)
   uint64_t data_base;         // YR_MEMORY_BLOCK.base (fixed-offset strings)
   const uint64_t* positions;  // ascending candidates (unused when all)
   uint64_t count;             // candidates (size + 1 when all)

@@ -108,7 +108,8 @@ __device__ __forceinline__ ByteWindow stage_window(const VerifyParams& p, const 
                                                    bool backwards, uint32_t lds) {
   const uint8_t* s = backwards ? start - 32 : start;
   const uint8_t* lo = reinterpret_cast<const uint8_t*>((uintptr_t)s & ~(uintptr_t)15);
-  if (lds == 0xFFFFFFFFu || lo < p.data || lo + kWinBytes > p.data + p.size) return {nullptr, lds};
+  if (lds == 0xFFFFFFFFu || lo < p.data + p.win_lo || lo + kWinBytes > p.data + p.win_hi)
+    return {nullptr, lds};
   typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
   const u32x4* g = reinterpret_cast<const u32x4*>(lo);
   const u32x4 a = g[0], b = g[1], c = g[2];
@@ -459,10 +460,24 @@ __device__ bool call_matters(const VerifyParams& p, uint32_t k, uint64_t offset,
   // scan.c:1023-1025
   if ((st.flags & kStrFixedOffset) && st.fixed_offset != (int64_t)(p.data_base + offset))
     return false;
+  if ((st.flags & (kStrLiteral | kStrFitsInAtom)) == (kStrLiteral | kStrFitsInAtom) &&
+      !(st.flags & kStrUnmodelled))
+    return p.pool_backtrack[k] != 0;   // scan.c:907-915: decided without reading data
+  // Every byte the call may read lies in [offset - YR_RE_SCAN_LIMIT, offset +
+  // max(YR_RE_SCAN_LIMIT, 2 * length)) (regexp scans are limited to
+  // YR_RE_SCAN_LIMIT each way, re.c:1753-1760, :2172-2174; a wide literal compares 2 * length
+  // bytes).  A shard holding only [win_lo, win_hi) of the block keeps a call
+  // whose bytes are not all there (a shard sized with the tables' verify halo,
+  // yr_amd_tables_info, never does).
+  if (p.win_lo != 0 || p.win_hi != p.size) {
+    const uint64_t need_lo = offset - min<uint64_t>(offset, (uint64_t)kReScanLimit);
+    const uint64_t need_hi =
+        min<uint64_t>(p.size, offset + max<uint64_t>((uint64_t)kReScanLimit, 2ull * st.length));
+    if (need_lo < p.win_lo || need_hi > p.win_hi) return true;
+  }
   if (!(st.flags & kStrLiteral)) return re_call_matters(p, k, st.flags, offset, lds);
   if (st.flags & kStrUnmodelled) return true;            // conservative
   // _yr_scan_verify_literal_match, scan.c:907-972
-  if (st.flags & kStrFitsInAtom) return p.pool_backtrack[k] != 0;
   const uint8_t* d = p.data + offset;
   const uint64_t avail = p.size - offset;
   const uint8_t* s = p.str_bytes + st.bytes_off;

@@ -2,18 +2,29 @@
 
 One process per GPU (torch.distributed, backend "nccl" = RCCL over xGMI).  Rank
 r owns the byte range [begin_r, end_r) of the block -- i.e. candidate positions
-(begin_r, end_r] -- and reads up to YR_MAX_ATOM_LENGTH bytes before begin_r as
-warm-up (libyara's trie is at most 4 deep, limits.h:68), so no data-path
-exchange is needed.  The only collective is the final gather of the per-rank
-candidate lists to rank 0; concatenated in rank order they are exactly the
-full block's ascending candidate stream.
+(begin_r, end_r] (rank 0 also position 0) -- and holds a WINDOW of the block
+around it in HBM:
+
+  * candidates only: 4 bytes before begin_r (libyara's trie is at most 4 deep,
+    limits.h:68, so the walk restarts exactly there);
+  * verification-complete (the default): the tables' verify halos
+    (yr_amd_tables_info: max backtrack + YR_RE_SCAN_LIMIT before, max(
+    YR_RE_SCAN_LIMIT, 2 x longest string) after), so yr_amd_verify_device
+    decides every verify call of the rank's candidates exactly as on the whole
+    block (literal comparisons, regexp scans of up to 4096 bytes each way,
+    limits.h:162-163).
+
+yr_amd_scan_window addresses the window by block positions, so candidates and
+records come out block-global.  No data-path exchange; the only collective is
+the final gather to rank 0 of either the candidate lists or the pre-verified
+{offset, pool index} records (every verify call that can have an effect, the
+rest dropped on the device), concatenated in rank order = exactly the whole
+block's stream.
 """
 import torch
 import torch.distributed as dist
 
-# halo kept in front of a shard: >= YR_MAX_ATOM_LENGTH (4) and a multiple of 16
-# so the shard's first byte stays 16-byte aligned for the scan kernel
-HALO = 16
+WARMUP = 4        # YR_MAX_ATOM_LENGTH
 
 
 def shard_bounds(n: int, world: int, rank: int, align: int = 1 << 20):
@@ -29,48 +40,78 @@ def shard_bounds(n: int, world: int, rank: int, align: int = 1 << 20):
     return begin, end
 
 
-def local_window(begin: int, end: int):
-    """(first byte a rank must hold, byte offset of its shard inside it)."""
-    halo = min(HALO, begin)
-    return begin - halo, halo
+def shard_window(n: int, begin: int, end: int, halo_before: int = WARMUP, halo_after: int = 0):
+    """[lo, hi): the bytes of the block a rank holds for the shard [begin, end):
+    halo_before bytes in front (lo rounded down to 16 for the kernels'
+    alignment), halo_after behind, clipped to the block."""
+    if not 0 <= begin <= end <= n:
+        raise ValueError("bad shard")
+    lo = max(0, begin - max(halo_before, WARMUP)) // 16 * 16
+    hi = min(n, end + halo_after)
+    return lo, hi
 
 
-def gather_positions(local: torch.Tensor, group=None, dst: int = 0):
-    """Gather every rank's ascending int64 candidate positions to `dst`.
+def tables_halos(tables):
+    """(halo_before, halo_after) a verification-complete shard needs
+    (yr_amd_tables_get_info)."""
+    info = tables.info()
+    return int(info["verify_halo_before"]), int(info["verify_halo_after"])
 
-    all_gather of the counts, then one padded gather (payloads are KB-MB, far
-    below what the xGMI links move per microsecond).  Returns the rank-ordered
-    concatenation on `dst`, None elsewhere.
-    """
+
+def _gather_backend(group):
+    """Gather strategy, chosen from the backend up front (every rank takes the
+    same branch, so no rank is left waiting in a collective another abandoned):
+    nccl (RCCL) and gloo implement gather; anything else all-gathers."""
+    return "gather" if dist.get_backend(group) in ("nccl", "gloo") else "all_gather"
+
+
+def gather_rows(local: torch.Tensor, group=None, dst: int = 0):
+    """Gather every rank's int64 rows [m_r, w] to `dst`: all_gather of the
+    counts, one padded gather (payloads are KB-MB, far below what the xGMI
+    links move per microsecond).  Returns the rank-ordered concatenation on
+    `dst`, None elsewhere."""
+    if local.dim() != 2 or local.dtype != torch.int64:
+        raise ValueError("rows must be a 2-d int64 tensor")
     world = dist.get_world_size(group)
     rank = dist.get_rank(group)
     if dist.get_backend(group) == "gloo":
         local = local.cpu()                  # gloo collectives run on host tensors
-    n = torch.tensor([local.numel()], dtype=torch.int64, device=local.device)
+    w = local.shape[1]
+    n = torch.tensor([local.shape[0]], dtype=torch.int64, device=local.device)
     counts_t = torch.empty(world, dtype=torch.int64, device=local.device)
     dist.all_gather_into_tensor(counts_t, n, group=group)
     counts = counts_t.tolist()               # one host sync for all ranks' counts
     width = max(max(counts), 1)
-    if local.numel() == width:
+    if local.shape[0] == width:
         padded = local.contiguous()
     else:
-        padded = torch.empty((width,), dtype=torch.int64, device=local.device)
-        padded[:local.numel()] = local
-        padded[local.numel():] = -1
-    global _GATHER_OK
-    if _GATHER_OK:
+        padded = torch.full((width, w), -1, dtype=torch.int64, device=local.device)
+        padded[:local.shape[0]] = local
+    if _gather_backend(group) == "gather":
         bufs = [torch.empty_like(padded) for _ in range(world)] if rank == dst else None
-        try:
-            dist.gather(padded, bufs, dst=dst, group=group)
-        except RuntimeError:   # a backend without gather: every rank takes the same branch
-            _GATHER_OK = False
-    if not _GATHER_OK:
-        flat = torch.empty(world * width, dtype=torch.int64, device=local.device)
+        dist.gather(padded, bufs, dst=dst, group=group)
+    else:
+        flat = torch.empty((world * width, w), dtype=torch.int64, device=local.device)
         dist.all_gather_into_tensor(flat, padded, group=group)
-        bufs = list(flat.view(world, width))
+        bufs = list(flat.view(world, width, w))
     if rank != dst:
         return None
     return torch.cat([b[:c] for b, c in zip(bufs, counts)])
 
 
-_GATHER_OK = True
+def gather_positions(local: torch.Tensor, group=None, dst: int = 0):
+    """Gather every rank's ascending int64 candidate positions to `dst`."""
+    out = gather_rows(local.reshape(-1, 1).to(torch.int64), group, dst)
+    return None if out is None else out.reshape(-1)
+
+
+def records_to_rows(d_records: int, count: int, device) -> torch.Tensor:
+    """Device yr_amd_verify_rec[count] -> int64 rows [count, 2] = {offset,
+    pool index} (the record's 32-bit candidate index is local to the shard's
+    stream and dropped)."""
+    from ._hip import memcpy
+    rows = torch.empty((max(count, 1), 2), dtype=torch.int64, device=device)
+    memcpy(rows.data_ptr(), d_records, count * 16, 3)      # D2D, 16 B per record
+    rows = rows[:count]
+    rows[:, 1] &= 0xFFFFFFFF
+    return rows
