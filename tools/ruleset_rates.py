@@ -1,0 +1,88 @@
+"""Scan-kernel and pre-verification times of many rule-set shapes on the same
+device-resident input (SURVEY.md §8d data generator, seed 1).
+
+For each rule set: the scan kernel's HIP-event time (median of --reps after a
+warm-up), the candidate count, the filter's pass rate, and the on-device
+pre-verification time and record count.  Root-accepting sets make every
+position a candidate; their verify pass is limited to blocks below 2^32
+candidates, so they run on --root-gib.
+
+    python tools/ruleset_rates.py [--gib 4] [--sets short,rx,...] > rates.json
+"""
+import argparse
+import json
+import os
+import statistics
+import sys
+import time
+
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, REPO)
+HBM_PEAK_GBS = 8000.0
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gib", type=float, default=4.0)
+    ap.add_argument("--root-gib", type=float, default=1.0)
+    ap.add_argument("--sets", default="C,B,E,lit,hex,rx,short,fuzz0,fuzz3,fuzz7,root")
+    ap.add_argument("--reps", type=int, default=10)
+    ap.add_argument("--no-verify", action="store_true")
+    a = ap.parse_args()
+    import torch
+    import yara_amd
+    n_max = int(a.gib * (1 << 30))
+    buf = torch.empty(n_max + 16, dtype=torch.uint8, device="cuda")
+    yara_amd.fill_xorshift64(buf.data_ptr(), n_max, 1)
+    torch.cuda.synchronize()
+    out = {}
+    for name in a.sets.split(","):
+        t = yara_amd.Tables.from_npz(os.path.join(REPO, "tests", "golden", "tables", name + ".npz"),
+                                     device=0, strings=True)
+        info = t.info()
+        n = int(a.root_gib * (1 << 30)) if info["root_accepting"] else n_max
+        sc = yara_amd.Scanner(t)
+        for _ in range(5):
+            sc.scan_device(buf.data_ptr(), n)
+            sc.device_result()
+        rec = {"bytes": n}
+        if info["root_accepting"]:
+            # every position is a candidate: no scan kernel runs at all
+            rec.update({"kernel_ms": 0.0, "candidates": n + 1})
+        else:
+            sc.set_timing(True)
+            ks, cnt = [], 0
+            for _ in range(a.reps):
+                sc.scan_device(buf.data_ptr(), n)
+                cnt = sc.device_result()[1]
+                ks.append(sc.kernel_ms())
+            sc.set_timing(False)
+            k = statistics.median(ks)
+            rec.update({"kernel_ms": round(k, 4), "GB/s": round(n / (k * 1e-3) / 1e9, 1),
+                        "frac": round(n / (k * 1e-3) / 1e9 / HBM_PEAK_GBS, 4),
+                        "candidates": int(cnt)})
+        rec.update({"root_accepting": bool(info["root_accepting"]),
+               "keys_by_length": info["keys_by_length"],
+               "filter_fill": round(info["filter_set_bits"] / float(1 << info["filter_bits"]), 4)})
+        if not a.no_verify:
+            sc.scan_device(buf.data_ptr(), n)
+            sc.device_result()
+            sc.verify_device(0)
+            vs = []
+            for _ in range(3):
+                sc.scan_device(buf.data_ptr(), n)
+                sc.device_result()
+                torch.cuda.synchronize()
+                t0 = time.perf_counter()
+                _, nrec = sc.verify_device(0)
+                vs.append((time.perf_counter() - t0) * 1e3)
+            rec["verify_ms"] = round(statistics.median(vs), 3)
+            rec["records"] = int(nrec)
+        out[name] = rec
+        print(name, rec, file=sys.stderr, flush=True)
+        del sc, t
+    print(json.dumps(out, indent=1))
+
+
+if __name__ == "__main__":
+    main()
