@@ -210,6 +210,16 @@ static int run(YR_RULES* rules, YR_GPU_SCANNER* gs, const uint8_t* data, size_t 
   if (getenv("E2E_TIMEOUT")) yr_scanner_set_timeout(sc, atoi(getenv("E2E_TIMEOUT")));
   c->abort_after = getenv("E2E_ABORT") ? atoi(getenv("E2E_ABORT")) : 0;
   yr_scanner_set_callback(sc, cb, c);
+#ifdef E2E_BLOCK_SCANNER
+  /* libyara patched with integration/libyara-block-scanner.patch: the GPU
+   * side runs through libyara's OWN entry points, the block scanner attached */
+  if (gs != NULL)
+  {
+    r = yr_gpu_scanner_attach(sc, gs);
+    if (r) return r;
+    gs = NULL;
+  }
+#endif
   double t0 = now();
   if (strcmp(g_mode, "file") == 0 && c->rules != NULL && data == NULL)
   {

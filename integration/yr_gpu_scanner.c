@@ -20,6 +20,11 @@
  * as in the reference, by yr_execute_code (exec.c:418) and the rule-report
  * loop (scanner.c:524-556).  scan_file / scan_fd / scan_proc wrap it exactly
  * like scanner.c:674-722.
+ *
+ * Built with -DYR_HAVE_BLOCK_SCANNER against a libyara patched with
+ * integration/libyara-block-scanner.patch, it also provides
+ * yr_gpu_scanner_attach(): the patched libyara's own driver then calls the
+ * per-block replacement here, and the re-hosted driver above is not needed.
  */
 #include "yr_gpu_scanner.h"
 
@@ -57,6 +62,9 @@ struct YR_GPU_SCANNER
   uint32_t depth;
   uint32_t inflight;
   int direct;            /* single in-memory block (scan_mem): no staging copy */
+#ifdef YR_HAVE_BLOCK_SCANNER
+  YR_BLOCK_SCANNER block_scanner; /* yr_gpu_scanner_attach */
+#endif
 };
 
 /* Length (incl. MATCH) of a linear fast-exec program (the opcodes
@@ -465,6 +473,78 @@ static int _direct_block(
   return result;
 }
 
+/* One block: the replacement of the walk at scanner.c:493-496. */
+static int _scan_one_block(
+    YR_SCANNER* scanner,
+    YR_GPU_SCANNER* gs,
+    const uint8_t* data,
+    YR_MEMORY_BLOCK* block)
+{
+  /* Pre-verification takes candidate streams below 2^32 (yr_amd_verify_device):
+   * a root-accepting rule set on a block of 4 GiB or more makes every
+   * position a candidate, so that block is replayed from the GPU scan's
+   * stream instead -- after the blocks still in flight, in order. */
+  int replay_block = !gs->preverify ||
+                     (scanner->rules->ac_match_table[0] != 0 && block->size >= 0xFFFFFFFFull);
+  while (replay_block && gs->inflight > 0)
+    FAIL_ON_ERROR(_replay_next(scanner, gs));
+  if (replay_block) return _yr_gpu_scan_mem_block(scanner, gs, data, block);
+  if (gs->direct) return _direct_block(scanner, gs, data, block);
+  return _pipeline_block(scanner, gs, data, block);
+}
+
+/* The blocks still on the GPU, in order (after the iterator's last block). */
+static int _finish_blocks(YR_SCANNER* scanner, YR_GPU_SCANNER* gs)
+{
+  while (gs->inflight > 0) FAIL_ON_ERROR(_replay_next(scanner, gs));
+  return ERROR_SUCCESS;
+}
+
+static void _abort_blocks(YR_GPU_SCANNER* gs)
+{
+  if (gs->inflight > 0)
+  {
+    yr_amd_pipeline_drain(gs->pipe);
+    gs->inflight = 0;
+  }
+}
+
+#ifdef YR_HAVE_BLOCK_SCANNER
+/* With libyara patched by integration/libyara-block-scanner.patch, the
+ * unmodified driver (yr_scanner_scan_mem_blocks and every entry point above
+ * it) calls these in place of its CPU walk. */
+static int _bs_scan_block(
+    void* ctx,
+    YR_SCANNER* scanner,
+    const uint8_t* data,
+    YR_MEMORY_BLOCK* block)
+{
+  return _scan_one_block(scanner, (YR_GPU_SCANNER*) ctx, data, block);
+}
+
+static int _bs_finish(void* ctx, YR_SCANNER* scanner)
+{
+  return _finish_blocks(scanner, (YR_GPU_SCANNER*) ctx);
+}
+
+static void _bs_abort(void* ctx, YR_SCANNER* scanner)
+{
+  (void) scanner;
+  _abort_blocks((YR_GPU_SCANNER*) ctx);
+}
+
+int yr_gpu_scanner_attach(YR_SCANNER* scanner, YR_GPU_SCANNER* gs)
+{
+  if (gs->gpu_rules->rules != scanner->rules) return ERROR_INVALID_ARGUMENT;
+  gs->block_scanner.scan_block = _bs_scan_block;
+  gs->block_scanner.finish = _bs_finish;
+  gs->block_scanner.abort = _bs_abort;
+  gs->block_scanner.ctx = gs;
+  yr_scanner_set_block_scanner(scanner, &gs->block_scanner);
+  return ERROR_SUCCESS;
+}
+#endif
+
 /* _yr_scanner_clean_matches (scanner.c:178-203) is static: same memsets. */
 static void _clean_matches(YR_SCANNER* scanner)
 {
@@ -542,33 +622,13 @@ int yr_gpu_scanner_scan_mem_blocks(
           {});
     }
 
-    /* Pre-verification takes candidate streams below 2^32 (yr_amd_verify_device):
-     * a root-accepting rule set on a block of 4 GiB or more makes every
-     * position a candidate, so that block is replayed from the GPU scan's
-     * stream instead -- after the blocks still in flight, in order. */
-    int replay_block = !gs->preverify ||
-                       (scanner->rules->ac_match_table[0] != 0 && block->size >= 0xFFFFFFFFull);
-    while (replay_block && gs->inflight > 0)
-    {
-      result = _replay_next(scanner, gs);
-      if (result != ERROR_SUCCESS) goto _exit;
-    }
-    if (replay_block)
-      result = _yr_gpu_scan_mem_block(scanner, gs, data, block);
-    else if (gs->direct)
-      result = _direct_block(scanner, gs, data, block);
-    else
-      result = _pipeline_block(scanner, gs, data, block);
+    result = _scan_one_block(scanner, gs, data, block);
     if (result != ERROR_SUCCESS) goto _exit;
     block = iterator->next(iterator);
   }
 
-  /* the blocks still on the GPU, in order */
-  while (gs->inflight > 0)
-  {
-    result = _replay_next(scanner, gs);
-    if (result != ERROR_SUCCESS) goto _exit;
-  }
+  result = _finish_blocks(scanner, gs);
+  if (result != ERROR_SUCCESS) goto _exit;
 
   result = iterator->last_error;
   if (result != ERROR_SUCCESS) goto _exit;
@@ -614,11 +674,7 @@ int yr_gpu_scanner_scan_mem_blocks(
   scanner->callback(scanner, CALLBACK_MSG_SCAN_FINISHED, NULL, scanner->user_data);
 
 _exit:
-  if (gs->inflight > 0)
-  {
-    yr_amd_pipeline_drain(gs->pipe);
-    gs->inflight = 0;
-  }
+  _abort_blocks(gs);
   if (result != ERROR_BLOCK_NOT_READY)
   {
     _clean_matches(scanner);

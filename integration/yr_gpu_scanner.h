@@ -40,6 +40,14 @@ int yr_gpu_scanner_scan_mem(
     const uint8_t* buffer,
     size_t buffer_size);
 
+#ifdef YR_HAVE_BLOCK_SCANNER
+/* libyara patched with integration/libyara-block-scanner.patch: make the
+ * scanner's own driver (yr_scanner_scan_mem / _mem_blocks / _file / _fd /
+ * _proc, yr_rules_* above them) use the GPU for every block.  gs must be
+ * created on the scanner's rules; one gs per scanner. */
+int yr_gpu_scanner_attach(YR_SCANNER* scanner, YR_GPU_SCANNER* gs);
+#endif
+
 /* ... and of yr_scanner_scan_file / _fd / _proc (scanner.c:674-722). */
 int yr_gpu_scanner_scan_file(YR_SCANNER* scanner, YR_GPU_SCANNER* gs, const char* filename);
 int yr_gpu_scanner_scan_fd(YR_SCANNER* scanner, YR_GPU_SCANNER* gs, YR_FILE_DESCRIPTOR fd);

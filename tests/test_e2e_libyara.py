@@ -24,6 +24,9 @@ from conftest import ALPHA, GOLDEN, REPO
 pytestmark = pytest.mark.gpu
 
 CHECK = os.path.join(REPO, "integration", "_build", "e2e_check")
+# the same checker built against libyara + integration/libyara-block-scanner.patch:
+# its GPU side calls libyara's OWN yr_scanner_scan_* with the block scanner attached
+CHECK_HOOK = os.path.join(REPO, "integration", "_build", "e2e_check_hook")
 needs_check = pytest.mark.skipif(not os.path.exists(CHECK),
                                  reason="integration/_build/e2e_check not built "
                                         "(needs the reference headers at build time)")
@@ -38,8 +41,8 @@ def _rules_file(tmp_path, name):
     return str(p)
 
 
-def _run(rules, data_spec, block=0, overlap=0, preverify=True, mode="mem", **extra):
-    cmd = [CHECK, rules, data_spec] + ([str(block), str(overlap)] if block else [])
+def _run(rules, data_spec, block=0, overlap=0, preverify=True, mode="mem", check=None, **extra):
+    cmd = [check or CHECK, rules, data_spec] + ([str(block), str(overlap)] if block else [])
     env = dict(os.environ, E2E_PREVERIFY="1" if preverify else "0", E2E_MODE=mode, **extra)
     r = subprocess.run(cmd, capture_output=True, text=True, timeout=600, env=env)
     assert r.stdout, r.stderr
@@ -235,3 +238,51 @@ def test_threads_share_one_gpu_rules(tmp_path, rules, block):
     assert res["threads"] == 6 and res["threads_ok"], res
     assert res["same_matches"] and res["matches_stock"] > 0, res
     assert rc == 0
+
+
+needs_hook = pytest.mark.skipif(not os.path.exists(CHECK_HOOK),
+                                reason="integration/_build/e2e_check_hook not built "
+                                       "(oracle/refpatch.mk needs the reference tree)")
+
+
+@needs_hook
+@pytest.mark.parametrize("mode,block", [("mem", 0), ("mem", 65536), ("file", 0), ("fd", 0),
+                                        ("proc", 0), ("truncmap", 0)])
+@pytest.mark.parametrize("rules", ["lit", "rx", "C"])
+def test_patched_libyara_block_scanner(tmp_path, rules, mode, block):
+    """libyara patched with integration/libyara-block-scanner.patch: the GPU
+    scanner attached with yr_gpu_scanner_attach, the scan made through
+    libyara's own yr_scanner_scan_mem / _mem_blocks / _file / _fd / _proc.
+    Match sets and rule reports equal the same library's CPU walk (no block
+    scanner attached = stock behaviour)."""
+    rf = _rules_file(tmp_path, rules)
+    if rules == "lit":
+        buf = planted.lit_buffer(oracle.xorshift, 4 << 20, 13)
+    elif rules == "rx":
+        buf = planted.rx_buffer(oracle.xorshift, 4 << 20, 19)
+    else:
+        buf = planted.planted_buffer(oracle.xorshift, gen_rules.gen("C"), 4 << 20, 3)
+    spec = _data_file(tmp_path, buf, "d.bin")
+    rc, res = _run(rf, spec, block, 100 if block else 0, mode=mode, check=CHECK_HOOK)
+    if mode == "proc" and res["rc_stock"] != 0:
+        pytest.skip("process memory not readable here (rc %d)" % res["rc_stock"])
+    if mode == "truncmap":
+        assert res["rc_stock"] == 4 and res["rc_gpu"] == 4, res
+        return
+    assert res["rc_stock"] == 0 and res["rc_gpu"] == 0, res
+    assert res["same_matches"] and res["same_rule_reports"] and res["matches_stock"] > 0, res
+    assert rc == 0
+
+
+@needs_hook
+def test_patched_libyara_timeout_and_threads(tmp_path):
+    short = _rules_file(tmp_path, "short")
+    spec = _alpha_file(tmp_path, 16 << 20)
+    rc, res = _run(short, spec, 1 << 20, 64, check=CHECK_HOOK, E2E_TIMEOUT="1",
+                   E2E_SLEEP_TOO_MANY="1200")
+    assert res["rc_stock"] == 26 and res["rc_gpu"] == 26, res
+    rf = _rules_file(tmp_path, "C")
+    buf = planted.planted_buffer(oracle.xorshift, gen_rules.gen("C"), 4 << 20, 3)
+    rc, res = _run(rf, _data_file(tmp_path, buf, "d.bin"), check=CHECK_HOOK, E2E_THREADS="4",
+                   E2E_THREAD_REPS="2")
+    assert res["threads_ok"] and res["same_matches"], res
