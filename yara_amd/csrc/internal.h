@@ -115,6 +115,17 @@ __host__ __device__ inline uint32_t bucket_hash2(uint32_t key) {
   return h ^ (h >> 13);
 }
 
+// Accepting trie nodes by string, for the pre-verification kernels (one
+// uint32 array): [0, 256) head of the 1-byte node b (0 = none), [256, 65792)
+// head of the 2-byte node (little endian), then two-choice bucketed tables of
+// the 3- and 4-byte nodes, 2 entries {key, head} per 16-byte bucket (3-byte
+// keys carry 1 << 24; 0 = empty; the 4-byte node 0x00000000 sits in word
+// kNodeZero4).  head = M[slot], the 1-based pool index of the node's list.
+constexpr uint32_t kNodeL1 = 0;
+constexpr uint32_t kNodeL2 = 256;
+constexpr uint32_t kNodeZero4 = 256 + 65536;
+constexpr uint32_t kNodeHeadWords = kNodeZero4 + 4;   // (keeps the buckets 16-B aligned)
+
 struct ScanParams {
   const uint8_t* data;      // block base in HBM (16-byte aligned)
   uint64_t block_size;      // bytes in the block

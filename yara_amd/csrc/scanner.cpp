@@ -83,16 +83,12 @@ struct yr_amd_tables {
 
   // on-device literal pre-verification (yr_amd_tables_set_strings)
   bool has_strings = false;
-  uint32_t* d_T = nullptr;
-  uint32_t* d_M = nullptr;
-  uint32_t* d_pool_next = nullptr;
-  uint16_t* d_pool_backtrack = nullptr;
-  uint32_t* d_pool_string = nullptr;
-  DevString* d_strings = nullptr;
+  uint32_t* d_nodes = nullptr;        // accepting nodes by string (FlatTables::nodes)
+  DevPoolRec* d_pool = nullptr;       // per pool entry: link, backtrack, string, programs
   uint8_t* d_str_bytes = nullptr;
   uint8_t* d_lowercase = nullptr;
-  DevRe* d_re = nullptr;          // yr_amd_tables_set_re_code
-  uint8_t* d_re_code = nullptr;
+  uint8_t* d_re_code = nullptr;       // yr_amd_tables_set_re_code
+  std::vector<DevPoolRec> h_pool;     // host copy of the records (set_re_code fills .re)
   std::vector<uint32_t> h_str_flags, h_pool_string;   // host copies (validation)
   uint64_t max_str_bytes = 0;     // max over strings of the bytes a comparison reads
 };
@@ -264,10 +260,8 @@ int yr_amd_tables_create(const uint32_t* transition_table, const uint32_t* match
 
 int yr_amd_tables_destroy(yr_amd_tables* t) {
   if (t == nullptr) return YR_AMD_SUCCESS;
-  for (void* p : {(void*)t->d_filter, (void*)t->d_exact, (void*)t->d_T, (void*)t->d_M,
-                  (void*)t->d_pool_next, (void*)t->d_pool_backtrack, (void*)t->d_pool_string,
-                  (void*)t->d_strings, (void*)t->d_str_bytes, (void*)t->d_lowercase,
-                  (void*)t->d_re, (void*)t->d_re_code})
+  for (void* p : {(void*)t->d_filter, (void*)t->d_exact, (void*)t->d_nodes, (void*)t->d_pool,
+                  (void*)t->d_str_bytes, (void*)t->d_lowercase, (void*)t->d_re_code})
     if (p) (void)hipFree(p);
   delete t;
   return YR_AMD_SUCCESS;
@@ -546,23 +540,30 @@ int yr_amd_tables_set_strings(yr_amd_tables* t, const uint32_t* pool_string, uin
     return YR_AMD_INVALID_ARGUMENT;
   for (uint32_t k = 0; k < n_pool; ++k)
     if (pool_string[k] >= n_strings) return YR_AMD_INVALID_ARGUMENT;
-  std::vector<DevString> ds(n_strings);
   for (uint32_t k = 0; k < n_strings; ++k) {
     const yr_amd_string& x = strings[k];
     if (x.bytes_offset > n_bytes || x.length > n_bytes - x.bytes_offset)
       return YR_AMD_INVALID_ARGUMENT;
-    ds[k] = DevString{x.flags, x.length, x.fixed_offset, x.bytes_offset};
   }
   if (t->device < 0) return YR_AMD_INVALID_ARGUMENT;   // device feature
-  HIP_TRY(hipSetDevice(t->device));
   const FlatTables& f = t->flat;
+  // one record per pool entry with its string's fields (verify.h DevPoolRec)
+  t->h_pool.assign(n_pool, DevPoolRec{});
+  for (uint32_t k = 0; k < n_pool; ++k) {
+    const yr_amd_string& x = strings[pool_string[k]];
+    DevPoolRec& e = t->h_pool[k];
+    e.next = f.pool_next[k];
+    e.backtrack = f.pool_backtrack[k];
+    e.flags = x.flags;
+    e.length = x.length;
+    e.fixed_offset = x.fixed_offset;
+    e.bytes_off = x.bytes_offset;
+    e.re = DevRe{0, 0, 0, 0};
+  }
+  HIP_TRY(hipSetDevice(t->device));
   int r = YR_AMD_SUCCESS;
-  if (!r) r = upload(t->d_T, f.T.data(), f.T.size());
-  if (!r) r = upload(t->d_M, f.M.data(), f.M.size());
-  if (!r) r = upload(t->d_pool_next, f.pool_next.data(), f.pool_next.size());
-  if (!r) r = upload(t->d_pool_backtrack, f.pool_backtrack.data(), f.pool_backtrack.size());
-  if (!r) r = upload(t->d_pool_string, pool_string, n_pool);
-  if (!r) r = upload(t->d_strings, ds.data(), ds.size());
+  if (!r) r = upload(t->d_nodes, f.nodes.data(), f.nodes.size());
+  if (!r) r = upload(t->d_pool, t->h_pool.data(), t->h_pool.size());
   if (!r) r = upload(t->d_str_bytes, bytes, n_bytes);
   if (!r) r = upload(t->d_lowercase, lowercase, 256);
   if (r) return r;   // partial uploads are freed with the tables
@@ -611,8 +612,7 @@ int yr_amd_re_code_extent(const uint8_t* code, uint64_t avail, uint32_t* extent)
 int yr_amd_tables_set_re_code(yr_amd_tables* t, uint32_t n_pool, const uint32_t* fwd_off,
                               const uint32_t* fwd_len, const uint32_t* bwd_off,
                               const uint32_t* bwd_len, const uint8_t* code, uint64_t code_len) {
-  if (t == nullptr || !t->has_strings || t->d_re != nullptr || t->d_re_code != nullptr)
-    return YR_AMD_INVALID_ARGUMENT;
+  if (t == nullptr || !t->has_strings || t->d_re_code != nullptr) return YR_AMD_INVALID_ARGUMENT;
   if (n_pool != t->flat.pool_next.size()) return YR_AMD_INVALID_ARGUMENT;
   if (n_pool > 0 && (fwd_off == nullptr || fwd_len == nullptr || bwd_off == nullptr ||
                      bwd_len == nullptr))
@@ -639,8 +639,13 @@ int yr_amd_tables_set_re_code(yr_amd_tables* t, uint32_t n_pool, const uint32_t*
   }
   HIP_TRY(hipSetDevice(t->device));
   int r = upload(t->d_re_code, code, (size_t)code_len);
-  if (!r) r = upload(t->d_re, re.data(), re.size());
-  return r;
+  if (r) return r;
+  // the programs go into the pool records (uploaded again)
+  for (uint32_t k = 0; k < n_pool; ++k) t->h_pool[k].re = re[k];
+  if (n_pool > 0 && hipMemcpy(t->d_pool, t->h_pool.data(), n_pool * sizeof(DevPoolRec),
+                              hipMemcpyHostToDevice) != hipSuccess)
+    return YR_AMD_INTERNAL_FATAL_ERROR;
+  return YR_AMD_SUCCESS;
 }
 
 int yr_amd_verify_device(yr_amd_scanner* s, uint64_t data_base, const yr_amd_verify_rec** d_records,
@@ -665,15 +670,17 @@ int yr_amd_verify_device(yr_amd_scanner* s, uint64_t data_base, const yr_amd_ver
     v.positions = s->d_positions;
     v.count = s->last_count;
   }
-  v.T = t->d_T;
-  v.M = t->d_M;
-  v.pool_next = t->d_pool_next;
-  v.pool_backtrack = t->d_pool_backtrack;
-  v.pool_string = t->d_pool_string;
-  v.strings = t->d_strings;
+  const FlatTables& f = t->flat;
+  v.nodes = t->d_nodes;
+  v.n3_off = f.n3_off;
+  v.n3_mask = f.n3_mask;
+  v.n4_off = f.n4_off;
+  v.n4_mask = f.n4_mask;
+  v.root_head = f.M[0];
+  v.pool = t->d_pool;
   v.str_bytes = t->d_str_bytes;
   v.lowercase = t->d_lowercase;
-  v.re = t->d_re;
+  v.re_on = t->d_re_code != nullptr ? 1 : 0;
   v.re_code = t->d_re_code;
   uint64_t total = 0;
   // records carry a 32-bit candidate index, and the launch is one thread per
@@ -694,7 +701,7 @@ int yr_amd_verify_device(yr_amd_scanner* s, uint64_t data_base, const yr_amd_ver
     if (r) return r;
     v.counts = s->d_vcount;
     v.keep = s->d_vkeep;
-    v.states = s->d_vkeep + v.count;
+    v.heads = s->d_vkeep + v.count;
     v.block_off = s->d_vblock;
     v.out = s->d_vrec;
     v.out_cap = s->vrec_cap;

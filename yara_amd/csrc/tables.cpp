@@ -22,6 +22,7 @@
 #include <string.h>
 
 #include <unordered_map>
+#include <utility>
 
 #include "../../include/yara_amd.h"
 #include "internal.h"
@@ -76,6 +77,48 @@ bool build_bucket_table(const std::vector<uint32_t>& keys, std::vector<uint32_t>
         }
       }
       if (!placed) { ok = false; break; }
+    }
+    if (ok) {
+      n_buckets = nb;
+      return true;
+    }
+  }
+  return false;
+}
+
+// Two-choice, 2-way bucketed cuckoo table of {key, value} pairs (non-zero
+// keys): 4 words per bucket, load <= 1/4 to start, doubled until it fits.
+bool build_pair_table(const std::vector<uint32_t>& keys, const std::vector<uint32_t>& vals,
+                      std::vector<uint32_t>& table, uint32_t& n_buckets) {
+  uint32_t nb = 4;
+  while (nb * 2 < 4 * keys.size()) nb <<= 1;
+  for (; nb <= (1u << 26); nb <<= 1) {
+    table.assign((size_t)nb * 4, 0u);
+    uint32_t rng = 0x9E3779B9u;
+    bool ok = true;
+    for (size_t i = 0; i < keys.size() && ok; ++i) {
+      uint32_t key = keys[i], val = vals[i];
+      bool placed = false;
+      for (int kick = 0; kick < 512 && !placed; ++kick) {
+        const uint32_t b[2] = {bucket_hash1(key) & (nb - 1), bucket_hash2(key) & (nb - 1)};
+        for (int c = 0; c < 2 && !placed; ++c)
+          for (int e = 0; e < 2; ++e) {
+            uint32_t* slot = &table[(size_t)b[c] * 4 + 2 * e];
+            if (slot[0] == 0 || slot[0] == key) {
+              slot[0] = key;
+              slot[1] = val;
+              placed = true;
+              break;
+            }
+          }
+        if (!placed) {
+          rng ^= rng << 13; rng ^= rng >> 17; rng ^= rng << 5;
+          uint32_t* victim = &table[(size_t)b[rng & 1] * 4 + 2 * ((rng >> 1) & 1)];
+          std::swap(victim[0], key);
+          std::swap(victim[1], val);
+        }
+      }
+      ok = placed;
     }
     if (ok) {
       n_buckets = nb;
@@ -166,6 +209,34 @@ int flatten_tables(const uint32_t* T, const uint32_t* M, uint32_t n_slots,
     if (M[n.slot] != 0) out.accepting++;
   }
   out.root_accepting = M[0] != 0;
+
+  // accepting nodes by string (pre-verification, internal.h kNode*)
+  {
+    out.nodes.assign(kNodeHeadWords, 0u);
+    std::vector<uint32_t> k3, v3, k4, v4;
+    for (const Node& n : nodes) {
+      const uint32_t head = M[n.slot];
+      if (n.depth == 0 || head == 0) continue;
+      switch (n.depth) {
+        case 1: out.nodes[kNodeL1 + n.bytes] = head; break;
+        case 2: out.nodes[kNodeL2 + n.bytes] = head; break;
+        case 3: k3.push_back(n.bytes | (1u << 24)); v3.push_back(head); break;
+        default:
+          if (n.bytes == 0) out.nodes[kNodeZero4] = head;
+          else { k4.push_back(n.bytes); v4.push_back(head); }
+      }
+    }
+    std::vector<uint32_t> t3, t4;
+    uint32_t nb3 = 0, nb4 = 0;
+    if (!build_pair_table(k3, v3, t3, nb3) || !build_pair_table(k4, v4, t4, nb4))
+      return YR_AMD_INTERNAL_FATAL_ERROR;
+    out.n3_off = (uint32_t)out.nodes.size();
+    out.n3_mask = nb3 - 1;
+    out.nodes.insert(out.nodes.end(), t3.begin(), t3.end());
+    out.n4_off = (uint32_t)out.nodes.size();
+    out.n4_mask = nb4 - 1;
+    out.nodes.insert(out.nodes.end(), t4.begin(), t4.end());
+  }
 
   // 2. minimal accepting strings; verify monotonicity along true failure links
   for (const Node& n : nodes) {

@@ -31,6 +31,13 @@ struct FlatTables {
   std::vector<uint32_t> exact;     // exact key sets (internal.h layout)
   uint32_t t3_off = 0, t3_mask = 0, t4_off = 0, t4_mask = 0, exact_flags = 0;
   uint32_t len_mask = 0;
+
+  // accepting trie nodes -> match-list head M[slot], by the node's string
+  // (pre-verification: the walk's state at a candidate is its longest
+  // accepting suffix, found with independent probes instead of 4 dependent
+  // transitions; internal.h node_* layout)
+  std::vector<uint32_t> nodes;
+  uint32_t n3_off = 0, n3_mask = 0, n4_off = 0, n4_mask = 0;
 };
 
 // Returns a YR_AMD_* error code.

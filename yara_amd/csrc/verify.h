@@ -33,12 +33,20 @@ constexpr uint8_t kReAny = 0xA0, kReLiteral = 0xA2, kReMaskedLiteral = 0xA4, kRe
                   kReNotLiteral = 0xAE, kReMaskedNotLiteral = 0xAF, kReRepeatAnyUngreedy = 0xB5;
 constexpr int kReScanLimit = 4096;   // YR_RE_SCAN_LIMIT (limits.h:163)
 
-struct DevString {
-  uint32_t flags;
-  uint32_t length;
-  int64_t fixed_offset;
-  uint64_t bytes_off;   // into the string byte blob
+// One pool entry (YR_AC_MATCH, types.h:324-344) with everything a verify call
+// reads about it -- list link, backtrack, its YR_STRING's fields, its regexp
+// programs -- in one 48-byte record, so walking a list costs one memory round
+// trip per entry (three independent 16-byte loads).
+struct DevPoolRec {
+  uint32_t next;          // 1-based pool index of ac_match_pool[k].next, 0 = end
+  uint32_t backtrack;
+  uint32_t flags;         // YR_STRING.flags
+  uint32_t length;        // YR_STRING.length
+  int64_t fixed_offset;   // YR_STRING.fixed_offset
+  uint64_t bytes_off;     // YR_STRING.string in the byte blob
+  DevRe re;               // regexp programs (fwd_len 0: none)
 };
+static_assert(sizeof(DevPoolRec) == 48, "pool record layout");
 
 // Same layout as yr_amd_verify_rec (include/yara_amd.h).
 struct VerifyRec {
@@ -56,21 +64,19 @@ struct VerifyParams {
   uint64_t count;             // candidates (size + 1 when all)
   int all;                    // every position of a range is a candidate:
   uint64_t all_first;         //   i = all_first + c
-  const uint32_t* T;          // ac_transition_table
-  const uint32_t* M;          // ac_match_table
-  const uint32_t* pool_next;  // 1-based, 0 = end
-  const uint16_t* pool_backtrack;
-  const uint32_t* pool_string;
-  const DevString* strings;
+  const uint32_t* nodes;      // accepting trie nodes by string (internal.h kNode*)
+  uint32_t n3_off, n3_mask, n4_off, n4_mask;
+  uint32_t root_head;         // ac_match_table[0]
+  const DevPoolRec* pool;     // per pool entry
   const uint8_t* str_bytes;
   const uint8_t* lowercase;   // the host's yr_lowercase[256]
-  const DevRe* re;            // per pool entry, or null (no regex decisions)
+  int re_on;                  // regexp programs attached (else every regexp call is kept)
   const uint8_t* re_code;
   uint32_t* counts;           // [count] records per candidate (pass 0)
   uint32_t* keep;             // [count] pass 0's decisions for pass 1: bit t = the t-th
                               // entry of the candidate's list is kept (t < 31); bit 31 =
                               // the list is longer, pass 1 decides again
-  uint32_t* states;           // [count] the candidate's AC state (pass 0)
+  uint32_t* heads;            // [count] the candidate's match-list head M[state] (pass 0)
   uint64_t* block_off;        // [verify_blocks(count)] pass 0: records per 256-candidate
                               // block; then (launch_block_offsets) exclusive offsets
   VerifyRec* out;             // records (pass 1)

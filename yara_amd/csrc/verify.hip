@@ -29,17 +29,51 @@
 
 namespace yamd {
 
-// libyara/scanner.c:124-141 (the transition rule; T resident in L2).
-__device__ __forceinline__ uint32_t dev_ac_step(const uint32_t* __restrict__ T, uint32_t state,
-                                                uint32_t byte) {
-  const uint32_t index = byte + 1;
-  uint32_t t = T[state + index];
-  while ((t & 0x1FFu) != index) {
-    if (state == 0) return 0;
-    state = T[state] >> 9;
-    t = T[state + index];
+// The match-list head of the walk's state at candidate position i
+// (libyara/scanner.c:98, :144: ac_match_table[state]).  The trie is at most 4
+// deep (limits.h:68), so the state after data[0..i) is the longest suffix of
+// data[i-4..i) that is a trie node; at a candidate that node accepts, and so
+// it is the longest ACCEPTING suffix (acceptance is monotone along suffixes,
+// tables.cpp).  The four suffixes are looked up in the accepting-node tables
+// (internal.h kNode*) with independent loads -- one memory round trip instead
+// of four dependent transitions (scanner.c:124-141).  No accepting suffix:
+// the root (a root-accepting rule set, every position a candidate).
+__device__ __forceinline__ bool node_bucket_get(const uint4& b, uint32_t key, uint32_t& head) {
+  if (b.x == key) { head = b.y; return true; }
+  if (b.z == key) { head = b.w; return true; }
+  return false;
+}
+__device__ __forceinline__ uint32_t node_head(const VerifyParams& p, uint64_t i) {
+  const uint32_t n = i < 4 ? (uint32_t)i : 4u;
+  uint32_t w = 0;   // data[i-n .. i), oldest byte lowest, at the top (bytes i-4.. i-1)
+#pragma unroll
+  for (uint32_t j = 0; j < 4; ++j)
+    if (j < n) w |= (uint32_t)p.data[i - n + j] << (8 * (4 - n + j));
+  const uint32_t k1 = w >> 24, k2 = w >> 16, k3 = (w >> 8) | (1u << 24), k4 = w;
+  const uint32_t* __restrict__ t = p.nodes;
+  const uint32_t h1 = n >= 1 ? t[kNodeL1 + k1] : 0u;
+  const uint32_t h2 = n >= 2 ? t[kNodeL2 + k2] : 0u;
+  uint4 a3 = make_uint4(0, 0, 0, 0), b3 = a3, a4 = a3, b4 = a3;
+  if (n >= 3) {
+    a3 = *reinterpret_cast<const uint4*>(t + p.n3_off + (bucket_hash1(k3) & p.n3_mask) * 4);
+    b3 = *reinterpret_cast<const uint4*>(t + p.n3_off + (bucket_hash2(k3) & p.n3_mask) * 4);
   }
-  return t >> 9;
+  if (n >= 4 && k4 != 0) {
+    a4 = *reinterpret_cast<const uint4*>(t + p.n4_off + (bucket_hash1(k4) & p.n4_mask) * 4);
+    b4 = *reinterpret_cast<const uint4*>(t + p.n4_off + (bucket_hash2(k4) & p.n4_mask) * 4);
+  }
+  uint32_t head;
+  if (n >= 4) {
+    if (k4 == 0) {
+      if (t[kNodeZero4]) return t[kNodeZero4];
+    } else if (node_bucket_get(a4, k4, head) || node_bucket_get(b4, k4, head)) {
+      return head;
+    }
+  }
+  if (n >= 3 && (node_bucket_get(a3, k3, head) || node_bucket_get(b3, k3, head))) return head;
+  if (h2) return h2;
+  if (h1) return h1;
+  return p.root_head;
 }
 
 // _yr_scan_compare / _yr_scan_icompare (scan.c:142-179): forward match length
@@ -404,11 +438,11 @@ __device__ int general_re_reachable(const uint8_t* __restrict__ code, uint32_t l
 // forward program from `offset` must reach MATCH (else forward_matches == -1:
 // return), a zero-length forward match needs a backward program, and with a
 // backward program its MATCHes are the only way to _yr_scan_match_callback.
-__device__ bool re_call_matters(const VerifyParams& p, uint32_t k, uint32_t flags,
+__device__ bool re_call_matters(const VerifyParams& p, const DevPoolRec& e, uint32_t flags,
                                 uint64_t offset, uint32_t lds) {
   if (YAMD_VERIFY_DIAG == 2) return true;
-  if (p.re == nullptr) return true;
-  const DevRe r = p.re[k];
+  if (!p.re_on) return true;
+  const DevRe r = e.re;
   if (r.fwd_len == 0) return true;
   const uint8_t* d = p.data + offset;
   const uint8_t* fwd = p.re_code + r.fwd_off;
@@ -452,17 +486,17 @@ __device__ bool re_call_matters(const VerifyParams& p, uint32_t k, uint32_t flag
 // Does yr_scan_verify_match(ctx, &pool[k], data, size, base, offset) possibly
 // have an effect?  false only where the reference provably returns without
 // touching the context.
-__device__ bool call_matters(const VerifyParams& p, uint32_t k, uint64_t offset, uint32_t lds) {
+__device__ bool call_matters(const VerifyParams& p, const DevPoolRec& st, uint64_t offset,
+                             uint32_t lds) {
   if (YAMD_VERIFY_DIAG == 1) return false;
   // scan.c:1013: data_size - offset <= 0 (size_t) <=> offset == size
   if (offset >= p.size) return false;
-  const DevString st = p.strings[p.pool_string[k]];
   // scan.c:1023-1025
   if ((st.flags & kStrFixedOffset) && st.fixed_offset != (int64_t)(p.data_base + offset))
     return false;
   if ((st.flags & (kStrLiteral | kStrFitsInAtom)) == (kStrLiteral | kStrFitsInAtom) &&
       !(st.flags & kStrUnmodelled))
-    return p.pool_backtrack[k] != 0;   // scan.c:907-915: decided without reading data
+    return st.backtrack != 0;   // scan.c:907-915: decided without reading data
   // Every byte the call may read lies in [offset - YR_RE_SCAN_LIMIT, offset +
   // max(YR_RE_SCAN_LIMIT, 2 * length)) (regexp scans are limited to
   // YR_RE_SCAN_LIMIT each way, re.c:1753-1760, :2172-2174; a wide literal compares 2 * length
@@ -475,7 +509,7 @@ __device__ bool call_matters(const VerifyParams& p, uint32_t k, uint64_t offset,
         min<uint64_t>(p.size, offset + max<uint64_t>((uint64_t)kReScanLimit, 2ull * st.length));
     if (need_lo < p.win_lo || need_hi > p.win_hi) return true;
   }
-  if (!(st.flags & kStrLiteral)) return re_call_matters(p, k, st.flags, offset, lds);
+  if (!(st.flags & kStrLiteral)) return re_call_matters(p, st, st.flags, offset, lds);
   if (st.flags & kStrUnmodelled) return true;            // conservative
   // _yr_scan_verify_literal_match, scan.c:907-972
   const uint8_t* d = p.data + offset;
@@ -503,26 +537,28 @@ __device__ bool call_matters(const VerifyParams& p, uint32_t k, uint64_t offset,
 constexpr uint32_t kKeepOverflow = 1u << 31;
 template <int PASS>
 __device__ __forceinline__ void verify_one(const VerifyParams& p, uint64_t c, uint32_t lds,
-                                           uint32_t keep, uint32_t state, uint64_t o,
+                                           uint32_t keep, uint32_t head, uint64_t o,
                                            uint32_t& count) {
   const uint64_t i = p.all ? p.all_first + c : p.positions[c];
-  if (!PASS)
-    for (uint64_t j = i > 4 ? i - 4 : 0; j < i; ++j) state = dev_ac_step(p.T, state, p.data[j]);
+  if (!PASS) head = node_head(p, i);
   const bool decide = !PASS || (keep & kKeepOverflow);
   uint32_t n = 0, t = 0, mask = 0;
   // scanner.c:105-121: the list of state_i in pool order
-  for (uint32_t k = p.M[state]; k != 0; k = p.pool_next[k - 1], ++t) {
-    const uint32_t bt = p.pool_backtrack[k - 1];
+  for (uint32_t k = head; k != 0; ++t) {
+    const DevPoolRec e = p.pool[k - 1];
+    const uint32_t bt = e.backtrack;
     bool kept;
     if (decide)
-      kept = bt <= i && call_matters(p, k - 1, i - bt, lds);
+      kept = bt <= i && call_matters(p, e, i - bt, lds);
     else
       kept = t < 31 && ((keep >> t) & 1u);
+    const uint32_t kk = k;
+    k = e.next;
     if (!kept) continue;
     if (PASS) {
       VerifyRec r;
       r.offset = i - bt;
-      r.pool_index = k - 1;
+      r.pool_index = kk - 1;
       r.candidate = (uint32_t)c;
       if (o < p.out_cap) p.out[o] = r;
       ++o;
@@ -534,7 +570,7 @@ __device__ __forceinline__ void verify_one(const VerifyParams& p, uint64_t c, ui
   if (!PASS) {
     p.counts[c] = n;
     p.keep[c] = n == 0 ? 0u : (t > 31 ? kKeepOverflow : mask);
-    p.states[c] = state;
+    p.heads[c] = head;
   }
   count = n;
 }
@@ -585,7 +621,7 @@ __global__ __launch_bounds__(256) void verify_kernel(VerifyParams p) {
   n = keep == 0 ? 0u : p.counts[c];
   const uint32_t pre = block_exclusive_scan(n, wsum, total);
   if (total == 0 || keep == 0) return;
-  verify_one<1>(p, c, lds, keep, p.states[c], p.block_off[blockIdx.x] + pre, n);
+  verify_one<1>(p, c, lds, keep, p.heads[c], p.block_off[blockIdx.x] + pre, n);
 }
 
 // Exclusive scan, in place, of the per-block record counts (one workgroup),
