@@ -369,17 +369,47 @@ static int re_sz(uint8_t op)
   return 0;
 }
 
-static int general_reachable(const uint8_t* code, uint32_t len, const uint8_t* input,
-                             uint64_t avail, int backwards, int wide, int nocase, int dotall,
-                             const uint8_t* lower)
+/* _yr_re_is_word_char (re.c:114-122) with yr_isalnum (strutils.c:240-244) */
+static int re_is_word(const uint8_t* ch, int cs)
 {
-  struct { int32_t ip; int b, j, jmax, step; } st[16];
-  int sp = 0;
+  uint8_t c = ch[0];
+  int w = (c >= 0x30 && c <= 0x39) || (c >= 0x41 && c <= 0x5a) || (c >= 0x61 && c <= 0x7a) ||
+          c == '_';
+  return cs == 2 ? (w && ch[1] == 0) : w;
+}
+
+/*
+ * yr_re_exec (re.c:1693-2072) as "can some path reach MATCH": every opcode
+ * with the reference's semantics -- character tests incl. \w \s \d, the
+ * prolog, REPEAT_ANY ranges whose repeated characters pass ANY's test, counted
+ * REPEAT_START/END loops with the fiber's counter stack (re.c:1533-1582), the
+ * \b \B ^ $ assertions (re.c:1937-1981), both SPLIT branches.  Returns 0 (no
+ * path), 1 (a path), 2 (budget of 1000 steps / 16 choices / 4 nested loops
+ * exceeded, or unknown code: keep the call).  fwd/bwd = the input sizes
+ * yr_re_exec receives (data_size - offset, offset; scan.c:820-876).
+ */
+static int general_reachable(const uint8_t* code, uint32_t len, const uint8_t* input,
+                             uint64_t fwd, uint64_t bwd, int backwards, int wide, int nocase,
+                             int dotall, const uint8_t* lower)
+{
+  struct { int32_t ip; int b, j, jmax, step, sp; uint16_t cnt[4]; } st[16];
+  int csp = 0;
   int cs = wide ? 2 : 1;
+  uint64_t avail = backwards ? bwd : fwd;
   int maxb = (int) (avail < RE_SCAN_LIMIT ? avail : RE_SCAN_LIMIT);
   maxb -= maxb % cs;
   int32_t ip = 0;
-  int b = 0;
+  int b = 0, sp = -1;
+  uint16_t cnt[4] = {0, 0, 0, 0};
+#define AT(bb) (backwards ? input - cs - (bb) : input + (bb))
+#define PUSH(cip, cb, cj, cjmax, cstep)                                   \
+  do {                                                                  \
+    if (csp == 16) return 2;                                            \
+    st[csp].ip = (cip); st[csp].b = (cb); st[csp].j = (cj);             \
+    st[csp].jmax = (cjmax); st[csp].step = (cstep); st[csp].sp = sp;    \
+    memcpy(st[csp].cnt, cnt, sizeof cnt);                               \
+    csp++;                                                              \
+  } while (0)
   for (int steps = 0; steps < 1000; steps++)
   {
     if (ip < 0 || (uint32_t) ip >= len) return 2;
@@ -389,9 +419,7 @@ static int general_reachable(const uint8_t* code, uint32_t len, const uint8_t* i
     if (op == 0xC2) { ip += (int16_t) (code[ip + 1] | (code[ip + 2] << 8)); continue; }
     if (op == 0xC0 || op == 0xC1)
     {
-      if (sp == 16) return 2;
-      st[sp].ip = ip + (int16_t) (code[ip + 2] | (code[ip + 3] << 8));
-      st[sp].b = b; st[sp].j = 0; st[sp].jmax = 0; st[sp].step = 0; sp++;
+      PUSH(ip + (int16_t) (code[ip + 2] | (code[ip + 3] << 8)), b, 0, 0, 0);
       ip += 4;
       continue;
     }
@@ -399,31 +427,64 @@ static int general_reachable(const uint8_t* code, uint32_t len, const uint8_t* i
     {
       int32_t off = (int32_t) ((uint32_t) code[ip + 5] | ((uint32_t) code[ip + 6] << 8) |
                                ((uint32_t) code[ip + 7] << 16) | ((uint32_t) code[ip + 8] << 24));
-      int is_start = op == 0xC3 || op == 0xC5;
-      int min0 = (code[ip + 1] | (code[ip + 2] << 8)) == 0;
-      if (!is_start || min0)
+      int mn = code[ip + 1] | (code[ip + 2] << 8), mx = code[ip + 3] | (code[ip + 4] << 8);
+      if (op == 0xC3 || op == 0xC5)   /* REPEAT_START, re.c:1533-1553 */
       {
-        if (sp == 16) return 2;
-        st[sp].ip = ip + off; st[sp].b = b; st[sp].j = 0; st[sp].jmax = 0; st[sp].step = 0; sp++;
+        if (mn == 0) PUSH(ip + off, b, 0, 0, 0);
+        if (sp + 1 >= 4) return 2;
+        cnt[++sp] = 0;
+        ip += 9;
+        continue;
       }
+      /* REPEAT_END, re.c:1555-1582 */
+      if (sp < 0) return 2;
+      cnt[sp]++;
+      if (cnt[sp] < mn) { ip += off; continue; }
+      if (cnt[sp] < mx) PUSH(ip + off, b, 0, 0, 0);
+      sp--;
       ip += 9;
       continue;
     }
-    if (op >= 0xB0 && op <= 0xB3) { ip += 1; continue; }
-    if (op == 0xB4 || op == 0xB5)
+    if (op == 0xB2 || op == 0xB3)   /* \b \B, re.c:1937-1965 */
     {
-      int mn = code[ip + 1] | (code[ip + 2] << 8), mx = code[ip + 3] | (code[ip + 4] << 8);
-      int jmax = (maxb - b) / cs;
-      if (mx < jmax) jmax = mx;
-      if (mn > jmax) alive = 0;
+      int m;
+      if (b == 0 && bwd < (uint64_t) cs) m = 1;
+      else if (b >= maxb) m = 1;
       else
       {
-        if (mn < jmax)
-        {
-          if (sp == 16) return 2;
-          st[sp].ip = ip + 5; st[sp].b = b; st[sp].j = mn + 1; st[sp].jmax = jmax; st[sp].step = cs;
-          sp++;
-        }
+        const uint8_t* cur = AT(b);
+        m = re_is_word(cur, cs) != re_is_word(backwards ? cur + cs : cur - cs, cs);
+      }
+      if (op == 0xB3) m = !m;
+      alive = m;
+      ip += 1;
+    }
+    else if (op == 0xB1)   /* ^, re.c:1967-1974 */
+    {
+      alive = backwards ? !(bwd > (uint64_t) b) : !(bwd > 0 || b != 0);
+      ip += 1;
+    }
+    else if (op == 0xB0)   /* $, re.c:1976-1981 */
+    {
+      alive = !(backwards || fwd > (uint64_t) b);
+      ip += 1;
+    }
+    else if (op == 0xB4 || op == 0xB5)   /* REPEAT_ANY, re.c:1810-1821, :1584-1641 */
+    {
+      int mn = code[ip + 1] | (code[ip + 2] << 8), mx = code[ip + 3] | (code[ip + 4] << 8);
+      int k = 0;
+      while (k < mx)
+      {
+        int bb = b + k * cs;
+        if (bb >= maxb) break;
+        const uint8_t* ch = AT(bb);
+        if ((wide && ch[1] != 0) || (!dotall && ch[0] == 0x0A)) break;
+        k++;
+      }
+      if (k < mn) alive = 0;
+      else
+      {
+        if (mn < k) PUSH(ip + 5, b, mn + 1, k, cs);
         b += mn * cs;
         ip += 5;
         continue;
@@ -436,7 +497,7 @@ static int general_reachable(const uint8_t* code, uint32_t len, const uint8_t* i
       if (b >= maxb) alive = 0;
       else
       {
-        const uint8_t* ch = backwards ? input - cs - b : input + b;
+        const uint8_t* ch = AT(b);
         if (wide && ch[1] != 0) alive = 0;
         else
         {
@@ -461,7 +522,18 @@ static int general_reachable(const uint8_t* code, uint32_t len, const uint8_t* i
             ok = code[ip + 1] ? !in : in;
             break;
           }
-          default: ok = 1; /* \w \W \s \S \d \D */
+          case 0xA7: ok = re_is_word(ch, cs); break;
+          case 0xA8: ok = !re_is_word(ch, cs); break;
+          case 0xA9:
+          case 0xAA:
+          {
+            int s_ = c == ' ' || c == '\t' || c == '\r' || c == '\n' || c == '\v' || c == '\f';
+            ok = op == 0xA9 ? s_ : !s_;
+            break;
+          }
+          case 0xAB: ok = c >= '0' && c <= '9'; break;
+          case 0xAC: ok = !(c >= '0' && c <= '9'); break;
+          default: ok = 1;
           }
           if (!ok) alive = 0;
           else { b += cs; ip += sz; continue; }
@@ -469,11 +541,15 @@ static int general_reachable(const uint8_t* code, uint32_t len, const uint8_t* i
       }
     }
     if (alive) continue;
-    if (sp == 0) return 0;
-    ip = st[sp - 1].ip;
-    b = st[sp - 1].b + st[sp - 1].j * st[sp - 1].step;
-    if (++st[sp - 1].j > st[sp - 1].jmax) sp--;
+    if (csp == 0) return 0;
+    ip = st[csp - 1].ip;
+    b = st[csp - 1].b + st[csp - 1].j * st[csp - 1].step;
+    sp = st[csp - 1].sp;
+    memcpy(cnt, st[csp - 1].cnt, sizeof cnt);
+    if (++st[csp - 1].j > st[csp - 1].jmax) csp--;
   }
+#undef AT
+#undef PUSH
   return 2;
 }
 
@@ -497,10 +573,11 @@ static int general_call_effect(uint32_t flags, const uint8_t* fwd, uint32_t fl, 
   for (int w = 0; w < 2; w++)
   {
     if (w == 0 ? !try_ascii : !try_wide) continue;
-    int f = general_reachable(fwd, fl, data + off, size - off, 0, w, nocase, dotall, lower);
+    int f = general_reachable(fwd, fl, data + off, size - off, off, 0, w, nocase, dotall, lower);
     if (f == 2) return 1;
     if (f == 0) continue;
-    if (bl == 0 || general_reachable(bwd, bl, data + off, off, 1, w, nocase, dotall, lower) != 0)
+    if (bl == 0 ||
+        general_reachable(bwd, bl, data + off, size - off, off, 1, w, nocase, dotall, lower) != 0)
       return 1;
   }
   return 0;

@@ -638,7 +638,11 @@ int yr_amd_tables_set_re_code(yr_amd_tables* t, uint32_t n_pool, const uint32_t*
     if (bwd_len[k] > 0 && !ok(bwd_off[k], bwd_len[k])) return YR_AMD_INVALID_ARGUMENT;
   }
   HIP_TRY(hipSetDevice(t->device));
-  int r = upload(t->d_re_code, code, (size_t)code_len);
+  // the blob with 64 bytes of zero padding: the verify kernel stages programs
+  // with aligned 16-byte loads that may reach past the last one
+  std::vector<uint8_t> padded((size_t)code_len + 64, 0);
+  if (code_len > 0) memcpy(padded.data(), code, (size_t)code_len);
+  int r = upload(t->d_re_code, padded.data(), padded.size());
   if (r) return r;
   // the programs go into the pool records (uploaded again)
   for (uint32_t k = 0; k < n_pool; ++k) t->h_pool[k].re = re[k];

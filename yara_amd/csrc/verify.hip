@@ -286,6 +286,28 @@ __device__ int fast_re_set(const uint8_t* __restrict__ code, uint32_t len,
   return 1;
 }
 
+// A fast program is interpreted one opcode at a time, each step depending on
+// the previous one's position in the code: read from memory that is one L2
+// round trip per opcode.  Programs that fit are staged first -- three
+// independent 16-byte loads into this lane's kCodeBytes of LDS -- and
+// interpreted from there.  (The code blob is allocated with kCodeBytes of
+// padding, so the aligned loads never leave it.)
+constexpr uint32_t kCodeBytes = 48;
+__device__ __forceinline__ const uint8_t* stage_code(const uint8_t* code, uint32_t len,
+                                                     uint8_t* buf) {
+  const uintptr_t a = (uintptr_t)code, lo = a & ~(uintptr_t)15;
+  const uint32_t head = (uint32_t)(a - lo);
+  if (buf == nullptr || head + len > kCodeBytes) return code;
+  typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
+  const u32x4* g = reinterpret_cast<const u32x4*>(lo);
+  const u32x4 c0 = g[0], c1 = g[1], c2 = g[2];
+  u32x4* d = reinterpret_cast<u32x4*>(buf);
+  d[0] = c0;
+  d[1] = c1;
+  d[2] = c2;
+  return buf + head;
+}
+
 __device__ __forceinline__ bool fast_re_decide(const uint8_t* code, uint32_t len,
                                                const uint8_t* input, uint64_t avail,
                                                bool backwards, const ByteWindow& win) {
@@ -293,39 +315,72 @@ __device__ __forceinline__ bool fast_re_decide(const uint8_t* code, uint32_t len
   return v == 2 ? fast_re_reachable(code, len, input, avail, backwards, win) : v == 1;
 }
 
-// yr_re_exec (re.c:1693-2072) as a reachability question, over-approximated:
-// can some path from the program's start reach RE_OPCODE_MATCH?  Character
-// tests are exact where they are locale-free (LITERAL with the host's case
-// folding, NOT/MASKED literals, CLASS, ANY with DOT_ALL), every character
-// consumes character_size bytes subject to the prolog (bytes_matched <
-// max_bytes_matched, and for wide input a zero high byte, re.c:1727-1735);
-// everything else is allowed: both branches of SPLIT, every iteration count
-// of REPEAT_START/END loops and REPEAT_ANY ranges, word-boundary and anchor
-// assertions, the \w \s \d classes.  A reference fiber's path is therefore
-// always one of these paths, and "unreachable" proves forward_matches == -1.
-// Depth-first with an explicit choice stack.  Stack or step budget exhausted,
-// or code this analysis does not know -> kPathUnknown, and the caller keeps the
-// call outright.  The budget (1000 steps) is below RE_MAX_FIBERS (1024,
-// limits.h:168): every live reference fiber is a distinct node of this search
-// tree, so an exec that would fail with ERROR_TOO_MANY_RE_FIBERS
+// yr_re_exec (re.c:1693-2072) as a reachability question: can some path from
+// the program's start reach RE_OPCODE_MATCH?  Every opcode is modelled with the
+// reference's own semantics: character tests (LITERAL with the host's case
+// folding, NOT / MASKED literals, CLASS with yr_altercase, ANY, and \w \W \s
+// \S \d \D, all locale-free in libyara: yr_isalnum, strutils.c:240-244), the
+// prolog of every consuming opcode (bytes_matched < max_bytes_matched, zero
+// high byte for wide input, re.c:1729-1737), REPEAT_ANY ranges with every
+// repeated character passing ANY's test (re.c:1810-1821, :1584-1641),
+// counted REPEAT_START / REPEAT_END loops with the fiber's counter stack
+// (re.c:1533-1582), the zero-width \b \B ^ $ assertions (re.c:1937-1981),
+// both branches of SPLIT and JUMP.  A reference fiber's path is one of the
+// search's paths, and every path the search takes is one a fiber can take --
+// except where the reference kills a fiber for re-executing a SPLIT inside one
+// synchronisation (re.c:1482-1495; only loops that can match empty strings)
+// -- so "no path" proves forward_matches == -1 and "a path" is exact up to
+// that case.  Depth-first with an explicit choice stack (each choice keeps the
+// counter stack).  Stack or step budget exhausted, deeper loop nesting than
+// kReCounters, or code this search does not know -> kPathUnknown, and the
+// caller keeps the call outright.  The budget (1000 steps) is below
+// RE_MAX_FIBERS (1024, limits.h:168): every live reference fiber is a
+// distinct reachable state, each visited by this search before it can answer
+// "no path", so an exec that would fail with ERROR_TOO_MANY_RE_FIBERS
 // (re.c:1228-1229, a scan error the host must still see) always exhausts it.
 constexpr int kPathDead = 0, kPathMatch = 1, kPathUnknown = 2;
 constexpr int kReGeneralBudget = 1000;
+constexpr int kReCounters = 4;
+__device__ __forceinline__ bool re_is_word(const uint8_t* ch, int cs) {   // re.c:114-122
+  const uint8_t c = ch[0];
+  const bool w = (c >= 0x30 && c <= 0x39) || (c >= 0x41 && c <= 0x5a) || (c >= 0x61 && c <= 0x7a) ||
+                 c == '_';
+  return cs == 2 ? (w && ch[1] == 0) : w;
+}
 __device__ int general_re_reachable(const uint8_t* __restrict__ code, uint32_t len,
-                                     const uint8_t* __restrict__ input, uint64_t avail,
-                                     bool backwards, bool wide, bool nocase, bool dotall,
-                                     const uint8_t* __restrict__ lower) {
+                                     const uint8_t* __restrict__ input, uint64_t fwd_size,
+                                     uint64_t bwd_size, bool backwards, bool wide, bool nocase,
+                                     bool dotall, const uint8_t* __restrict__ lower) {
   constexpr int kMaxChoices = 16;
   struct Choice {
     int32_t ip;
-    int b, j, jmax, step;
+    int16_t b, j, jmax;
+    int8_t step, sp;
+    uint16_t cnt[kReCounters];
   } st[kMaxChoices];
-  int sp = 0;
+  int csp = 0;
   const int cs = wide ? 2 : 1;
-  int maxb = (int)min<uint64_t>(avail, (uint64_t)kReScanLimit);
+  int maxb = (int)min<uint64_t>(backwards ? bwd_size : fwd_size, (uint64_t)kReScanLimit);
   maxb -= maxb % cs;
   int32_t ip = 0;
-  int b = 0;
+  int b = 0, sp = -1;
+  uint16_t cnt[kReCounters] = {0, 0, 0, 0};
+  // the character bytes_matched = bb reads (forward: input[bb]; backward: the
+  // character ending at input - bb)
+  auto at = [&](int bb) { return backwards ? input - cs - bb : input + bb; };
+  auto push = [&](int32_t cip, int cb, int j, int jmax, int step) -> bool {
+    if (csp == kMaxChoices) return false;
+    Choice& c = st[csp++];
+    c.ip = cip;
+    c.b = (int16_t)cb;
+    c.j = (int16_t)j;
+    c.jmax = (int16_t)jmax;
+    c.step = (int8_t)step;
+    c.sp = (int8_t)sp;
+#pragma unroll
+    for (int q = 0; q < kReCounters; ++q) c.cnt[q] = cnt[q];
+    return true;
+  };
   for (int budget = 0; budget < kReGeneralBudget; ++budget) {
     if (ip < 0 || (uint32_t)ip >= len) return kPathUnknown;
     const uint8_t op = code[ip];
@@ -338,79 +393,117 @@ __device__ int general_re_reachable(const uint8_t* __restrict__ code, uint32_t l
         continue;
       case kOpSplitA:
       case kOpSplitB:
-        if (sp == kMaxChoices) return kPathUnknown;
-        st[sp++] = Choice{ip + re_i16(code + ip + 2), b, 0, 0, 0};
+        if (!push(ip + re_i16(code + ip + 2), b, 0, 0, 0)) return kPathUnknown;
         ip += 4;
         continue;
       case kOpRepeatStartGreedy:
-      case kOpRepeatStartUngreedy:
-        if (re_u16(code + ip + 1) == 0) {   // min == 0: the body may be skipped
-          if (sp == kMaxChoices) return kPathUnknown;
-          st[sp++] = Choice{ip + re_i32(code + ip + 5), b, 0, 0, 0};
-        }
+      case kOpRepeatStartUngreedy:   // re.c:1533-1553
+        if (re_u16(code + ip + 1) == 0 && !push(ip + re_i32(code + ip + 5), b, 0, 0, 0))
+          return kPathUnknown;   // min == 0: the loop may be skipped (no counter)
+        if (sp + 1 >= kReCounters) return kPathUnknown;
+        cnt[++sp] = 0;
         ip += 9;
         continue;
       case kOpRepeatEndGreedy:
-      case kOpRepeatEndUngreedy:   // loop back or leave, any number of times
-        if (sp == kMaxChoices) return kPathUnknown;
-        st[sp++] = Choice{ip + re_i32(code + ip + 5), b, 0, 0, 0};
+      case kOpRepeatEndUngreedy: {   // re.c:1555-1582
+        if (sp < 0) return kPathUnknown;
+        const int mn = re_u16(code + ip + 1), mx = re_u16(code + ip + 3);
+        ++cnt[sp];
+        if (cnt[sp] < mn) {
+          ip += re_i32(code + ip + 5);
+          continue;
+        }
+        if (cnt[sp] < mx && !push(ip + re_i32(code + ip + 5), b, 0, 0, 0)) return kPathUnknown;
+        --sp;   // leave the loop
         ip += 9;
         continue;
+      }
       case kOpWordBoundary:
-      case kOpNonWordBoundary:
-      case kOpMatchAtStart:
-      case kOpMatchAtEnd:
+      case kOpNonWordBoundary: {   // re.c:1937-1965
+        bool m;
+        if (b == 0 && bwd_size < (uint64_t)cs) {
+          m = true;
+        } else if (b >= maxb) {
+          m = true;
+        } else {
+          const uint8_t* cur = at(b);
+          m = re_is_word(cur, cs) != re_is_word(backwards ? cur + cs : cur - cs, cs);
+        }
+        if (op == kOpNonWordBoundary) m = !m;
+        dead = !m;
         ip += 1;
-        continue;
+        break;
+      }
+      case kOpMatchAtStart:   // re.c:1967-1974
+        dead = backwards ? bwd_size > (uint64_t)b : (bwd_size > 0 || b != 0);
+        ip += 1;
+        break;
+      case kOpMatchAtEnd:     // re.c:1976-1981
+        dead = backwards || fwd_size > (uint64_t)b;
+        ip += 1;
+        break;
       case kOpRepeatAnyGreedy:
-      case kOpRepeatAnyUngreedy: {
+      case kOpRepeatAnyUngreedy: {   // re.c:1810-1821 + the rc spin of :1584-1641
         const int mn = re_u16(code + ip + 1), mx = re_u16(code + ip + 3);
-        const int jmax = min(mx, (maxb - b) / cs);   // every repetition passes the prolog
-        if (mn > jmax) {
+        int k = 0;   // consecutive characters from b that pass the prolog and ANY
+        while (k < mx) {
+          const int bb = b + k * cs;
+          if (bb >= maxb) break;
+          const uint8_t* ch = at(bb);
+          if ((wide && ch[1] != 0) || (!dotall && ch[0] == 0x0A)) break;
+          ++k;
+        }
+        if (k < mn) {
           dead = true;
           break;
         }
-        if (mn < jmax) {
-          if (sp == kMaxChoices) return kPathUnknown;
-          st[sp++] = Choice{ip + 5, b, mn + 1, jmax, cs};
-        }
+        if (mn < k && !push(ip + 5, b, mn + 1, k, cs)) return kPathUnknown;
         b += mn * cs;
         ip += 5;
         continue;
       }
       default: {
         const uint32_t sz = re_op_size(op);
-        if (sz == 0) return kPathUnknown;   // not a program this analysis knows
+        if (sz == 0) return kPathUnknown;   // not a program this search knows
         if (b >= maxb) {
           dead = true;
           break;
         }
-        const uint8_t* ch = backwards ? input - cs - b : input + b;
+        const uint8_t* ch = at(b);
         if (wide && ch[1] != 0) {
           dead = true;
           break;
         }
         const uint8_t c = ch[0];
         bool ok = true;
-        if (op == kOpAny) {
-          ok = dotall || c != 0x0A;
-        } else if (op == kOpLiteral) {
-          ok = nocase ? lower[c] == lower[code[ip + 1]] : c == code[ip + 1];
-        } else if (op == kOpNotLiteral) {
-          ok = c != code[ip + 1];
-        } else if (op == kOpMaskedLiteral) {
-          ok = (c & code[ip + 2]) == code[ip + 1];
-        } else if (op == kOpMaskedNotLiteral) {
-          ok = (c & code[ip + 2]) != code[ip + 1];
-        } else if (op == kOpClass) {
-          const uint8_t* bm = code + ip + 2;
-          bool in = (bm[c >> 3] >> (c & 7)) & 1;
-          if (nocase) {   // yr_altercase (libyara.c:249-256): ASCII case swap
-            const uint8_t a = (c >= 'a' && c <= 'z') ? c - 32 : (c >= 'A' && c <= 'Z') ? c + 32 : c;
-            in = in || ((bm[a >> 3] >> (a & 7)) & 1);
+        switch (op) {
+          case kOpAny: ok = dotall || c != 0x0A; break;
+          case kOpLiteral: ok = nocase ? lower[c] == lower[code[ip + 1]] : c == code[ip + 1]; break;
+          case kOpNotLiteral: ok = c != code[ip + 1]; break;
+          case kOpMaskedLiteral: ok = (c & code[ip + 2]) == code[ip + 1]; break;
+          case kOpMaskedNotLiteral: ok = (c & code[ip + 2]) != code[ip + 1]; break;
+          case kOpClass: {   // re.c:97-112 with yr_altercase (libyara.c:249-256)
+            const uint8_t* bm = code + ip + 2;
+            bool in = (bm[c >> 3] >> (c & 7)) & 1;
+            if (nocase) {
+              const uint8_t a = (c >= 'a' && c <= 'z') ? c - 32 : (c >= 'A' && c <= 'Z') ? c + 32 : c;
+              in = in || ((bm[a >> 3] >> (a & 7)) & 1);
+            }
+            ok = code[ip + 1] ? !in : in;
+            break;
           }
-          ok = code[ip + 1] ? !in : in;
-        }   // \w \W \s \S \d \D: allowed (locale-dependent in the reference)
+          case kOpWordChar: ok = re_is_word(ch, cs); break;
+          case kOpNonWordChar: ok = !re_is_word(ch, cs); break;
+          case kOpSpace:
+          case kOpNonSpace: {   // re.c:1897-1921
+            const bool sp_ = c == ' ' || c == '\t' || c == '\r' || c == '\n' || c == '\v' || c == '\f';
+            ok = op == kOpSpace ? sp_ : !sp_;
+            break;
+          }
+          case kOpDigit: ok = c >= '0' && c <= '9'; break;    // isdigit, re.c:1923-1935
+          case kOpNonDigit: ok = !(c >= '0' && c <= '9'); break;
+          default: break;
+        }
         if (!ok) {
           dead = true;
           break;
@@ -421,11 +514,14 @@ __device__ int general_re_reachable(const uint8_t* __restrict__ code, uint32_t l
       }
     }
     if (!dead) continue;
-    if (sp == 0) return kPathDead;
-    Choice& t = st[sp - 1];
+    if (csp == 0) return kPathDead;
+    Choice& t = st[csp - 1];
     ip = t.ip;
     b = t.b + t.j * t.step;
-    if (++t.j > t.jmax) --sp;
+    sp = t.sp;
+#pragma unroll
+    for (int q = 0; q < kReCounters; ++q) cnt[q] = t.cnt[q];
+    if (++t.j > t.jmax) --csp;
   }
   return kPathUnknown;
 }
@@ -439,7 +535,7 @@ __device__ int general_re_reachable(const uint8_t* __restrict__ code, uint32_t l
 // return), a zero-length forward match needs a backward program, and with a
 // backward program its MATCHes are the only way to _yr_scan_match_callback.
 __device__ bool re_call_matters(const VerifyParams& p, const DevPoolRec& e, uint32_t flags,
-                                uint64_t offset, uint32_t lds) {
+                                uint64_t offset, uint32_t lds, uint8_t* codebuf) {
   if (YAMD_VERIFY_DIAG == 2) return true;
   if (!p.re_on) return true;
   const DevRe r = e.re;
@@ -449,6 +545,13 @@ __device__ bool re_call_matters(const VerifyParams& p, const DevPoolRec& e, uint
   const uint8_t* bwd = p.re_code + r.bwd_off;
   if (flags & kStrFastRegexp) {
     if (!(flags & kStrAscii) || (flags & (kStrWide | kStrBase64Any))) return true;
+    // forward and backward programs are contiguous in the blob (the shim and
+    // yarc.cpp lay them out so): stage both at once when they fit
+    if (r.bwd_len == 0 || r.bwd_off == r.fwd_off + r.fwd_len) {
+      const uint8_t* both = stage_code(fwd, r.fwd_len + r.bwd_len, codebuf);
+      fwd = both;
+      bwd = both + r.fwd_len;
+    }
     if (r.fwd_len == 1)   // forward program = MATCH: forward_matches = 0
       return r.bwd_len > 0 &&
              fast_re_decide(bwd, r.bwd_len, d, offset, true, stage_window(p, d, true, lds));
@@ -471,13 +574,13 @@ __device__ bool re_call_matters(const VerifyParams& p, const DevPoolRec& e, uint
   // attempt runs: both branches are covered by trying every attempt.
   for (int w = 0; w < 2; ++w) {
     if (w == 0 ? !try_ascii : !try_wide) continue;
-    const int f = general_re_reachable(fwd, r.fwd_len, d, p.size - offset, false, w == 1, nocase,
-                                       dotall, p.lowercase);
+    const int f = general_re_reachable(fwd, r.fwd_len, d, p.size - offset, offset, false, w == 1,
+                                       nocase, dotall, p.lowercase);
     if (f == kPathUnknown) return true;
     if (f == kPathDead) continue;
     if (r.bwd_len == 0) return true;
-    const int b = general_re_reachable(bwd, r.bwd_len, d, offset, true, w == 1, nocase, dotall,
-                                       p.lowercase);
+    const int b = general_re_reachable(bwd, r.bwd_len, d, p.size - offset, offset, true, w == 1,
+                                       nocase, dotall, p.lowercase);
     if (b != kPathDead) return true;
   }
   return false;
@@ -487,7 +590,7 @@ __device__ bool re_call_matters(const VerifyParams& p, const DevPoolRec& e, uint
 // have an effect?  false only where the reference provably returns without
 // touching the context.
 __device__ bool call_matters(const VerifyParams& p, const DevPoolRec& st, uint64_t offset,
-                             uint32_t lds) {
+                             uint32_t lds, uint8_t* codebuf) {
   if (YAMD_VERIFY_DIAG == 1) return false;
   // scan.c:1013: data_size - offset <= 0 (size_t) <=> offset == size
   if (offset >= p.size) return false;
@@ -509,7 +612,7 @@ __device__ bool call_matters(const VerifyParams& p, const DevPoolRec& st, uint64
         min<uint64_t>(p.size, offset + max<uint64_t>((uint64_t)kReScanLimit, 2ull * st.length));
     if (need_lo < p.win_lo || need_hi > p.win_hi) return true;
   }
-  if (!(st.flags & kStrLiteral)) return re_call_matters(p, st, st.flags, offset, lds);
+  if (!(st.flags & kStrLiteral)) return re_call_matters(p, st, st.flags, offset, lds, codebuf);
   if (st.flags & kStrUnmodelled) return true;            // conservative
   // _yr_scan_verify_literal_match, scan.c:907-972
   const uint8_t* d = p.data + offset;
@@ -537,8 +640,8 @@ __device__ bool call_matters(const VerifyParams& p, const DevPoolRec& st, uint64
 constexpr uint32_t kKeepOverflow = 1u << 31;
 template <int PASS>
 __device__ __forceinline__ void verify_one(const VerifyParams& p, uint64_t c, uint32_t lds,
-                                           uint32_t keep, uint32_t head, uint64_t o,
-                                           uint32_t& count) {
+                                           uint8_t* codebuf, uint32_t keep, uint32_t head,
+                                           uint64_t o, uint32_t& count) {
   const uint64_t i = p.all ? p.all_first + c : p.positions[c];
   if (!PASS) head = node_head(p, i);
   const bool decide = !PASS || (keep & kKeepOverflow);
@@ -549,7 +652,7 @@ __device__ __forceinline__ void verify_one(const VerifyParams& p, uint64_t c, ui
     const uint32_t bt = e.backtrack;
     bool kept;
     if (decide)
-      kept = bt <= i && call_matters(p, e, i - bt, lds);
+      kept = bt <= i && call_matters(p, e, i - bt, lds, codebuf);
     else
       kept = t < 31 && ((keep >> t) & 1u);
     const uint32_t kk = k;
@@ -605,14 +708,16 @@ __device__ __forceinline__ uint32_t block_exclusive_scan(uint32_t v, uint32_t* w
 template <int PASS>
 __global__ __launch_bounds__(256) void verify_kernel(VerifyParams p) {
   __shared__ __attribute__((aligned(16))) uint8_t win[256 * kWinBytes];
+  __shared__ __attribute__((aligned(16))) uint8_t code[256 * kCodeBytes];
   __shared__ uint32_t wsum[4];
   // (the low 32 bits of a flat LDS address are the LDS offset)
   const uint32_t lds = (uint32_t)(uintptr_t)(win + threadIdx.x * kWinBytes);
+  uint8_t* codebuf = code + threadIdx.x * kCodeBytes;
   const uint64_t c = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
   const bool in = c < p.count;
   uint32_t n = 0, total = 0;
   if (!PASS) {
-    if (in) verify_one<0>(p, c, lds, 0, 0, 0, n);
+    if (in) verify_one<0>(p, c, lds, codebuf, 0, 0, 0, n);
     (void)block_exclusive_scan(n, wsum, total);
     if (threadIdx.x == 0) p.block_off[blockIdx.x] = total;
     return;
@@ -621,7 +726,7 @@ __global__ __launch_bounds__(256) void verify_kernel(VerifyParams p) {
   n = keep == 0 ? 0u : p.counts[c];
   const uint32_t pre = block_exclusive_scan(n, wsum, total);
   if (total == 0 || keep == 0) return;
-  verify_one<1>(p, c, lds, keep, p.heads[c], p.block_off[blockIdx.x] + pre, n);
+  verify_one<1>(p, c, lds, codebuf, keep, p.heads[c], p.block_off[blockIdx.x] + pre, n);
 }
 
 // Exclusive scan, in place, of the per-block record counts (one workgroup),
