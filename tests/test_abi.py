@@ -256,3 +256,27 @@ def test_pipeline_and_verify_reject_bad_handles():
     assert L.yr_amd_pipeline_destroy(None) == yara_amd.SUCCESS
     assert L.yr_amd_verify_device(None, 0, None, None) == yara_amd.INVALID_ARGUMENT
     assert L.yr_amd_scan_block_verified(None, None, 0, 0, None, None) == yara_amd.INVALID_ARGUMENT
+
+
+def test_debug_verbosity_dumps_candidate_states(tmp_path):
+    """YR_DEBUG_VERBOSITY=2 (libyara's own switch, globals.h:51-90): the host
+    replay prints every candidate's state and match-table entry, the analogue
+    of scanner.c:83-96 (CPU: host-only tables, oracle candidates)."""
+    import subprocess
+    import sys
+    code = (
+        "import sys, numpy as np; sys.path[:0] = %r\n"
+        "import oracle, yara_amd\n"
+        "from conftest import ref_tables, tables_npz\n"
+        "t = yara_amd.Tables.from_npz(tables_npz('short'), device=-1)\n"
+        "d = np.frombuffer(b'xxabcdxxaaaa', np.uint8)\n"
+        "c = oracle.candidates(ref_tables('short'), d)\n"
+        "yara_amd.replay(t, d, c, False, lambda k, o: 0)\n"
+        "print(len(c))\n" % [REPO, os.path.join(REPO, "tests"), os.path.join(REPO, "tests", "golden")])
+    env = dict(os.environ, YR_DEBUG_VERBOSITY="2")
+    p = subprocess.run([sys.executable, "-c", code], capture_output=True, text=True, env=env,
+                       timeout=120)
+    assert p.returncode == 0, p.stderr
+    n = int(p.stdout.strip().splitlines()[-1])
+    lines = [l for l in p.stderr.splitlines() if "match_table[state=" in l]
+    assert n > 0 and len(lines) == n, (n, p.stderr[-2000:])

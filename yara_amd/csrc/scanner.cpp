@@ -8,6 +8,8 @@
 // and the host replay of candidates into the caller's verifier in the exact
 // order of scanner.c:98-122 / :144-163.
 #include <hip/hip_runtime.h>
+#include <stdio.h>
+#include <stdlib.h>
 #include <string.h>
 
 #include <algorithm>
@@ -149,6 +151,19 @@ struct yr_amd_scanner {
 };
 
 static_assert(sizeof(VerifyRec) == sizeof(yr_amd_verify_rec), "record layout");
+
+// Debug output, the analogue of libyara's YR_DEBUG_VERBOSITY (globals.h:51-90):
+// the same environment variable; at level >= 2 the host replay prints every
+// candidate's state and match-table entry as the reference walk does at
+// scanner.c:83-96, and pre-verification prints its records.
+static int debug_level() {
+  static int level = -1;
+  if (level < 0) {
+    const char* e = getenv("YR_DEBUG_VERBOSITY");
+    level = e ? atoi(e) : 0;
+  }
+  return level;
+}
 
 #define HIP_TRY(expr)                                   \
   do {                                                  \
@@ -727,6 +742,18 @@ int yr_amd_verify_device(yr_amd_scanner* s, uint64_t data_base, const yr_amd_ver
       HIP_TRY(hipStreamSynchronize(s->stream));
     }
   }
+  if (debug_level() >= 2 && total > 0) {
+    std::vector<yr_amd_verify_rec> h(total);
+    if (hipMemcpy(h.data(), s->d_vrec, total * sizeof(yr_amd_verify_rec), hipMemcpyDeviceToHost) ==
+        hipSuccess)
+      for (const yr_amd_verify_rec& r : h)
+        fprintf(stderr, "- verify pool=%u offset=%llu candidate=%u base=0x%llx // yr_amd_verify_device()\n",
+                r.pool_index, (unsigned long long)r.offset, r.candidate,
+                (unsigned long long)data_base);
+  }
+  if (debug_level() >= 1)
+    fprintf(stderr, "- %llu candidates -> %llu verify calls // yr_amd_verify_device()\n",
+            (unsigned long long)v.count, (unsigned long long)total);
   if (d_records) *d_records = reinterpret_cast<const yr_amd_verify_rec*>(s->d_vrec);
   if (count) *count = total;
   return YR_AMD_SUCCESS;
@@ -782,6 +809,9 @@ int yr_amd_replay(const yr_amd_tables* t, const uint8_t* data, size_t size,
     for (uint64_t j = i > YR_AMD_MAX_ATOM_LENGTH ? i - YR_AMD_MAX_ATOM_LENGTH : 0; j < i; ++j)
       state = ac_step(T, state, data[j]);
     if (M[state] == 0) return YR_AMD_INTERNAL_FATAL_ERROR;
+    if (debug_level() >= 2)
+      fprintf(stderr, "- match_table[state=%u]=%u i=%llu block_data=%p // yr_amd_replay()\n", state,
+              M[state], (unsigned long long)i, (const void*)data);
     // scanner.c:105-121
     for (uint32_t k = M[state]; k != 0; k = nx[k - 1]) {
       if (bt[k - 1] <= i) {
