@@ -238,8 +238,7 @@ template <int MODE>
 constexpr bool kDeferFl = YAMD_DEFER_FL && (MODE == 0 || MODE == 12);
 
 // Consume a deferred drain's first-level words: the lanes' hits that pass go,
-// in order, to the pending list (or, if they are more than a wave's worth,
-// are bucket-probed in place).
+// in order, to the pending list.
 template <int MODE>
 __device__ __forceinline__ void drain_complete(const ScanParams& p, WaveQueue& q, uint32_t lane,
                                                uint64_t seg_start, uint32_t* out, uint32_t& found) {
@@ -251,30 +250,24 @@ __device__ __forceinline__ void drain_complete(const ScanParams& p, WaveQueue& q
   const uint32_t incl = wave_inclusive_scan(c);
   const uint32_t total = __builtin_amdgcn_readlane(incl, kWave - 1);
   if (total == 0) return;
-  if (q.pend_n + total > kWave) flush_pending<MODE>(p, q, lane, seg_start, out, found);
-  if (total <= kWave) {
-    uint32_t idx = q.pend_n + incl - c;
-    if (ha) lds_store2(q.pend + 8 * idx++, q.wa, q.oa);
-    if (hb) lds_store2(q.pend + 8 * idx, q.wb, q.ob);
-    q.pend_n += total;
-    return;
+  // in order to the pending list, bucket-probed (one round trip for 64 hits)
+  // each time it fills up
+  const uint32_t end = q.pend_n + total;
+  const uint32_t i0 = q.pend_n + incl - c, i1 = i0 + (uint32_t)ha;
+  for (uint32_t base = 0;; base += kWave) {
+    if (ha && i0 - base < kWave) lds_store2(q.pend + 8 * (i0 - base), q.wa, q.oa);
+    if (hb && i1 - base < kWave) lds_store2(q.pend + 8 * (i1 - base), q.wb, q.ob);
+    if (end <= base + kWave) {
+      q.pend_n = end - base;
+      return;
+    }
+    q.pend_n = kWave;
+    flush_pending<MODE>(p, q, lane, seg_start, out, found);
   }
-  const bool ka = ha && (MODE == 12 || exact_check(q.wa, seg_start + q.oa + 1, p));
-  const bool kb = hb && (MODE == 12 || exact_check(q.wb, seg_start + q.ob + 1, p));
-  const uint32_t kc = (uint32_t)ka + (uint32_t)kb;
-  const uint32_t kincl = wave_inclusive_scan(kc);
-  uint32_t idx = found + kincl - kc;
-  if (ka) {
-    if (idx < p.seg_cap) out[idx] = q.oa;
-    ++idx;
-  }
-  if (kb && idx < p.seg_cap) out[idx] = q.ob;
-  found += __builtin_amdgcn_readlane(kincl, kWave - 1);
 }
 
 // First-level check of the hits of up to 64 ring entries; survivors go to
-// the pending list (or, if a drain alone yields more than 64 of them, are
-// bucket-probed in place).  kAsync (drains inside a tile step): when no lane
+// the pending list.  kAsync (drains inside a tile step): when no lane
 // has more than two hits, only compute the first-level indices and leave the
 // loads to the tile step (WaveQueue).
 template <int MODE, bool kAsync = false>
@@ -325,7 +318,9 @@ __device__ __forceinline__ void drain(const ScanParams& p, WaveQueue& q, uint32_
       return;
     }
   }
-  {
+  if (MODE == 0 && (p.len_mask & 6u) != 0u) {
+    maybe = m;   // 1-/2-byte keys: no first level, every hit goes to the buckets
+  } else {
     while (m) {
       const uint32_t j = (uint32_t)__builtin_ctz(m);
       m &= m - 1;
@@ -350,27 +345,25 @@ __device__ __forceinline__ void drain(const ScanParams& p, WaveQueue& q, uint32_
   }
   const uint32_t total = __builtin_amdgcn_readlane(incl, kWave - 1);
   if (total == 0) return;
-  if (q.pend_n + total > kWave) flush_pending<MODE>(p, q, lane, seg_start, out, found);
-  if (total <= kWave) {
-    uint32_t idx = q.pend_n + incl - c;
-    while (maybe) {
+  // in order to the pending list, bucket-probed (one round trip for 64 hits)
+  // each time it fills up -- dense true hits (1-byte keys) can yield up to 16
+  // per lane; probing them in place would cost one round trip per hit
+  const uint32_t end = q.pend_n + total;
+  uint32_t idx = q.pend_n + incl - c;
+  for (uint32_t base = 0;; base += kWave) {
+    while (maybe != 0u && idx < base + kWave) {
       const uint32_t j = (uint32_t)__builtin_ctz(maybe);
       maybe &= maybe - 1;
-      lds_store2(q.pend + 8 * idx, window4(ent, j), off0 + j);
+      lds_store2(q.pend + 8 * (idx - base), window4(ent, j), off0 + j);
       ++idx;
     }
-    q.pend_n += total;
-    return;
+    if (end <= base + kWave) {
+      q.pend_n = end - base;
+      return;
+    }
+    q.pend_n = kWave;
+    flush_pending<MODE>(p, q, lane, seg_start, out, found);
   }
-  // more than a wave's worth from one drain (dense true hits): probe in place
-  uint32_t keep = 0;
-  while (maybe) {
-    const uint32_t j = (uint32_t)__builtin_ctz(maybe);
-    maybe &= maybe - 1;
-    keep |= (uint32_t)exact_check(window4(ent, j), seg_start + off0 + j + 1, p) << j;
-  }
-  const uint32_t kc = __popc(keep);
-  append_hits(p, keep, kc, wave_inclusive_scan(kc), off0, out, found);
 }
 
 // A tile entirely inside the block: one 16-byte non-temporal load per lane
