@@ -43,12 +43,31 @@ __device__ __forceinline__ bool node_bucket_get(const uint4& b, uint32_t key, ui
   if (b.z == key) { head = b.w; return true; }
   return false;
 }
+#ifndef YAMD_VERIFY_DIAG
+#define YAMD_VERIFY_DIAG 0   // profiling builds only: 1 = decide nothing, 2 = no regex decisions,
+                             // 3 = positions only, 4 = + list heads, 5 = 4 with the data
+                             // read only, 6 = 4 without the data read
+#endif
+
 __device__ __forceinline__ uint32_t node_head(const VerifyParams& p, uint64_t i) {
   const uint32_t n = i < 4 ? (uint32_t)i : 4u;
   uint32_t w = 0;   // data[i-n .. i), oldest byte lowest, at the top (bytes i-4.. i-1)
+  const uint64_t a = (i - 4) & ~3ull;   // p.data is 16-byte aligned
+  if (i >= 4 && a >= p.win_lo && a + 8 <= p.win_hi) {
+    // one 8-byte load (4 byte loads per lane cost 2-3x the time: the random
+    // reads of the candidates' neighbourhoods are the count pass's largest item)
+    const uint2 v = *reinterpret_cast<const uint2*>(p.data + a);
+    w = __builtin_amdgcn_alignbyte(v.y, v.x, (uint32_t)(i - 4 - a));
+  } else {
 #pragma unroll
-  for (uint32_t j = 0; j < 4; ++j)
-    if (j < n) w |= (uint32_t)p.data[i - n + j] << (8 * (4 - n + j));
+    for (uint32_t j = 0; j < 4; ++j)
+      if (j < n) w |= (uint32_t)p.data[i - n + j] << (8 * (4 - n + j));
+  }
+#if YAMD_VERIFY_DIAG == 5
+  return w | 1u;   // profiling: the data read only
+#elif YAMD_VERIFY_DIAG == 6
+  w = (uint32_t)i * 2654435761u;   // profiling: the probes without the data read
+#endif
   const uint32_t k1 = w >> 24, k2 = w >> 16, k3 = (w >> 8) | (1u << 24), k4 = w;
   const uint32_t* __restrict__ t = p.nodes;
   const uint32_t h1 = n >= 1 ? t[kNodeL1 + k1] : 0u;
@@ -74,49 +93,6 @@ __device__ __forceinline__ uint32_t node_head(const VerifyParams& p, uint64_t i)
   if (h2) return h2;
   if (h1) return h1;
   return p.root_head;
-}
-
-// _yr_scan_compare / _yr_scan_icompare (scan.c:142-179): forward match length
-// of the ascii form, 0 if none.
-__device__ bool cmp_ascii(const uint8_t* d, uint64_t avail, const uint8_t* s, uint32_t n,
-                          const uint8_t* lower) {
-  if (avail < n) return false;
-  if (lower == nullptr) {
-    for (uint32_t i = 0; i < n; ++i)
-      if (d[i] != s[i]) return false;
-  } else {
-    for (uint32_t i = 0; i < n; ++i)
-      if (lower[d[i]] != lower[s[i]]) return false;
-  }
-  return true;
-}
-
-// _yr_scan_wcompare / _yr_scan_wicompare (scan.c:181-255): the wide form
-// (every character followed by 0x00).
-__device__ bool cmp_wide(const uint8_t* d, uint64_t avail, const uint8_t* s, uint32_t n,
-                         const uint8_t* lower) {
-  if (avail < 2ull * n) return false;
-  for (uint32_t i = 0; i < n; ++i) {
-    const uint8_t a = d[2 * i], b = s[i];
-    if ((lower == nullptr ? a != b : lower[a] != lower[b]) || d[2 * i + 1] != 0) return false;
-  }
-  return true;
-}
-
-// _yr_scan_xor_compare (scan.c:62-101) and _yr_scan_xor_wcompare (:103-140):
-// key k = data[0] ^ string[0], then every byte (and, wide, every 0x00 ^ k).
-__device__ bool cmp_xor(const uint8_t* d, uint64_t avail, const uint8_t* s, uint32_t n, bool wide) {
-  if (avail < (wide ? 2ull * n : (uint64_t)n)) return false;
-  if (n == 0) return false;   // both reference loops yield 0 for an empty string
-  const uint8_t k = d[0] ^ s[0];
-  for (uint32_t i = 0; i < n; ++i) {
-    if (wide) {
-      if (d[2 * i] != (uint8_t)(s[i] ^ k) || (uint8_t)(d[2 * i + 1] ^ k) != 0) return false;
-    } else if (d[i] != (uint8_t)(s[i] ^ k)) {
-      return false;
-    }
-  }
-  return true;
 }
 
 // yr_re_fast_exec (re.c:2150-2391) as a reachability question: is MATCH
@@ -160,7 +136,70 @@ __device__ __forceinline__ uint8_t window_byte(const ByteWindow& w, const uint8_
   return *at;
 }
 
-__device__ bool fast_re_reachable(const uint8_t* __restrict__ code, uint32_t len,
+// _yr_scan_compare / _yr_scan_icompare (scan.c:142-179): forward match length
+// of the ascii form, 0 if none.
+__device__ bool cmp_ascii(const uint8_t* d, uint64_t avail, const uint8_t* s, uint32_t n,
+                          const uint8_t* lower, const ByteWindow& w) {
+  if (avail < n) return false;
+  if (lower == nullptr) {
+    for (uint32_t i = 0; i < n; ++i)
+      if (window_byte(w, d + i) != s[i]) return false;
+  } else {
+    for (uint32_t i = 0; i < n; ++i)
+      if (lower[window_byte(w, d + i)] != lower[s[i]]) return false;
+  }
+  return true;
+}
+
+// _yr_scan_wcompare / _yr_scan_wicompare (scan.c:181-255): the wide form
+// (every character followed by 0x00).
+__device__ bool cmp_wide(const uint8_t* d, uint64_t avail, const uint8_t* s, uint32_t n,
+                         const uint8_t* lower, const ByteWindow& w) {
+  if (avail < 2ull * n) return false;
+  for (uint32_t i = 0; i < n; ++i) {
+    const uint8_t a = window_byte(w, d + 2 * i), b = s[i];
+    if ((lower == nullptr ? a != b : lower[a] != lower[b]) || window_byte(w, d + 2 * i + 1) != 0)
+      return false;
+  }
+  return true;
+}
+
+// _yr_scan_xor_compare (scan.c:62-101) and _yr_scan_xor_wcompare (:103-140):
+// key k = data[0] ^ string[0], then every byte (and, wide, every 0x00 ^ k).
+__device__ bool cmp_xor(const uint8_t* d, uint64_t avail, const uint8_t* s, uint32_t n, bool wide,
+                        const ByteWindow& w) {
+  if (avail < (wide ? 2ull * n : (uint64_t)n)) return false;
+  if (n == 0) return false;   // both reference loops yield 0 for an empty string
+  const uint8_t k = window_byte(w, d) ^ s[0];
+  for (uint32_t i = 0; i < n; ++i) {
+    if (wide) {
+      if (window_byte(w, d + 2 * i) != (uint8_t)(s[i] ^ k) ||
+          (uint8_t)(window_byte(w, d + 2 * i + 1) ^ k) != 0)
+        return false;
+    } else if (window_byte(w, d + i) != (uint8_t)(s[i] ^ k)) {
+      return false;
+    }
+  }
+  return true;
+}
+
+
+// Regexp code, read either from the blob in global memory or from this lane's
+// LDS copy (stage_code): typed LDS reads (ds_read_u8) rather than flat ones,
+// whose waits also cover every outstanding global load.
+struct GlobalCode {
+  const uint8_t* __restrict__ p;
+  __device__ uint8_t operator[](uint32_t i) const { return p[i]; }
+};
+struct LdsCode {
+  uint32_t a;   // LDS byte address
+  __device__ uint8_t operator[](uint32_t i) const {
+    return *reinterpret_cast<const __attribute__((address_space(3))) uint8_t*>((uintptr_t)(a + i));
+  }
+};
+
+template <class Code>
+__device__ bool fast_re_reachable(const Code code, uint32_t len,
                                   const uint8_t* __restrict__ input, uint64_t avail,
                                   bool backwards, const ByteWindow& win) {
   constexpr int kMaxChoices = 8;
@@ -224,62 +263,74 @@ __device__ bool fast_re_reachable(const uint8_t* __restrict__ code, uint32_t len
 // leave the window or come near YR_RE_SCAN_LIMIT, or an opcode outside the
 // fast set: the caller then runs the depth-first search, whose answer this
 // form equals wherever it answers.
-__device__ int fast_re_set(const uint8_t* __restrict__ code, uint32_t len,
-                           const uint8_t* __restrict__ input, uint64_t avail, bool backwards,
-                           const ByteWindow& win) {
+template <class Code>
+__device__ int fast_re_set(const Code code, uint32_t len, const uint8_t* __restrict__ input,
+                           uint64_t avail, bool backwards, const ByteWindow& win) {
   const int maxb = (int)min<uint64_t>(avail, (uint64_t)kReScanLimit);
   int base = 0;
   uint64_t m = 1;
   uint32_t ip = 0;
+  // Lanes interpret different programs, so the opcode kinds differ across the
+  // wave: every byte test is one branch-free form, (c & mask) == val, negated
+  // for the NOT forms, and the operand bytes are read together with the
+  // opcode (independent LDS reads; the blob and the staging buffer are padded).
   while (ip < len) {
-    const uint8_t op = code[ip];
+    const uint8_t op = code[ip], b1 = code[ip + 1], b2 = code[ip + 2];
     if (op == kReMatch) return m != 0 ? 1 : 0;
     const int lim = maxb - base;   // bits i < lim are live (b < max_bytes_matched)
     const uint64_t live = lim >= 64 ? m : (lim <= 0 ? 0ull : m & ((1ull << lim) - 1));
     if (live == 0) return 0;
     if (op == kReRepeatAnyUngreedy) {
-      const int mn = code[ip + 1] | (code[ip + 2] << 8);
+      const int mn = b1 | (b2 << 8);
       const int mx = code[ip + 3] | (code[ip + 4] << 8);
       const int lo = __builtin_ctzll(live), hi = 63 - __builtin_clzll(live);
       const int span = hi - lo + (mx - mn);
       const int nb = base + lo + mn;
       if (span > 63 || nb + span >= kReScanLimit) return 2;
-      const uint64_t t = live >> lo;
-      uint64_t more = 0;
-      for (int k = 1; k <= mx - mn; ++k) more |= t << k;
+      // t | t << 1 | ... | t << (mx - mn), by doubling
+      uint64_t acc = live >> lo;
+      const int r = mx - mn + 1;   // copies
+      int have = 1;
+      while (2 * have <= r) {
+        acc |= acc << have;
+        have *= 2;
+      }
+      if (have < r) acc |= acc << (r - have);
       const int lim2 = maxb - nb;
-      more &= lim2 >= 64 ? ~0ull : (lim2 <= 0 ? 0ull : (1ull << lim2) - 1);
-      m = t | more;
+      acc &= lim2 >= 64 ? ~0ull : (lim2 <= 0 ? 0ull : (1ull << lim2) - 1);
+      m = acc;
       base = nb;
       ip += 5;
       continue;
     }
-    uint32_t sz;
+    uint32_t mask, val, sz;
+    bool neg = false;
     switch (op) {
-      case kReAny: sz = 1; break;
-      case kReLiteral: case kReNotLiteral: sz = 2; break;
-      case kReMaskedLiteral: case kReMaskedNotLiteral: sz = 3; break;
+      case kReAny: mask = 0; val = 0; sz = 1; break;
+      case kReLiteral: mask = 0xFF; val = b1; sz = 2; break;
+      case kReNotLiteral: mask = 0xFF; val = b1; sz = 2; neg = true; break;
+      case kReMaskedLiteral: mask = b2; val = b1; sz = 3; break;
+      case kReMaskedNotLiteral: mask = b2; val = b1; sz = 3; neg = true; break;
       default: return 2;
     }
-    const uint8_t a1 = sz > 1 ? code[ip + 1] : 0, a2 = sz > 2 ? code[ip + 2] : 0;
-    uint64_t r = 0, x = live;
-    while (x) {
+    uint64_t res = 0, x = live;
+    while (x) {   // live positions, four at a time (independent LDS reads)
       const int i = __builtin_ctzll(x);
-      x &= x - 1;
-      const int b = base + i;
-      const uint8_t c = window_byte(win, backwards ? input - 1 - b : input + b);
-      bool pass;
-      switch (op) {
-        case kReAny: pass = true; break;
-        case kReLiteral: pass = c == a1; break;
-        case kReNotLiteral: pass = c != a1; break;
-        case kReMaskedLiteral: pass = (c & a2) == a1; break;
-        default: pass = (c & a2) != a1; break;
+      const int bb = base + i;
+      uint32_t pass = 0;
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        const int iq = i + q;   // only live positions are read (never past the block)
+        if (iq < 64 && ((x >> iq) & 1u)) {
+          const uint8_t c = window_byte(win, backwards ? input - 1 - (bb + q) : input + (bb + q));
+          pass |= (uint32_t)((((uint32_t)c & mask) == val) != neg) << q;
+        }
       }
-      if (pass) r |= 1ull << i;
+      res |= ((uint64_t)pass << i) & x;
+      x &= i + 4 >= 64 ? 0ull : ~0ull << (i + 4);
     }
-    if (r == 0) return 0;
-    m = r;
+    if (res == 0) return 0;
+    m = res;
     base += 1;
     ip += sz;
   }
@@ -293,22 +344,45 @@ __device__ int fast_re_set(const uint8_t* __restrict__ code, uint32_t len,
 // interpreted from there.  (The code blob is allocated with kCodeBytes of
 // padding, so the aligned loads never leave it.)
 constexpr uint32_t kCodeBytes = 48;
-__device__ __forceinline__ const uint8_t* stage_code(const uint8_t* code, uint32_t len,
-                                                     uint8_t* buf) {
+constexpr uint32_t kNoLds = 0xFFFFFFFFu;
+__device__ __forceinline__ uint32_t stage_code(const uint8_t* code, uint32_t len, uint32_t buf) {
   const uintptr_t a = (uintptr_t)code, lo = a & ~(uintptr_t)15;
   const uint32_t head = (uint32_t)(a - lo);
-  if (buf == nullptr || head + len > kCodeBytes) return code;
+  if (buf == kNoLds || head + len > kCodeBytes) return kNoLds;
   typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
   const u32x4* g = reinterpret_cast<const u32x4*>(lo);
   const u32x4 c0 = g[0], c1 = g[1], c2 = g[2];
-  u32x4* d = reinterpret_cast<u32x4*>(buf);
+  typedef __attribute__((address_space(3))) u32x4 lds_u4;
+  lds_u4* d = reinterpret_cast<lds_u4*>((uintptr_t)buf);
   d[0] = c0;
   d[1] = c1;
   d[2] = c2;
   return buf + head;
 }
 
-__device__ __forceinline__ bool fast_re_decide(const uint8_t* code, uint32_t len,
+// scan.c:778-880 for a fast-exec string: the forward program from the call's
+// offset, then (if it matched) the backward one.
+template <class Code>
+__device__ __forceinline__ bool fast_re_call(const VerifyParams& p, const DevRe& r, Code fwd,
+                                             Code bwd, const uint8_t* d, uint64_t offset,
+                                             uint32_t lds) {
+  if (YAMD_VERIFY_DIAG == 8) {   // profiling: the staging loads without interpretation
+    const ByteWindow w = stage_window(p, d, false, lds);
+    return (window_byte(w, d) ^ fwd[0]) == 0x5Au;
+  }
+  if (r.fwd_len == 1)   // forward program = MATCH: forward_matches = 0
+    return r.bwd_len > 0 &&
+           fast_re_decide(bwd, r.bwd_len, d, offset, true, stage_window(p, d, true, lds));
+  if (!fast_re_decide(fwd, r.fwd_len, d, p.size - offset, false, stage_window(p, d, false, lds)))
+    return false;
+  if (r.bwd_len > 0 &&
+      !fast_re_decide(bwd, r.bwd_len, d, offset, true, stage_window(p, d, true, lds)))
+    return false;
+  return true;
+}
+
+template <class Code>
+__device__ __forceinline__ bool fast_re_decide(const Code code, uint32_t len,
                                                const uint8_t* input, uint64_t avail,
                                                bool backwards, const ByteWindow& win) {
   const int v = fast_re_set(code, len, input, avail, backwards, win);
@@ -526,16 +600,13 @@ __device__ int general_re_reachable(const uint8_t* __restrict__ code, uint32_t l
   return kPathUnknown;
 }
 
-#ifndef YAMD_VERIFY_DIAG
-#define YAMD_VERIFY_DIAG 0   // profiling builds only: 1 = decide nothing, 2 = no regex decisions
-#endif
 
 // _yr_scan_verify_re_match (scan.c:778-880) for FAST ascii hex strings: the
 // forward program from `offset` must reach MATCH (else forward_matches == -1:
 // return), a zero-length forward match needs a backward program, and with a
 // backward program its MATCHes are the only way to _yr_scan_match_callback.
 __device__ bool re_call_matters(const VerifyParams& p, const DevPoolRec& e, uint32_t flags,
-                                uint64_t offset, uint32_t lds, uint8_t* codebuf) {
+                                uint64_t offset, uint32_t lds, uint32_t codebuf) {
   if (YAMD_VERIFY_DIAG == 2) return true;
   if (!p.re_on) return true;
   const DevRe r = e.re;
@@ -548,20 +619,11 @@ __device__ bool re_call_matters(const VerifyParams& p, const DevPoolRec& e, uint
     // forward and backward programs are contiguous in the blob (the shim and
     // yarc.cpp lay them out so): stage both at once when they fit
     if (r.bwd_len == 0 || r.bwd_off == r.fwd_off + r.fwd_len) {
-      const uint8_t* both = stage_code(fwd, r.fwd_len + r.bwd_len, codebuf);
-      fwd = both;
-      bwd = both + r.fwd_len;
+      const uint32_t at = stage_code(fwd, r.fwd_len + r.bwd_len, codebuf);
+      if (at != kNoLds)
+        return fast_re_call(p, r, LdsCode{at}, LdsCode{at + r.fwd_len}, d, offset, lds);
     }
-    if (r.fwd_len == 1)   // forward program = MATCH: forward_matches = 0
-      return r.bwd_len > 0 &&
-             fast_re_decide(bwd, r.bwd_len, d, offset, true, stage_window(p, d, true, lds));
-    if (!fast_re_decide(fwd, r.fwd_len, d, p.size - offset, false,
-                        stage_window(p, d, false, lds)))
-      return false;
-    if (r.bwd_len > 0 &&
-        !fast_re_decide(bwd, r.bwd_len, d, offset, true, stage_window(p, d, true, lds)))
-      return false;
-    return true;
+    return fast_re_call(p, r, GlobalCode{fwd}, GlobalCode{bwd}, d, offset, lds);
   }
   // yr_re_exec strings: the ascii attempt runs for ASCII / base64 strings, the
   // wide one (flags | RE_FLAGS_WIDE) for WIDE non-base64 strings when the
@@ -590,7 +652,7 @@ __device__ bool re_call_matters(const VerifyParams& p, const DevPoolRec& e, uint
 // have an effect?  false only where the reference provably returns without
 // touching the context.
 __device__ bool call_matters(const VerifyParams& p, const DevPoolRec& st, uint64_t offset,
-                             uint32_t lds, uint8_t* codebuf) {
+                             uint32_t lds, uint32_t codebuf) {
   if (YAMD_VERIFY_DIAG == 1) return false;
   // scan.c:1013: data_size - offset <= 0 (size_t) <=> offset == size
   if (offset >= p.size) return false;
@@ -619,16 +681,19 @@ __device__ bool call_matters(const VerifyParams& p, const DevPoolRec& st, uint64
   const uint64_t avail = p.size - offset;
   const uint8_t* s = p.str_bytes + st.bytes_off;
   const uint32_t n = st.length;
+  // the compared bytes from LDS (one round trip of 16-byte loads) instead of
+  // one dependent byte load per character
+  const ByteWindow w = stage_window(p, d, false, lds);
   if (st.flags & kStrNoCase) {
-    if ((st.flags & kStrAscii) && cmp_ascii(d, avail, s, n, p.lowercase)) return n != 0;
-    if ((st.flags & kStrWide) && cmp_wide(d, avail, s, n, p.lowercase)) return n != 0;
+    if ((st.flags & kStrAscii) && cmp_ascii(d, avail, s, n, p.lowercase, w)) return n != 0;
+    if ((st.flags & kStrWide) && cmp_wide(d, avail, s, n, p.lowercase, w)) return n != 0;
     return false;
   }
-  if ((st.flags & kStrAscii) && cmp_ascii(d, avail, s, n, nullptr)) return n != 0;
-  if ((st.flags & kStrWide) && cmp_wide(d, avail, s, n, nullptr)) return n != 0;
+  if ((st.flags & kStrAscii) && cmp_ascii(d, avail, s, n, nullptr, w)) return n != 0;
+  if ((st.flags & kStrWide) && cmp_wide(d, avail, s, n, nullptr, w)) return n != 0;
   if (st.flags & kStrXor) {
-    if ((st.flags & kStrWide) && cmp_xor(d, avail, s, n, true)) return true;
-    if (cmp_xor(d, avail, s, n, false)) return true;
+    if ((st.flags & kStrWide) && cmp_xor(d, avail, s, n, true, w)) return true;
+    if (cmp_xor(d, avail, s, n, false, w)) return true;
   }
   return false;
 }
@@ -640,10 +705,16 @@ __device__ bool call_matters(const VerifyParams& p, const DevPoolRec& st, uint64
 constexpr uint32_t kKeepOverflow = 1u << 31;
 template <int PASS>
 __device__ __forceinline__ void verify_one(const VerifyParams& p, uint64_t c, uint32_t lds,
-                                           uint8_t* codebuf, uint32_t keep, uint32_t head,
+                                           uint32_t codebuf, uint32_t keep, uint32_t head,
                                            uint64_t o, uint32_t& count) {
   const uint64_t i = p.all ? p.all_first + c : p.positions[c];
+  if (!PASS && YAMD_VERIFY_DIAG == 3) {   // profiling: candidate positions only
+    p.counts[c] = 0; p.keep[c] = 0; p.heads[c] = (uint32_t)i; count = 0; return;
+  }
   if (!PASS) head = node_head(p, i);
+  if (!PASS && YAMD_VERIFY_DIAG >= 4) {   // profiling: + the state's list head
+    p.counts[c] = 0; p.keep[c] = 0; p.heads[c] = head; count = 0; return;
+  }
   const bool decide = !PASS || (keep & kKeepOverflow);
   uint32_t n = 0, t = 0, mask = 0;
   // scanner.c:105-121: the list of state_i in pool order
@@ -712,7 +783,7 @@ __global__ __launch_bounds__(256) void verify_kernel(VerifyParams p) {
   __shared__ uint32_t wsum[4];
   // (the low 32 bits of a flat LDS address are the LDS offset)
   const uint32_t lds = (uint32_t)(uintptr_t)(win + threadIdx.x * kWinBytes);
-  uint8_t* codebuf = code + threadIdx.x * kCodeBytes;
+  const uint32_t codebuf = (uint32_t)(uintptr_t)(code + threadIdx.x * kCodeBytes);
   const uint64_t c = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
   const bool in = c < p.count;
   uint32_t n = 0, total = 0;
