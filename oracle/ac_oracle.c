@@ -220,7 +220,8 @@ void oracle_xorshift_fill(uint8_t* buf, uint64_t n, uint64_t seed)
  *     wicompare; else ascii compare, wide wcompare, then (XOR) wide xor then
  *     xor; no effect iff forward_matches == 0 (:974-975);
  *   - the comparisons _yr_scan_compare / icompare / wcompare / wicompare /
- *     xor_compare / xor_wcompare (scan.c:62-255), lowercase = yr_lowercase.
+ *     xor_compare / xor_wcompare (scan.c:62-255), lowercase = yr_lowercase;
+ *   - the FULL_WORD test of _yr_scan_match_callback (scan.c:672-694).
  * Base64 literal strings are not restated: always kept (as on the device).
  * Non-literal strings: decided by re_call_effect when the pool entry has a
  * fast-exec program (re_kind[k] == 1, tests/golden tables v2), else kept.
@@ -229,11 +230,18 @@ void oracle_xorshift_fill(uint8_t* buf, uint64_t n, uint64_t seed)
 #define SF_NO_CASE 0x04u
 #define SF_ASCII 0x08u
 #define SF_WIDE 0x10u
+#define SF_FULL_WORD 0x80u
 #define SF_LITERAL 0x400u
 #define SF_FITS_IN_ATOM 0x800u
 #define SF_FIXED_OFFSET 0x8000u
 #define SF_XOR 0x80000u
 #define SF_BASE64_ANY (0x200000u | 0x400000u)
+
+/* yr_isalnum (strutils.c:240-244) */
+static int re_is_alnum(uint8_t c)
+{
+  return (c >= 0x30 && c <= 0x39) || (c >= 0x41 && c <= 0x5a) || (c >= 0x61 && c <= 0x7a);
+}
 
 static uint64_t fwd_plain(const uint8_t* d, uint64_t avail, const uint8_t* s, uint32_t n,
                           const uint8_t* low)
@@ -646,6 +654,24 @@ int64_t oracle_literal_effect(
         {
           if (f & SF_WIDE) fm = fwd_xor(d, avail, str, n, 1);
           if (fm == 0) fm = fwd_xor(d, avail, str, n, 0);
+        }
+      }
+      /* _yr_scan_match_callback (scan.c:672-694): a FULL_WORD match touching an
+       * alphanumeric character (yr_isalnum, strutils.c:240-244) is dropped;
+       * wide (forward_matches == 2 * length, scan.c:977-978): an alphanumeric
+       * followed by 0x00 */
+      if (fm != 0 && (f & SF_FULL_WORD))
+      {
+        if (fm == 2ull * n)
+        {
+          if (off >= 2 && data[off - 1] == 0 && re_is_alnum(data[off - 2])) fm = 0;
+          else if (off + fm + 1 < size && data[off + fm + 1] == 0 && re_is_alnum(data[off + fm]))
+            fm = 0;
+        }
+        else
+        {
+          if (off >= 1 && re_is_alnum(data[off - 1])) fm = 0;
+          else if (off + fm < size && re_is_alnum(data[off + fm])) fm = 0;
         }
       }
     }

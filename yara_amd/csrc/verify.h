@@ -10,6 +10,7 @@ namespace yamd {
 constexpr uint32_t kStrNoCase = 0x04;
 constexpr uint32_t kStrAscii = 0x08;
 constexpr uint32_t kStrWide = 0x10;
+constexpr uint32_t kStrFullWord = 0x80;
 constexpr uint32_t kStrLiteral = 0x400;
 constexpr uint32_t kStrFitsInAtom = 0x800;
 constexpr uint32_t kStrFixedOffset = 0x8000;

@@ -660,7 +660,7 @@ __device__ bool call_matters(const VerifyParams& p, const DevPoolRec& st, uint64
   if ((st.flags & kStrFixedOffset) && st.fixed_offset != (int64_t)(p.data_base + offset))
     return false;
   if ((st.flags & (kStrLiteral | kStrFitsInAtom)) == (kStrLiteral | kStrFitsInAtom) &&
-      !(st.flags & kStrUnmodelled))
+      !(st.flags & (kStrUnmodelled | kStrFullWord)))
     return st.backtrack != 0;   // scan.c:907-915: decided without reading data
   // Every byte the call may read lies in [offset - YR_RE_SCAN_LIMIT, offset +
   // max(YR_RE_SCAN_LIMIT, 2 * length)) (regexp scans are limited to
@@ -681,21 +681,40 @@ __device__ bool call_matters(const VerifyParams& p, const DevPoolRec& st, uint64
   const uint64_t avail = p.size - offset;
   const uint8_t* s = p.str_bytes + st.bytes_off;
   const uint32_t n = st.length;
-  // the compared bytes from LDS (one round trip of 16-byte loads) instead of
-  // one dependent byte load per character
-  const ByteWindow w = stage_window(p, d, false, lds);
-  if (st.flags & kStrNoCase) {
-    if ((st.flags & kStrAscii) && cmp_ascii(d, avail, s, n, p.lowercase, w)) return n != 0;
-    if ((st.flags & kStrWide) && cmp_wide(d, avail, s, n, p.lowercase, w)) return n != 0;
-    return false;
+  uint64_t fm = 0;   // forward_matches
+  ByteWindow w = {nullptr, lds};
+  if (st.flags & kStrFitsInAtom) {
+    fm = st.backtrack;   // scan.c:912-915
+  } else {
+    // the compared bytes from LDS (one round trip of 16-byte loads) instead of
+    // one dependent byte load per character
+    w = stage_window(p, d, false, lds);
+    const uint8_t* lower = (st.flags & kStrNoCase) ? p.lowercase : nullptr;
+    if ((st.flags & kStrAscii) && cmp_ascii(d, avail, s, n, lower, w)) fm = n;
+    if (fm == 0 && (st.flags & kStrWide) && cmp_wide(d, avail, s, n, lower, w)) fm = 2ull * n;
+    if (fm == 0 && !(st.flags & kStrNoCase) && (st.flags & kStrXor)) {
+      if ((st.flags & kStrWide) && cmp_xor(d, avail, s, n, true, w)) fm = 2ull * n;
+      if (fm == 0 && cmp_xor(d, avail, s, n, false, w)) fm = n;
+    }
   }
-  if ((st.flags & kStrAscii) && cmp_ascii(d, avail, s, n, nullptr, w)) return n != 0;
-  if ((st.flags & kStrWide) && cmp_wide(d, avail, s, n, nullptr, w)) return n != 0;
-  if (st.flags & kStrXor) {
-    if ((st.flags & kStrWide) && cmp_xor(d, avail, s, n, true, w)) return true;
-    if (cmp_xor(d, avail, s, n, false, w)) return true;
+  if (fm == 0) return false;   // scan.c:974-975
+  if (!(st.flags & kStrFullWord)) return true;
+  // _yr_scan_match_callback's FULL_WORD test (scan.c:672-694): the match is
+  // dropped when an alphanumeric character (yr_isalnum) touches it -- for the
+  // wide form, an alphanumeric followed by 0x00
+  auto at = [&](uint64_t k) { return window_byte(w, p.data + k); };
+  auto alnum = [](uint8_t c) {
+    return (c >= 0x30 && c <= 0x39) || (c >= 0x41 && c <= 0x5a) || (c >= 0x61 && c <= 0x7a);
+  };
+  if (fm == 2ull * n) {   // RE_FLAGS_WIDE (scan.c:977-978)
+    if (offset >= 2 && at(offset - 1) == 0 && alnum(at(offset - 2))) return false;
+    if (offset + fm + 1 < p.size && at(offset + fm + 1) == 0 && alnum(at(offset + fm)))
+      return false;
+  } else {
+    if (offset >= 1 && alnum(at(offset - 1))) return false;
+    if (offset + fm < p.size && alnum(at(offset + fm))) return false;
   }
-  return false;
+  return true;
 }
 
 // One candidate: PASS 0 decides every call of its list, counts the records and
