@@ -325,14 +325,16 @@ typedef struct
  * of the reference loop (scanner.c:105-121) minus those that provably return
  * without effect: a literal string whose comparison fails
  * (_yr_scan_verify_literal_match returns before _yr_scan_match_callback,
- * scan.c:974-975), a FIXED_OFFSET string at another offset (scan.c:1023),
- * offset == size (scan.c:1013), and -- with yr_amd_tables_set_re_code -- a
- * regexp string whose program provably cannot match from the call's offset
- * (_yr_scan_verify_re_match, scan.c:778-880): hex strings' fast-exec programs
- * (yr_re_fast_exec, re.c:2150-2391) are decided exactly as a reachability
- * question; other regexps' yr_re_exec programs (re.c:1693-2072) over an
- * over-approximation (locale-dependent classes, assertions and repeat counts
- * unconstrained) with a 1000-step search budget below RE_MAX_FIBERS, so calls
+ * scan.c:974-975) or whose FULL_WORD match touches an alphanumeric character
+ * (_yr_scan_match_callback, scan.c:672-694), a FIXED_OFFSET string at another
+ * offset (scan.c:1023), offset == size (scan.c:1013), and -- with
+ * yr_amd_tables_set_re_code -- a regexp string whose program provably cannot
+ * match from the call's offset (_yr_scan_verify_re_match, scan.c:778-880):
+ * hex strings' fast-exec programs (yr_re_fast_exec, re.c:2150-2391) in the
+ * reference's position-set form; other regexps' yr_re_exec programs
+ * (re.c:1693-2072) by an exact search over every opcode's semantics (keeping
+ * a call where the reference's SPLIT fiber-kill rule, re.c:1482-1495, might
+ * end the only path) with a 1000-step budget below RE_MAX_FIBERS, so calls
  * that could fail with ERROR_TOO_MANY_RE_FIBERS are always kept.  Base64
  * strings are always kept.  Kept calls are verified by re.c / scan.c on the
  * host.  data_base = YR_MEMORY_BLOCK.base.  After yr_amd_scan_window, a call
