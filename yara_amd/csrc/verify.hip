@@ -136,6 +136,28 @@ __device__ __forceinline__ uint8_t window_byte(const ByteWindow& w, const uint8_
   return *at;
 }
 
+// The input bytes of one regexp direction through the staged window with
+// 32-bit offsets: byte b (0, 1, ... away from the call's offset, backwards
+// or forwards) is window byte rel0 + b (forwards) or rel0 - 1 - b
+// (backwards); outside the window it is read from memory.  (window_byte's
+// 64-bit pointer compares cost several VOP3 instructions per byte.)
+struct DirWindow {
+  int32_t rel0;   // window index of input[0]
+  uint32_t lds;
+  const uint8_t* input;
+  bool backwards;
+  __device__ DirWindow(const ByteWindow& w, const uint8_t* in, bool bw)
+      : rel0(w.lo != nullptr ? (int32_t)(in - w.lo) : -(1 << 30)), lds(w.lds), input(in),
+        backwards(bw) {}
+  __device__ uint8_t operator()(int b) const {
+    const int32_t k = backwards ? rel0 - 1 - b : rel0 + b;
+    if ((uint32_t)k < (uint32_t)kWinBytes)
+      return *reinterpret_cast<const __attribute__((address_space(3))) uint8_t*>(
+          (uintptr_t)(lds + (uint32_t)k));
+    return backwards ? input[-1 - b] : input[b];
+  }
+};
+
 // _yr_scan_compare / _yr_scan_icompare (scan.c:142-179): forward match length
 // of the ascii form, 0 if none.
 __device__ bool cmp_ascii(const uint8_t* d, uint64_t avail, const uint8_t* s, uint32_t n,
@@ -267,6 +289,7 @@ template <class Code>
 __device__ int fast_re_set(const Code code, uint32_t len, const uint8_t* __restrict__ input,
                            uint64_t avail, bool backwards, const ByteWindow& win) {
   const int maxb = (int)min<uint64_t>(avail, (uint64_t)kReScanLimit);
+  const DirWindow in(win, input, backwards);
   int base = 0;
   uint64_t m = 1;
   uint32_t ip = 0;
@@ -322,7 +345,7 @@ __device__ int fast_re_set(const Code code, uint32_t len, const uint8_t* __restr
       for (int q = 0; q < 4; ++q) {
         const int iq = i + q;   // only live positions are read (never past the block)
         if (iq < 64 && ((x >> iq) & 1u)) {
-          const uint8_t c = window_byte(win, backwards ? input - 1 - (bb + q) : input + (bb + q));
+          const uint8_t c = in(bb + q);
           pass |= (uint32_t)((((uint32_t)c & mask) == val) != neg) << q;
         }
       }
