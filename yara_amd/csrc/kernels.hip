@@ -278,7 +278,7 @@ __device__ __forceinline__ void drain(const ScanParams& p, WaveQueue& q, uint32_
     if (q.defer) drain_complete<MODE>(p, q, lane, seg_start, out, found);
   const uint32_t n = q.count;   // <= kQueueCap = kWave
   q.count = 0;
-  if constexpr (MODE == 7) return;   // ablation: ring appends only, entries dropped
+  if constexpr (MODE == 7 || MODE == 8) return;   // ablations: appends only, entries dropped
   __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
   uint32_t maybe = 0, off0 = 0, m = 0;   // m: bit j = lane byte j passes the filter
   const uint32_t ent = q.ring + lane * (kQueueEntryWords * 4);
@@ -545,9 +545,13 @@ __device__ __forceinline__ void ring_append(const ScanParams& p, WaveQueue& q, S
       asm("v_mad_u32_u24 %0, %1, 24, %2" : "=v"(ent) : "v"(below), "s"(base));
       // 24-byte entry: the lane's 16 bytes (as loaded: no register moves),
       // the 4 bytes before them, the lane index in the segment
-      lds_store2(ent, S[1], S[2]);
-      lds_store2(ent + 8, S[3], S[4]);
-      lds_store2(ent + 16, S[0], (tile_off >> 4) + lane);
+      if constexpr (MODE == 8) {   // ablation: the append's slot arithmetic, no LDS writes
+        asm volatile("" ::"v"(ent), "v"((tile_off >> 4) + lane));
+      } else {
+        lds_store2(ent, S[1], S[2]);
+        lds_store2(ent + 8, S[3], S[4]);
+        lds_store2(ent + 16, S[0], (tile_off >> 4) + lane);
+      }
     }
     q.count += n;
   }
@@ -603,7 +607,7 @@ __device__ __forceinline__ void tile_step(const ScanParams& p, WaveQueue& q, Seg
 // (no queue), 3 = input streaming only (no filter), 4 = stage 1 with
 // bank-conflict-free LDS addresses, 5 = stage 1 VALU without the LDS reads,
 // 6 = stage 1 addresses + LDS reads without the bit tests, 7 = stage 1 +
-// ring appends, drains drop the entries, 8 = (unused), 9 = exact check replaced by one L2 dword
+// ring appends, drains drop the entries, 8 = 7 without the ring's LDS writes, 9 = exact check replaced by one L2 dword
 // load per hit, 10 = exact-check VALU with the bucket loads replaced by values,
 // 11 = product with all 8 filter reads of a tile issued before any test,
 // 12 = product without the bucket probes (first level only).
@@ -813,6 +817,7 @@ hipError_t launch_scan(const ScanParams& p, int grid, hipStream_t s, int mode) {
     case 5: hipLaunchKernelGGL(scan_segments_kernel<5>, dim3(grid), dim3(kWGThreads), lds, s, p); break;
     case 6: hipLaunchKernelGGL(scan_segments_kernel<6>, dim3(grid), dim3(kWGThreads), lds, s, p); break;
     case 7: hipLaunchKernelGGL(scan_segments_kernel<7>, dim3(grid), dim3(kWGThreads), lds, s, p); break;
+    case 8: hipLaunchKernelGGL(scan_segments_kernel<8>, dim3(grid), dim3(kWGThreads), lds, s, p); break;
     case 9: hipLaunchKernelGGL(scan_segments_kernel<9>, dim3(grid), dim3(kWGThreads), lds, s, p); break;
     case 10: hipLaunchKernelGGL(scan_segments_kernel<10>, dim3(grid), dim3(kWGThreads), lds, s, p); break;
     case 11: hipLaunchKernelGGL(scan_segments_kernel<11>, dim3(grid), dim3(kWGThreads), lds, s, p); break;
