@@ -688,11 +688,20 @@ __global__ __launch_bounds__(kWGThreads, 1) void scan_segments_kernel(ScanParams
   // bounds, loop counts, ring base) stays in SGPRs with scalar branches
   const uint32_t wid = __builtin_amdgcn_readfirstlane(threadIdx.x / kWave);
   const uint32_t total_waves = gridDim.x * kWavesPerWG;
-  for (uint32_t seg = blockIdx.x * kWavesPerWG + wid; seg < p.n_segments; seg += total_waves) {
+  uint32_t seg = blockIdx.x * kWavesPerWG + wid;
+  while (seg < p.n_segments) {
     WaveQueue q;   // (per segment: its per-lane state then stays in registers)
     q.ring = kFilterBytes + wid * (kQueueCap * kQueueEntryWords * 4);
     q.pend = kFilterBytes + kQueueBytes + wid * (kWave * 8);
     scan_segment<MODE>(p, q, seg, lane);
+    if (p.seg_next == nullptr) {
+      seg += total_waves;
+    } else {
+      // dynamic: the next unclaimed segment (one vector atomic per wave)
+      uint32_t t = 0;
+      if (lane == 0) t = atomicAdd(p.seg_next, 1u);
+      seg = __builtin_amdgcn_readfirstlane(t);
+    }
   }
 }
 
@@ -712,6 +721,9 @@ __global__ __launch_bounds__(1024) void seg_offsets_kernel(const uint32_t* seg_c
   const uint32_t lo = min(t * per, n), hi = min(lo + per, n);
   uint64_t s = 0;
   uint32_t mx = 0;
+  // (unrolled: the loads of a run are independent and go out together -- one
+  // round trip per 16 segments instead of one per segment)
+#pragma unroll 16
   for (uint32_t i = lo; i < hi; ++i) {
     const uint32_t c = seg_count[i];
     s += min(c, cap);
@@ -745,6 +757,7 @@ __global__ __launch_bounds__(1024) void seg_offsets_kernel(const uint32_t* seg_c
   }
   __syncthreads();
   uint64_t run = wsum[w] + incl - s;
+#pragma unroll 16
   for (uint32_t i = lo; i < hi; ++i) {
     seg_offset[i] = run;
     run += min(seg_count[i], cap);
@@ -756,13 +769,15 @@ __global__ __launch_bounds__(256) void seg_scatter_kernel(const uint32_t* seg_co
                                                           const uint64_t* seg_base,
                                                           const uint64_t* seg_offset, uint32_t cap,
                                                           uint64_t byte_begin, uint32_t seg_bytes,
-                                                          uint64_t* positions) {
-  const uint32_t seg = blockIdx.x;
+                                                          uint32_t n_segments, uint64_t* positions) {
+  // one wave per segment (segments hold tens to hundreds of candidates)
+  const uint32_t seg = blockIdx.x * (blockDim.x / kWave) + threadIdx.x / kWave;
+  if (seg >= n_segments) return;
   const uint32_t c = min(seg_count[seg], cap);
   const uint64_t base = byte_begin + (uint64_t)seg * seg_bytes + 1;  // position = byte + 1
   const uint32_t* src = seg_out + (seg_base ? seg_base[seg] : (size_t)seg * cap);
   uint64_t* dst = positions + seg_offset[seg];
-  for (uint32_t i = threadIdx.x; i < c; i += blockDim.x) dst[i] = base + src[i];
+  for (uint32_t i = threadIdx.x % kWave; i < c; i += kWave) dst[i] = base + src[i];
 }
 
 // ---------------------------------------------------------------------------
@@ -833,9 +848,9 @@ hipError_t launch_compact(const ScanParams& p, uint64_t* seg_offset, uint64_t* s
     hipLaunchKernelGGL(seg_offsets_kernel, dim3(1), dim3(1024), 0, s, p.seg_count, p.n_segments,
                        p.seg_cap, seg_offset, summary);
   } else {
-    hipLaunchKernelGGL(seg_scatter_kernel, dim3(p.n_segments), dim3(256), 0, s, p.seg_count,
-                       p.seg_out, p.seg_base, seg_offset, p.seg_cap, p.byte_begin, p.seg_bytes,
-                       positions);
+    hipLaunchKernelGGL(seg_scatter_kernel, dim3((p.n_segments + 3) / 4), dim3(256), 0, s,
+                       p.seg_count, p.seg_out, p.seg_base, seg_offset, p.seg_cap, p.byte_begin,
+                       p.seg_bytes, p.n_segments, positions);
   }
   return hipGetLastError();
 }

@@ -135,6 +135,7 @@ struct yr_amd_scanner {
 
   int diag_mode = 0;   // profiling ablation of the scan kernel (0 = product)
   uint64_t* d_seg_base = nullptr; // exact per-segment output offsets (overflow rerun)
+  uint32_t* d_seg_next = nullptr; // dynamic segment counter (YAMD_SEG_KIB experiments)
   size_t seg_base_cap = 0;
   uint64_t rerun_total = 0;
 
@@ -203,10 +204,15 @@ int ensure_segments(yr_amd_scanner* s, uint32_t n_segments, uint32_t seg_cap) {
   return grow(s->d_seg_out, s->seg_out_cap, (size_t)n_segments * seg_cap);
 }
 
-uint32_t choose_seg_bytes(uint64_t nbytes, int num_cus) {
-  // aim for >= 1 segment per wave of a full-chip launch, 4-64 tiles each
+uint32_t choose_seg_bytes(uint64_t nbytes, int num_cus, uint32_t target) {
+  // k segments of at most `target` bytes per wave of a full-chip launch (the
+  // same k for every wave: waves take segments round-robin), 4+ tiles each.
+  // (One 1 MiB segment per wave for a 4 GiB block.  128 KiB segments, 8 per
+  // wave, measured 3-4 % faster in back-to-back kernel timings but 1-2 %
+  // slower in the bench's pipelined steps, profiles/r02_segment_size.json.)
   const uint64_t waves = (uint64_t)num_cus * kWavesPerWG;
-  uint64_t per = (nbytes + waves - 1) / waves;
+  const uint64_t k = std::max<uint64_t>(1, (nbytes + waves * target - 1) / (waves * target));
+  uint64_t per = (nbytes + waves * k - 1) / (waves * k);
   per = (per + kTile - 1) / kTile * kTile;
   return (uint32_t)std::min<uint64_t>(std::max<uint64_t>(per, 4 * kTile), kSegment);
 }
@@ -350,7 +356,7 @@ int yr_amd_scanner_destroy(yr_amd_scanner* s) {
                   (void*)s->d_seg_offset,
                   (void*)s->d_seg_out, (void*)s->d_positions, (void*)s->d_summary,
                   (void*)s->d_vcount, (void*)s->d_vkeep, (void*)s->d_vblock, (void*)s->d_vrec,
-                  (void*)s->d_seg_base})
+                  (void*)s->d_seg_base, (void*)s->d_seg_next})
     if (p) (void)hipFree(p);
   if (s->h_summary) (void)hipHostFree(s->h_summary);
   if (s->ev_begin) (void)hipEventDestroy(s->ev_begin);
@@ -426,7 +432,16 @@ int yr_amd_scan_window(yr_amd_scanner* s, const uint8_t* d_window, uint64_t wind
   HIP_TRY(hipSetDevice(t->device));
 
   const uint64_t nbytes = byte_end - byte_begin;
-  const uint32_t seg_bytes = choose_seg_bytes(nbytes, t->num_cus);
+  // YAMD_SEG_KIB=<k>: segment target k KiB instead of kSegmentTarget, and with
+  // YAMD_SEG_DYNAMIC set, segments after a wave's first are claimed from a
+  // counter (scan_segments_kernel's seg_next) -- profiling experiments only
+  static const uint32_t seg_target = [] {
+    const char* e = getenv("YAMD_SEG_KIB");
+    const uint32_t k = e ? (uint32_t)atoi(e) : 0u;
+    return k >= 4 && k * 1024u <= kSegment ? k * 1024u : kSegmentTarget;
+  }();
+  static const bool dynamic = getenv("YAMD_SEG_DYNAMIC") != nullptr;
+  const uint32_t seg_bytes = choose_seg_bytes(nbytes, t->num_cus, seg_target);
   const uint64_t n_segments64 = (nbytes + seg_bytes - 1) / seg_bytes;
   if (n_segments64 > 0xFFFFFFFFull) return YR_AMD_INVALID_ARGUMENT;
   const uint32_t n_segments = (uint32_t)n_segments64;
@@ -455,6 +470,13 @@ int yr_amd_scan_window(yr_amd_scanner* s, const uint8_t* d_window, uint64_t wind
   p.seg_base = nullptr;
   s->last_grid = (int)std::min<uint64_t>((n_segments + kWavesPerWG - 1) / kWavesPerWG,
                                          (uint64_t)t->num_cus);
+  p.seg_next = nullptr;
+  if (dynamic) {
+    if (s->d_seg_next == nullptr) HIP_TRY(hipMalloc(&s->d_seg_next, sizeof(uint32_t)));
+    p.seg_next = s->d_seg_next;
+    HIP_TRY(hipMemsetD32Async((hipDeviceptr_t)s->d_seg_next,
+                              (int)((uint32_t)s->last_grid * kWavesPerWG), 1, s->stream));
+  }
   return run_scan(s);
 }
 
