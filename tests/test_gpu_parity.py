@@ -290,3 +290,35 @@ def test_scan_window_rejects_bad_windows():
         with pytest.raises(yara_amd.YaraAmdError) as e:
             sc.scan_window(d.data_ptr(), *args)
         assert e.value.code == yara_amd.INVALID_ARGUMENT
+
+
+@pytest.mark.parametrize("env", [{"YAMD_SEG_KIB": "4"},
+                                 {"YAMD_SEG_KIB": "4", "YAMD_SEG_DYNAMIC": "1"},
+                                 {"YAMD_SEG_KIB": "8", "YAMD_SEG_DYNAMIC": "1"}])
+def test_segment_schedules(env):
+    """The profiling switches of the segment schedule (several segments per
+    wave, round-robin or claimed from a counter; read once per process, hence
+    a child process) give the same candidate stream.  48 MiB with 4-8 KiB
+    segments: several segments per wave of the full-chip grid."""
+    import os
+    import subprocess
+    import sys
+    repo = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    code = (
+        "import sys; sys.path[:0] = [%r, %r, %r]\n"
+        "import numpy as np, torch, yara_amd, oracle\n"
+        "from conftest import ref_tables, tables_npz\n"
+        "n = (48 << 20) + 777\n"
+        "d = torch.empty(n + 16, dtype=torch.uint8, device='cuda')\n"
+        "yara_amd.fill_xorshift64(d.data_ptr(), n, 3); torch.cuda.synchronize()\n"
+        "sc = yara_amd.Scanner(yara_amd.Tables.from_npz(tables_npz('C'), device=0))\n"
+        "from yara_amd._hip import d2h_u64\n"
+        "sc.scan_device(d.data_ptr(), n); p, c = sc.device_result()[:2]\n"
+        "got = d2h_u64(p, c)\n"
+        "ref = oracle.candidates(ref_tables('C'), d[:n].cpu().numpy())\n"
+        "assert np.array_equal(got, ref), (len(got), len(ref))\n"
+        "print('ok', len(got))\n" % (repo, os.path.join(repo, "tests"),
+                                     os.path.join(repo, "tests", "golden")))
+    r = subprocess.run([sys.executable, "-c", code], capture_output=True, text=True, timeout=240,
+                       env=dict(os.environ, **env))
+    assert r.returncode == 0 and "ok" in r.stdout, r.stdout + r.stderr

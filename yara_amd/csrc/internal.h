@@ -20,7 +20,8 @@ constexpr int kWave = 64;
 constexpr int kBytesPerLane = 16;
 constexpr int kTile = kWave * kBytesPerLane;        // 1024 B
 constexpr uint32_t kSegment = 1u << 20;   // max segment: 1 MiB (ring entries hold offset/16 in 16 bits)
-constexpr uint32_t kSegmentTarget = kSegment;   // preferred segment size (scanner.cpp)
+constexpr uint32_t kSegmentTarget = kSegment;
+constexpr uint32_t kMaxByteKeys = 4;   // 1-byte keys tested in stage 1 (more: filter)   // preferred segment size (scanner.cpp)
 constexpr int kWavesPerWG = 16;
 constexpr int kWGThreads = kWave * kWavesPerWG;     // 1024
 
@@ -145,6 +146,8 @@ struct ScanParams {
   uint32_t* seg_out;        // [n_segments * seg_cap] byte offset within segment
   const uint64_t* seg_base; // null: segment s writes at seg_out + s * seg_cap; else at
                             // seg_out + seg_base[s] (exact-size rerun after an overflow)
+  uint32_t byte_keys;       // FlatTables::byte_keys / n_byte_keys (stage-1 byte test)
+  uint32_t n_byte_keys;
   uint32_t* seg_next;       // null: wave w takes segments w, w + waves, ...; else each wave
                             // takes its first segment by index and the next ones from this
                             // counter (initialised to the launch's wave count)

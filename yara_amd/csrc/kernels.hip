@@ -180,6 +180,12 @@ struct WaveQueue {
   uint32_t wb, ob, ib, db;
 };
 constexpr uint32_t kNoHit = 0xFFFFFFFFu;
+// Kernel variant: the product kernel for rule sets whose 1-byte keys are tested
+// byte by byte in stage 1 (byte_keys_any below) instead of in the filter.
+constexpr int kModeByteKeys = 20;
+// A pending entry's offset with this bit set is a certain candidate (its last
+// byte is a 1-byte key): no bucket probe.  (Segment offsets are < 2^20.)
+constexpr uint32_t kConfirmed = 0x80000000u;
 static_assert(kQueueCap == kWave, "a drain takes the whole ring, one entry per lane");
 
 // Bucket-probe every pending hit (one lane each) and append the survivors,
@@ -190,7 +196,17 @@ __device__ __forceinline__ void flush_pending(const ScanParams& p, WaveQueue& q,
   __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
   bool keep = false;
   uint32_t off = 0;
-  if (lane < q.pend_n) {
+  if constexpr (MODE == kModeByteKeys) {
+    // confirmed entries need no probe; a flush of nothing else makes no
+    // memory round trip at all
+    u32x2 e = {0u, 0u};
+    if (lane < q.pend_n) e = lds_load<u32x2>(q.pend + 8 * lane);
+    const bool conf = (e.y & kConfirmed) != 0u;
+    off = e.y & ~kConfirmed;
+    const bool probe = lane < q.pend_n && !conf;
+    keep = lane < q.pend_n && conf;
+    if (__ballot(probe) != 0 && probe) keep = exact_check(e.x, seg_start + off + 1, p);
+  } else if (lane < q.pend_n) {
     const u32x2 e = lds_load<u32x2>(q.pend + 8 * lane);
     off = e.y;
     keep = MODE == 12 ? true : exact_check(e.x, seg_start + off + 1, p);   // 12: ablation
@@ -230,12 +246,48 @@ __device__ __forceinline__ uint32_t dense_mask(uint32_t h) {
   return (h | (h >> 8)) & 0xFFFFu;
 }
 
+// The product kernel for rule sets with up to kMaxByteKeys 1-byte keys: those
+// keys are not in the window filter (each would set 65,536 windows of it) but
+// tested here, on every byte of the lane, with the zero-byte test of
+// x ^ key * 0x01010101 -- one v_xor, one v_add and one v_bitop3 per dword and
+// key.  Positions whose last byte is such a key are 1/256 of random input per
+// key: they are candidates in their own right, not filter noise.
+// Does some byte of the lane's 16 equal a 1-byte key?  (nonzero = yes)
+__device__ __forceinline__ uint32_t byte_keys_any(const uint32_t (&S)[6], const ScanParams& p) {
+  uint32_t acc = 0;
+  for (uint32_t k = 0; k < p.n_byte_keys; ++k) {   // wave-uniform, 1..kMaxByteKeys
+    const uint32_t v = ((p.byte_keys >> (8 * k)) & 0xFFu) * 0x01010101u;
+#pragma unroll
+    for (int d = 1; d <= 4; ++d) {
+      const uint32_t t = S[d] ^ v;
+      // acc |= (t - 0x01010101) & ~t: nonzero in bit 7 of some byte iff a byte of t is 0
+      asm("v_bitop3_b32 %0, %1, %2, %0 bitop3:0xba" : "+v"(acc) : "v"(t - 0x01010101u), "v"(t));
+    }
+  }
+  return acc & 0x80808080u;
+}
+
+// Per-position form (drains): bit j <=> lane byte j equals a 1-byte key.
+__device__ __forceinline__ uint32_t byte_keys_mask(const uint32_t (&S)[6], const ScanParams& p) {
+  uint32_t m = 0;
+  for (uint32_t k = 0; k < p.n_byte_keys; ++k) {
+    const uint32_t v = ((p.byte_keys >> (8 * k)) & 0xFFu) * 0x01010101u;
+#pragma unroll
+    for (int d = 0; d < 4; ++d) {
+      const uint32_t t = S[1 + d] ^ v;
+      const uint32_t z = ~(((t & 0x7F7F7F7Fu) + 0x7F7F7F7Fu) | t) & 0x80808080u;   // exact
+      m |= (((z >> 7) & 1u) | ((z >> 14) & 2u) | ((z >> 21) & 4u) | ((z >> 28) & 8u)) << (4 * d);
+    }
+  }
+  return m;
+}
+
 // Kernel variants whose drains defer their first-level loads (WaveQueue).
 #ifndef YAMD_DEFER_FL
 #define YAMD_DEFER_FL 1
 #endif
 template <int MODE>
-constexpr bool kDeferFl = YAMD_DEFER_FL && (MODE == 0 || MODE == 12);
+constexpr bool kDeferFl = YAMD_DEFER_FL && (MODE == 0 || MODE == 12 || MODE == kModeByteKeys);
 
 // Consume a deferred drain's first-level words: the lanes' hits that pass go,
 // in order, to the pending list.
@@ -281,6 +333,7 @@ __device__ __forceinline__ void drain(const ScanParams& p, WaveQueue& q, uint32_
   if constexpr (MODE == 7 || MODE == 8) return;   // ablations: appends only, entries dropped
   __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
   uint32_t maybe = 0, off0 = 0, m = 0;   // m: bit j = lane byte j passes the filter
+  uint32_t kmask = 0;                    // bit j = lane byte j is a 1-byte key (certain)
   const uint32_t ent = q.ring + lane * (kQueueEntryWords * 4);
   if (lane < n) {
     // the entry's 16 positions again, now with a per-position result: the
@@ -291,6 +344,10 @@ __device__ __forceinline__ void drain(const ScanParams& p, WaveQueue& q, uint32_
     const uint32_t S[6] = {e45.x, e01.x, e01.y, e23.x, e23.y, 0u};
     off0 = (e45.y & 0xFFFFu) * kBytesPerLane;
     m = dense_mask(stage1<0, false>(S, lane));
+    if constexpr (MODE == kModeByteKeys) {
+      kmask = byte_keys_mask(S, p);
+      m |= kmask;
+    }
     if (off0 + kBytesPerLane > seg_len) {   // the segment's partial last tile
       const uint32_t lim = off0 >= seg_len ? 0u : seg_len - off0;
       m &= lim >= 16u ? 0xFFFFu : (1u << lim) - 1u;
@@ -318,7 +375,7 @@ __device__ __forceinline__ void drain(const ScanParams& p, WaveQueue& q, uint32_
       return;
     }
   }
-  if (MODE == 0 && (p.len_mask & 6u) != 0u) {
+  if ((MODE == 0 || MODE == kModeByteKeys) && (p.len_mask & 6u) != 0u) {
     maybe = m;   // 1-/2-byte keys: no first level, every hit goes to the buckets
   } else {
     while (m) {
@@ -354,7 +411,8 @@ __device__ __forceinline__ void drain(const ScanParams& p, WaveQueue& q, uint32_
     while (maybe != 0u && idx < base + kWave) {
       const uint32_t j = (uint32_t)__builtin_ctz(maybe);
       maybe &= maybe - 1;
-      lds_store2(q.pend + 8 * (idx - base), window4(ent, j), off0 + j);
+      lds_store2(q.pend + 8 * (idx - base), window4(ent, j),
+                 (off0 + j) | (MODE == kModeByteKeys && ((kmask >> j) & 1u) ? kConfirmed : 0u));
       ++idx;
     }
     if (end <= base + kWave) {
@@ -591,7 +649,8 @@ __device__ __forceinline__ void tile_step(const ScanParams& p, WaveQueue& q, Seg
                                           uint4 cur, uint32_t tile_off, uint32_t lane) {
   uint32_t S[6];
   tile_context(st, cur, S);
-  const uint32_t any = stage1<MODE, true>(S, lane);
+  uint32_t any = stage1<MODE == kModeByteKeys ? 0 : MODE, true>(S, lane);
+  if constexpr (MODE == kModeByteKeys) any |= byte_keys_any(S, p);
   if constexpr (kDeferFl<MODE>)
     if (q.defer) drain_complete<MODE>(p, q, lane, st.seg_start, st.out, st.found);
   ring_append<MODE, TAIL>(p, q, st, S, any, tile_off, lane);
@@ -837,7 +896,13 @@ hipError_t launch_scan(const ScanParams& p, int grid, hipStream_t s, int mode) {
     case 10: hipLaunchKernelGGL(scan_segments_kernel<10>, dim3(grid), dim3(kWGThreads), lds, s, p); break;
     case 11: hipLaunchKernelGGL(scan_segments_kernel<11>, dim3(grid), dim3(kWGThreads), lds, s, p); break;
     case 12: hipLaunchKernelGGL(scan_segments_kernel<12>, dim3(grid), dim3(kWGThreads), lds, s, p); break;
-    default: hipLaunchKernelGGL(scan_segments_kernel<0>, dim3(grid), dim3(kWGThreads), lds, s, p); break;
+    default:
+      if (p.n_byte_keys != 0)
+        hipLaunchKernelGGL(scan_segments_kernel<kModeByteKeys>, dim3(grid), dim3(kWGThreads), lds,
+                           s, p);
+      else
+        hipLaunchKernelGGL(scan_segments_kernel<0>, dim3(grid), dim3(kWGThreads), lds, s, p);
+      break;
   }
   return hipGetLastError();
 }
@@ -871,7 +936,8 @@ hipError_t configure_scan_kernel() {
                         (const void*)scan_segments_kernel<6>, (const void*)scan_segments_kernel<7>,
                         (const void*)scan_segments_kernel<8>, (const void*)scan_segments_kernel<9>,
                         (const void*)scan_segments_kernel<10>, (const void*)scan_segments_kernel<11>,
-                        (const void*)scan_segments_kernel<12>}) {
+                        (const void*)scan_segments_kernel<12>,
+                        (const void*)scan_segments_kernel<kModeByteKeys>}) {
     hipError_t r = hipFuncSetAttribute(k, hipFuncAttributeMaxDynamicSharedMemorySize, lds);
     if (r != hipSuccess) e = r;
   }

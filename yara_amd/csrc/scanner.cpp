@@ -462,6 +462,8 @@ int yr_amd_scan_window(yr_amd_scanner* s, const uint8_t* d_window, uint64_t wind
   p.t4_mask = t->flat.t4_mask;
   p.exact_flags = t->flat.exact_flags;
   p.len_mask = t->flat.len_mask;
+  p.byte_keys = t->flat.byte_keys;
+  p.n_byte_keys = t->flat.n_byte_keys;
   p.n_segments = n_segments;
   p.seg_bytes = seg_bytes;
   p.seg_cap = seg_cap;

@@ -260,9 +260,15 @@ int flatten_tables(const uint32_t* T, const uint32_t* M, uint32_t n_slots,
     out.len_mask |= 1u << k.len;
   }
 
-  // 3a. LDS window filter over the 3 bytes ending at each position
+  // 3a. LDS window filter over the 3 bytes ending at each position; up to
+  //     kMaxByteKeys 1-byte keys are tested by the kernel byte by byte instead
+  if (out.keys_by_len[1] <= kMaxByteKeys) {
+    for (const Key& k : out.keys)
+      if (k.len == 1) out.byte_keys |= (k.bytes & 0xFFu) << (8 * out.n_byte_keys++);
+  }
   out.filter.assign(kFilterWords, 0u);
   for (const Key& k : out.keys) {
+    if (k.len == 1 && out.n_byte_keys != 0) continue;
     switch (k.len) {
       case 4: filter_set(out.filter, k.bytes >> 8); break;
       case 3: filter_set(out.filter, k.bytes); break;

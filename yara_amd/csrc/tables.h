@@ -31,6 +31,10 @@ struct FlatTables {
   std::vector<uint32_t> exact;     // exact key sets (internal.h layout)
   uint32_t t3_off = 0, t3_mask = 0, t4_off = 0, t4_mask = 0, exact_flags = 0;
   uint32_t len_mask = 0;
+  // 1-byte keys tested byte by byte in the scan kernel's stage 1 instead of
+  // being inserted into the window filter (each would fill it with 65,536
+  // windows): up to kMaxByteKeys key bytes, packed low byte first
+  uint32_t byte_keys = 0, n_byte_keys = 0;
 
   // accepting trie nodes -> match-list head M[slot], by the node's string
   // (pre-verification: the walk's state at a candidate is its longest
