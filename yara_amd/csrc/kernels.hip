@@ -186,6 +186,7 @@ constexpr int kModeByteKeys = 20;
 // A pending entry's offset with this bit set is a certain candidate (its last
 // byte is a 1-byte key): no bucket probe.  (Segment offsets are < 2^20.)
 constexpr uint32_t kConfirmed = 0x80000000u;
+static_assert(kSegment <= kConfirmed, "segment offsets must leave the confirmed bit free");
 static_assert(kQueueCap == kWave, "a drain takes the whole ring, one entry per lane");
 
 // Bucket-probe every pending hit (one lane each) and append the survivors,
