@@ -322,3 +322,31 @@ def test_segment_schedules(env):
     r = subprocess.run([sys.executable, "-c", code], capture_output=True, text=True, timeout=240,
                        env=dict(os.environ, **env))
     assert r.returncode == 0 and "ok" in r.stdout, r.stdout + r.stderr
+
+
+def test_byte_keys_stage1_path():
+    """1-byte keys (incl. 0x00 and 0xFF) tested byte by byte in stage 1
+    (kernels.hip kModeByteKeys) instead of the window filter: candidate streams
+    equal the oracle's on ragged sizes, all-zero blocks, and blocks whose last
+    bytes are zeros (the ragged tail tile is zero-filled past the block end,
+    which must not turn into candidates).  Tables: tests/golden/rules/
+    bytekeys.yar compiled by the stock libyara (make_golden.py)."""
+    tab = ref_tables("bytekeys")
+    sc = yara_amd.Scanner(yara_amd.Tables.from_npz(tables_npz("bytekeys"), device=0))
+    rng = np.random.default_rng(17)
+    alpha = np.frombuffer(b"\x00\x41\x51\xffabcwxyzrstQ", np.uint8)
+    sizes = [1, 2, 3, 15, 16, 17, 1023, 1024, 1025, 4095, 65537, (1 << 20) + 13, 3 << 20]
+    for n in sizes:
+        data = alpha[rng.integers(0, len(alpha), n)]
+        for variant in (data, np.zeros(n, np.uint8), np.concatenate(
+                [data[: n // 2], np.zeros(n - n // 2, np.uint8)])):
+            variant = np.ascontiguousarray(variant)
+            pos, allp = sc.candidates(variant)
+            assert not allp
+            np.testing.assert_array_equal(pos, oracle.candidates(tab, variant), err_msg=str(n))
+    # random bytes: 1/256 of positions per byte key
+    data = oracle.xorshift(8 << 20, 5)
+    pos, _ = sc.candidates(data)
+    ref = oracle.candidates(tab, data)
+    assert len(ref) > 3 * (8 << 20) // 256 * 0.9
+    np.testing.assert_array_equal(pos, ref)
