@@ -472,7 +472,8 @@ struct SegState {
   uint32_t seg_len;
   uint32_t* out;
   uint32_t found;
-  uint32_t carry;   // the 4 bytes before the current tile (lane 0's window head)
+  uint32_t carry;   // lane 0: the 4 bytes before the current tile (its window head)
+  bool lane0;
 };
 
 // Stage 1 of one 1 KiB tile: the filter over its 1024 byte positions.  Returns
@@ -625,8 +626,14 @@ __device__ __forceinline__ void ring_append(const ScanParams& p, WaveQueue& q, S
 // The lane's window context: the previous lane's last dword (lane 0: the
 // previous tile's, or the halo), then its own 16 bytes.
 __device__ __forceinline__ void tile_context(SegState& st, const uint4& cur, uint32_t (&S)[6]) {
-  S[0] = __builtin_amdgcn_update_dpp(st.carry, cur.w, 0x138, 0xF, 0xF, false);  // wave_shr:1
-  st.carry = __builtin_amdgcn_readlane(cur.w, kWave - 1);
+  // wave_ror:1 gives lanes 1..63 the previous lane's last dword and lane 0
+  // this tile's lane 63 -- the next tile's lane-0 context; lane 0 takes the
+  // one kept from the previous tile (st.carry, meaningful in lane 0 only).
+  // (One DPP move and one select: 1 % faster than a wave_shr:1 into the
+  // carry plus a v_readlane of the next one, profiles/r02_carry_ror_ab.json.)
+  const uint32_t rot = __builtin_amdgcn_mov_dpp(cur.w, 0x13C, 0xF, 0xF, true);
+  S[0] = st.lane0 ? st.carry : rot;
+  st.carry = rot;
   S[1] = cur.x;
   S[2] = cur.y;
   S[3] = cur.z;
@@ -690,6 +697,7 @@ __device__ __forceinline__ void scan_segment(const ScanParams& p, WaveQueue& q, 
   st.seg_len = (uint32_t)(seg_end - st.seg_start);
   st.out = p.seg_out + (p.seg_base ? p.seg_base[seg] : (size_t)seg * p.seg_cap);
   st.found = 0;
+  st.lane0 = lane == 0;
   // bytes read: [seg_start - 4, seg_end) only -- never past byte_end, so a
   // shard that holds just its window of the block is never read beyond it
   const uint64_t avail = p.byte_end - st.seg_start;
