@@ -18,7 +18,8 @@ import oracle
 import yara_amd
 from conftest import GOLDEN, case_arrays, case_data, golden, ref_tables, tables_npz
 
-SETS = ["B", "C", "E", "lit", "hex", "rx", "short", "root"] + ["fuzz%d" % s for s in range(12)]
+SETS = ["B", "C", "E", "lit", "hex", "rx", "short", "root", "bytekeys"] + [
+    "fuzz%d" % s for s in range(12)]
 CASES = golden()["cases"]
 
 
@@ -35,7 +36,7 @@ def test_yarc_tables_equal_compiler_tables(name):
 
 
 @pytest.mark.parametrize("case", [c for c in ("B_64M", "short_1M", "lit_1M", "hex_1M", "rx_1M",
-                                               "root_4K", "short_3")])
+                                               "root_4K", "short_3", "bytekeys_1M")])
 def test_yarc_tables_replay_reference_stream(case):
     rec = CASES[case]
     arr = case_arrays(case)
