@@ -34,7 +34,7 @@ needs_check = pytest.mark.skipif(not os.path.exists(CHECK),
 
 def _rules_file(tmp_path, name):
     p = tmp_path / ("%s.yar" % name)
-    if name in ("short", "root", "lit", "hex", "rx"):
+    if name in ("short", "root", "lit", "hex", "rx", "bytekeys"):
         p.write_text(open(os.path.join(GOLDEN, "rules", name + ".yar")).read())
     else:
         p.write_text(gen_rules.gen(name))
@@ -75,6 +75,8 @@ CASES = [
     ("rx", "rx", 1 << 20, 0, 0),
     ("rx", "rx", 1 << 20, 8192, 1024),
     ("rx", "rx", 4 << 20, 3000, 64),
+    ("bytekeys", "alpha", 2 << 20, 0, 0),          # 1-byte keys in stage 1 (kModeByteKeys)
+    ("bytekeys", "alpha", 2 << 20, 4096, 512),
 ]
 
 
