@@ -350,3 +350,29 @@ def test_byte_keys_stage1_path():
     ref = oracle.candidates(tab, data)
     assert len(ref) > 3 * (8 << 20) // 256 * 0.9
     np.testing.assert_array_equal(pos, ref)
+
+
+def test_block_larger_than_4gib():
+    """A single 8 GiB block (past 32-bit byte offsets: 8,192 segments, positions
+    above 2^32): its candidates up to 4 GiB equal the golden C_4G stream (the
+    input is the same xorshift64 prefix), and the block's stream equals the
+    concatenation of three device shards scanned separately."""
+    torch = _torch()
+    rec = CASES["C_4G"]
+    n = (8 << 30) + 4096 + 7
+    d = torch.empty(n + 16, dtype=torch.uint8, device="cuda")
+    yara_amd.fill_xorshift64(d.data_ptr(), n, rec["data"][1])
+    torch.cuda.synchronize()
+    sc = yara_amd.Scanner(dev_tables("C"))
+    sc.scan_device(d.data_ptr(), n)
+    full = _d2h(torch, *sc.device_result()[:2])
+    assert np.all(np.diff(full.astype(np.int64)) > 0) and int(full[-1]) > (1 << 32)
+    head = full[full <= rec["size"]]
+    assert len(head) == rec["candidate_count"]
+    assert oracle.positions_sha(head) == rec["candidate_sha"]
+    cuts = [0, (3 << 30) + 16, (6 << 30) + 4096, n]
+    parts = []
+    for a, b in zip(cuts[:-1], cuts[1:]):
+        sc.scan_device(d.data_ptr(), n, a, b)
+        parts.append(_d2h(torch, *sc.device_result()[:2]))
+    np.testing.assert_array_equal(np.concatenate(parts), full)
