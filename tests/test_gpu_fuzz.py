@@ -1,0 +1,66 @@
+"""Randomised GPU parity on fresh rule sets (beyond the committed fixtures).
+
+For 48 rule sets from tests/golden/fuzz_rules.py (seeds 300..347, disjoint from
+the 12 fixtures and the 200 CPU fuzz seeds) the stock compiler builds the
+Aho-Corasick tables and string records (oracle/_ref/refdump, compiled in the
+build container; it reads only the generated rules file) and the HIP path
+scans a planted 1 MiB buffer:
+
+  * the candidate stream equals the oracle's restatement of scanner.c:45-176
+    (oracle.candidates, itself pinned to stock libyara by test_oracle_fuzz.py);
+  * the on-device pre-verification records equal the oracle's verify-call
+    stream (oracle.walk_verify) filtered by the oracle's restatement of the
+    scan.c / re.c decisions (oracle.literal_effect), call for call.
+
+The sets mix 1- to 4-byte atoms (incl. the stage-1 byte-key kernel variant),
+literal flags and hex / regexp strings.  Skipped where refdump is absent.
+"""
+import os
+import subprocess
+
+import numpy as np
+import pytest
+
+import fuzz_rules
+import make_golden
+import oracle
+import yara_amd
+from conftest import REPO
+from oracle.tables import read_tables
+
+REFDUMP = os.path.join(REPO, "oracle", "_ref", "refdump")
+SEEDS = range(300, 348)
+SIZE = 1 << 20
+
+pytestmark = [pytest.mark.gpu,
+              pytest.mark.skipif(not os.access(REFDUMP, os.X_OK),
+                                 reason="oracle/_ref/refdump not built (needs /root/reference)")]
+
+
+@pytest.mark.parametrize("seed", SEEDS)
+def test_fresh_rule_set_on_gpu(tmp_path, seed):
+    rules = str(tmp_path / "f.yar")
+    with open(rules, "w") as f:
+        f.write(fuzz_rules.gen(seed))
+    subprocess.run([REFDUMP, "tables", rules, str(tmp_path / "t.bin")], check=True,
+                   stdout=subprocess.DEVNULL)
+    t = read_tables(str(tmp_path / "t.bin"))
+    z = make_golden.tables_dict(t)
+    npz = str(tmp_path / "t.npz")
+    np.savez(npz, **z)
+    data = fuzz_rules.buffer(oracle.xorshift, seed, SIZE)
+
+    sc = yara_amd.Scanner(yara_amd.Tables.from_npz(npz, device=0, strings=True))
+    pos, allp = sc.candidates(data)
+    if t.M[0] != 0:
+        assert allp
+    else:
+        assert not allp
+        np.testing.assert_array_equal(pos, oracle.candidates(t, data))
+
+    vpos, vidx = oracle.walk_verify(t, data)
+    keep = oracle.literal_effect(np.load(npz), vpos, vidx, data)
+    want_off = (vpos.astype(np.int64) - t.pool_backtrack[vidx].astype(np.int64))[keep]
+    recs = sc.verify_calls(data)
+    np.testing.assert_array_equal(recs["offset"].astype(np.int64), want_off)
+    np.testing.assert_array_equal(recs["pool_index"], vidx[keep])
