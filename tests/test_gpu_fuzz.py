@@ -10,7 +10,10 @@ scans a planted 1 MiB buffer:
     (oracle.candidates, itself pinned to stock libyara by test_oracle_fuzz.py);
   * the on-device pre-verification records equal the oracle's verify-call
     stream (oracle.walk_verify) filtered by the oracle's restatement of the
-    scan.c / re.c decisions (oracle.literal_effect), call for call.
+    scan.c / re.c decisions (oracle.literal_effect), call for call;
+  * three shards of the block, each scanned from a device window holding only
+    the shard plus the rule set's verify halos (yr_amd_scan_window, the
+    multi-GPU path), give the same records concatenated.
 
 The sets mix 1- to 4-byte atoms (incl. the stage-1 byte-key kernel variant),
 literal flags and hex / regexp strings.  Skipped where refdump is absent.
@@ -64,3 +67,25 @@ def test_fresh_rule_set_on_gpu(tmp_path, seed):
     recs = sc.verify_calls(data)
     np.testing.assert_array_equal(recs["offset"].astype(np.int64), want_off)
     np.testing.assert_array_equal(recs["pool_index"], vidx[keep])
+
+    if t.M[0] != 0:
+        return
+    import torch
+    from yara_amd import dist as ydist
+    from yara_amd._hip import memcpy
+    before, after = ydist.tables_halos(sc.tables)
+    got = []
+    for r in range(3):
+        b, e = ydist.shard_bounds(SIZE, 3, r, align=1 << 12)
+        lo, hi = ydist.shard_window(SIZE, b, e, before, after)
+        win = torch.from_numpy(np.ascontiguousarray(data[lo:hi])).cuda()
+        sc.scan_window(win.data_ptr(), lo, hi, SIZE, b, e)
+        sc.device_result()
+        ptr, cnt = sc.verify_device(0)
+        h = torch.empty(max(cnt, 1) * 16, dtype=torch.uint8, device="cuda")
+        memcpy(h.data_ptr(), ptr, cnt * 16, 3)
+        got.append(np.frombuffer(h[:cnt * 16].cpu().numpy().tobytes(),
+                                 dtype=yara_amd._lib.VERIFY_REC_DTYPE))
+    got = np.concatenate(got)
+    np.testing.assert_array_equal(got["offset"].astype(np.int64), want_off)
+    np.testing.assert_array_equal(got["pool_index"], vidx[keep])
