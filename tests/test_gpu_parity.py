@@ -197,26 +197,6 @@ def test_device_shards_concatenate_to_full_stream():
         sc.scan_device(d.data_ptr(), n, a, b)
         parts.append(_d2h(torch, *sc.device_result()[:2]))
     np.testing.assert_array_equal(np.concatenate(parts), full)
-    # on-device pre-verification of the 8 GiB block: its records up to 4 GiB
-    # equal those of the 4 GiB block (offsets past 2^32 in the records)
-    from yara_amd._hip import memcpy
-
-    def records(scanner, size):
-        scanner.scan_device(d.data_ptr(), size)
-        scanner.device_result()
-        ptr, cnt = scanner.verify_device(0)
-        h = torch.empty(max(cnt, 1) * 16, dtype=torch.uint8, device="cuda")
-        memcpy(h.data_ptr(), ptr, cnt * 16, 3)
-        return np.frombuffer(h[:cnt * 16].cpu().numpy().tobytes(),
-                             dtype=yara_amd._lib.VERIFY_REC_DTYPE)
-    sv = yara_amd.Scanner(yara_amd.Tables.from_npz(tables_npz("C"), device=0, strings=True))
-    r8 = records(sv, n)
-    r4 = records(sv, rec["size"])
-    assert len(r4) > 0 and len(r8) > len(r4) and int(r8["offset"].max()) > (1 << 32)
-    head8 = r8[r8["offset"] < rec["size"] - 64]
-    head4 = r4[r4["offset"] < rec["size"] - 64]
-    np.testing.assert_array_equal(head8["offset"], head4["offset"])
-    np.testing.assert_array_equal(head8["pool_index"], head4["pool_index"])
     np.testing.assert_array_equal(full, oracle.candidates(ref_tables("C"), d[:n].cpu().numpy()))
 
 
@@ -396,3 +376,23 @@ def test_block_larger_than_4gib():
         sc.scan_device(d.data_ptr(), n, a, b)
         parts.append(_d2h(torch, *sc.device_result()[:2]))
     np.testing.assert_array_equal(np.concatenate(parts), full)
+    # on-device pre-verification of the 8 GiB block: its records up to 4 GiB
+    # equal those of the 4 GiB block (offsets past 2^32 in the records)
+    from yara_amd._hip import memcpy
+
+    def records(scanner, size):
+        scanner.scan_device(d.data_ptr(), size)
+        scanner.device_result()
+        ptr, cnt = scanner.verify_device(0)
+        h = torch.empty(max(cnt, 1) * 16, dtype=torch.uint8, device="cuda")
+        memcpy(h.data_ptr(), ptr, cnt * 16, 3)
+        return np.frombuffer(h[:cnt * 16].cpu().numpy().tobytes(),
+                             dtype=yara_amd._lib.VERIFY_REC_DTYPE)
+    sv = yara_amd.Scanner(yara_amd.Tables.from_npz(tables_npz("C"), device=0, strings=True))
+    r8 = records(sv, n)
+    r4 = records(sv, rec["size"])
+    assert len(r4) > 0 and len(r8) > len(r4) and int(r8["offset"].max()) > (1 << 32)
+    head8 = r8[r8["offset"] < rec["size"] - 64]
+    head4 = r4[r4["offset"] < rec["size"] - 64]
+    np.testing.assert_array_equal(head8["offset"], head4["offset"])
+    np.testing.assert_array_equal(head8["pool_index"], head4["pool_index"])
