@@ -128,6 +128,10 @@ typedef struct
    * records (candidates only): the 4-byte warm-up before, 0 after. */
   uint64_t verify_halo_before;
   uint64_t verify_halo_after;
+  /* Stage-1 filter form: 0 = pair filter (every position's window), 1 =
+   * even-position filter (rule sets whose keys are all 4 bytes long: the
+   * windows ending at even positions only, each key's prefix and suffix). */
+  uint32_t filter_mode;
 } yr_amd_tables_info;
 
 int yr_amd_tables_get_info(const yr_amd_tables* tables, yr_amd_tables_info* info);

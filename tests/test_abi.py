@@ -56,6 +56,14 @@ def test_flattening_stats(name, states, depth, keys):
     assert inf["max_depth"] == 4 and inf["root_accepting"] == 0
     # filter density bounds the stage-2 rate
     assert inf["filter_set_bits"] / (1 << inf["filter_bits"]) < 0.05
+    # 4-byte keys only: the even-position filter (internal.h kFilterEven)
+    assert inf["filter_mode"] == (1 if keys[:4] == [0, 0, 0, 0] else 0)
+
+
+def test_pair_filter_switch(monkeypatch):
+    monkeypatch.setenv("YAMD_PAIR_FILTER", "1")
+    inf = yara_amd.Tables.from_npz(tables_npz("E"), device=-1).info()
+    assert inf["filter_mode"] == 0
 
 
 def test_short_and_root_tables():

@@ -396,3 +396,37 @@ def test_block_larger_than_4gib():
     head4 = r4[r4["offset"] < rec["size"] - 64]
     np.testing.assert_array_equal(head8["offset"], head4["offset"])
     np.testing.assert_array_equal(head8["pool_index"], head4["pool_index"])
+
+
+@pytest.mark.parametrize("rules", ["B", "E"])
+@pytest.mark.parametrize("stride", [5, 7, 16, 33, 1021])
+def test_even_filter_planted_keys(rules, stride, monkeypatch):
+    """Rule sets whose keys are all 4 bytes scan with the even-position filter
+    (internal.h kFilterEven: only the windows ending at even positions are
+    tested, each key inserted as its 3-byte prefix and suffix).  Strings planted
+    every `stride` bytes end at both parities and at every lane byte (lane,
+    tile and segment edges included; strides 5 and 7 put several hits in one
+    lane, the drains' synchronous path): candidates equal the oracle's and the
+    pair filter's."""
+    import planted
+    import gen_rules
+    tab = ref_tables(rules)
+    inst = [b for b, _ in planted.string_instances(gen_rules.gen(rules))]
+    size = (2 << 20) + 12345
+    data = oracle.xorshift(size, 43).copy()
+    k, off = 0, 3
+    while off + 40 < size:
+        s = inst[k % len(inst)][: max(4, stride - 1)]
+        data[off:off + len(s)] = np.frombuffer(s, np.uint8)
+        k += 1
+        off += stride + (k % 3 == 0)                # drift through every residue mod 16
+    even = dev_tables(rules)
+    assert even.info()["filter_mode"] == 1
+    pos, allp = yara_amd.Scanner(even).candidates(data)
+    ref = oracle.candidates(tab, data)
+    assert not allp and len(ref) > size // stride // 8
+    np.testing.assert_array_equal(pos, ref)
+    monkeypatch.setenv("YAMD_PAIR_FILTER", "1")
+    pair = yara_amd.Tables.from_npz(tables_npz(rules), device=0)
+    assert pair.info()["filter_mode"] == 0
+    np.testing.assert_array_equal(yara_amd.Scanner(pair).candidates(data)[0], ref)

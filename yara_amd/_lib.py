@@ -45,6 +45,7 @@ class TablesInfo(ctypes.Structure):
         ("max_backtrack", ctypes.c_uint32),
         ("verify_halo_before", ctypes.c_uint64),
         ("verify_halo_after", ctypes.c_uint64),
+        ("filter_mode", ctypes.c_uint32),
     ]
 
 

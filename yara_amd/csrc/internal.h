@@ -53,6 +53,14 @@ constexpr uint32_t kScanLdsBytes = kFilterBytes + kQueueBytes + kPendBytes;     
 // (config C: 0.39% of random positions pass instead of 0.15%), but one
 // ds_read_b64 now serves two positions: the LDS bank conflicts of these
 // random reads were the kernel's bound.
+// Even-position filter (kFilterEven, rule sets whose keys are all 4 bytes):
+// the left role alone, tested at the even positions only (half of stage 1's
+// work).  A 4-byte key ending at an even position has its last 3 bytes as the
+// window there; one ending at an odd position k + 1 has its first 3 bytes as
+// the window ending at k.  Both are inserted in the left role, so a pass at
+// even k makes k and k + 1 filter hits; the exact stages are unchanged.
+constexpr uint32_t kFilterPair = 0;
+constexpr uint32_t kFilterEven = 1;
 struct FilterProbe {
   uint32_t block;  // index into the kFilterWords / 2 blocks; words 2*block, 2*block+1
   uint32_t b_lo, b_hi;
@@ -148,6 +156,7 @@ struct ScanParams {
                             // seg_out + seg_base[s] (exact-size rerun after an overflow)
   uint32_t byte_keys;       // FlatTables::byte_keys / n_byte_keys (stage-1 byte test)
   uint32_t n_byte_keys;
+  uint32_t filter_mode;     // kFilterPair / kFilterEven (FlatTables::filter_mode)
   uint32_t* seg_next;       // null: wave w takes segments w, w + waves, ...; else each wave
                             // takes its first segment by index and the next ones from this
                             // counter (initialised to the launch's wave count)

@@ -183,6 +183,9 @@ constexpr uint32_t kNoHit = 0xFFFFFFFFu;
 // Kernel variant: the product kernel for rule sets whose 1-byte keys are tested
 // byte by byte in stage 1 (byte_keys_any below) instead of in the filter.
 constexpr int kModeByteKeys = 20;
+// Kernel variant: the product kernel for the even-position filter
+// (internal.h kFilterEven: rule sets whose keys are all 4 bytes long).
+constexpr int kModeEven = 21;
 // A pending entry's offset with this bit set is a certain candidate (its last
 // byte is a 1-byte key): no bucket probe.  (Segment offsets are < 2^20.)
 constexpr uint32_t kConfirmed = 0x80000000u;
@@ -247,6 +250,20 @@ __device__ __forceinline__ uint32_t dense_mask(uint32_t h) {
   return (h | (h >> 8)) & 0xFFFFu;
 }
 
+// Per-position filter hits of a lane under the even-position filter (drains):
+// a pass of the window ending at even lane byte 2j makes bytes 2j and 2j + 1
+// hits (bit j <=> lane byte j).
+__device__ __forceinline__ uint32_t even_mask(const uint32_t (&S)[6]) {
+  uint32_t m = 0;
+#pragma unroll
+  for (int j = 0; j < kBytesPerLane / 2; ++j) {
+    const uint32_t x = pair_window(S, (uint32_t)j);
+    const u32x2 w = lds_load<u32x2>((x >> 7) & (kFilterBytes - 8));
+    m |= ((w.x >> (x & 31u)) & (w.y >> ((x >> 5) & 31u)) & 1u) << (2 * j);
+  }
+  return m | (m << 1);
+}
+
 // The product kernel for rule sets with up to kMaxByteKeys 1-byte keys: those
 // keys are not in the window filter (each would set 65,536 windows of it) but
 // tested here, on every byte of the lane, with the zero-byte test of
@@ -288,7 +305,8 @@ __device__ __forceinline__ uint32_t byte_keys_mask(const uint32_t (&S)[6], const
 #define YAMD_DEFER_FL 1
 #endif
 template <int MODE>
-constexpr bool kDeferFl = YAMD_DEFER_FL && (MODE == 0 || MODE == 12 || MODE == kModeByteKeys);
+constexpr bool kDeferFl =
+    YAMD_DEFER_FL && (MODE == 0 || MODE == 12 || MODE == kModeByteKeys || MODE == kModeEven);
 
 // Consume a deferred drain's first-level words: the lanes' hits that pass go,
 // in order, to the pending list.
@@ -344,7 +362,8 @@ __device__ __forceinline__ void drain(const ScanParams& p, WaveQueue& q, uint32_
     const u32x2 e45 = lds_load<u32x2>(ent + 16);
     const uint32_t S[6] = {e45.x, e01.x, e01.y, e23.x, e23.y, 0u};
     off0 = (e45.y & 0xFFFFu) * kBytesPerLane;
-    m = dense_mask(stage1<0, false>(S, lane));
+    if constexpr (MODE == kModeEven) m = even_mask(S);
+    else m = dense_mask(stage1<0, false>(S, lane));
     if constexpr (MODE == kModeByteKeys) {
       kmask = byte_keys_mask(S, p);
       m |= kmask;
@@ -513,7 +532,22 @@ __device__ __forceinline__ uint32_t stage1(const uint32_t (&S)[6], uint32_t lane
   // straight into byte n of accumulator r (position 4n + r), so bit 0 of that
   // byte is the position's result and no separate accumulate instruction is
   // needed; bits 1..7 of each byte are don't-care and masked off below.
-  if constexpr (kAny && MODE != 3 && MODE != 6) {
+  if constexpr (kAny && MODE == kModeEven) {
+    // the even-position filter: the left windows only (pairs 0-3, 4-7 into
+    // two accumulators), any pass of the lane in bit 0
+    uint32_t a[2];
+#pragma unroll
+    for (int j = 0; j < kPairs; ++j) {
+      const uint32_t x = xs[j];
+      const uint32_t ul = ws[j].x >> (x & 31u), vl = ws[j].y >> ((x >> 5) & 31u);
+      uint32_t& aq = a[j >> 2];
+      if ((j & 3) == 0) aq = ul & vl;
+      else asm("v_bitop3_b32 %0, %1, %2, %0 bitop3:0xea" : "+v"(aq) : "v"(ul), "v"(vl));
+    }
+    uint32_t t;
+    asm("v_bitop3_b32 %0, %1, %2, 1 bitop3:0xa8" : "=v"(t) : "v"(a[0]), "v"(a[1]));
+    return t;
+  } else if constexpr (kAny && MODE != 3 && MODE != 6) {
     // the main loop only needs "does any position of this lane pass?": OR the
     // shifted-word ANDs together (v_bitop3: full rate, unlike SDWA) and keep
     // bit 0; the drain recomputes the per-position results of the few lanes
@@ -915,6 +949,8 @@ hipError_t launch_scan(const ScanParams& p, int grid, hipStream_t s, int mode) {
       if (p.n_byte_keys != 0)
         hipLaunchKernelGGL(scan_segments_kernel<kModeByteKeys>, dim3(grid), dim3(kWGThreads), lds,
                            s, p);
+      else if (p.filter_mode == kFilterEven)
+        hipLaunchKernelGGL(scan_segments_kernel<kModeEven>, dim3(grid), dim3(kWGThreads), lds, s, p);
       else
         hipLaunchKernelGGL(scan_segments_kernel<0>, dim3(grid), dim3(kWGThreads), lds, s, p);
       break;
@@ -952,7 +988,8 @@ hipError_t configure_scan_kernel() {
                         (const void*)scan_segments_kernel<8>, (const void*)scan_segments_kernel<9>,
                         (const void*)scan_segments_kernel<10>, (const void*)scan_segments_kernel<11>,
                         (const void*)scan_segments_kernel<12>,
-                        (const void*)scan_segments_kernel<kModeByteKeys>}) {
+                        (const void*)scan_segments_kernel<kModeByteKeys>,
+                        (const void*)scan_segments_kernel<kModeEven>}) {
     hipError_t r = hipFuncSetAttribute(k, hipFuncAttributeMaxDynamicSharedMemorySize, lds);
     if (r != hipSuccess) e = r;
   }

@@ -303,6 +303,7 @@ int yr_amd_tables_get_info(const yr_amd_tables* t, yr_amd_tables_info* info) {
   info->root_accepting = f.root_accepting ? 1 : 0;
   info->filter_bits = kFilterLog2Bits;
   info->filter_set_bits = f.filter_set_bits;
+  info->filter_mode = f.filter_mode;
   info->exact_slots = 4 * (f.t3_mask + 1 + f.t4_mask + 1);
   uint32_t mb = 0;
   for (uint16_t b : f.pool_backtrack) mb = std::max<uint32_t>(mb, b);
@@ -464,6 +465,7 @@ int yr_amd_scan_window(yr_amd_scanner* s, const uint8_t* d_window, uint64_t wind
   p.len_mask = t->flat.len_mask;
   p.byte_keys = t->flat.byte_keys;
   p.n_byte_keys = t->flat.n_byte_keys;
+  p.filter_mode = t->flat.filter_mode;
   p.n_segments = n_segments;
   p.seg_bytes = seg_bytes;
   p.seg_cap = seg_cap;

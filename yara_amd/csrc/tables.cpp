@@ -19,6 +19,7 @@
 //    open-addressed hash table for the second stage.
 #include "tables.h"
 
+#include <stdlib.h>
 #include <string.h>
 
 #include <unordered_map>
@@ -39,11 +40,13 @@ struct Node {
 
 inline uint64_t node_key(uint32_t bytes, uint32_t depth) { return ((uint64_t)depth << 32) | bytes; }
 
+void filter_put(std::vector<uint32_t>& f, const FilterProbe& fp) {
+  f[2 * fp.block] |= 1u << fp.b_lo;
+  f[2 * fp.block + 1] |= 1u << fp.b_hi;
+}
 void filter_set(std::vector<uint32_t>& f, uint32_t w3) {
-  for (const FilterProbe fp : {filter_probe_left(w3), filter_probe_right(w3)}) {
-    f[2 * fp.block] |= 1u << fp.b_lo;
-    f[2 * fp.block + 1] |= 1u << fp.b_hi;
-  }
+  filter_put(f, filter_probe_left(w3));
+  filter_put(f, filter_probe_right(w3));
 }
 
 // Two-choice, 4-way bucketed cuckoo table of non-zero keys.  Load <= 1/2 to
@@ -267,7 +270,19 @@ int flatten_tables(const uint32_t* T, const uint32_t* M, uint32_t n_slots,
       if (k.len == 1) out.byte_keys |= (k.bytes & 0xFFu) << (8 * out.n_byte_keys++);
   }
   out.filter.assign(kFilterWords, 0u);
+  // 4-byte keys only: the even-position filter (internal.h kFilterEven).  A key
+  // ending at an even position has its suffix window there; one ending at an
+  // odd position has its prefix window ending at the even position before it.
+  // (YAMD_PAIR_FILTER: the pair filter regardless -- A/B measurements.)
+  if (out.len_mask == (1u << 4) && getenv("YAMD_PAIR_FILTER") == nullptr) {
+    out.filter_mode = kFilterEven;
+    for (const Key& k : out.keys) {
+      filter_put(out.filter, filter_probe_left(k.bytes >> 8));       // suffix
+      filter_put(out.filter, filter_probe_left(k.bytes & 0xFFFFFFu));  // prefix
+    }
+  }
   for (const Key& k : out.keys) {
+    if (out.filter_mode == kFilterEven) break;
     if (k.len == 1 && out.n_byte_keys != 0) continue;
     switch (k.len) {
       case 4: filter_set(out.filter, k.bytes >> 8); break;
