@@ -641,6 +641,69 @@ uint32_t fast_program_ok(const uint8_t* c, uint32_t len) {
   }
   return 0;
 }
+
+// The guard of a linear fast-exec program (verify.h DevGuard): 4 consecutive
+// positions the program must consume at a fixed distance from its start, or
+// right after its first REPEAT_ANY, with their (mask, value) byte tests; the
+// set with the most tested bits, ignoring the first `skip` positions (the
+// atom's bytes, which every candidate has).  Returns false when no such set
+// tests anything.
+bool fast_guard(const uint8_t* c, uint32_t len, uint32_t skip, bool backwards, DevGuard& g,
+                uint8_t& bs) {
+  struct Pos { uint8_t m, v; };
+  std::vector<Pos> head, tail;   // the run before the first REPEAT_ANY, the run after it
+  uint32_t mn = 0, mx = 0;
+  bool repeat = false;
+  for (uint32_t n = 0; n < len;) {
+    const uint8_t op = c[n];
+    std::vector<Pos>& run = repeat ? tail : head;
+    if (op == kReMatch) break;
+    if (op == kReRepeatAnyUngreedy) {
+      if (repeat) break;
+      mn = c[n + 1] | (c[n + 2] << 8);
+      mx = c[n + 3] | (c[n + 4] << 8);
+      repeat = true;
+      n += 5;
+      continue;
+    }
+    switch (op) {
+      case kReLiteral: run.push_back({0xFF, c[n + 1]}); n += 2; break;
+      case kReMaskedLiteral: run.push_back({c[n + 2], c[n + 1]}); n += 3; break;
+      case kReNotLiteral: run.push_back({0, 0}); n += 2; break;          // consumes, not tested
+      case kReMaskedNotLiteral: run.push_back({0, 0}); n += 3; break;
+      case kReAny: run.push_back({0, 0}); n += 1; break;
+      default: return false;
+    }
+    if (repeat && tail.size() >= 4) break;
+  }
+  auto bits = [](const std::vector<Pos>& r, uint32_t s, uint32_t from) {
+    uint32_t b = 0;
+    for (uint32_t t = 0; t < 4 && s + t < r.size(); ++t)
+      if (s + t >= from) b += (uint32_t)__builtin_popcount(r[s + t].m);
+    return b;
+  };
+  uint32_t best = 0, base = 0, span = 0;
+  const std::vector<Pos>* src = nullptr;
+  uint32_t src_at = 0;
+  for (uint32_t s0 = 0; s0 < std::max<size_t>(head.size(), 1) && s0 <= 15; ++s0) {
+    const uint32_t b = bits(head, s0, skip);
+    if (b > best) { best = b; base = s0; span = 0; src = &head; src_at = s0; }
+  }
+  if (repeat && head.size() + mn <= 15 && mx - mn <= 8) {
+    const uint32_t b = bits(tail, 0, 0);
+    if (b > best) { best = b; base = (uint32_t)head.size() + mn; span = mx - mn; src = &tail; src_at = 0; }
+  }
+  if (best == 0) return false;
+  g = DevGuard{0u, 0u};
+  for (uint32_t t = 0; t < 4 && src_at + t < src->size(); ++t) {
+    const Pos q = (*src)[src_at + t];
+    const uint32_t sh = 8 * (backwards ? 3 - t : t);
+    g.m |= (uint32_t)q.m << sh;
+    g.v |= (uint32_t)(q.m ? q.v : 0) << sh;
+  }
+  bs = (uint8_t)(base | span << 4);
+  return true;
+}
 }  // namespace
 
 int yr_amd_re_code_extent(const uint8_t* code, uint64_t avail, uint32_t* extent) {
@@ -685,8 +748,22 @@ int yr_amd_tables_set_re_code(yr_amd_tables* t, uint32_t n_pool, const uint32_t*
   if (code_len > 0) memcpy(padded.data(), code, (size_t)code_len);
   int r = upload(t->d_re_code, padded.data(), padded.size());
   if (r) return r;
-  // the programs go into the pool records (uploaded again)
-  for (uint32_t k = 0; k < n_pool; ++k) t->h_pool[k].re = re[k];
+  // the programs go into the pool records (uploaded again), fast programs with
+  // their guards (the forward program starts at the atom: its first
+  // `backtrack` bytes are the atom's)
+  for (uint32_t k = 0; k < n_pool; ++k) {
+    DevPoolRec& e = t->h_pool[k];
+    e.re = re[k];
+    e.fguard = e.bguard = DevGuard{0u, 0u};
+    e.fguard_bs = e.bguard_bs = 0;
+    if (re[k].fwd_len == 0 || !(t->h_str_flags[t->h_pool_string[k]] & kStrFastRegexp)) continue;
+    if (getenv("YAMD_NO_GUARDS") != nullptr) continue;   // A/B measurements only
+    if (!fast_guard(code + re[k].fwd_off, re[k].fwd_len, e.backtrack, false, e.fguard, e.fguard_bs))
+      e.fguard = DevGuard{0u, 0u};
+    if (re[k].bwd_len == 0 ||
+        !fast_guard(code + re[k].bwd_off, re[k].bwd_len, 0, true, e.bguard, e.bguard_bs))
+      e.bguard = DevGuard{0u, 0u};
+  }
   if (n_pool > 0 && hipMemcpy(t->d_pool, t->h_pool.data(), n_pool * sizeof(DevPoolRec),
                               hipMemcpyHostToDevice) != hipSuccess)
     return YR_AMD_INTERNAL_FATAL_ERROR;

@@ -34,20 +34,36 @@ constexpr uint8_t kReAny = 0xA0, kReLiteral = 0xA2, kReMaskedLiteral = 0xA4, kRe
                   kReNotLiteral = 0xAE, kReMaskedNotLiteral = 0xAF, kReRepeatAnyUngreedy = 0xB5;
 constexpr int kReScanLimit = 4096;   // YR_RE_SCAN_LIMIT (limits.h:163)
 
+// A necessary condition of a fast-exec program matching, computed on the host
+// from its opcodes (scanner.cpp fast_guard): with x_b the b-th input byte the
+// program reads (forwards x_b = data[offset + b], backwards data[offset - 1 -
+// b]), some j in [0, span] has (x_{base + j + t} & m_t) == v_t for t = 0..3
+// (m_t, v_t = byte t of m, v; forwards in program order, backwards in memory
+// order, i.e. byte 3 - t).  The positions are 4 consecutive bytes the program
+// must consume at a fixed distance (span 0: its first run of literal / masked /
+// any opcodes), or right after its first REPEAT_ANY {min, max} (base = the
+// run before it + min, span = max - min).  m == 0: no guard.
+struct DevGuard {
+  uint32_t m, v;
+};
+
 // One pool entry (YR_AC_MATCH, types.h:324-344) with everything a verify call
 // reads about it -- list link, backtrack, its YR_STRING's fields, its regexp
-// programs -- in one 48-byte record, so walking a list costs one memory round
-// trip per entry (three independent 16-byte loads).
+// programs and their guards -- in one 64-byte record, so walking a list costs
+// one memory round trip per entry (four independent 16-byte loads).
 struct DevPoolRec {
   uint32_t next;          // 1-based pool index of ac_match_pool[k].next, 0 = end
-  uint32_t backtrack;
+  uint16_t backtrack;     // YR_AC_MATCH.backtrack (uint16_t, types.h:330)
+  uint8_t fguard_bs;      // forward guard: base | span << 4 (DevGuard)
+  uint8_t bguard_bs;      // backward guard
   uint32_t flags;         // YR_STRING.flags
   uint32_t length;        // YR_STRING.length
   int64_t fixed_offset;   // YR_STRING.fixed_offset
   uint64_t bytes_off;     // YR_STRING.string in the byte blob
   DevRe re;               // regexp programs (fwd_len 0: none)
+  DevGuard fguard, bguard;
 };
-static_assert(sizeof(DevPoolRec) == 48, "pool record layout");
+static_assert(sizeof(DevPoolRec) == 64, "pool record layout");
 
 // Same layout as yr_amd_verify_rec (include/yara_amd.h).
 struct VerifyRec {

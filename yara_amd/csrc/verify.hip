@@ -624,6 +624,40 @@ __device__ int general_re_reachable(const uint8_t* __restrict__ code, uint32_t l
 }
 
 
+// A fast program's guard (verify.h DevGuard) against the input: false only if
+// no j in [0, span] passes, i.e. the program cannot reach MATCH.  Bytes not all
+// in the block or the staged window: true (the interpreter decides).  The
+// guard's 4 + span bytes come from four LDS dwords of the staged window and
+// byte shifts; every j is one AND and one compare.
+__device__ bool guard_ok(const VerifyParams& p, const uint8_t* d, uint64_t offset, bool backwards,
+                         uint32_t bs, DevGuard g, uint32_t lds) {
+  const uint32_t base = bs & 15u, span = bs >> 4, L = base + span + 4;
+  if (backwards ? offset < L : p.size - offset < L) return true;
+  const ByteWindow w = stage_window(p, d, backwards, lds);
+  if (w.lo == nullptr) return true;
+  const int32_t rel0 = (int32_t)(d - w.lo);
+  // lowest window byte of the guard's region: forwards x_base, backwards
+  // x_{base + span + 3}; the region is inside the window (base + span + 4 <= 27
+  // bytes from the start, the window covers 32 from it)
+  const uint32_t a = w.lds + (uint32_t)(backwards ? rel0 - (int32_t)L : rel0 + (int32_t)base);
+  const uint32_t a0 = a & ~3u, sh = a & 3u;
+  typedef const __attribute__((address_space(3))) uint32_t lds_u32;
+  const uint32_t d0 = *reinterpret_cast<lds_u32*>((uintptr_t)a0);
+  const uint32_t d1 = *reinterpret_cast<lds_u32*>((uintptr_t)(a0 + 4));
+  const uint32_t d2 = *reinterpret_cast<lds_u32*>((uintptr_t)(a0 + 8));
+  const uint32_t d3 = *reinterpret_cast<lds_u32*>((uintptr_t)(a0 + 12));
+  const uint32_t W[3] = {__builtin_amdgcn_alignbyte(d1, d0, sh), __builtin_amdgcn_alignbyte(d2, d1, sh),
+                         __builtin_amdgcn_alignbyte(d3, d2, sh)};
+  bool hit = false;
+#pragma unroll
+  for (uint32_t q = 0; q <= 8; ++q) {
+    // region bytes q .. q + 3 (forwards j = q, backwards j = span - q)
+    const uint32_t r = (q & 3) == 0 ? W[q >> 2] : __builtin_amdgcn_alignbyte(W[(q >> 2) + 1], W[q >> 2], q & 3);
+    hit |= q <= span && (r & g.m) == g.v;
+  }
+  return hit;
+}
+
 // _yr_scan_verify_re_match (scan.c:778-880) for FAST ascii hex strings: the
 // forward program from `offset` must reach MATCH (else forward_matches == -1:
 // return), a zero-length forward match needs a backward program, and with a
@@ -639,6 +673,12 @@ __device__ bool re_call_matters(const VerifyParams& p, const DevPoolRec& e, uint
   const uint8_t* bwd = p.re_code + r.bwd_off;
   if (flags & kStrFastRegexp) {
     if (!(flags & kStrAscii) || (flags & (kStrWide | kStrBase64Any))) return true;
+    // the guards first: most calls are atom hits whose next bytes already
+    // rule the program out (no code staging, no interpretation)
+    if (e.fguard.m != 0 && !guard_ok(p, d, offset, false, e.fguard_bs, e.fguard, lds)) return false;
+    if (r.bwd_len > 0 && e.bguard.m != 0 &&
+        !guard_ok(p, d, offset, true, e.bguard_bs, e.bguard, lds))
+      return false;
     // forward and backward programs are contiguous in the blob (the shim and
     // yarc.cpp lay them out so): stage both at once when they fit
     if (r.bwd_len == 0 || r.bwd_off == r.fwd_off + r.fwd_len) {
