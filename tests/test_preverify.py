@@ -137,3 +137,53 @@ def test_preverify_requires_strings():
     with pytest.raises(yara_amd.YaraAmdError) as e:
         sc.verify_calls(np.zeros(16, np.uint8))
     assert e.value.code == yara_amd.INVALID_ARGUMENT
+
+
+def _planted_jumps(seeds=range(7, 15), size=8 << 20):
+    """Config C's strings, one instance per string per seed (hex jumps and
+    wildcards drawn anew for every seed, so every jump length occurs), planted
+    back to back into random bytes."""
+    import gen_rules
+    import planted
+    text = gen_rules.gen("C")
+    data = oracle.xorshift(size, 51).copy()
+    off = 100
+    for seed in seeds:
+        for b, _ in planted.string_instances(text, seed=seed):
+            if off + len(b) + 64 > size:
+                return data
+            data[off:off + len(b)] = np.frombuffer(b, np.uint8)
+            off += len(b) + 37
+    return data
+
+
+def test_oracle_keeps_planted_hex_matches():
+    """The CPU side of the guard test below: the oracle keeps calls of fast-exec
+    (hex) strings on the planted instances, i.e. the GPU comparison is not
+    vacuous."""
+    from conftest import ref_tables
+    z = np.load(tables_npz("C"))
+    data = _planted_jumps(seeds=range(7, 8), size=1 << 20)
+    P, K = oracle.walk_verify(ref_tables("C"), data)
+    keep = oracle.literal_effect(z, P, K, data)
+    fast = z["re_kind"][K] != 0
+    assert (keep & fast).sum() > 1000 and (~keep & fast).sum() > 0
+
+
+@pytest.mark.gpu
+def test_guards_keep_every_planted_match():
+    """Fast-exec guards (verify.h DevGuard, checked before any program is
+    interpreted) reject only calls whose program cannot match: with config C's
+    hex strings planted with every jump length and wildcard byte, the device
+    records equal the oracle's kept calls exactly."""
+    import yara_amd
+    from conftest import ref_tables
+    z = np.load(tables_npz("C"))
+    data = _planted_jumps()
+    P, K = oracle.walk_verify(ref_tables("C"), data)
+    keep = oracle.literal_effect(z, P, K, data)
+    assert (keep & (z["re_kind"][K] != 0)).sum() > 10000
+    r = yara_amd.Scanner(yara_amd.Tables.from_npz(tables_npz("C"), device=0, strings=True)).verify_calls(data)
+    off = P.astype(np.uint64) - z["pool_backtrack"][K].astype(np.uint64)
+    np.testing.assert_array_equal(r["offset"], off[keep])
+    np.testing.assert_array_equal(r["pool_index"], K[keep])
