@@ -642,21 +642,55 @@ uint32_t fast_program_ok(const uint8_t* c, uint32_t len) {
   return 0;
 }
 
-// The guard of a linear fast-exec program (verify.h DevGuard): 4 consecutive
-// positions the program must consume at a fixed distance from its start, or
-// right after its first REPEAT_ANY, with their (mask, value) byte tests; the
-// set with the most tested bits, ignoring the first `skip` positions (the
-// atom's bytes, which every candidate has).  Returns false when no such set
-// tests anything.
+struct GuardPos { uint8_t m, v; };   // one consumed position: (mask, value), m = 0 untested
+
+// The guard (verify.h DevGuard) from a program's consumed positions: `head` =
+// the positions from its start at fixed distances, `tail` = those right after a
+// REPEAT_ANY {mn, mx} that follows `head` (repeat), the 4 positions with the
+// most tested bits, ignoring the first `skip` (the atom's bytes, which every
+// candidate has).  false when nothing would be tested.
+bool pick_guard(const std::vector<GuardPos>& head, const std::vector<GuardPos>& tail, bool repeat,
+                uint32_t mn, uint32_t mx, uint32_t skip, bool backwards, DevGuard& g, uint8_t& bs) {
+  auto bits = [](const std::vector<GuardPos>& r, uint32_t s, uint32_t from) {
+    uint32_t b = 0;
+    for (uint32_t t = 0; t < 4 && s + t < r.size(); ++t)
+      if (s + t >= from) b += (uint32_t)__builtin_popcount(r[s + t].m);
+    return b;
+  };
+  uint32_t best = 0, base = 0, span = 0;
+  const std::vector<GuardPos>* src = nullptr;
+  uint32_t src_at = 0;
+  for (uint32_t s0 = 0; s0 < std::max<size_t>(head.size(), 1) && s0 <= 15; ++s0) {
+    const uint32_t b = bits(head, s0, skip);
+    if (b > best) { best = b; base = s0; span = 0; src = &head; src_at = s0; }
+  }
+  if (repeat && head.size() + mn <= 15 && mx - mn <= 8) {
+    const uint32_t b = bits(tail, 0, 0);
+    if (b > best) { best = b; base = (uint32_t)head.size() + mn; span = mx - mn; src = &tail; src_at = 0; }
+  }
+  if (best == 0) return false;
+  g = DevGuard{0u, 0u};
+  for (uint32_t t = 0; t < 4 && src_at + t < src->size(); ++t) {
+    const GuardPos q = (*src)[src_at + t];
+    const uint32_t sh = 8 * (backwards ? 3 - t : t);
+    g.m |= (uint32_t)q.m << sh;
+    g.v |= (uint32_t)(q.m ? q.v : 0) << sh;
+  }
+  bs = (uint8_t)(base | span << 4);
+  return true;
+}
+
+// The guard of a linear fast-exec program (yr_re_fast_exec, re.c:2150-2391):
+// its run of literal / masked / any opcodes from the start, and the run right
+// after its first REPEAT_ANY.
 bool fast_guard(const uint8_t* c, uint32_t len, uint32_t skip, bool backwards, DevGuard& g,
                 uint8_t& bs) {
-  struct Pos { uint8_t m, v; };
-  std::vector<Pos> head, tail;   // the run before the first REPEAT_ANY, the run after it
+  std::vector<GuardPos> head, tail;
   uint32_t mn = 0, mx = 0;
   bool repeat = false;
   for (uint32_t n = 0; n < len;) {
     const uint8_t op = c[n];
-    std::vector<Pos>& run = repeat ? tail : head;
+    std::vector<GuardPos>& run = repeat ? tail : head;
     if (op == kReMatch) break;
     if (op == kReRepeatAnyUngreedy) {
       if (repeat) break;
@@ -676,33 +710,48 @@ bool fast_guard(const uint8_t* c, uint32_t len, uint32_t skip, bool backwards, D
     }
     if (repeat && tail.size() >= 4) break;
   }
-  auto bits = [](const std::vector<Pos>& r, uint32_t s, uint32_t from) {
-    uint32_t b = 0;
-    for (uint32_t t = 0; t < 4 && s + t < r.size(); ++t)
-      if (s + t >= from) b += (uint32_t)__builtin_popcount(r[s + t].m);
-    return b;
-  };
-  uint32_t best = 0, base = 0, span = 0;
-  const std::vector<Pos>* src = nullptr;
-  uint32_t src_at = 0;
-  for (uint32_t s0 = 0; s0 < std::max<size_t>(head.size(), 1) && s0 <= 15; ++s0) {
-    const uint32_t b = bits(head, s0, skip);
-    if (b > best) { best = b; base = s0; span = 0; src = &head; src_at = s0; }
+  return pick_guard(head, tail, repeat, mn, mx, skip, backwards, g, bs);
+}
+
+// The guard of a yr_re_exec program (re.c:1693-2072), for its ascii attempt:
+// the consuming opcodes from its start, following JUMPs and stepping over the
+// zero-width assertions, up to its first SPLIT, REPEAT or MATCH.  Until there
+// the program is a single fiber, so every byte test on the way must pass (and
+// a call that fails one cannot run out of fibers).  Nocase strings compare
+// through the host's case folding: their literals are left untested.
+bool general_guard(const uint8_t* c, uint32_t len, uint32_t skip, bool backwards, bool nocase,
+                   DevGuard& g, uint8_t& bs) {
+  std::vector<GuardPos> head;
+  uint32_t n = 0;
+  for (int steps = 0; steps < 256 && n < len && head.size() < 20; ++steps) {
+    const uint8_t op = c[n];
+    const uint32_t sz = re_op_size(op);
+    if (sz == 0 || n + sz > len) break;
+    if (op == kOpJump) {
+      const int64_t t = (int64_t)n + re_i16(c + n + 1);
+      if (t < 0 || t >= (int64_t)len) break;
+      n = (uint32_t)t;
+      continue;
+    }
+    if (op == kOpWordBoundary || op == kOpNonWordBoundary || op == kOpMatchAtStart ||
+        op == kOpMatchAtEnd) {
+      n += sz;   // zero width
+      continue;
+    }
+    if (op == kOpLiteral) {
+      head.push_back(nocase ? GuardPos{0, 0} : GuardPos{0xFF, c[n + 1]});
+    } else if (op == kOpMaskedLiteral) {
+      head.push_back(nocase ? GuardPos{0, 0} : GuardPos{c[n + 2], c[n + 1]});
+    } else if (op == kOpAny || op == kOpClass || op == kOpNotLiteral || op == kOpMaskedNotLiteral ||
+               op == kOpWordChar || op == kOpNonWordChar || op == kOpSpace || op == kOpNonSpace ||
+               op == kOpDigit || op == kOpNonDigit) {
+      head.push_back({0, 0});   // consumes one byte, not tested here
+    } else {
+      break;                    // MATCH, SPLIT, REPEAT*: the single fiber ends
+    }
+    n += sz;
   }
-  if (repeat && head.size() + mn <= 15 && mx - mn <= 8) {
-    const uint32_t b = bits(tail, 0, 0);
-    if (b > best) { best = b; base = (uint32_t)head.size() + mn; span = mx - mn; src = &tail; src_at = 0; }
-  }
-  if (best == 0) return false;
-  g = DevGuard{0u, 0u};
-  for (uint32_t t = 0; t < 4 && src_at + t < src->size(); ++t) {
-    const Pos q = (*src)[src_at + t];
-    const uint32_t sh = 8 * (backwards ? 3 - t : t);
-    g.m |= (uint32_t)q.m << sh;
-    g.v |= (uint32_t)(q.m ? q.v : 0) << sh;
-  }
-  bs = (uint8_t)(base | span << 4);
-  return true;
+  return pick_guard(head, {}, false, 0, 0, skip, backwards, g, bs);
 }
 }  // namespace
 
@@ -748,21 +797,26 @@ int yr_amd_tables_set_re_code(yr_amd_tables* t, uint32_t n_pool, const uint32_t*
   if (code_len > 0) memcpy(padded.data(), code, (size_t)code_len);
   int r = upload(t->d_re_code, padded.data(), padded.size());
   if (r) return r;
-  // the programs go into the pool records (uploaded again), fast programs with
-  // their guards (the forward program starts at the atom: its first
-  // `backtrack` bytes are the atom's)
+  // the programs go into the pool records (uploaded again) with their guards
+  // (the forward program starts at the atom: its first `backtrack` bytes are
+  // the atom's)
   for (uint32_t k = 0; k < n_pool; ++k) {
     DevPoolRec& e = t->h_pool[k];
     e.re = re[k];
     e.fguard = e.bguard = DevGuard{0u, 0u};
     e.fguard_bs = e.bguard_bs = 0;
-    if (re[k].fwd_len == 0 || !(t->h_str_flags[t->h_pool_string[k]] & kStrFastRegexp)) continue;
+    if (re[k].fwd_len == 0) continue;
     if (getenv("YAMD_NO_GUARDS") != nullptr) continue;   // A/B measurements only
-    if (!fast_guard(code + re[k].fwd_off, re[k].fwd_len, e.backtrack, false, e.fguard, e.fguard_bs))
-      e.fguard = DevGuard{0u, 0u};
-    if (re[k].bwd_len == 0 ||
-        !fast_guard(code + re[k].bwd_off, re[k].bwd_len, 0, true, e.bguard, e.bguard_bs))
-      e.bguard = DevGuard{0u, 0u};
+    const uint32_t sflags = t->h_str_flags[t->h_pool_string[k]];
+    const bool nocase = sflags & kStrNoCase;
+    auto guard = [&](uint32_t off, uint32_t len, uint32_t skip, bool bw, DevGuard& g, uint8_t& bs) {
+      const bool ok = (sflags & kStrFastRegexp)
+                          ? fast_guard(code + off, len, skip, bw, g, bs)
+                          : general_guard(code + off, len, skip, bw, nocase, g, bs);
+      if (!ok) g = DevGuard{0u, 0u};
+    };
+    guard(re[k].fwd_off, re[k].fwd_len, e.backtrack, false, e.fguard, e.fguard_bs);
+    if (re[k].bwd_len > 0) guard(re[k].bwd_off, re[k].bwd_len, 0, true, e.bguard, e.bguard_bs);
   }
   if (n_pool > 0 && hipMemcpy(t->d_pool, t->h_pool.data(), n_pool * sizeof(DevPoolRec),
                               hipMemcpyHostToDevice) != hipSuccess)

@@ -697,13 +697,20 @@ __device__ bool re_call_matters(const VerifyParams& p, const DevPoolRec& e, uint
   const bool try_wide = (flags & kStrWide) && !(flags & kStrBase64Any);
   // A forward "match" here may be a reference miss, after which the wide
   // attempt runs: both branches are covered by trying every attempt.
+  // The guards (host-compiled, scanner.cpp general_guard) hold for the ascii
+  // attempt: a failing one proves that attempt dead in that direction without
+  // running the search (and without any fiber to run out of).
   for (int w = 0; w < 2; ++w) {
     if (w == 0 ? !try_ascii : !try_wide) continue;
+    if (w == 0 && e.fguard.m != 0 && !guard_ok(p, d, offset, false, e.fguard_bs, e.fguard, lds))
+      continue;
     const int f = general_re_reachable(fwd, r.fwd_len, d, p.size - offset, offset, false, w == 1,
                                        nocase, dotall, p.lowercase);
     if (f == kPathUnknown) return true;
     if (f == kPathDead) continue;
     if (r.bwd_len == 0) return true;
+    if (w == 0 && e.bguard.m != 0 && !guard_ok(p, d, offset, true, e.bguard_bs, e.bguard, lds))
+      continue;
     const int b = general_re_reachable(bwd, r.bwd_len, d, p.size - offset, offset, true, w == 1,
                                        nocase, dotall, p.lowercase);
     if (b != kPathDead) return true;
