@@ -130,7 +130,8 @@ typedef struct
   uint64_t verify_halo_after;
   /* Stage-1 filter form: 0 = pair filter (every position's window), 1 =
    * even-position filter (rule sets whose keys are all 4 bytes long: the
-   * windows ending at even positions only, each key's prefix and suffix). */
+   * windows ending at even positions only, each key's prefix and suffix),
+   * 2 = the same with a hashed block index. */
   uint32_t filter_mode;
 } yr_amd_tables_info;
 

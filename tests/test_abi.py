@@ -56,14 +56,22 @@ def test_flattening_stats(name, states, depth, keys):
     assert inf["max_depth"] == 4 and inf["root_accepting"] == 0
     # filter density bounds the stage-2 rate
     assert inf["filter_set_bits"] / (1 << inf["filter_bits"]) < 0.05
-    # 4-byte keys only: the even-position filter (internal.h kFilterEven)
-    assert inf["filter_mode"] == (1 if keys[:4] == [0, 0, 0, 0] else 0)
+    # 4-byte keys only: the even-position filter (internal.h kFilterEven), its
+    # block hashed where that lets fewer random windows pass (config E)
+    assert inf["filter_mode"] == {"B": 1, "C": 0, "E": 2}[name]
 
 
 def test_pair_filter_switch(monkeypatch):
     monkeypatch.setenv("YAMD_PAIR_FILTER", "1")
     inf = yara_amd.Tables.from_npz(tables_npz("E"), device=-1).info()
     assert inf["filter_mode"] == 0
+
+
+@pytest.mark.parametrize("form,mode", [("plain", 1), ("hash", 2)])
+def test_even_filter_forms(monkeypatch, form, mode):
+    monkeypatch.setenv("YAMD_EVEN_FILTER", form)
+    for name in ("B", "E"):
+        assert yara_amd.Tables.from_npz(tables_npz(name), device=-1).info()["filter_mode"] == mode
 
 
 def test_short_and_root_tables():

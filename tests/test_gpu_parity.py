@@ -406,8 +406,8 @@ def test_even_filter_planted_keys(rules, stride, monkeypatch):
     tested, each key inserted as its 3-byte prefix and suffix).  Strings planted
     every `stride` bytes end at both parities and at every lane byte (lane,
     tile and segment edges included; strides 5 and 7 put several hits in one
-    lane, the drains' synchronous path): candidates equal the oracle's and the
-    pair filter's."""
+    lane, the drains' synchronous path): candidates equal the oracle's with the
+    plain and the hashed even filter and the pair filter."""
     import planted
     import gen_rules
     tab = ref_tables(rules)
@@ -421,12 +421,16 @@ def test_even_filter_planted_keys(rules, stride, monkeypatch):
         k += 1
         off += stride + (k % 3 == 0)                # drift through every residue mod 16
     even = dev_tables(rules)
-    assert even.info()["filter_mode"] == 1
+    assert even.info()["filter_mode"] in (1, 2)
     pos, allp = yara_amd.Scanner(even).candidates(data)
     ref = oracle.candidates(tab, data)
     assert not allp and len(ref) > size // stride // 8
     np.testing.assert_array_equal(pos, ref)
-    monkeypatch.setenv("YAMD_PAIR_FILTER", "1")
-    pair = yara_amd.Tables.from_npz(tables_npz(rules), device=0)
-    assert pair.info()["filter_mode"] == 0
-    np.testing.assert_array_equal(yara_amd.Scanner(pair).candidates(data)[0], ref)
+    # every form: the plain and the hashed even filter, the pair filter
+    for env, val, mode in (("YAMD_EVEN_FILTER", "plain", 1), ("YAMD_EVEN_FILTER", "hash", 2),
+                           ("YAMD_PAIR_FILTER", "1", 0)):
+        monkeypatch.setenv(env, val)
+        t = yara_amd.Tables.from_npz(tables_npz(rules), device=0)
+        monkeypatch.delenv(env)
+        assert t.info()["filter_mode"] == mode
+        np.testing.assert_array_equal(yara_amd.Scanner(t).candidates(data)[0], ref)

@@ -61,6 +61,15 @@ constexpr uint32_t kScanLdsBytes = kFilterBytes + kQueueBytes + kPendBytes;     
 // even k makes k and k + 1 filter hits; the exact stages are unchanged.
 constexpr uint32_t kFilterPair = 0;
 constexpr uint32_t kFilterEven = 1;
+// kFilterEvenHash: the even-position filter with its block picked by a
+// multiplicative hash of all three bytes (x * K, bits 18..31: one
+// v_mul_u32_u24 more per test); the bits by the raw fields as in the left
+// role.  Sets of many similar keys crowd a few plain blocks (config E's nocase
+// variants share their middle bytes: 0.30 % of random windows pass the plain
+// filter, 0.18 % the hashed one); the host picks the form whose blocks pass
+// fewer random windows (tables.cpp).
+constexpr uint32_t kFilterEvenHash = 2;
+constexpr uint32_t kEvenHashK = 0xEBCA77u;
 struct FilterProbe {
   uint32_t block;  // index into the kFilterWords / 2 blocks; words 2*block, 2*block+1
   uint32_t b_lo, b_hi;
@@ -69,6 +78,12 @@ struct FilterProbe {
 __host__ __device__ inline FilterProbe filter_probe_left(uint32_t w3) {
   const uint32_t x = w3 & 0xFFFFFFu;
   return FilterProbe{x >> 10, x & 31u, (x >> 5) & 31u};
+}
+// a window of the even-position filter (kFilterEven / kFilterEvenHash)
+__host__ __device__ inline FilterProbe filter_probe_even(uint32_t w3, bool hashed) {
+  const uint32_t x = w3 & 0xFFFFFFu;
+  const uint32_t block = hashed ? (x * kEvenHashK) >> 18 : x >> 10;   // (x, K < 2^24)
+  return FilterProbe{block, x & 31u, (x >> 5) & 31u};
 }
 // the same window in the right role (p, q, r) = (b, c, d)
 __host__ __device__ inline FilterProbe filter_probe_right(uint32_t w3) {
@@ -156,7 +171,7 @@ struct ScanParams {
                             // seg_out + seg_base[s] (exact-size rerun after an overflow)
   uint32_t byte_keys;       // FlatTables::byte_keys / n_byte_keys (stage-1 byte test)
   uint32_t n_byte_keys;
-  uint32_t filter_mode;     // kFilterPair / kFilterEven (FlatTables::filter_mode)
+  uint32_t filter_mode;     // kFilterPair / kFilterEven / kFilterEvenHash (FlatTables)
   uint32_t* seg_next;       // null: wave w takes segments w, w + waves, ...; else each wave
                             // takes its first segment by index and the next ones from this
                             // counter (initialised to the launch's wave count)

@@ -186,6 +186,10 @@ constexpr int kModeByteKeys = 20;
 // Kernel variant: the product kernel for the even-position filter
 // (internal.h kFilterEven: rule sets whose keys are all 4 bytes long).
 constexpr int kModeEven = 21;
+// ... with the hashed block index (internal.h kFilterEvenHash).
+constexpr int kModeEvenHash = 22;
+template <int MODE>
+constexpr bool kEven = MODE == kModeEven || MODE == kModeEvenHash;
 // A pending entry's offset with this bit set is a certain candidate (its last
 // byte is a 1-byte key): no bucket probe.  (Segment offsets are < 2^20.)
 constexpr uint32_t kConfirmed = 0x80000000u;
@@ -250,15 +254,24 @@ __device__ __forceinline__ uint32_t dense_mask(uint32_t h) {
   return (h | (h >> 8)) & 0xFFFFu;
 }
 
+// LDS byte address of the even-position filter block of window x[0..23]
+// (internal.h filter_block_even: one v_mul_u32_u24, a shift and a mask).
+template <bool kHash>
+__device__ __forceinline__ uint32_t even_addr(uint32_t x) {
+  if constexpr (kHash) return (__umul24(x, kEvenHashK) >> 15) & (kFilterBytes - 8);
+  return (x >> 7) & (kFilterBytes - 8);
+}
+
 // Per-position filter hits of a lane under the even-position filter (drains):
 // a pass of the window ending at even lane byte 2j makes bytes 2j and 2j + 1
 // hits (bit j <=> lane byte j).
+template <bool kHash>
 __device__ __forceinline__ uint32_t even_mask(const uint32_t (&S)[6]) {
   uint32_t m = 0;
 #pragma unroll
   for (int j = 0; j < kBytesPerLane / 2; ++j) {
     const uint32_t x = pair_window(S, (uint32_t)j);
-    const u32x2 w = lds_load<u32x2>((x >> 7) & (kFilterBytes - 8));
+    const u32x2 w = lds_load<u32x2>(even_addr<kHash>(x));
     m |= ((w.x >> (x & 31u)) & (w.y >> ((x >> 5) & 31u)) & 1u) << (2 * j);
   }
   return m | (m << 1);
@@ -306,7 +319,7 @@ __device__ __forceinline__ uint32_t byte_keys_mask(const uint32_t (&S)[6], const
 #endif
 template <int MODE>
 constexpr bool kDeferFl =
-    YAMD_DEFER_FL && (MODE == 0 || MODE == 12 || MODE == kModeByteKeys || MODE == kModeEven);
+    YAMD_DEFER_FL && (MODE == 0 || MODE == 12 || MODE == kModeByteKeys || kEven<MODE>);
 
 // Consume a deferred drain's first-level words: the lanes' hits that pass go,
 // in order, to the pending list.
@@ -362,7 +375,7 @@ __device__ __forceinline__ void drain(const ScanParams& p, WaveQueue& q, uint32_
     const u32x2 e45 = lds_load<u32x2>(ent + 16);
     const uint32_t S[6] = {e45.x, e01.x, e01.y, e23.x, e23.y, 0u};
     off0 = (e45.y & 0xFFFFu) * kBytesPerLane;
-    if constexpr (MODE == kModeEven) m = even_mask(S);
+    if constexpr (kEven<MODE>) m = even_mask<MODE == kModeEvenHash>(S);
     else m = dense_mask(stage1<0, false>(S, lane));
     if constexpr (MODE == kModeByteKeys) {
       kmask = byte_keys_mask(S, p);
@@ -511,7 +524,8 @@ __device__ __forceinline__ uint32_t stage1(const uint32_t (&S)[6], uint32_t lane
     xs[j] = pair_window(S, j);
     if constexpr (MODE != 3) {
       const uint32_t x = xs[j];
-      uint32_t addr = (x >> 7) & (kFilterBytes - 8);   // block x[10..23], 8 B each
+      uint32_t addr = MODE == kModeEvenHash ? even_addr<true>(x)      // hashed block
+                                            : (x >> 7) & (kFilterBytes - 8);   // block x[10..23], 8 B each
       if constexpr (MODE == 4) addr = ((lane & 31u) * 8u + (uint32_t)j * 256u) & (kFilterBytes - 8);
       if constexpr (MODE == 5) {
         ws[j] = make_uint2(addr ^ x, addr + x);
@@ -532,7 +546,7 @@ __device__ __forceinline__ uint32_t stage1(const uint32_t (&S)[6], uint32_t lane
   // straight into byte n of accumulator r (position 4n + r), so bit 0 of that
   // byte is the position's result and no separate accumulate instruction is
   // needed; bits 1..7 of each byte are don't-care and masked off below.
-  if constexpr (kAny && MODE == kModeEven) {
+  if constexpr (kAny && kEven<MODE>) {
     // the even-position filter: the left windows only (pairs 0-3, 4-7 into
     // two accumulators), any pass of the lane in bit 0
     uint32_t a[2];
@@ -951,6 +965,9 @@ hipError_t launch_scan(const ScanParams& p, int grid, hipStream_t s, int mode) {
                            s, p);
       else if (p.filter_mode == kFilterEven)
         hipLaunchKernelGGL(scan_segments_kernel<kModeEven>, dim3(grid), dim3(kWGThreads), lds, s, p);
+      else if (p.filter_mode == kFilterEvenHash)
+        hipLaunchKernelGGL(scan_segments_kernel<kModeEvenHash>, dim3(grid), dim3(kWGThreads), lds, s,
+                           p);
       else
         hipLaunchKernelGGL(scan_segments_kernel<0>, dim3(grid), dim3(kWGThreads), lds, s, p);
       break;
@@ -989,7 +1006,8 @@ hipError_t configure_scan_kernel() {
                         (const void*)scan_segments_kernel<10>, (const void*)scan_segments_kernel<11>,
                         (const void*)scan_segments_kernel<12>,
                         (const void*)scan_segments_kernel<kModeByteKeys>,
-                        (const void*)scan_segments_kernel<kModeEven>}) {
+                        (const void*)scan_segments_kernel<kModeEven>,
+                        (const void*)scan_segments_kernel<kModeEvenHash>}) {
     hipError_t r = hipFuncSetAttribute(k, hipFuncAttributeMaxDynamicSharedMemorySize, lds);
     if (r != hipSuccess) e = r;
   }

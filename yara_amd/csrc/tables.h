@@ -31,7 +31,8 @@ struct FlatTables {
   // kFilterEven: every key is 4 bytes long, and the filter holds each key's
   // 3-byte prefix and suffix in the left role only -- the scan tests the
   // windows ending at even positions, each pass standing for that position
-  // and the next (internal.h); kFilterPair: both roles, every position
+  // and the next (internal.h; kFilterEvenHash: its block hashed); kFilterPair:
+  // both roles, every position
   uint32_t filter_mode = 0;
   std::vector<uint32_t> exact;     // exact key sets (internal.h layout)
   uint32_t t3_off = 0, t3_mask = 0, t4_off = 0, t4_mask = 0, exact_flags = 0;
