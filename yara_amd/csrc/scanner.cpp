@@ -800,13 +800,14 @@ int yr_amd_tables_set_re_code(yr_amd_tables* t, uint32_t n_pool, const uint32_t*
   // the programs go into the pool records (uploaded again) with their guards
   // (the forward program starts at the atom: its first `backtrack` bytes are
   // the atom's)
+  const bool no_guards = getenv("YAMD_NO_GUARDS") != nullptr;   // A/B measurements only
   for (uint32_t k = 0; k < n_pool; ++k) {
     DevPoolRec& e = t->h_pool[k];
     e.re = re[k];
     e.fguard = e.bguard = DevGuard{0u, 0u};
     e.fguard_bs = e.bguard_bs = 0;
     if (re[k].fwd_len == 0) continue;
-    if (getenv("YAMD_NO_GUARDS") != nullptr) continue;   // A/B measurements only
+    if (no_guards) continue;
     const uint32_t sflags = t->h_str_flags[t->h_pool_string[k]];
     const bool nocase = sflags & kStrNoCase;
     auto guard = [&](uint32_t off, uint32_t len, uint32_t skip, bool bw, DevGuard& g, uint8_t& bs) {
