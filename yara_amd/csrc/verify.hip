@@ -624,8 +624,9 @@ __device__ int general_re_reachable(const uint8_t* __restrict__ code, uint32_t l
 }
 
 
-// A fast program's guard (verify.h DevGuard) against the input: false only if
-// no j in [0, span] passes, i.e. the program cannot reach MATCH.  Bytes not all
+// A program's guard (verify.h DevGuard; scanner.cpp fast_guard / general_guard)
+// against the input: false only if no j in [0, span] passes, i.e. the program
+// cannot reach MATCH.  Bytes not all
 // in the block or the staged window: true (the interpreter decides).  The
 // guard's 4 + span bytes come from four LDS dwords of the staged window and
 // byte shifts; every j is one AND and one compare.
