@@ -755,6 +755,22 @@ bool general_guard(const uint8_t* c, uint32_t len, uint32_t skip, bool backwards
 }
 }  // namespace
 
+// Not declared in include/yara_amd.h: the guard compiler on one program, for
+// the CPU tests (tests/test_guards.py).  Returns 1 and the guard (verify.h
+// DevGuard: m, v, base | span << 4) if the program has one, else 0.
+int yr_amd__program_guard(const uint8_t* code, uint32_t len, uint32_t skip, int backwards,
+                          int general, int nocase, uint32_t* m, uint32_t* v, uint32_t* bs) {
+  if (code == nullptr || m == nullptr || v == nullptr || bs == nullptr) return -1;
+  DevGuard g{0u, 0u};
+  uint8_t b = 0;
+  const bool ok = general ? general_guard(code, len, skip, backwards != 0, nocase != 0, g, b)
+                          : fast_guard(code, len, skip, backwards != 0, g, b);
+  *m = ok ? g.m : 0u;
+  *v = ok ? g.v : 0u;
+  *bs = ok ? b : 0u;
+  return ok ? 1 : 0;
+}
+
 int yr_amd_re_code_extent(const uint8_t* code, uint64_t avail, uint32_t* extent) {
   using yamd::re_general_extent;
   if (code == nullptr || extent == nullptr) return YR_AMD_INVALID_ARGUMENT;
