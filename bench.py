@@ -51,7 +51,8 @@ def parse():
     ap.add_argument("--cpu-sample-mib", type=int, default=3072)
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--no-check", action="store_true")
-    ap.add_argument("--no-other", action="store_true", help="skip the B / E kernel timings")
+    ap.add_argument("--no-other", action="store_true",
+                    help="skip the other rule sets' kernel timings (B, E, rx, short, fuzz0, fuzz3)")
     ap.add_argument("--backend", default="nccl", help="nccl (= RCCL) or gloo (rehearsal)")
     return ap.parse_args()
 
@@ -231,11 +232,13 @@ def main():
     # (profiles/r02_baseline_kernel_stats.csv), which W = 5 warm-up steps alone
     # do not cover.
     # the same input under the other rule sets of SURVEY.md §8d (kernel time only,
-    # not the bench value): B = 1,000 4-byte hex atoms, E = 2,000 nocase/masked
+    # not the bench value): B = 1,000 4-byte hex atoms, E = 2,000 nocase/masked;
+    # and the shapes with 1-byte keys, whose candidates are dense:
+    # rx = regexps, short = short literals, fuzz0 / fuzz3 = generated rule sets
     other = None
     if rank == 0 and world == 1 and not args.no_other and args.rules == "C":
         other = {}
-        for name in ("B", "E"):
+        for name in ("B", "E", "rx", "short", "fuzz0", "fuzz3"):
             t_o = yara_amd.Tables.from_npz(os.path.join(REPO, "tests", "golden", "tables",
                                                         "%s.npz" % name), device=dev.index)
             s_o = yara_amd.Scanner(t_o, stream=stream.cuda_stream)
