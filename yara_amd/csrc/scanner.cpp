@@ -134,6 +134,11 @@ struct yr_amd_scanner {
   bool ev_valid = false;
 
   int diag_mode = 0;   // profiling ablation of the scan kernel (0 = product)
+  // candidates per KiB a segment has needed (x 1.25), learned from the last
+  // overflowing scan: later scans size the segments' output for it, so a
+  // rule set with dense candidates (1-byte keys) pays the exact-offset rerun
+  // once per scanner instead of on every scan
+  uint32_t dense_per_kib = 0;
   uint64_t* d_seg_base = nullptr; // exact per-segment output offsets (overflow rerun)
   uint32_t* d_seg_next = nullptr; // dynamic segment counter (YAMD_SEG_KIB experiments)
   size_t seg_base_cap = 0;
@@ -446,7 +451,9 @@ int yr_amd_scan_window(yr_amd_scanner* s, const uint8_t* d_window, uint64_t wind
   const uint64_t n_segments64 = (nbytes + seg_bytes - 1) / seg_bytes;
   if (n_segments64 > 0xFFFFFFFFull) return YR_AMD_INVALID_ARGUMENT;
   const uint32_t n_segments = (uint32_t)n_segments64;
-  const uint32_t seg_cap = std::max<uint32_t>(64, seg_bytes / 256);
+  const uint32_t learned = (uint32_t)std::min<uint64_t>(
+      (uint64_t)s->dense_per_kib * seg_bytes / 1024, seg_bytes / 64);   // (bounded workspace)
+  const uint32_t seg_cap = std::max<uint32_t>(std::max<uint32_t>(64, seg_bytes / 256), learned);
   int r = ensure_segments(s, n_segments, seg_cap);
   if (r) return r;
 
@@ -497,6 +504,12 @@ int yr_amd_scan_device_result(yr_amd_scanner* s, const uint64_t** d_positions, u
   HIP_TRY(hipEventSynchronize(s->ev_done));
   uint64_t total = s->h_summary[0];
   const uint64_t maxc = s->h_summary[1];
+  static const bool no_learn = getenv("YAMD_NO_CAP_LEARN") != nullptr;   // A/B only
+  if (maxc > s->last.seg_cap && !no_learn) {
+    s->dense_per_kib = std::max<uint32_t>(
+        s->dense_per_kib, (uint32_t)std::min<uint64_t>((maxc * 1280 + s->last.seg_bytes - 1) /
+                                                           s->last.seg_bytes, 1u << 20));
+  }
   if (maxc > s->last.seg_cap) {
     // some segment overflowed its capacity: rerun once with every segment
     // writing at its exact offset (counts are kept past the capacity), so the
