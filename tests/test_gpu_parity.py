@@ -434,3 +434,24 @@ def test_even_filter_planted_keys(rules, stride, monkeypatch):
         monkeypatch.delenv(env)
         assert t.info()["filter_mode"] == mode
         np.testing.assert_array_equal(yara_amd.Scanner(t).candidates(data)[0], ref)
+
+
+def test_dense_rescans_after_capacity_learning():
+    """A scanner whose scan overflowed the default segment output (1 candidate
+    per 256 bytes) sizes the following scans' outputs from it (scanner.cpp
+    dense_per_kib): a 64 MiB block with ~1 candidate per 100 bytes overflows
+    once, then fits; every scan, and a sparse block after them, gives the
+    oracle's candidates."""
+    tab = ref_tables("short")
+    sc = yara_amd.Scanner(dev_tables("short"))
+    n = 64 << 20
+    x = oracle.xorshift(n, 19)
+    data = x.copy()
+    pick = (x % 100) < 1                           # 1 % of the bytes from the key alphabet
+    data[pick] = np.frombuffer(b"abcdxyzHeloC\x00\x01\xff", np.uint8)[(x[pick] >> 3) % 15]
+    ref = oracle.candidates(tab, data)
+    assert n // 256 < len(ref) < n // 80
+    for _ in range(3):
+        np.testing.assert_array_equal(sc.candidates(data)[0], ref)
+    sparse = oracle.xorshift(3 << 20, 20)
+    np.testing.assert_array_equal(sc.candidates(sparse)[0], oracle.candidates(tab, sparse))
