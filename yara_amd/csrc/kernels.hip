@@ -317,6 +317,15 @@ __device__ __forceinline__ uint32_t byte_keys_mask(const uint32_t (&S)[6], const
 #ifndef YAMD_DEFER_FL
 #define YAMD_DEFER_FL 1
 #endif
+// The product and byte-key kernels hold the deferred words' registers until
+// the next loads are issued (issue_first_level): C 0.850 -> 0.835-0.843 ms,
+// the 1-byte-key sets 1.5-2 % faster; the even-position kernels not (B 2.7 %
+// slower, E equal), profiles/r02_hold_fl_ab.json.
+#ifndef YAMD_HOLD_FL
+#define YAMD_HOLD_FL 1
+#endif
+template <int MODE>
+constexpr bool kHoldFl = YAMD_HOLD_FL && !kEven<MODE>;
 template <int MODE>
 constexpr bool kDeferFl =
     YAMD_DEFER_FL && (MODE == 0 || MODE == 12 || MODE == kModeByteKeys || kEven<MODE>);
@@ -696,6 +705,13 @@ __device__ __forceinline__ void tile_context(SegState& st, const uint4& cur, uin
 template <int MODE>
 __device__ __forceinline__ void issue_first_level(const ScanParams& p, WaveQueue& q) {
   if constexpr (kDeferFl<MODE>) {
+    if constexpr (kHoldFl<MODE>) {
+      // keep the previous words' registers live up to here, so the loads below
+      // land in registers nothing else in the tile step writes (otherwise the
+      // compiler reuses them, e.g. for the ring entry's lane index, and that
+      // write must wait for a possibly still outstanding load)
+      asm volatile("" : "+v"(q.da), "+v"(q.db));
+    }
     const char* ex = reinterpret_cast<const char*>(p.exact);
     q.da = __hip_atomic_load(reinterpret_cast<const uint32_t*>(ex + q.ia), __ATOMIC_RELAXED,
                              __HIP_MEMORY_SCOPE_WAVEFRONT);
