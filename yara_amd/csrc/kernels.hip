@@ -324,6 +324,13 @@ __device__ __forceinline__ uint32_t byte_keys_mask(const uint32_t (&S)[6], const
 #ifndef YAMD_HOLD_FL
 #define YAMD_HOLD_FL 1
 #endif
+// The lane-0 window context by a second DPP move (tile_context): frees the
+// lane-0 SGPR mask, which the byte-key kernel spilled (two v_readlane per
+// tile): rx 1.20 -> 1.175 ms, short/fuzz 1-2 % faster, C and B/E equal
+// (profiles/r02_carry_dpp2_ab.json).
+#ifndef YAMD_CARRY_DPP2
+#define YAMD_CARRY_DPP2 1
+#endif
 template <int MODE>
 constexpr bool kHoldFl = YAMD_HOLD_FL && !kEven<MODE>;
 template <int MODE>
@@ -689,7 +696,13 @@ __device__ __forceinline__ void tile_context(SegState& st, const uint4& cur, uin
   // (One DPP move and one select: 1 % faster than a wave_shr:1 into the
   // carry plus a v_readlane of the next one, profiles/r02_carry_ror_ab.json.)
   const uint32_t rot = __builtin_amdgcn_mov_dpp(cur.w, 0x13C, 0xF, 0xF, true);
+#if YAMD_CARRY_DPP2
+  // wave_shr:1 without bound_ctrl leaves lane 0 its old value (the carry):
+  // a second DPP move instead of a select on a lane-0 SGPR mask
+  S[0] = __builtin_amdgcn_update_dpp(st.carry, cur.w, 0x138, 0xF, 0xF, false);
+#else
   S[0] = st.lane0 ? st.carry : rot;
+#endif
   st.carry = rot;
   S[1] = cur.x;
   S[2] = cur.y;
