@@ -347,10 +347,14 @@ typedef struct
  * bytes).
  * On success *d_records is a DEVICE pointer owned by the scanner (valid until
  * its next verify) to *count records.  Synchronous.  The record's candidate
- * field is a 32-bit index: a candidate stream of 2^32 or more (root-accepting
- * rules on a block >= 4 GiB) returns YR_AMD_INVALID_ARGUMENT.
+ * field is a 32-bit index: a candidate stream longer than
+ * YR_AMD_VERIFY_MAX_CANDIDATES returns YR_AMD_INVALID_ARGUMENT.  A block (or a
+ * window's byte range) of size bytes has at most size + 1 candidates, so any
+ * block below 4 GiB is accepted; callers route larger ones to yr_amd_replay
+ * when size + 1 exceeds the limit (integration/yr_gpu_scanner.c).
  * Requires yr_amd_tables_set_strings; YR_AMD_INVALID_ARGUMENT otherwise.
  */
+#define YR_AMD_VERIFY_MAX_CANDIDATES 0x100000000ull
 int yr_amd_verify_device(
     yr_amd_scanner* scanner,
     uint64_t data_base,

@@ -480,12 +480,14 @@ static int _scan_one_block(
     const uint8_t* data,
     YR_MEMORY_BLOCK* block)
 {
-  /* Pre-verification takes candidate streams below 2^32 (yr_amd_verify_device):
-   * a root-accepting rule set on a block of 4 GiB or more makes every
-   * position a candidate, so that block is replayed from the GPU scan's
-   * stream instead -- after the blocks still in flight, in order. */
+  /* Pre-verification takes candidate streams of at most
+   * YR_AMD_VERIFY_MAX_CANDIDATES (yr_amd_verify_device), and a block of size
+   * bytes has at most size + 1 candidates (every position of a root-accepting
+   * rule set, or a dense key): a block that could exceed it is replayed from
+   * the GPU scan's stream instead -- after the blocks still in flight, in
+   * order.  The same limit as the library's, so no block reaches a refusal. */
   int replay_block = !gs->preverify ||
-                     (scanner->rules->ac_match_table[0] != 0 && block->size >= 0xFFFFFFFFull);
+                     (uint64_t) block->size + 1 > YR_AMD_VERIFY_MAX_CANDIDATES;
   while (replay_block && gs->inflight > 0)
     FAIL_ON_ERROR(_replay_next(scanner, gs));
   if (replay_block) return _yr_gpu_scan_mem_block(scanner, gs, data, block);

@@ -74,6 +74,23 @@ def case_data(rec):
     raise ValueError(kind)
 
 
+# The diagnostic build of the library (make -C yara_amd/csrc diag): the only
+# one that reads the A/B environment switches (internal.h YAMD_DIAG).
+DIAG_LIB = os.path.join(REPO, "yara_amd", "_diag", "libyara_amd.so")
+
+
+def run_diag_child(code, env=None, timeout=240):
+    """Run `code` in a child Python with the diagnostic library loaded (the
+    switches are read once per process); returns its stdout, asserts exit 0."""
+    import subprocess
+    prelude = "import sys; sys.path[:0] = [%r, %r, %r]\n" % (
+        REPO, os.path.join(REPO, "tests"), GOLDEN)
+    r = subprocess.run([sys.executable, "-c", prelude + code], capture_output=True, text=True,
+                       timeout=timeout, env=dict(os.environ, YARA_AMD_LIB=DIAG_LIB, **(env or {})))
+    assert r.returncode == 0, r.stdout + r.stderr
+    return r.stdout
+
+
 def gpu_available():
     try:
         import torch

@@ -11,7 +11,7 @@ import pytest
 import oracle
 import yara_amd
 from yara_amd import _lib
-from conftest import REPO, case_arrays, case_data, golden, ref_tables, tables_npz
+from conftest import REPO, case_arrays, case_data, golden, ref_tables, run_diag_child, tables_npz
 
 HEADER = os.path.join(REPO, "include", "yara_amd.h")
 
@@ -61,17 +61,33 @@ def test_flattening_stats(name, states, depth, keys):
     assert inf["filter_mode"] == {"B": 1, "C": 0, "E": 2}[name]
 
 
-def test_pair_filter_switch(monkeypatch):
-    monkeypatch.setenv("YAMD_PAIR_FILTER", "1")
-    inf = yara_amd.Tables.from_npz(tables_npz("E"), device=-1).info()
-    assert inf["filter_mode"] == 0
+FORM_CODE = ("import yara_amd\nfrom conftest import tables_npz\n"
+             "print('modes', *[yara_amd.Tables.from_npz(tables_npz(n), device=-1).info()"
+             "['filter_mode'] for n in ('B', 'E')])\n")
+
+
+def test_pair_filter_switch():
+    """YAMD_PAIR_FILTER (diagnostic build): the pair filter for 4-byte-key sets."""
+    assert run_diag_child(FORM_CODE, {"YAMD_PAIR_FILTER": "1"}).split()[-3:] == ["modes", "0", "0"]
 
 
 @pytest.mark.parametrize("form,mode", [("plain", 1), ("hash", 2)])
-def test_even_filter_forms(monkeypatch, form, mode):
-    monkeypatch.setenv("YAMD_EVEN_FILTER", form)
-    for name in ("B", "E"):
-        assert yara_amd.Tables.from_npz(tables_npz(name), device=-1).info()["filter_mode"] == mode
+def test_even_filter_forms(form, mode):
+    """YAMD_EVEN_FILTER (diagnostic build) forces one even-filter block form."""
+    out = run_diag_child(FORM_CODE, {"YAMD_EVEN_FILTER": form})
+    assert out.split()[-3:] == ["modes", str(mode), str(mode)]
+
+
+def test_product_library_ignores_ab_switches(monkeypatch):
+    """The product library reads none of the A/B switches: with
+    them set, B and E still get the host's own filter choice."""
+    monkeypatch.setenv("YAMD_PAIR_FILTER", "1")
+    monkeypatch.setenv("YAMD_EVEN_FILTER", "plain")
+    monkeypatch.setenv("YAMD_NO_GUARDS", "1")
+    modes = [yara_amd.Tables.from_npz(tables_npz(n), device=-1).info()["filter_mode"]
+             for n in ("B", "E")]
+    assert modes == [1, 2]
+    assert not hasattr(yara_amd._lib.lib(), "yr_amd__diag_kernel_mode")
 
 
 def test_short_and_root_tables():

@@ -297,8 +297,8 @@ def test_scan_window_rejects_bad_windows():
                                  {"YAMD_SEG_KIB": "8", "YAMD_SEG_DYNAMIC": "1"}])
 def test_segment_schedules(env):
     """The profiling switches of the segment schedule (several segments per
-    wave, round-robin or claimed from a counter; read once per process, hence
-    a child process) give the same candidate stream.  48 MiB with 4-8 KiB
+    wave, round-robin or claimed from a counter; read once per process by the
+    diagnostic build, hence a child process) give the same candidate stream.  48 MiB with 4-8 KiB
     segments: several segments per wave of the full-chip grid."""
     import os
     import subprocess
@@ -319,8 +319,9 @@ def test_segment_schedules(env):
         "assert np.array_equal(got, ref), (len(got), len(ref))\n"
         "print('ok', len(got))\n" % (repo, os.path.join(repo, "tests"),
                                      os.path.join(repo, "tests", "golden")))
+    from conftest import DIAG_LIB   # the switches exist in the diagnostic build only
     r = subprocess.run([sys.executable, "-c", code], capture_output=True, text=True, timeout=240,
-                       env=dict(os.environ, **env))
+                       env=dict(os.environ, YARA_AMD_LIB=DIAG_LIB, **env))
     assert r.returncode == 0 and "ok" in r.stdout, r.stdout + r.stderr
 
 
@@ -398,19 +399,11 @@ def test_block_larger_than_4gib():
     np.testing.assert_array_equal(head8["pool_index"], head4["pool_index"])
 
 
-@pytest.mark.parametrize("rules", ["B", "E"])
-@pytest.mark.parametrize("stride", [5, 7, 16, 33, 1021])
-def test_even_filter_planted_keys(rules, stride, monkeypatch):
-    """Rule sets whose keys are all 4 bytes scan with the even-position filter
-    (internal.h kFilterEven: only the windows ending at even positions are
-    tested, each key inserted as its 3-byte prefix and suffix).  Strings planted
-    every `stride` bytes end at both parities and at every lane byte (lane,
-    tile and segment edges included; strides 5 and 7 put several hits in one
-    lane, the drains' synchronous path): candidates equal the oracle's with the
-    plain and the hashed even filter and the pair filter."""
+def even_planted(rules, stride):
+    """Strings of rule set `rules` planted every `stride` bytes (drifting through
+    every residue mod 16) into 2 MiB + 12345 random bytes."""
     import planted
     import gen_rules
-    tab = ref_tables(rules)
     inst = [b for b, _ in planted.string_instances(gen_rules.gen(rules))]
     size = (2 << 20) + 12345
     data = oracle.xorshift(size, 43).copy()
@@ -419,21 +412,57 @@ def test_even_filter_planted_keys(rules, stride, monkeypatch):
         s = inst[k % len(inst)][: max(4, stride - 1)]
         data[off:off + len(s)] = np.frombuffer(s, np.uint8)
         k += 1
-        off += stride + (k % 3 == 0)                # drift through every residue mod 16
+        off += stride + (k % 3 == 0)
+    return data
+
+
+EVEN_STRIDES = [5, 7, 16, 33, 1021]
+
+
+@pytest.mark.parametrize("rules", ["B", "E"])
+@pytest.mark.parametrize("stride", EVEN_STRIDES)
+def test_even_filter_planted_keys(rules, stride):
+    """Rule sets whose keys are all 4 bytes scan with the even-position filter
+    (internal.h kFilterEven: only the windows ending at even positions are
+    tested, each key inserted as its 3-byte prefix and suffix).  Strings planted
+    every `stride` bytes end at both parities and at every lane byte (lane,
+    tile and segment edges included; strides 5 and 7 put several hits in one
+    lane, the drains' synchronous path): candidates equal the oracle's."""
+    data = even_planted(rules, stride)
     even = dev_tables(rules)
     assert even.info()["filter_mode"] in (1, 2)
     pos, allp = yara_amd.Scanner(even).candidates(data)
-    ref = oracle.candidates(tab, data)
-    assert not allp and len(ref) > size // stride // 8
+    ref = oracle.candidates(ref_tables(rules), data)
+    assert not allp and len(ref) > data.size // stride // 8
     np.testing.assert_array_equal(pos, ref)
-    # every form: the plain and the hashed even filter, the pair filter
-    for env, val, mode in (("YAMD_EVEN_FILTER", "plain", 1), ("YAMD_EVEN_FILTER", "hash", 2),
-                           ("YAMD_PAIR_FILTER", "1", 0)):
-        monkeypatch.setenv(env, val)
-        t = yara_amd.Tables.from_npz(tables_npz(rules), device=0)
-        monkeypatch.delenv(env)
-        assert t.info()["filter_mode"] == mode
-        np.testing.assert_array_equal(yara_amd.Scanner(t).candidates(data)[0], ref)
+
+
+def test_every_filter_form_on_planted_keys():
+    """Every filter form the host can pick -- the plain and the hashed even
+    filter and the pair filter -- forced in turn through the diagnostic build's
+    switches (one child process): candidates equal the oracle's on the planted
+    B and E buffers of every stride."""
+    from conftest import run_diag_child
+    code = (
+        "import os, numpy as np, torch, yara_amd, oracle\n"
+        "from conftest import ref_tables, tables_npz\n"
+        "from test_gpu_parity import even_planted, EVEN_STRIDES\n"
+        "n = 0\n"
+        "for rules in ('B', 'E'):\n"
+        "  for stride in EVEN_STRIDES:\n"
+        "    data = even_planted(rules, stride)\n"
+        "    ref = oracle.candidates(ref_tables(rules), data)\n"
+        "    for env, val, mode in (('YAMD_EVEN_FILTER', 'plain', 1),\n"
+        "                           ('YAMD_EVEN_FILTER', 'hash', 2), ('YAMD_PAIR_FILTER', '1', 0)):\n"
+        "      os.environ[env] = val\n"
+        "      t = yara_amd.Tables.from_npz(tables_npz(rules), device=0)\n"
+        "      del os.environ[env]\n"
+        "      assert t.info()['filter_mode'] == mode\n"
+        "      got = yara_amd.Scanner(t).candidates(data)[0]\n"
+        "      assert np.array_equal(got, ref), (rules, stride, mode)\n"
+        "      n += 1\n"
+        "print('forms ok', n)\n")
+    assert "forms ok 30" in run_diag_child(code, timeout=600)
 
 
 def test_dense_rescans_after_capacity_learning():

@@ -2,6 +2,10 @@
 by construction).  Interleaved rounds in one process (guide §5.4 rule 24).
 
     python tools/ablate.py [--gib 4] [--rules C] [--rounds 5] [--modes 0,1,2,3]
+
+Modes other than 0 exist only in the diagnostic build (make -C yara_amd/csrc
+diag -> yara_amd/_diag/libyara_amd.so), which is loaded unless YARA_AMD_LIB
+names another build; with --modes 0 any build (e.g. a variant) is timed.
 """
 import argparse
 import ctypes
@@ -28,18 +32,24 @@ def main():
     ap.add_argument("--reps", type=int, default=3)
     ap.add_argument("--modes", default="0,1,2,3,4,5,6")
     a = ap.parse_args()
+    modes = [int(m) for m in a.modes.split(",")]
+    if any(modes) and not os.environ.get("YARA_AMD_LIB"):
+        os.environ["YARA_AMD_LIB"] = os.path.join(REPO, "yara_amd", "_diag", "libyara_amd.so")
     import torch
     import yara_amd
     from yara_amd import _lib
     L = _lib.lib()
-    L.yr_amd__diag_kernel_mode.argtypes = [ctypes.c_void_p, ctypes.c_int]
+    set_mode = getattr(L, "yr_amd__diag_kernel_mode", None)
+    if set_mode is not None:
+        set_mode.argtypes = [ctypes.c_void_p, ctypes.c_int]
+    elif any(modes):
+        raise SystemExit("modes != 0 need the diagnostic build (make -C yara_amd/csrc diag)")
     n = int(a.gib * (1 << 30))
     buf = torch.empty(n + 16, dtype=torch.uint8, device="cuda")
     yara_amd.fill_xorshift64(buf.data_ptr(), n, 1)
     t = yara_amd.Tables.from_npz(os.path.join(REPO, "tests", "golden", "tables", a.rules + ".npz"))
     sc = yara_amd.Scanner(t)
     sc.set_timing(True)
-    modes = [int(m) for m in a.modes.split(",")]
     res = {m: [] for m in modes}
     counts = {}
     for _ in range(60):                 # clock ramp (see bench.py)
@@ -47,12 +57,14 @@ def main():
         sc.device_result()
     for _ in range(a.rounds):
         for m in modes:
-            assert L.yr_amd__diag_kernel_mode(sc.handle if hasattr(sc, "handle") else sc._h, m) == 0
+            if set_mode is not None:
+                assert set_mode(sc._h, m) == 0
             for _ in range(a.reps):
                 sc.scan_device(buf.data_ptr(), n)
                 counts[m] = sc.device_result()[1]
                 res[m].append(sc.kernel_ms())
-    L.yr_amd__diag_kernel_mode(sc._h, 0)
+    if set_mode is not None:
+        set_mode(sc._h, 0)
     out = {}
     for m in modes:
         med = statistics.median(res[m])

@@ -3,10 +3,22 @@
 #pragma once
 
 #include <stdint.h>
+#include <stdlib.h>
 
 #include <hip/hip_runtime.h>
 
+// Diagnostic builds (make -C yara_amd/csrc diag -> yara_amd/_diag/libyara_amd.so,
+// used by tools/ only): the scan kernel's profiling ablations
+// (yr_amd__diag_kernel_mode) and the A/B environment switches.  The product
+// library instantiates only the product kernels and reads none of the switches.
+#ifndef YAMD_DIAG
+#define YAMD_DIAG 0
+#endif
+
 namespace yamd {
+
+// An A/B experiment switch (tools/README.md): null in the product library.
+inline const char* diag_env(const char* name) { return YAMD_DIAG ? getenv(name) : nullptr; }
 
 // ---------------------------------------------------------------------------
 // Geometry of the scan kernel (gfx950: wave64, 160 KiB LDS per CU).
@@ -20,8 +32,8 @@ constexpr int kWave = 64;
 constexpr int kBytesPerLane = 16;
 constexpr int kTile = kWave * kBytesPerLane;        // 1024 B
 constexpr uint32_t kSegment = 1u << 20;   // max segment: 1 MiB (ring entries hold offset/16 in 16 bits)
-constexpr uint32_t kSegmentTarget = kSegment;
-constexpr uint32_t kMaxByteKeys = 4;   // 1-byte keys tested in stage 1 (more: filter)   // preferred segment size (scanner.cpp)
+constexpr uint32_t kSegmentTarget = kSegment;   // preferred segment size (scanner.cpp)
+constexpr uint32_t kMaxByteKeys = 4;   // 1-byte keys tested in stage 1 (more: filter)
 constexpr int kWavesPerWG = 16;
 constexpr int kWGThreads = kWave * kWavesPerWG;     // 1024
 

@@ -385,13 +385,16 @@ int yr_amd_scanner_set_timing(yr_amd_scanner* s, int enable) {
   return YR_AMD_SUCCESS;
 }
 
-// Not declared in include/yara_amd.h: profiling ablations of the scan kernel
-// (tools/ablate.py).  Any mode other than 0 produces wrong results.
+#if YAMD_DIAG
+// Diagnostic builds only (not declared in include/yara_amd.h): profiling
+// ablations of the scan kernel (tools/ablate.py).  Any mode other than 0
+// produces wrong results.
 int yr_amd__diag_kernel_mode(yr_amd_scanner* s, int mode) {
   if (s == nullptr || mode < 0 || mode > 12) return YR_AMD_INVALID_ARGUMENT;
   s->diag_mode = mode;
   return YR_AMD_SUCCESS;
 }
+#endif
 
 int yr_amd_scanner_kernel_ms(yr_amd_scanner* s, float* ms) {
   if (s == nullptr || ms == nullptr || !s->ev_valid) return YR_AMD_INVALID_ARGUMENT;
@@ -440,13 +443,13 @@ int yr_amd_scan_window(yr_amd_scanner* s, const uint8_t* d_window, uint64_t wind
   const uint64_t nbytes = byte_end - byte_begin;
   // YAMD_SEG_KIB=<k>: segment target k KiB instead of kSegmentTarget, and with
   // YAMD_SEG_DYNAMIC set, segments after a wave's first are claimed from a
-  // counter (scan_segments_kernel's seg_next) -- profiling experiments only
+  // counter (scan_segments_kernel's seg_next) -- diagnostic builds only
   static const uint32_t seg_target = [] {
-    const char* e = getenv("YAMD_SEG_KIB");
+    const char* e = diag_env("YAMD_SEG_KIB");
     const uint32_t k = e ? (uint32_t)atoi(e) : 0u;
     return k >= 4 && k * 1024u <= kSegment ? k * 1024u : kSegmentTarget;
   }();
-  static const bool dynamic = getenv("YAMD_SEG_DYNAMIC") != nullptr;
+  static const bool dynamic = diag_env("YAMD_SEG_DYNAMIC") != nullptr;
   const uint32_t seg_bytes = choose_seg_bytes(nbytes, t->num_cus, seg_target);
   const uint64_t n_segments64 = (nbytes + seg_bytes - 1) / seg_bytes;
   if (n_segments64 > 0xFFFFFFFFull) return YR_AMD_INVALID_ARGUMENT;
@@ -504,7 +507,7 @@ int yr_amd_scan_device_result(yr_amd_scanner* s, const uint64_t** d_positions, u
   HIP_TRY(hipEventSynchronize(s->ev_done));
   uint64_t total = s->h_summary[0];
   const uint64_t maxc = s->h_summary[1];
-  static const bool no_learn = getenv("YAMD_NO_CAP_LEARN") != nullptr;   // A/B only
+  static const bool no_learn = diag_env("YAMD_NO_CAP_LEARN") != nullptr;   // A/B only
   if (maxc > s->last.seg_cap && !no_learn) {
     s->dense_per_kib = std::max<uint32_t>(
         s->dense_per_kib, (uint32_t)std::min<uint64_t>((maxc * 1280 + s->last.seg_bytes - 1) /
@@ -625,7 +628,9 @@ int yr_amd_tables_set_strings(yr_amd_tables* t, const uint32_t* pool_string, uin
   t->h_str_flags.resize(n_strings);
   for (uint32_t k = 0; k < n_strings; ++k) {
     t->h_str_flags[k] = strings[k].flags;
-    t->max_str_bytes = std::max<uint64_t>(t->max_str_bytes, 2ull * strings[k].length);
+    // a wide literal compares 2 * length bytes; its FULL_WORD test reads the
+    // two after them (scan.c:680-682, verify.hip call_matters)
+    t->max_str_bytes = std::max<uint64_t>(t->max_str_bytes, 2ull * strings[k].length + 2);
   }
   t->has_strings = true;
   return YR_AMD_SUCCESS;
@@ -829,7 +834,7 @@ int yr_amd_tables_set_re_code(yr_amd_tables* t, uint32_t n_pool, const uint32_t*
   // the programs go into the pool records (uploaded again) with their guards
   // (the forward program starts at the atom: its first `backtrack` bytes are
   // the atom's)
-  const bool no_guards = getenv("YAMD_NO_GUARDS") != nullptr;   // A/B measurements only
+  const bool no_guards = diag_env("YAMD_NO_GUARDS") != nullptr;   // A/B measurements only
   for (uint32_t k = 0; k < n_pool; ++k) {
     DevPoolRec& e = t->h_pool[k];
     e.re = re[k];
@@ -889,11 +894,11 @@ int yr_amd_verify_device(yr_amd_scanner* s, uint64_t data_base, const yr_amd_ver
   v.re_on = t->d_re_code != nullptr ? 1 : 0;
   v.re_code = t->d_re_code;
   uint64_t total = 0;
-  // records carry a 32-bit candidate index, and the launch is one thread per
-  // candidate: a candidate stream of 2^32 or more (a root-accepting rule set
-  // on a block of 4 GiB or more) is refused -- replay it on the host
-  // (yr_amd_scan_block + yr_amd_replay) instead
-  if (v.count >= 0xFFFFFFFFull) return YR_AMD_INVALID_ARGUMENT;
+  // records carry a 32-bit candidate index: a candidate stream longer than
+  // YR_AMD_VERIFY_MAX_CANDIDATES (2^32; possible only on blocks of 4 GiB or
+  // more) is refused -- replay it on the host (yr_amd_scan_block +
+  // yr_amd_replay) instead, as the libyara shim does for such blocks
+  if (v.count > YR_AMD_VERIFY_MAX_CANDIDATES) return YR_AMD_INVALID_ARGUMENT;
   if (v.count > 0) {
     if (v.data == nullptr) return YR_AMD_INVALID_ARGUMENT;
     int r = grow(s->d_vcount, s->vcount_cap, v.count);

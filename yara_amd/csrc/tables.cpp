@@ -274,7 +274,7 @@ int flatten_tables(const uint32_t* T, const uint32_t* M, uint32_t n_slots,
   // ending at an even position has its suffix window there; one ending at an
   // odd position has its prefix window ending at the even position before it.
   // (YAMD_PAIR_FILTER: the pair filter regardless -- A/B measurements.)
-  if (out.len_mask == (1u << 4) && getenv("YAMD_PAIR_FILTER") == nullptr) {
+  if (out.len_mask == (1u << 4) && diag_env("YAMD_PAIR_FILTER") == nullptr) {
     // both block forms; the one whose blocks pass fewer random windows
     // (sum over blocks of |lo bits| x |hi bits|) unless the plain form is
     // within 25 % (its test is one instruction shorter).  YAMD_EVEN_FILTER =
@@ -290,7 +290,7 @@ int flatten_tables(const uint32_t* T, const uint32_t* M, uint32_t n_slots,
       for (uint32_t b = 0; b < kFilterWords / 2; ++b)
         pass[h] += (uint64_t)__builtin_popcount(f[h][2 * b]) * __builtin_popcount(f[h][2 * b + 1]);
     }
-    const char* e = getenv("YAMD_EVEN_FILTER");
+    const char* e = diag_env("YAMD_EVEN_FILTER");
     const bool hashed = e ? strcmp(e, "hash") == 0 : 4 * pass[1] < 3 * pass[0];
     out.filter_mode = hashed ? kFilterEvenHash : kFilterEven;
     out.filter = std::move(f[hashed ? 1 : 0]);

@@ -734,15 +734,15 @@ __device__ bool call_matters(const VerifyParams& p, const DevPoolRec& st, uint64
       !(st.flags & (kStrUnmodelled | kStrFullWord)))
     return st.backtrack != 0;   // scan.c:907-915: decided without reading data
   // Every byte the call may read lies in [offset - YR_RE_SCAN_LIMIT, offset +
-  // max(YR_RE_SCAN_LIMIT, 2 * length)) (regexp scans are limited to
+  // max(YR_RE_SCAN_LIMIT, 2 * length + 2)) (regexp scans are limited to
   // YR_RE_SCAN_LIMIT each way, re.c:1753-1760, :2172-2174; a wide literal compares 2 * length
-  // bytes).  A shard holding only [win_lo, win_hi) of the block keeps a call
+  // bytes and its FULL_WORD test reads the two after them, scan.c:680-682).  A shard holding only [win_lo, win_hi) of the block keeps a call
   // whose bytes are not all there (a shard sized with the tables' verify halo,
   // yr_amd_tables_info, never does).
   if (p.win_lo != 0 || p.win_hi != p.size) {
     const uint64_t need_lo = offset - min<uint64_t>(offset, (uint64_t)kReScanLimit);
     const uint64_t need_hi =
-        min<uint64_t>(p.size, offset + max<uint64_t>((uint64_t)kReScanLimit, 2ull * st.length));
+        min<uint64_t>(p.size, offset + max<uint64_t>((uint64_t)kReScanLimit, 2ull * st.length + 2));
     if (need_lo < p.win_lo || need_hi > p.win_hi) return true;
   }
   if (!(st.flags & kStrLiteral)) return re_call_matters(p, st, st.flags, offset, lds, codebuf);
