@@ -15,10 +15,13 @@ same plus on-device pre-verification per rank and, for N > 1, the gather of
 the pre-verified {offset, pool index} records.
 
     python bench.py [--gpus N] [--steps K] [--warmup W]
-
-The default warm-up (50 steps, ~60 ms) lets the GPU reach its steady clocks:
-with 3 warm-up steps the kernel averages ~1.14 ms, settled ~1.05 ms.
     torchrun --nproc-per-node N bench.py --gpus N ...
+
+Clocks: from idle the scan kernel's first launches take up to 1.2 ms and
+settle at ~0.86 ms after ~25 ms of kernel time.  Every rank, for every N,
+first scans back to back for --clock-warmup-s seconds (default 0.4 s, ~450
+scans) before any measured leg, so the headline of N = 1 and of N > 1 is taken
+on the same settled clock; W warm-up steps follow as usual.
 
 Rank 0 prints one JSON line.  value = total bytes scanned by all ranks per
 second (decimal GB/s).  roofline = the scan kernel's algorithmic HBM bytes
@@ -54,6 +57,8 @@ def parse():
     ap.add_argument("--no-other", action="store_true",
                     help="skip the other rule sets' kernel timings (B, E, rx, short, fuzz0, fuzz3)")
     ap.add_argument("--backend", default="nccl", help="nccl (= RCCL) or gloo (rehearsal)")
+    ap.add_argument("--clock-warmup-s", type=float, default=0.4,
+                    help="back-to-back scans before the measured legs, on every rank")
     return ap.parse_args()
 
 
@@ -224,13 +229,25 @@ def main():
             kms.append(t)
         return out, kms
 
+    # Clock warm-up, the same on every rank for every N: back-to-back scans of
+    # the rank's own window for a fixed wall time (from idle the scan kernel's
+    # first launches take up to 1.2 ms and settle at ~0.86 ms over ~25 ms of
+    # work, profiles/r02_baseline_kernel_stats.csv -- W = 5 warm-up steps alone
+    # do not cover that).
+    t_w = time.perf_counter()
+    n_clock = 0
+    while time.perf_counter() - t_w < args.clock_warmup_s:
+        launch(n_clock)
+        if n_clock >= depth - 1:
+            scanners[(n_clock - depth + 1) % depth].device_result()
+        n_clock += 1
+    for k in range(max(0, n_clock - depth + 1), n_clock):
+        scanners[k % depth].device_result()
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
     # Order of the legs: the secondary measurements first (the other rule sets'
-    # kernel times, the verification-complete step), the headline last.  All of
-    # them are reported in the line; running the headline last also means it is
-    # taken at the GPU's settled clocks -- from idle, the scan kernel's first
-    # launches take up to 1.2 ms and settle at ~0.85 ms over ~25 ms of work
-    # (profiles/r02_baseline_kernel_stats.csv), which W = 5 warm-up steps alone
-    # do not cover.
+    # kernel times, the verification-complete step), the headline last.
     # the same input under the other rule sets of SURVEY.md §8d (kernel time only,
     # not the bench value): B = 1,000 4-byte hex atoms, E = 2,000 nocase/masked;
     # and the shapes with 1-byte keys, whose candidates are dense:
@@ -291,8 +308,9 @@ def main():
                 "value": round(total * args.steps / v_elapsed / 1e9, 3), "unit": "GB/s",
                 "records": int(v_out if world == 1 else (v_out.shape[0] if v_out is not None else -1)),
                 "what": "scan + compaction + on-device pre-verification (yr_amd_verify_device)"
-                        + ("" if world == 1 else " of each rank's window + RCCL gather of the "
-                           "{offset, pool index} records to rank 0")}
+                        + ("" if world == 1 else " of each rank's window + %s gather of the "
+                           "{offset, pool index} records to rank 0"
+                           % ("RCCL" if args.backend == "nccl" else args.backend))}
 
     run(args.warmup)
     for sc in scanners:
@@ -347,13 +365,20 @@ def main():
         p = pos.cpu().numpy()
         ok = bool((p[1:] > p[:-1]).all()) if p.size > 1 else True
         check = {"ascending": ok, "candidates": int(p.size)}
-        if world == 1 and args.rules == "C" and shard == 4 * GiB and args.seed == 1:
-            from conftest import golden
+        if args.rules == "C" and shard == 4 * GiB and args.seed == 1 and world <= 8:
+            # every rank's shard against its golden (tests/golden/config_d.json,
+            # shard 0 = the stock golden C_4G): count and SHA-256 of its positions
             import oracle
-            rec = golden()["cases"]["C_4G"]
-            check["golden_candidate_count"] = rec["candidate_count"]
-            check["match_golden"] = (int(p.size) == rec["candidate_count"] and
-                                     oracle.positions_sha(p) == rec["candidate_sha"])
+            with open(os.path.join(REPO, "tests", "golden", "config_d.json")) as f:
+                gold = json.load(f)["shards"][:world]
+            bounds = [ydist.shard_bounds(total, world, r) for r in range(world)]
+            parts = [p[(p > b) & (p <= e)] if b > 0 else p[p <= e] for b, e in bounds]
+            check["golden_candidate_count"] = sum(g["count"] for g in gold)
+            check["match_golden"] = all(
+                q.size == g["count"] and oracle.positions_sha(q) == g["sha"]
+                for q, g in zip(parts, gold))
+            check["golden"] = ("tests/golden/config_d.json, %d shard(s); shard 0 = stock "
+                               "golden C_4G" % world)
 
     if rank == 0:
         traffic, traffic_src = load_traffic(shard)

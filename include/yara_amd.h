@@ -426,6 +426,53 @@ int yr_amd_pipeline_next(
 int yr_amd_pipeline_drain(yr_amd_pipeline* pipeline);
 
 /*
+ * ---- Multi-device block scans ----
+ *
+ * One process, n devices (n <= YR_AMD_MAX_DEVICES; a device may repeat: n
+ * logical devices on fewer GPUs).  A block is split into n byte ranges, equal
+ * 1 MiB-aligned slices with the last taking the rest (yara_amd/dist.py
+ * shard_bounds); device k holds only its WINDOW of the block -- its range plus
+ * the tables' verify halos (yr_amd_tables_info) -- scans it
+ * (yr_amd_scan_window) and pre-verifies its own candidates
+ * (yr_amd_verify_device), each device on its own stream and host thread.
+ * Records are block-global: their concatenation in device order is exactly
+ * yr_amd_scan_block_verified's on the whole block, candidate indices rebased
+ * onto the whole block's stream.  The input buffers shard across the GPUs of
+ * a node with no data-path exchange (the north star's 8-GPU layout inside one
+ * libyara process; torch.distributed ranks use the same windows, dist.py).
+ */
+#define YR_AMD_MAX_DEVICES 64
+typedef struct yr_amd_multi yr_amd_multi;
+
+/* tables[k]: the same rule set built on device k (yr_amd_tables_create +
+ * yr_amd_tables_set_strings [+ _set_re_code]), one per device; owned by the
+ * caller and kept alive while the multi scanner exists.  One multi scanner per
+ * thread (like yr_amd_scanner). */
+int yr_amd_multi_create(yr_amd_tables* const* tables, uint32_t n, yr_amd_multi** multi);
+int yr_amd_multi_destroy(yr_amd_multi* multi);
+
+/* Device k's byte range [*begin, *end) of a block of `size` bytes and the
+ * window [*window_begin, *window_end) it holds (any pointer may be NULL). */
+int yr_amd_multi_shard(const yr_amd_multi* multi, uint64_t size, uint32_t k, uint64_t* begin,
+                       uint64_t* end, uint64_t* window_begin, uint64_t* window_end);
+
+/* yr_amd_scan_block_verified across the devices: *records / *count are host
+ * records owned by the multi scanner (valid until its next call).  A device
+ * whose range could exceed YR_AMD_VERIFY_MAX_CANDIDATES candidates (range + 1
+ * > the limit) makes it return YR_AMD_INVALID_ARGUMENT before any work: use
+ * the single-device replay (yr_amd_scan_block + yr_amd_replay) then. */
+int yr_amd_multi_scan_block_verified(
+    yr_amd_multi* multi,
+    const uint8_t* data,
+    size_t size,
+    uint64_t data_base,
+    const yr_amd_verify_rec** records,
+    uint64_t* count);
+
+/* The device a table set lives on (-1: host-only tables). */
+int yr_amd_tables_device(const yr_amd_tables* tables);
+
+/*
  * Kernel timing (measurement support): when enabled, the scanner records HIP
  * events around its scan kernel on its own stream; yr_amd_scanner_kernel_ms
  * returns the duration of the last scan kernel launch (after the scan result

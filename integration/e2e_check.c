@@ -24,6 +24,9 @@
  *   E2E_MODE=truncmap: both sides scan_mem an mmap of the data file whose
  *   file was truncated to half its size (the tail faults: scanner.c:493-496
  *   maps that to ERROR_COULD_NOT_MAP_FILE).
+ *   E2E_DEVICES=d0,d1,...: the GPU side on several devices (a device may
+ *   repeat: logical devices on one GPU), blocks of at least E2E_MULTI_MIN
+ *   bytes split across them (yr_gpu_rules_create_multi).
  *   E2E_THREADS=n: afterwards n threads, each with its own YR_SCANNER and
  *   YR_GPU_SCANNER on the one shared YR_GPU_RULES, scan the data
  *   E2E_THREAD_REPS times concurrently; every result must equal stock's
@@ -353,8 +356,23 @@ int main(int argc, char** argv)
   int scan_whole = strcmp(g_mode, "mem") != 0; /* entry points take no data pointer */
   YR_GPU_RULES* gr;
   YR_GPU_SCANNER* gs;
-  int r = yr_gpu_rules_create(rules, 0, &gr);
+  /* E2E_DEVICES=d0,d1,...: the multi-device path (yr_gpu_rules_create_multi;
+   * devices may repeat), blocks of at least E2E_MULTI_MIN bytes split */
+  int devs[YR_AMD_MAX_DEVICES] = {0};
+  int n_devs = 1;
+  if (getenv("E2E_DEVICES"))
+  {
+    n_devs = 0;
+    for (const char* p = getenv("E2E_DEVICES"); *p && n_devs < YR_AMD_MAX_DEVICES;)
+    {
+      devs[n_devs++] = (int) strtol(p, (char**) &p, 10);
+      if (*p == ',') p++;
+    }
+  }
+  int r = yr_gpu_rules_create_multi(rules, devs, n_devs, &gr);
   if (r == 0) r = yr_gpu_scanner_create(gr, &gs);
+  if (r == 0 && getenv("E2E_MULTI_MIN"))
+    yr_gpu_scanner_set_multi_min_block(gs, strtoull(getenv("E2E_MULTI_MIN"), NULL, 10));
   const char* pv = getenv("E2E_PREVERIFY"); /* "0": replay the full candidate stream */
   if (r == 0 && pv != NULL && strcmp(pv, "0") == 0) yr_gpu_scanner_set_preverify(gs, 0);
   if (r)
@@ -432,10 +450,11 @@ int main(int argc, char** argv)
          "\"matches_stock\": %zu, \"matches_gpu\": %zu, \"rules_matching\": %d, "
          "\"same_matches\": %s, \"same_rule_reports\": %s, \"finished\": [%d, %d], "
          "\"stock_s\": %.4f, \"gpu_s\": %.4f, \"too_many\": [%d, %d], \"threads\": %d, "
-         "\"threads_ok\": %s}\n",
+         "\"threads_ok\": %s, \"devices\": %d, \"multi_blocks\": %llu}\n",
          g_mode, n, bsize, rs, rg, a.n, b.n, n_match_rules, same_matches ? "true" : "false",
          same_rules ? "true" : "false", a.finished, b.finished, ts, tg, a.too_many, b.too_many,
-         threads, threads_ok ? "true" : "false");
+         threads, threads_ok ? "true" : "false", n_devs,
+         (unsigned long long) yr_gpu_scanner_multi_blocks(gs));
   yr_gpu_scanner_destroy(gs);
   yr_gpu_rules_destroy(gr);
   yr_rules_destroy(rules);

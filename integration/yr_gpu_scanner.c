@@ -48,7 +48,9 @@
 struct YR_GPU_RULES
 {
   YR_RULES* rules;
-  yr_amd_tables* tables;
+  yr_amd_tables* tables;   /* == dev_tables[0]: single-device scans */
+  uint32_t n_devices;
+  yr_amd_tables* dev_tables[YR_AMD_MAX_DEVICES]; /* yr_gpu_rules_create_multi */
 };
 
 struct YR_GPU_SCANNER
@@ -62,6 +64,9 @@ struct YR_GPU_SCANNER
   uint32_t depth;
   uint32_t inflight;
   int direct;            /* single in-memory block (scan_mem): no staging copy */
+  yr_amd_multi* multi;   /* n_devices > 1: large blocks split across the devices */
+  uint64_t multi_min;    /* smallest block that is split */
+  uint64_t multi_blocks; /* blocks scanned across the devices (statistics) */
 #ifdef YR_HAVE_BLOCK_SCANNER
   YR_BLOCK_SCANNER block_scanner; /* yr_gpu_scanner_attach */
 #endif
@@ -190,12 +195,10 @@ static int _attach_strings(YR_RULES* rules, uint32_t n_pool, yr_amd_tables* t)
   return r;
 }
 
-int yr_gpu_rules_create(YR_RULES* rules, int device, YR_GPU_RULES** out)
+/* The device tables of one YR_RULES on one device (or host-only, device < 0). */
+static int _create_tables(YR_RULES* rules, int device, yr_amd_tables** out)
 {
   *out = NULL;
-  YR_GPU_RULES* g = (YR_GPU_RULES*) calloc(1, sizeof(YR_GPU_RULES));
-  if (g == NULL) return ERROR_INSUFFICIENT_MEMORY;
-
   /* table sizes exactly as yr_rules_get_stats computes them (rules.c:442) */
   uint32_t n_slots = (uint32_t) (yr_arena_get_current_offset(
                                      rules->arena, YR_AC_TRANSITION_TABLE) /
@@ -210,7 +213,6 @@ int yr_gpu_rules_create(YR_RULES* rules, int device, YR_GPU_RULES** out)
   {
     free(nx);
     free(bt);
-    free(g);
     return ERROR_INSUFFICIENT_MEMORY;
   }
   for (uint32_t k = 0; k < n_pool; k++)
@@ -219,6 +221,7 @@ int yr_gpu_rules_create(YR_RULES* rules, int device, YR_GPU_RULES** out)
     nx[k] = m->next ? (uint32_t) (m->next - rules->ac_match_pool) + 1 : 0;
     bt[k] = m->backtrack;
   }
+  yr_amd_tables* t = NULL;
   int r = yr_amd_tables_create(
       rules->ac_transition_table,
       rules->ac_match_table,
@@ -227,26 +230,60 @@ int yr_gpu_rules_create(YR_RULES* rules, int device, YR_GPU_RULES** out)
       bt,
       n_pool,
       device,
-      &g->tables);
+      &t);
   free(nx);
   free(bt);
-  if (r == ERROR_SUCCESS && device >= 0) r = _attach_strings(rules, n_pool, g->tables);
-  if (r == ERROR_SUCCESS && device >= 0) r = _attach_re_code(rules, n_pool, g->tables);
+  if (r == ERROR_SUCCESS && device >= 0) r = _attach_strings(rules, n_pool, t);
+  if (r == ERROR_SUCCESS && device >= 0) r = _attach_re_code(rules, n_pool, t);
   if (r != ERROR_SUCCESS)
   {
-    yr_amd_tables_destroy(g->tables);
-    free(g);
+    yr_amd_tables_destroy(t);
     return r;
   }
+  *out = t;
+  return ERROR_SUCCESS;
+}
+
+int yr_gpu_rules_create_multi(
+    YR_RULES* rules,
+    const int* devices,
+    int n_devices,
+    YR_GPU_RULES** out)
+{
+  *out = NULL;
+  if (devices == NULL || n_devices < 1 || n_devices > YR_AMD_MAX_DEVICES)
+    return ERROR_INVALID_ARGUMENT;
+  if (n_devices > 1)
+    for (int k = 0; k < n_devices; k++)
+      if (devices[k] < 0) return ERROR_INVALID_ARGUMENT;
+  YR_GPU_RULES* g = (YR_GPU_RULES*) calloc(1, sizeof(YR_GPU_RULES));
+  if (g == NULL) return ERROR_INSUFFICIENT_MEMORY;
+  int r = ERROR_SUCCESS;
+  for (int k = 0; k < n_devices && r == ERROR_SUCCESS; k++)
+  {
+    r = _create_tables(rules, devices[k], &g->dev_tables[k]);
+    if (r == ERROR_SUCCESS) g->n_devices++;
+  }
+  if (r != ERROR_SUCCESS)
+  {
+    yr_gpu_rules_destroy(g);
+    return r;
+  }
+  g->tables = g->dev_tables[0];
   g->rules = rules;
   *out = g;
   return ERROR_SUCCESS;
 }
 
+int yr_gpu_rules_create(YR_RULES* rules, int device, YR_GPU_RULES** out)
+{
+  return yr_gpu_rules_create_multi(rules, &device, 1, out);
+}
+
 void yr_gpu_rules_destroy(YR_GPU_RULES* g)
 {
   if (g == NULL) return;
-  yr_amd_tables_destroy(g->tables);
+  for (uint32_t k = 0; k < g->n_devices; k++) yr_amd_tables_destroy(g->dev_tables[k]);
   free(g);
 }
 
@@ -262,11 +299,21 @@ int yr_gpu_scanner_create(YR_GPU_RULES* g, YR_GPU_SCANNER** out)
     r = yr_amd_pipeline_create(g->tables, s->depth, &s->pipe);
     if (r != ERROR_SUCCESS) yr_amd_scanner_destroy(s->scanner);
   }
+  if (r == ERROR_SUCCESS && g->n_devices > 1)
+  {
+    r = yr_amd_multi_create(g->dev_tables, g->n_devices, &s->multi);
+    if (r != ERROR_SUCCESS)
+    {
+      yr_amd_pipeline_destroy(s->pipe);
+      yr_amd_scanner_destroy(s->scanner);
+    }
+  }
   if (r != ERROR_SUCCESS)
   {
     free(s);
     return r;
   }
+  s->multi_min = YR_GPU_MULTI_MIN_BLOCK;
   s->gpu_rules = g;
   s->preverify = 1;
   *out = s;
@@ -278,9 +325,20 @@ void yr_gpu_scanner_set_preverify(YR_GPU_SCANNER* s, int enable)
   s->preverify = enable != 0;
 }
 
+void yr_gpu_scanner_set_multi_min_block(YR_GPU_SCANNER* s, uint64_t bytes)
+{
+  s->multi_min = bytes;
+}
+
+uint64_t yr_gpu_scanner_multi_blocks(const YR_GPU_SCANNER* s)
+{
+  return s->multi_blocks;
+}
+
 void yr_gpu_scanner_destroy(YR_GPU_SCANNER* s)
 {
   if (s == NULL) return;
+  yr_amd_multi_destroy(s->multi);
   yr_amd_pipeline_destroy(s->pipe);
   yr_amd_scanner_destroy(s->scanner);
   free(s->staging);
@@ -443,7 +501,8 @@ static int _direct_block(
     YR_SCANNER* scanner,
     YR_GPU_SCANNER* gs,
     const uint8_t* data,
-    YR_MEMORY_BLOCK* block)
+    YR_MEMORY_BLOCK* block,
+    int use_multi)
 {
   int result = ERROR_SUCCESS;
   uint64_t next_check = 0;
@@ -465,12 +524,35 @@ static int _direct_block(
   if (result != ERROR_SUCCESS) return result;
   const yr_amd_verify_rec* recs = NULL;
   uint64_t n = 0;
-  FAIL_ON_ERROR(yr_amd_scan_block_verified(gs->scanner, data, block->size, block->base, &recs, &n));
+  if (use_multi)
+  {
+    FAIL_ON_ERROR(yr_amd_multi_scan_block_verified(
+        gs->multi, data, block->size, block->base, &recs, &n));
+  }
+  else
+  {
+    FAIL_ON_ERROR(
+        yr_amd_scan_block_verified(gs->scanner, data, block->size, block->base, &recs, &n));
+  }
   YR_TRYCATCH(
       !(scanner->flags & SCAN_FLAGS_NO_TRYCATCH),
       { result = _replay_records(scanner, recs, n, data, block->size, block->base, next_check); },
       { result = ERROR_COULD_NOT_MAP_FILE; });
   return result;
+}
+
+/* Can the multi-device path take a block of this size?  Every device's
+ * candidate stream must fit pre-verification (yr_amd_multi_scan_block_verified
+ * refuses it otherwise). */
+static int _multi_fits(YR_GPU_SCANNER* gs, uint64_t size)
+{
+  for (uint32_t k = 0; k < gs->gpu_rules->n_devices; k++)
+  {
+    uint64_t b = 0, e = 0;
+    if (yr_amd_multi_shard(gs->multi, size, k, &b, &e, NULL, NULL) != ERROR_SUCCESS) return 0;
+    if ((e - b) + (b == 0 ? 1 : 0) > YR_AMD_VERIFY_MAX_CANDIDATES) return 0;
+  }
+  return 1;
 }
 
 /* One block: the replacement of the walk at scanner.c:493-496. */
@@ -486,12 +568,22 @@ static int _scan_one_block(
    * rule set, or a dense key): a block that could exceed it is replayed from
    * the GPU scan's stream instead -- after the blocks still in flight, in
    * order.  The same limit as the library's, so no block reaches a refusal. */
-  int replay_block = !gs->preverify ||
-                     (uint64_t) block->size + 1 > YR_AMD_VERIFY_MAX_CANDIDATES;
-  while (replay_block && gs->inflight > 0)
+  int use_multi = gs->multi != NULL && gs->preverify && block->size >= gs->multi_min &&
+                  _multi_fits(gs, block->size);
+  int replay_block = !use_multi &&
+                     (!gs->preverify ||
+                      (uint64_t) block->size + 1 > YR_AMD_VERIFY_MAX_CANDIDATES);
+  while ((replay_block || use_multi) && gs->inflight > 0)
     FAIL_ON_ERROR(_replay_next(scanner, gs));
   if (replay_block) return _yr_gpu_scan_mem_block(scanner, gs, data, block);
-  if (gs->direct) return _direct_block(scanner, gs, data, block);
+  /* a large block across the devices, whole (the caller's buffer, probed
+   * inside the trycatch) -- after the blocks still in flight, in order */
+  if (use_multi)
+  {
+    gs->multi_blocks++;
+    return _direct_block(scanner, gs, data, block, 1);
+  }
+  if (gs->direct) return _direct_block(scanner, gs, data, block, 0);
   return _pipeline_block(scanner, gs, data, block);
 }
 

@@ -17,6 +17,19 @@ typedef struct YR_GPU_RULES YR_GPU_RULES;     /* device tables of one YR_RULES *
 typedef struct YR_GPU_SCANNER YR_GPU_SCANNER; /* one per YR_SCANNER / thread */
 
 int yr_gpu_rules_create(YR_RULES* rules, int device, YR_GPU_RULES** out);
+
+/* Device tables on n_devices devices (a device may repeat).  Scanners of these
+ * rules split every block of at least YR_GPU_MULTI_MIN_BLOCK bytes (see
+ * yr_gpu_scanner_set_multi_min_block) across the devices: each holds only its
+ * shard of the block plus the rule set's verify halos, scans and pre-verifies
+ * it (yr_amd_multi_*), and the records are replayed in block order -- the
+ * same match set as one device.  Smaller blocks run on devices[0]. */
+#define YR_GPU_MULTI_MIN_BLOCK (256ull << 20)
+int yr_gpu_rules_create_multi(
+    YR_RULES* rules,
+    const int* devices,
+    int n_devices,
+    YR_GPU_RULES** out);
 void yr_gpu_rules_destroy(YR_GPU_RULES* g);
 int yr_gpu_scanner_create(YR_GPU_RULES* g, YR_GPU_SCANNER** out);
 void yr_gpu_scanner_destroy(YR_GPU_SCANNER* s);
@@ -27,6 +40,12 @@ void yr_gpu_scanner_destroy(YR_GPU_SCANNER* s);
  * effect reach yr_scan_verify_match.  Off: one block at a time, every call of
  * the reference loop replayed (yr_amd_scan_block + yr_amd_replay). */
 void yr_gpu_scanner_set_preverify(YR_GPU_SCANNER* s, int enable);
+
+/* Smallest block the multi-device path takes (rules from
+ * yr_gpu_rules_create_multi; default YR_GPU_MULTI_MIN_BLOCK). */
+void yr_gpu_scanner_set_multi_min_block(YR_GPU_SCANNER* s, uint64_t bytes);
+/* How many blocks this scanner has split across its devices. */
+uint64_t yr_gpu_scanner_multi_blocks(const YR_GPU_SCANNER* s);
 
 /* Drop-in counterparts of yr_scanner_scan_mem_blocks / yr_scanner_scan_mem
  * (scanner.c:417, :633): same arguments, callbacks, flags and error codes. */

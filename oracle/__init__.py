@@ -53,6 +53,9 @@ def lib():
         L.oracle_count_parallel.argtypes = [_u32p, _u32p, _u8p, ctypes.c_uint64, ctypes.c_int]
         L.oracle_xorshift_fill.restype = None
         L.oracle_xorshift_fill.argtypes = [_u8p, ctypes.c_uint64, ctypes.c_uint64]
+        L.oracle_xorshift_continue.restype = None
+        L.oracle_xorshift_continue.argtypes = [_u8p, ctypes.c_uint64,
+                                               ctypes.POINTER(ctypes.c_uint64)]
         L.oracle_literal_effect.restype = ctypes.c_int64
         L.oracle_literal_effect.argtypes = [_u64p, _u32p, ctypes.c_uint64, _u16p, _u32p, _u32p,
                                             _u32p, ctypes.POINTER(ctypes.c_int64), _u64p, _u8p,
@@ -72,6 +75,47 @@ def xorshift(n: int, seed: int) -> np.ndarray:
     """SURVEY.md Appendix A buffer generator (bit-exact with refdump's)."""
     buf = np.empty(max(n, 1), dtype=np.uint8)
     lib().oracle_xorshift_fill(_p(buf, _u8p), n, seed)
+    return buf[:n]
+
+
+def xorshift_state(seed: int, offset: int) -> int:
+    """Generator state after `offset` bytes (GF(2) jump-ahead: xorshift64 is
+    linear over GF(2)^64, so the state after m steps is A^m x0)."""
+    def step(x):
+        x ^= (x << 13) & 0xFFFFFFFFFFFFFFFF
+        x ^= x >> 7
+        x ^= (x << 17) & 0xFFFFFFFFFFFFFFFF
+        return x
+
+    def apply(cols, v):
+        r = 0
+        j = 0
+        while v:
+            if v & 1:
+                r ^= cols[j]
+            v >>= 1
+            j += 1
+        return r
+
+    def compose(a, b):   # a(b(.))
+        return [apply(a, c) for c in b]
+
+    base = [step(1 << j) for j in range(64)]
+    acc = [1 << j for j in range(64)]
+    m = offset
+    while m:
+        if m & 1:
+            acc = compose(base, acc)
+        base = compose(base, base)
+        m >>= 1
+    return apply(acc, (0x9E3779B97F4A7C15 * seed) & 0xFFFFFFFFFFFFFFFF)
+
+
+def xorshift_at(n: int, seed: int, offset: int) -> np.ndarray:
+    """Bytes [offset, offset + n) of the canonical input of `seed`."""
+    buf = np.empty(max(n, 1), dtype=np.uint8)
+    st = ctypes.c_uint64(xorshift_state(seed, offset))
+    lib().oracle_xorshift_continue(_p(buf, _u8p), n, ctypes.byref(st))
     return buf[:n]
 
 

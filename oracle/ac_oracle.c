@@ -208,6 +208,21 @@ void oracle_xorshift_fill(uint8_t* buf, uint64_t n, uint64_t seed)
   }
 }
 
+/* The same generator continued from *state (updated): chunked generation of
+ * multi-GiB inputs (tests/golden/make_config_d.py). */
+void oracle_xorshift_continue(uint8_t* buf, uint64_t n, uint64_t* state)
+{
+  uint64_t x = *state;
+  for (uint64_t i = 0; i < n; i++)
+  {
+    x ^= x << 13;
+    x ^= x >> 7;
+    x ^= x << 17;
+    buf[i] = (uint8_t) (x >> 24);
+  }
+  *state = x;
+}
+
 /*
  * Literal pre-verification oracle.  For every
  * call (position i, pool index k) of a verify-call stream, decide whether

@@ -288,3 +288,44 @@ def test_patched_libyara_timeout_and_threads(tmp_path):
     rc, res = _run(rf, _data_file(tmp_path, buf, "d.bin"), check=CHECK_HOOK, E2E_THREADS="4",
                    E2E_THREAD_REPS="2")
     assert res["threads_ok"] and res["same_matches"], res
+
+
+MULTI_CASES = [
+    ("C", "planted", 24 << 20, 0, 0, "0,0,0"),
+    ("lit", "lit", 16 << 20, 0, 0, "0,0,0,0,0,0,0,0"),
+    ("hex", "hex", 8 << 20, 0, 0, "0,0"),
+    ("rx", "rx", 12 << 20, 5 << 20, 1024, "0,0,0"),      # blocks of 5 MiB, each split
+    ("bytekeys", "alpha", 6 << 20, 0, 0, "0,0,0"),
+]
+
+
+def _spec(tmp_path, rules, kind, size):
+    if kind == "lit":
+        return _data_file(tmp_path, planted.lit_buffer(oracle.xorshift, size, 13), "d.bin")
+    if kind == "hex":
+        return _data_file(tmp_path, planted.hex_buffer(oracle.xorshift, size, 17), "d.bin")
+    if kind == "rx":
+        return _data_file(tmp_path, planted.rx_buffer(oracle.xorshift, size, 19), "d.bin")
+    if kind == "planted":
+        return _data_file(tmp_path, planted.planted_buffer(oracle.xorshift, gen_rules.gen(rules),
+                                                           size, 3), "d.bin")
+    x = oracle.xorshift(size, 5)
+    return _data_file(tmp_path, np.frombuffer(ALPHA, np.uint8)[x % len(ALPHA)], "d.bin")
+
+
+@needs_check
+@pytest.mark.parametrize("rules,kind,size,block,overlap,devices", MULTI_CASES)
+def test_multi_device_match_set_equals_stock(tmp_path, rules, kind, size, block, overlap, devices):
+    """Multi-device scans through the shim (yr_gpu_rules_create_multi, N
+    logical devices on the box's GPU): every block of >= 1 MiB is split
+    across the devices (shard + verify halos each), and the match set and
+    rule reports equal stock libyara's."""
+    rf = _rules_file(tmp_path, rules)
+    spec = _spec(tmp_path, rules, kind, size)
+    rc, res = _run(rf, spec, block, overlap, E2E_DEVICES=devices, E2E_MULTI_MIN=str(1 << 20))
+    assert res["rc_stock"] == 0 and res["rc_gpu"] == 0, res
+    assert res["same_matches"] and res["same_rule_reports"], res
+    assert res["devices"] == devices.count(",") + 1 and res["multi_blocks"] > 0, res
+    if kind != "alpha":
+        assert res["matches_stock"] > 0, res
+    assert rc == 0

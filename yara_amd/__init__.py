@@ -365,3 +365,51 @@ class Pipeline:
             self.close()
         except Exception:
             pass
+
+
+class Multi:
+    """Multi-device block scans in one process (yr_amd_multi_*): the block is
+    split into per-device windows (shard + verify halos), each scanned and
+    pre-verified on its device; records concatenated in device order."""
+
+    def __init__(self, tables_list):
+        self.tables = list(tables_list)
+        arr = (ctypes.c_void_p * len(self.tables))(*[t.handle.value for t in self.tables])
+        h = ctypes.c_void_p()
+        _lib.check("yr_amd_multi_create",
+                   _lib.lib().yr_amd_multi_create(arr, len(self.tables), ctypes.byref(h)))
+        self._h = h
+
+    def shard(self, size: int, k: int):
+        """(begin, end, window_begin, window_end) of device k."""
+        v = [ctypes.c_uint64() for _ in range(4)]
+        _lib.check("yr_amd_multi_shard",
+                   _lib.lib().yr_amd_multi_shard(self._h, size, k, *[ctypes.byref(x) for x in v]))
+        return tuple(x.value for x in v)
+
+    def verify_calls(self, data: np.ndarray, data_base: int = 0):
+        """yr_amd_multi_scan_block_verified: the block's effective verify calls
+        as a structured array {offset, pool_index, candidate}."""
+        d = _arr(data, np.uint8)
+        ptr = ctypes.POINTER(_lib.VerifyRec)()
+        cnt = ctypes.c_uint64()
+        dp = d.ctypes.data_as(_lib._u8p) if d.size else None
+        _lib.check("yr_amd_multi_scan_block_verified",
+                   _lib.lib().yr_amd_multi_scan_block_verified(self._h, dp, d.size, data_base,
+                                                               ctypes.byref(ptr), ctypes.byref(cnt)))
+        n = cnt.value
+        out = np.zeros(n, dtype=_lib.VERIFY_REC_DTYPE)
+        if n:
+            ctypes.memmove(out.ctypes.data, ptr, n * 16)
+        return out
+
+    def close(self):
+        if getattr(self, "_h", None) is not None and self._h.value:
+            _lib.lib().yr_amd_multi_destroy(self._h)
+            self._h = ctypes.c_void_p()
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass

@@ -102,6 +102,14 @@ PROTOTYPES = {
     "yr_amd_scan_block_verified": (_int, [_vp, _u8p, ctypes.c_size_t, ctypes.c_uint64,
                                           ctypes.POINTER(ctypes.POINTER(VerifyRec)),
                                           ctypes.POINTER(ctypes.c_uint64)]),
+    "yr_amd_multi_create": (_int, [ctypes.POINTER(_vp), ctypes.c_uint32, ctypes.POINTER(_vp)]),
+    "yr_amd_multi_destroy": (_int, [_vp]),
+    "yr_amd_multi_shard": (_int, [_vp, ctypes.c_uint64, ctypes.c_uint32] +
+                           [ctypes.POINTER(ctypes.c_uint64)] * 4),
+    "yr_amd_multi_scan_block_verified": (_int, [_vp, _u8p, ctypes.c_size_t, ctypes.c_uint64,
+                                                ctypes.POINTER(ctypes.POINTER(VerifyRec)),
+                                                ctypes.POINTER(ctypes.c_uint64)]),
+    "yr_amd_tables_device": (_int, [_vp]),
 }
 
 _lib = None

@@ -293,6 +293,8 @@ int yr_amd_tables_destroy(yr_amd_tables* t) {
   return YR_AMD_SUCCESS;
 }
 
+int yr_amd_tables_device(const yr_amd_tables* t) { return t == nullptr ? -1 : t->device; }
+
 int yr_amd_tables_get_info(const yr_amd_tables* t, yr_amd_tables_info* info) {
   if (t == nullptr || info == nullptr) return YR_AMD_INVALID_ARGUMENT;
   memset(info, 0, sizeof(*info));
