@@ -473,6 +473,21 @@ int yr_amd_multi_scan_block_verified(
 int yr_amd_tables_device(const yr_amd_tables* tables);
 
 /*
+ * Profiling-counter parity (libyara built with YR_PROFILING_ENABLED).
+ * yr_scan_verify_match counts profiling_info[rule].atom_matches for every
+ * call that passes its early returns (scan.c:1013-1027, :1077-1083), whether or
+ * not the string matches.  With profiling enabled on a table set,
+ * pre-verification (yr_amd_verify_device and everything built on it) also
+ * emits every dropped call past those returns as a COUNT-ONLY record: its
+ * pool_index carries YR_AMD_REC_COUNT_ONLY, and the host counts it -- after
+ * the same temp-disabled / fast-mode tests, which depend on host state at that
+ * point of the call order -- without calling the verifier
+ * (integration/yr_gpu_scanner.c).  Default off.
+ */
+#define YR_AMD_REC_COUNT_ONLY 0x80000000u
+int yr_amd_tables_set_profiling(yr_amd_tables* tables, int enable);
+
+/*
  * Kernel timing (measurement support): when enabled, the scanner records HIP
  * events around its scan kernel on its own stream; yr_amd_scanner_kernel_ms
  * returns the duration of the last scan kernel launch (after the scan result

@@ -64,6 +64,7 @@ typedef struct
   int abort_after; /* E2E_ABORT=n: CALLBACK_ABORT on the n-th RULE_MATCHING */
   int n_matching;
   int too_many;    /* CALLBACK_MSG_TOO_MANY_MATCHES messages seen */
+  uint64_t* atom_matches; /* E2E profiling build: per rule, after the scan */
 } collect;
 
 static void push(collect* c, rec x)
@@ -249,6 +250,13 @@ static int run(YR_RULES* rules, YR_GPU_SCANNER* gs, const uint8_t* data, size_t 
     r = gs ? yr_gpu_scanner_scan_mem_blocks(sc, gs, &iter) : yr_scanner_scan_mem_blocks(sc, &iter);
   }
   *secs = now() - t0;
+#ifdef YR_PROFILING_ENABLED
+  /* libyara's per-rule verify-call counts (scan.c:1083) of this scan */
+  free(c->atom_matches);
+  c->atom_matches = (uint64_t*) calloc(rules->num_rules + 1, sizeof(uint64_t));
+  for (uint32_t i = 0; i < rules->num_rules; i++)
+    c->atom_matches[i] = sc->profiling_info[i].atom_matches;
+#endif
   yr_scanner_destroy(sc);
   return r;
 }
@@ -446,6 +454,20 @@ int main(int argc, char** argv)
   int same_rules = memcmp(a.rule_msg, b.rule_msg, rules->num_rules) == 0;
   int n_match_rules = 0;
   for (uint32_t i = 0; i < rules->num_rules; i++) n_match_rules += a.rule_msg[i] == 1;
+#ifdef YR_PROFILING_ENABLED
+  /* profiling-counter parity: every rule's atom_matches, stock vs GPU */
+  uint64_t am_stock = 0, am_gpu = 0;
+  int am_equal = a.atom_matches != NULL && b.atom_matches != NULL;
+  for (uint32_t i = 0; a.atom_matches != NULL && b.atom_matches != NULL && i < rules->num_rules; i++)
+  {
+    am_stock += a.atom_matches[i];
+    am_gpu += b.atom_matches[i];
+    if (a.atom_matches[i] != b.atom_matches[i]) am_equal = 0;
+  }
+  printf("{\"profiling\": true, \"atom_matches_equal\": %s, \"atom_matches_stock\": %llu, "
+         "\"atom_matches_gpu\": %llu}\n",
+         am_equal ? "true" : "false", (unsigned long long) am_stock, (unsigned long long) am_gpu);
+#endif
   printf("{\"mode\": \"%s\", \"size\": %zu, \"block\": %zu, \"rc_stock\": %d, \"rc_gpu\": %d, "
          "\"matches_stock\": %zu, \"matches_gpu\": %zu, \"rules_matching\": %d, "
          "\"same_matches\": %s, \"same_rule_reports\": %s, \"finished\": [%d, %d], "

@@ -235,6 +235,11 @@ static int _create_tables(YR_RULES* rules, int device, yr_amd_tables** out)
   free(bt);
   if (r == ERROR_SUCCESS && device >= 0) r = _attach_strings(rules, n_pool, t);
   if (r == ERROR_SUCCESS && device >= 0) r = _attach_re_code(rules, n_pool, t);
+#ifdef YR_PROFILING_ENABLED
+  /* libyara counts every verify call past its early returns: pre-verification
+   * reports the dropped ones as count-only records (_count_only) */
+  if (r == ERROR_SUCCESS && device >= 0) r = yr_amd_tables_set_profiling(t, 1);
+#endif
   if (r != ERROR_SUCCESS)
   {
     yr_amd_tables_destroy(t);
@@ -383,6 +388,26 @@ static int _verify(void* user, uint32_t pool_index, uint64_t offset)
   return yr_scan_verify_match(c->scanner, m, c->data, c->size, c->base, (size_t) offset);
 }
 
+#ifdef YR_PROFILING_ENABLED
+/* A count-only record (YR_AMD_REC_COUNT_ONLY: a call pre-verification dropped
+ * that still passes yr_scan_verify_match's early returns): the reference's own
+ * tests in its order (scan.c:1013-1027) on the host state at this point of
+ * the call sequence, then its atom_matches count (scan.c:1083) -- nothing
+ * else of the call can have an effect. */
+static void _count_only(YR_SCANNER* scanner, YR_AC_MATCH* m, size_t size, uint64_t base,
+                        uint64_t offset)
+{
+  YR_STRING* string = m->string;
+  if (size - offset <= 0) return;
+  if (yr_bitmask_is_set(scanner->strings_temp_disabled, string->idx)) return;
+  if (scanner->flags & SCAN_FLAGS_FAST_MODE && STRING_IS_SINGLE_MATCH(string) &&
+      scanner->matches[string->idx].head != NULL)
+    return;
+  if (STRING_IS_FIXED_OFFSET(string) && string->fixed_offset != base + offset) return;
+  scanner->profiling_info[string->rule_idx].atom_matches++;
+}
+#endif
+
 /* The effective verify calls of one block (pre-verification records), in the
  * reference's order, with the walk's timeout checks (_timeout_upto). */
 static int _replay_records(
@@ -396,7 +421,18 @@ static int _replay_records(
 {
   verify_ctx ctx = {scanner, data, size, base, next_check};
   for (uint64_t c = 0; c < n; c++)
+  {
+    if (recs[c].pool_index & YR_AMD_REC_COUNT_ONLY)
+    {
+#ifdef YR_PROFILING_ENABLED
+      YR_AC_MATCH* m = &scanner->rules->ac_match_pool[recs[c].pool_index & ~YR_AMD_REC_COUNT_ONLY];
+      FAIL_ON_ERROR(_timeout_upto(scanner, &ctx.next_check, recs[c].offset + m->backtrack, size));
+      _count_only(scanner, m, size, base, recs[c].offset);
+#endif
+      continue;
+    }
     FAIL_ON_ERROR(_verify(&ctx, recs[c].pool_index, recs[c].offset));
+  }
   /* the checks the walk makes after its last dispatch, up to size - 1 */
   return _timeout_upto(scanner, &ctx.next_check, size, size);
 }

@@ -329,3 +329,38 @@ def test_multi_device_match_set_equals_stock(tmp_path, rules, kind, size, block,
     if kind != "alpha":
         assert res["matches_stock"] > 0, res
     assert rc == 0
+
+
+CHECK_PROF = os.path.join(REPO, "integration", "_build", "e2e_check_prof")
+needs_prof = pytest.mark.skipif(not os.path.exists(CHECK_PROF),
+                                reason="integration/_build/e2e_check_prof not built "
+                                       "(oracle/refprof.mk needs the reference at build time)")
+
+
+@needs_prof
+@pytest.mark.parametrize("rules,kind,size,block,overlap,extra", [
+    ("lit", "lit", 1 << 20, 0, 0, {}),
+    ("lit", "lit", 1 << 20, 4096, 512, {"E2E_FAST": "1"}),
+    ("C", "planted", 4 << 20, 0, 0, {}),
+    ("hex", "hex", 1 << 20, 0, 0, {}),
+    ("rx", "rx", 1 << 20, 8192, 1024, {}),
+    ("short", "alpha", 16 << 20, 0, 0, {}),        # strings disabled after too many matches
+    ("C", "planted", 8 << 20, 0, 0, {"E2E_DEVICES": "0,0,0", "E2E_MULTI_MIN": str(1 << 20)}),
+])
+def test_profiling_counters_equal_stock(tmp_path, rules, kind, size, block, overlap, extra):
+    """libyara built with YR_PROFILING_ENABLED (oracle/refprof.mk): the
+    per-rule atom_matches counters (scan.c:1077-1083, reported by
+    yr_scanner_get_profiling_info, scanner.c:758-829) of the GPU scan equal
+    stock's, pre-verification on -- dropped calls come back as count-only
+    records counted on the host in the reference's call order."""
+    rf = _rules_file(tmp_path, rules)
+    spec = _spec(tmp_path, rules, kind, size)
+    cmd = [CHECK_PROF, rf, spec] + ([str(block), str(overlap)] if block else [])
+    env = dict(os.environ, E2E_PREVERIFY="1", E2E_MODE="mem", **extra)
+    r = subprocess.run(cmd, capture_output=True, text=True, timeout=600, env=env)
+    lines = [json.loads(x) for x in r.stdout.strip().splitlines() if x.startswith("{")]
+    prof, res = lines[-2], lines[-1]
+    assert res["rc_stock"] == 0 and res["rc_gpu"] == 0, res
+    assert res["same_matches"] and res["same_rule_reports"], res
+    assert prof["atom_matches_equal"], prof
+    assert prof["atom_matches_stock"] > 0, prof

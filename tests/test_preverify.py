@@ -187,3 +187,30 @@ def test_guards_keep_every_planted_match():
     off = P.astype(np.uint64) - z["pool_backtrack"][K].astype(np.uint64)
     np.testing.assert_array_equal(r["offset"], off[keep])
     np.testing.assert_array_equal(r["pool_index"], K[keep])
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("case", [k for k in FULL if not CASES[k]["block"]])
+def test_profiling_count_only_records(case):
+    """yr_amd_tables_set_profiling: besides the kept calls, every dropped call
+    that passes yr_scan_verify_match's early returns (offset < size, fixed
+    offset, scan.c:1013-1027) -- i.e. every call libyara's profiling counts,
+    scan.c:1083 -- comes out as a count-only record, in the reference's call
+    order; kept records are unchanged."""
+    import yara_amd
+    rec = CASES[case]
+    arr = case_arrays(case)
+    data = case_data(rec)
+    z, keep, off, idx, base = _expected(rec, arr, data)
+    sf = z["str_flags"][z["pool_string"][idx]]
+    fixed = z["str_fixed_offset"][z["pool_string"][idx]]
+    counted = (off < len(data)) & (((sf & 0x8000) == 0) | (fixed == off.astype(np.int64)))
+    tab = yara_amd.Tables.from_npz(tables_npz(rec["rules"]), device=0, strings=True)
+    tab.set_profiling(True)
+    r = yara_amd.Scanner(tab).verify_calls(data)
+    co = (r["pool_index"] & 0x80000000) != 0
+    want = keep | counted
+    assert len(r) == int(want.sum()), (case, len(r), int(want.sum()))
+    assert np.array_equal(r["offset"], off[want])
+    assert np.array_equal(r["pool_index"] & 0x7FFFFFFF, idx[want])
+    assert np.array_equal(co, ~keep[want])

@@ -128,6 +128,12 @@ class Tables:
             self._h, ps.ctypes.data_as(_lib._u32p), self._ps.size, recs, n,
             self._blob.ctypes.data_as(_lib._u8p), len(blob), self._lower.ctypes.data_as(_lib._u8p)))
 
+    def set_profiling(self, enable: bool = True):
+        """Count-only records for libyara's profiling counters
+        (yr_amd_tables_set_profiling)."""
+        _lib.check("yr_amd_tables_set_profiling",
+                   _lib.lib().yr_amd_tables_set_profiling(self._h, int(enable)))
+
     @property
     def handle(self):
         return self._h

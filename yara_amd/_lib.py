@@ -110,6 +110,7 @@ PROTOTYPES = {
                                                 ctypes.POINTER(ctypes.POINTER(VerifyRec)),
                                                 ctypes.POINTER(ctypes.c_uint64)]),
     "yr_amd_tables_device": (_int, [_vp]),
+    "yr_amd_tables_set_profiling": (_int, [_vp, _int]),
 }
 
 _lib = None

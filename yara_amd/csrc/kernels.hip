@@ -173,7 +173,6 @@ struct WaveQueue {
   uint32_t pend;    // LDS address: kWave pairs {w4, segment offset}
   uint32_t pend_n;  // wave-uniform
   bool defer;       // wave-uniform: the per-lane hits below await their words
-  uint32_t defer_u; // the same as 0/1 (stage2_fast's integer test)
   // per lane, the first (a) and second (b) deferred hit: window, segment
   // offset (kNoHit = none), byte offset into exact[] that the next tile step
   // loads (0 = none), the loaded word
@@ -332,10 +331,6 @@ __device__ __forceinline__ uint32_t byte_keys_mask(const uint32_t (&S)[6], const
 #ifndef YAMD_CARRY_DPP2
 #define YAMD_CARRY_DPP2 1
 #endif
-// The ring append without branches or lane-mask bookkeeping (ring_append).
-#ifndef YAMD_APPEND_ASM
-#define YAMD_APPEND_ASM 0
-#endif
 template <int MODE>
 constexpr bool kHoldFl = YAMD_HOLD_FL && !kEven<MODE>;
 template <int MODE>
@@ -350,7 +345,6 @@ __device__ __forceinline__ void drain_complete(const ScanParams& p, WaveQueue& q
   const bool ha = q.oa != kNoHit && first_level_test(q.da, q.wa);
   const bool hb = q.ob != kNoHit && first_level_test(q.db, q.wb);
   q.defer = false;
-  q.defer_u = 0u;
   q.ia = q.ib = 0u;
   const uint32_t c = (uint32_t)ha + (uint32_t)hb;
   const uint32_t incl = wave_inclusive_scan(c);
@@ -427,7 +421,6 @@ __device__ __forceinline__ void drain(const ScanParams& p, WaveQueue& q, uint32_
         q.ib = (kExactFl + fl_word(q.wb)) * 4u;
       }
       q.defer = true;
-      q.defer_u = 1u;
       return;
     }
   }
@@ -694,54 +687,6 @@ __device__ __forceinline__ void ring_append(const ScanParams& p, WaveQueue& q, S
   }
 }
 
-#if YAMD_APPEND_ASM
-// The tile step's stage 2 with one wave-uniform branch: the deferred
-// first-level completion (after a drain) and the drain of a full ring both sit
-// behind a single rare test, and the append itself is branch-free -- the
-// entry's stores run under exec = the ballot, set and restored around them
-// (no saveexec / execz branch, no lane-mask bookkeeping).  LDS operations
-// complete in order, so the compiler's lgkmcnt waits stay correct: the two
-// stores only make later waits wait for them too.
-template <int MODE, bool TAIL>
-__device__ __forceinline__ void stage2_fast(const ScanParams& p, WaveQueue& q, SegState& st,
-                                            const uint32_t (&S)[6], uint32_t any,
-                                            uint32_t tile_off, uint32_t lane) {
-  if constexpr (TAIL) {
-    if (tile_off + lane * kBytesPerLane >= st.seg_len) any = 0u;   // lanes past the end
-  }
-  const uint64_t lanes = __ballot(any != 0);
-  const uint32_t n = (uint32_t)__popcll(lanes);
-  // (integer arithmetic, so the test stays in SGPRs: count + n > kQueueCap
-  // <=> (count + n + 63) >> 7 != 0 for count + n <= 2 * kQueueCap)
-  static_assert(kQueueCap == 64, "the slow-path test below assumes a 64-entry ring");
-  if (__builtin_expect((q.defer_u | ((q.count + n + 63u) >> 7)) != 0u, 0)) {
-    if constexpr (kDeferFl<MODE>)
-      if (q.defer) drain_complete<MODE>(p, q, lane, st.seg_start, st.out, st.found);
-    if (q.count + n > kQueueCap)
-      drain<MODE, true>(p, q, lane, st.seg_start, st.seg_len, st.out, st.found);
-  }
-  const uint32_t below = __builtin_amdgcn_mbcnt_hi(
-      (uint32_t)(lanes >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)lanes, 0u));
-  const uint32_t base = q.ring + q.count * (kQueueEntryWords * 4);   // scalar
-  uint32_t ent;
-  asm("v_mad_u32_u24 %0, %1, 24, %2" : "=v"(ent) : "v"(below), "s"(base));
-  u32x2 s12, s34, s0i;
-  s12.x = S[1]; s12.y = S[2];
-  s34.x = S[3]; s34.y = S[4];
-  s0i.x = S[0]; s0i.y = (tile_off >> 4) + lane;
-  uint64_t saved;
-  asm volatile(
-      "s_and_saveexec_b64 %0, %1\n\t"
-      "ds_write2_b64 %2, %3, %4 offset1:1\n\t"
-      "ds_write_b64 %2, %5 offset:16\n\t"
-      "s_mov_b64 exec, %0"
-      : "=&s"(saved)
-      : "s"(lanes), "v"(ent), "v"(s12), "v"(s34), "v"(s0i)
-      : "memory");
-  q.count += n;
-}
-#endif
-
 // The lane's window context: the previous lane's last dword (lane 0: the
 // previous tile's, or the halo), then its own 16 bytes.
 __device__ __forceinline__ void tile_context(SegState& st, const uint4& cur, uint32_t (&S)[6]) {
@@ -797,13 +742,6 @@ __device__ __forceinline__ void tile_step(const ScanParams& p, WaveQueue& q, Seg
   tile_context(st, cur, S);
   uint32_t any = stage1<MODE == kModeByteKeys ? 0 : MODE, true>(S, lane);
   if constexpr (MODE == kModeByteKeys) any |= byte_keys_any(S, p);
-#if YAMD_APPEND_ASM
-  if constexpr (MODE == 0 || MODE == kModeByteKeys || kEven<MODE>) {
-    stage2_fast<MODE, TAIL>(p, q, st, S, any, tile_off, lane);
-    issue_first_level<MODE>(p, q);
-    return;
-  }
-#endif
   if constexpr (kDeferFl<MODE>)
     if (q.defer) drain_complete<MODE>(p, q, lane, st.seg_start, st.out, st.found);
   ring_append<MODE, TAIL>(p, q, st, S, any, tile_off, lane);
@@ -850,7 +788,6 @@ __device__ __forceinline__ void scan_segment(const ScanParams& p, WaveQueue& q, 
   q.count = 0;
   q.pend_n = 0;
   q.defer = false;
-  q.defer_u = 0u;
   q.ia = q.ib = 0u;
   q.da = q.db = 0u;
   q.wa = q.wb = 0u;

@@ -37,6 +37,7 @@ struct Lane {
   std::vector<yr_amd_verify_rec> recs;
   uint64_t candidates = 0;
   int status = YR_AMD_SUCCESS;
+  bool last = false;   // the last device (takes the rest of the block)
 };
 
 }  // namespace
@@ -71,6 +72,10 @@ void run_lane(Lane& L, const uint8_t* data, uint64_t size, uint64_t data_base, u
   L.recs.clear();
   L.candidates = 0;
   L.status = YR_AMD_SUCCESS;
+  // an empty range owns no position (a block smaller than one slice per
+  // device: the last device takes all of it, position 0 included); only an
+  // empty block is scanned, by the last device, for its position 0
+  if (begin == end && !(size == 0 && L.last)) return;
   if (hipSetDevice(L.device) != hipSuccess) {
     L.status = YR_AMD_INTERNAL_FATAL_ERROR;
     return;
@@ -143,6 +148,7 @@ int yr_amd_multi_create(yr_amd_tables* const* tables, uint32_t n, yr_amd_multi**
     Lane& L = m->lanes[k];
     L.tables = tables[k];
     L.device = yr_amd_tables_device(tables[k]);
+    L.last = k == n - 1;
     if (L.device < 0 || hipSetDevice(L.device) != hipSuccess ||
         hipStreamCreateWithFlags(&L.stream, hipStreamNonBlocking) != hipSuccess) {
       L.stream = nullptr;

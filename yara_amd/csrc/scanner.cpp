@@ -85,6 +85,7 @@ struct yr_amd_tables {
 
   // on-device literal pre-verification (yr_amd_tables_set_strings)
   bool has_strings = false;
+  bool profile = false;               // yr_amd_tables_set_profiling
   uint32_t* d_nodes = nullptr;        // accepting nodes by string (FlatTables::nodes)
   DevPoolRec* d_pool = nullptr;       // per pool entry: link, backtrack, string, programs
   uint8_t* d_str_bytes = nullptr;
@@ -294,6 +295,12 @@ int yr_amd_tables_destroy(yr_amd_tables* t) {
 }
 
 int yr_amd_tables_device(const yr_amd_tables* t) { return t == nullptr ? -1 : t->device; }
+
+int yr_amd_tables_set_profiling(yr_amd_tables* t, int enable) {
+  if (t == nullptr) return YR_AMD_INVALID_ARGUMENT;
+  t->profile = enable != 0;
+  return YR_AMD_SUCCESS;
+}
 
 int yr_amd_tables_get_info(const yr_amd_tables* t, yr_amd_tables_info* info) {
   if (t == nullptr || info == nullptr) return YR_AMD_INVALID_ARGUMENT;
@@ -894,6 +901,7 @@ int yr_amd_verify_device(yr_amd_scanner* s, uint64_t data_base, const yr_amd_ver
   v.str_bytes = t->d_str_bytes;
   v.lowercase = t->d_lowercase;
   v.re_on = t->d_re_code != nullptr ? 1 : 0;
+  v.profile = t->profile ? 1 : 0;
   v.re_code = t->d_re_code;
   uint64_t total = 0;
   // records carry a 32-bit candidate index: a candidate stream longer than

@@ -88,6 +88,8 @@ struct VerifyParams {
   const uint8_t* str_bytes;
   const uint8_t* lowercase;   // the host's yr_lowercase[256]
   int re_on;                  // regexp programs attached (else every regexp call is kept)
+  int profile;                // yr_amd_tables_set_profiling: dropped calls that stock
+                              // libyara's profiling counts come out as count-only records
   const uint8_t* re_code;
   uint32_t* counts;           // [count] records per candidate (pass 0)
   uint32_t* keep;             // [count] pass 0's decisions for pass 1: bit t = the t-th

@@ -793,6 +793,7 @@ __device__ bool call_matters(const VerifyParams& p, const DevPoolRec& st, uint64
 // on -- from the keep mask, without deciding again, except for lists longer
 // than 31 entries.
 constexpr uint32_t kKeepOverflow = 1u << 31;
+constexpr uint32_t kRecCountOnly = 0x80000000u;   // include/yara_amd.h YR_AMD_REC_COUNT_ONLY
 template <int PASS>
 __device__ __forceinline__ void verify_one(const VerifyParams& p, uint64_t c, uint32_t lds,
                                            uint32_t codebuf, uint32_t keep, uint32_t head,
@@ -805,24 +806,36 @@ __device__ __forceinline__ void verify_one(const VerifyParams& p, uint64_t c, ui
   if (!PASS && YAMD_VERIFY_DIAG >= 4) {   // profiling: + the state's list head
     p.counts[c] = 0; p.keep[c] = 0; p.heads[c] = head; count = 0; return;
   }
-  const bool decide = !PASS || (keep & kKeepOverflow);
+  // profiling: pass 1 decides again (the keep mask does not tell count-only
+  // records from kept ones)
+  const bool decide = !PASS || (keep & kKeepOverflow) || p.profile;
   uint32_t n = 0, t = 0, mask = 0;
   // scanner.c:105-121: the list of state_i in pool order
   for (uint32_t k = head; k != 0; ++t) {
     const DevPoolRec e = p.pool[k - 1];
     const uint32_t bt = e.backtrack;
-    bool kept;
-    if (decide)
+    bool kept, count_only = false;
+    if (decide) {
       kept = bt <= i && call_matters(p, e, i - bt, lds, codebuf);
-    else
+      // YR_PROFILING_ENABLED: yr_scan_verify_match counts atom_matches for
+      // every call past its early returns (scan.c:1013-1027, :1083), effect or
+      // not -- a dropped call past them becomes a count-only record, which the
+      // host counts without verifying (its temp-disabled / fast-mode tests
+      // are host state, applied at replay time, in the call order)
+      if (p.profile && !kept && bt <= i)
+        count_only = i - bt < p.size &&
+                     (!(e.flags & kStrFixedOffset) ||
+                      e.fixed_offset == (int64_t)(p.data_base + (i - bt)));
+    } else {
       kept = t < 31 && ((keep >> t) & 1u);
+    }
     const uint32_t kk = k;
     k = e.next;
-    if (!kept) continue;
+    if (!kept && !count_only) continue;
     if (PASS) {
       VerifyRec r;
       r.offset = i - bt;
-      r.pool_index = kk - 1;
+      r.pool_index = (kk - 1) | (count_only ? kRecCountOnly : 0u);
       r.candidate = (uint32_t)c;
       if (o < p.out_cap) p.out[o] = r;
       ++o;
@@ -833,7 +846,7 @@ __device__ __forceinline__ void verify_one(const VerifyParams& p, uint64_t c, ui
   }
   if (!PASS) {
     p.counts[c] = n;
-    p.keep[c] = n == 0 ? 0u : (t > 31 ? kKeepOverflow : mask);
+    p.keep[c] = n == 0 ? 0u : (t > 31 || p.profile ? kKeepOverflow : mask);
     p.heads[c] = head;
   }
   count = n;
