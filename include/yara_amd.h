@@ -408,6 +408,21 @@ int yr_amd_pipeline_submit(
     uint64_t base);
 
 /*
+ * The same without a host copy by the CPU: the block goes from the caller's
+ * buffer straight to the device (synchronous H2D in the calling thread; the
+ * buffer may be reused on return) and the host copy that yr_amd_pipeline_next
+ * hands back for the replay is made by a device-to-host DMA into pinned memory
+ * while the block is scanned.  Every page of the block must be readable: a
+ * fault inside the runtime's copy cannot be caught, so a libyara caller first
+ * touches each page inside its YR_TRYCATCH (integration/yr_gpu_scanner.c).
+ */
+int yr_amd_pipeline_submit_dma(
+    yr_amd_pipeline* pipeline,
+    const uint8_t* data,
+    size_t size,
+    uint64_t base);
+
+/*
  * Wait for the oldest submitted block.  Returns its scan status; on success
  * *records / *count are its effective verify calls (yr_amd_scan_block_verified
  * semantics) and *data / *size / *base its pipeline-owned bytes, all valid

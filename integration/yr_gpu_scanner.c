@@ -517,12 +517,23 @@ static int _pipeline_block(
     YR_MEMORY_BLOCK* block)
 {
   int result = ERROR_SUCCESS;
-  /* the block copy may fault on an mmap: same mapping to
-   * ERROR_COULD_NOT_MAP_FILE as scanner.c:493-496 */
+  /* The block goes to the GPU straight from the caller's buffer
+   * (yr_amd_pipeline_submit_dma: no host copy by the CPU; the copy the replay
+   * reads comes back by DMA), and that H2D reads the buffer inside the HIP
+   * runtime, where a fault cannot be unwound.  So every page is touched
+   * first, inside the trycatch: a block that faults (a truncated mapping)
+   * yields ERROR_COULD_NOT_MAP_FILE as scanner.c:493-496 does. */
   YR_TRYCATCH(
       !(scanner->flags & SCAN_FLAGS_NO_TRYCATCH),
-      { result = yr_amd_pipeline_submit(gs->pipe, data, block->size, block->base); },
+      {
+        volatile uint8_t sink = 0;
+        for (size_t o = 0; o < block->size; o += 4096) sink ^= data[o];
+        if (block->size > 0) sink ^= data[block->size - 1];
+        (void) sink;
+      },
       { result = ERROR_COULD_NOT_MAP_FILE; });
+  if (result != ERROR_SUCCESS) return result;
+  result = yr_amd_pipeline_submit_dma(gs->pipe, data, block->size, block->base);
   if (result != ERROR_SUCCESS) return result;
   gs->inflight++;
   if (gs->inflight == gs->depth) return _replay_next(scanner, gs);

@@ -20,8 +20,13 @@ def _blocks(data, sizes):
     return out
 
 
+@pytest.mark.parametrize("dma", [False, True], ids=["memcpy", "dma"])
 @pytest.mark.parametrize("depth", [1, 2, 4])
-def test_pipeline_equals_single_block_path(depth):
+def test_pipeline_equals_single_block_path(depth, dma):
+    """Either submit form (host memcpy, or H2D from the caller's buffer with
+    the host copy made by D2H into pinned memory): the same records and block
+    copies; the caller's buffer is overwritten right after each submit (it
+    may be reused on return)."""
     import yara_amd
     data = planted.lit_buffer(oracle.xorshift, 3 << 20, 13)
     tab = yara_amd.Tables.from_npz(tables_npz("lit"), device=0, strings=True)
@@ -32,11 +37,14 @@ def test_pipeline_equals_single_block_path(depth):
     want = [sc.verify_calls(blk, data_base=b) for b, blk in blocks]
     pipe = yara_amd.Pipeline(tab, depth=depth)
     got, inflight = [], 0
+    scratch = np.empty(max(sizes), np.uint8)
     for b, blk in blocks:
         if inflight == depth:
             got.append(pipe.next())
             inflight -= 1
-        pipe.submit(blk, base=b)
+        scratch[:len(blk)] = blk                    # the caller's reusable buffer
+        pipe.submit(scratch[:len(blk)], base=b, dma=dma)
+        scratch[:len(blk)] = 0x5A
         inflight += 1
     while inflight:
         got.append(pipe.next())

@@ -1,7 +1,8 @@
 """End-to-end rate of host-resident blocks (PCIe-inclusive; not the bench
 metric, which times HBM-resident data).  Blocks of a host buffer go through
   (a) yr_amd_scan_block_verified, one block at a time, and
-  (b) the block pipeline (yr_amd_pipeline_*) at several depths,
+  (b) the block pipeline (yr_amd_pipeline_*) at several depths, with the
+      host-memcpy submit and with the DMA submit (yr_amd_pipeline_submit_dma),
 and the records are fetched to the host (the replay into yr_scan_verify_match
 is the caller's and is not timed here).
 
@@ -50,27 +51,29 @@ def main():
         tot += len(sc.verify_calls(blk, data_base=b))
     res["single_block_GBps"] = round(n / (time.perf_counter() - t0) / 1e9, 2)
     res["records"] = tot
-    for depth in [int(x) for x in a.depths.split(",")]:
-        pipe = yara_amd.Pipeline(tab, depth=depth)
+    for dma in (False, True):
+        for depth in [int(x) for x in a.depths.split(",")]:
+            pipe = yara_amd.Pipeline(tab, depth=depth)
 
-        def run():
-            inflight, tot2 = 0, 0
-            for b, blk in blocks:
-                if inflight == depth:
+            def run():
+                inflight, tot2 = 0, 0
+                for b, blk in blocks:
+                    if inflight == depth:
+                        tot2 += len(pipe.next(copy_data=False)[0])
+                        inflight -= 1
+                    pipe.submit(blk, base=b, dma=dma)
+                    inflight += 1
+                while inflight:
                     tot2 += len(pipe.next(copy_data=False)[0])
                     inflight -= 1
-                pipe.submit(blk, base=b)
-                inflight += 1
-            while inflight:
-                tot2 += len(pipe.next(copy_data=False)[0])
-                inflight -= 1
-            return tot2
-        run()   # steady state: slot buffers and device workspaces allocated
-        t0 = time.perf_counter()
-        tot2 = run()
-        res["pipeline_depth%d_GBps" % depth] = round(n / (time.perf_counter() - t0) / 1e9, 2)
-        assert tot2 == tot
-        pipe.close()
+                return tot2
+            run()   # steady state: slot buffers and device workspaces allocated
+            t0 = time.perf_counter()
+            tot2 = run()
+            key = "pipeline%s_depth%d_GBps" % ("_dma" if dma else "", depth)
+            res[key] = round(n / (time.perf_counter() - t0) / 1e9, 2)
+            assert tot2 == tot
+            pipe.close()
     print(json.dumps(res), flush=True)
 
 

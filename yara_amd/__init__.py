@@ -329,11 +329,13 @@ class Pipeline:
         self.depth = depth
         self.tables = tables
 
-    def submit(self, data: np.ndarray, base: int = 0):
+    def submit(self, data: np.ndarray, base: int = 0, dma: bool = False):
+        """Submit a block: host memcpy in this thread (yr_amd_pipeline_submit),
+        or with ``dma`` straight to the device (yr_amd_pipeline_submit_dma)."""
         d = _arr(data, np.uint8)
         dp = d.ctypes.data_as(_lib._u8p) if d.size else None
-        _lib.check("yr_amd_pipeline_submit",
-                   _lib.lib().yr_amd_pipeline_submit(self._h, dp, d.size, base))
+        fn = "yr_amd_pipeline_submit_dma" if dma else "yr_amd_pipeline_submit"
+        _lib.check(fn, getattr(_lib.lib(), fn)(self._h, dp, d.size, base))
 
     def next(self, copy_data: bool = True):
         """(records {offset, pool_index, candidate}, block bytes copy or None,

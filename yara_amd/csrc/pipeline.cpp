@@ -10,6 +10,19 @@
 // copy of its block and a worker thread that runs
 // yr_amd_scan_block_verified for it.  Results are handed back strictly in
 // submission order, so the replay order is the reference's block order.
+//
+// Two ways in.  yr_amd_pipeline_submit copies the block with memcpy in the
+// caller's thread (a fault on an mmap'ed block unwinds through the caller's
+// YR_TRYCATCH), then the worker's H2D reads that copy: two host passes over
+// every byte (the memcpy and the runtime's pageable staging), ~23 GB/s.
+// yr_amd_pipeline_submit_dma instead copies the caller's bytes to the slot's
+// device buffer directly (hipMemcpy from pageable memory in the caller's
+// thread, returning once the bytes are on the device -- the caller's buffer is
+// free again), and the worker makes the host copy the replay reads with a
+// device-to-host DMA into pinned memory, concurrent with the scan: no CPU
+// copy at all, H2D and D2H on the two directions of the link.  The caller
+// must have made every page of the block readable (the shim touches each
+// page inside its YR_TRYCATCH first, as for its direct blocks).
 #include <hip/hip_runtime.h>
 #include <stdlib.h>
 #include <string.h>
@@ -39,6 +52,16 @@ struct Slot {
   const yr_amd_verify_rec* recs = nullptr;
   uint64_t count = 0;
   std::thread worker;
+  // submit_dma: the block on the device, its host copy in pinned memory, the
+  // records fetched by the worker
+  bool dma = false;
+  int device = 0;
+  hipStream_t copy_stream = nullptr;
+  uint8_t* d_buf = nullptr;
+  size_t d_cap = 0;
+  uint8_t* h_pinned = nullptr;
+  size_t h_cap = 0;
+  std::vector<yr_amd_verify_rec> h_recs;
 };
 
 }  // namespace
@@ -56,6 +79,33 @@ struct yr_amd_pipeline {
 
 namespace {
 
+// A submit_dma block on the worker: the host copy streams back (D2H into the
+// pinned buffer) while the block is scanned and pre-verified on the device.
+int run_dma(Slot& s, const yr_amd_verify_rec** recs, uint64_t* n) {
+  *recs = nullptr;
+  *n = 0;
+  if (hipSetDevice(s.device) != hipSuccess) return YR_AMD_INTERNAL_FATAL_ERROR;
+  if (s.size > 0 && hipMemcpyAsync(s.h_pinned, s.d_buf, s.size, hipMemcpyDeviceToHost,
+                                   s.copy_stream) != hipSuccess)
+    return YR_AMD_INTERNAL_FATAL_ERROR;
+  int r = yr_amd_scan_device(s.scanner, s.d_buf, s.size, 0, s.size);
+  if (!r) r = yr_amd_scan_device_result(s.scanner, nullptr, nullptr, nullptr);
+  const yr_amd_verify_rec* d_rec = nullptr;
+  uint64_t cnt = 0;
+  if (!r) r = yr_amd_verify_device(s.scanner, s.base, &d_rec, &cnt);
+  if (!r) {
+    s.h_recs.resize(cnt);
+    if (cnt > 0 && hipMemcpy(s.h_recs.data(), d_rec, cnt * sizeof(yr_amd_verify_rec),
+                             hipMemcpyDeviceToHost) != hipSuccess)
+      r = YR_AMD_INTERNAL_FATAL_ERROR;
+  }
+  if (hipStreamSynchronize(s.copy_stream) != hipSuccess && !r) r = YR_AMD_INTERNAL_FATAL_ERROR;
+  if (r) return r;
+  *recs = s.h_recs.data();
+  *n = cnt;
+  return YR_AMD_SUCCESS;
+}
+
 void worker_main(yr_amd_pipeline* p, uint32_t idx) {
   Slot& s = p->slots[idx];
   std::unique_lock<std::mutex> lk(p->mu);
@@ -65,7 +115,8 @@ void worker_main(yr_amd_pipeline* p, uint32_t idx) {
     lk.unlock();
     const yr_amd_verify_rec* recs = nullptr;
     uint64_t n = 0;
-    const int rc = yr_amd_scan_block_verified(s.scanner, s.buf, s.size, s.base, &recs, &n);
+    const int rc = s.dma ? run_dma(s, &recs, &n)
+                         : yr_amd_scan_block_verified(s.scanner, s.buf, s.size, s.base, &recs, &n);
     lk.lock();
     s.rc = rc;
     s.recs = recs;
@@ -97,6 +148,13 @@ int yr_amd_pipeline_destroy(yr_amd_pipeline* p) {
     if (s.worker.joinable()) s.worker.join();
     if (s.scanner) yr_amd_scanner_destroy(s.scanner);
     free(s.buf);
+    if (s.copy_stream) {
+      (void)hipSetDevice(s.device);
+      (void)hipStreamSynchronize(s.copy_stream);
+      (void)hipStreamDestroy(s.copy_stream);
+    }
+    if (s.d_buf) (void)hipFree(s.d_buf);
+    if (s.h_pinned) (void)hipHostFree(s.h_pinned);
   }
   delete p;
   return YR_AMD_SUCCESS;
@@ -109,11 +167,19 @@ int yr_amd_pipeline_create(yr_amd_tables* tables, uint32_t depth, yr_amd_pipelin
   if (p == nullptr) return YR_AMD_INSUFFICIENT_MEMORY;
   p->depth = depth;
   p->slots = std::vector<Slot>(depth + 1);
+  const int device = yr_amd_tables_device(tables);
   for (Slot& s : p->slots) {
+    s.device = device;
     const int r = yr_amd_scanner_create(tables, nullptr, &s.scanner);
     if (r != YR_AMD_SUCCESS) {
       yr_amd_pipeline_destroy(p);
       return r;
+    }
+    if (hipSetDevice(device) != hipSuccess ||
+        hipStreamCreateWithFlags(&s.copy_stream, hipStreamNonBlocking) != hipSuccess) {
+      s.copy_stream = nullptr;
+      yr_amd_pipeline_destroy(p);
+      return YR_AMD_INTERNAL_FATAL_ERROR;
     }
   }
   for (uint32_t i = 0; i <= depth; ++i) p->slots[i].worker = std::thread(worker_main, p, i);
@@ -145,6 +211,57 @@ int yr_amd_pipeline_submit(yr_amd_pipeline* p, const uint8_t* data, size_t size,
   if (size > 0) memcpy(s.buf, data, size);
   {
     std::lock_guard<std::mutex> lk(p->mu);
+    s.dma = false;
+    s.size = size;
+    s.base = base;
+    s.state = kSubmitted;
+    ++p->in_flight;
+  }
+  p->cv.notify_all();
+  return YR_AMD_SUCCESS;
+}
+
+int yr_amd_pipeline_submit_dma(yr_amd_pipeline* p, const uint8_t* data, size_t size,
+                               uint64_t base) {
+  if (p == nullptr || (data == nullptr && size > 0)) return YR_AMD_INVALID_ARGUMENT;
+  uint32_t idx;
+  {
+    std::lock_guard<std::mutex> lk(p->mu);
+    if (p->in_flight >= p->depth) return YR_AMD_INVALID_ARGUMENT;   // call pipeline_next first
+    idx = (p->head + p->in_flight) % (p->depth + 1);
+    if ((int)idx == p->held) release_held(p);
+    if (p->slots[idx].state != kIdle) return YR_AMD_INTERNAL_FATAL_ERROR;
+  }
+  Slot& s = p->slots[idx];
+  if (hipSetDevice(s.device) != hipSuccess) return YR_AMD_INTERNAL_FATAL_ERROR;
+  const size_t need = size > 0 ? size : 16;
+  if (need > s.d_cap) {
+    if (s.d_buf) (void)hipFree(s.d_buf);
+    s.d_buf = nullptr;
+    s.d_cap = 0;
+    if (hipMalloc((void**)&s.d_buf, need) != hipSuccess) {
+      s.d_buf = nullptr;
+      return YR_AMD_INSUFFICIENT_MEMORY;
+    }
+    s.d_cap = need;
+  }
+  if (need > s.h_cap) {
+    if (s.h_pinned) (void)hipHostFree(s.h_pinned);
+    s.h_pinned = nullptr;
+    s.h_cap = 0;
+    if (hipHostMalloc((void**)&s.h_pinned, need, hipHostMallocDefault) != hipSuccess) {
+      s.h_pinned = nullptr;
+      return YR_AMD_INSUFFICIENT_MEMORY;
+    }
+    s.h_cap = need;
+  }
+  // H2D straight from the caller's (pageable) buffer; when it returns the
+  // bytes are on the device and the caller may reuse its buffer
+  if (size > 0 && hipMemcpy(s.d_buf, data, size, hipMemcpyHostToDevice) != hipSuccess)
+    return YR_AMD_COULD_NOT_MAP_FILE;
+  {
+    std::lock_guard<std::mutex> lk(p->mu);
+    s.dma = true;
     s.size = size;
     s.base = base;
     s.state = kSubmitted;
@@ -168,7 +285,7 @@ int yr_amd_pipeline_next(yr_amd_pipeline* p, const yr_amd_verify_rec** records, 
   --p->in_flight;
   if (records) *records = s.recs;
   if (count) *count = s.rc == YR_AMD_SUCCESS ? s.count : 0;
-  if (data) *data = s.buf;
+  if (data) *data = s.dma ? s.h_pinned : s.buf;
   if (size) *size = s.size;
   if (base) *base = s.base;
   return s.rc;

@@ -845,9 +845,13 @@ __device__ __forceinline__ void verify_one(const VerifyParams& p, uint64_t c, ui
     ++n;
   }
   if (!PASS) {
-    p.counts[c] = n;
+    // pass 1 reads counts and heads only where keep != 0: most candidates of
+    // a dense rule set keep nothing and write 4 bytes here instead of 12
     p.keep[c] = n == 0 ? 0u : (t > 31 || p.profile ? kKeepOverflow : mask);
-    p.heads[c] = head;
+    if (n != 0) {
+      p.counts[c] = n;
+      p.heads[c] = head;
+    }
   }
   count = n;
 }
