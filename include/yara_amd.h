@@ -408,13 +408,14 @@ int yr_amd_pipeline_submit(
     uint64_t base);
 
 /*
- * The same without a host copy by the CPU: the block goes from the caller's
- * buffer straight to the device (synchronous H2D in the calling thread; the
- * buffer may be reused on return) and the host copy that yr_amd_pipeline_next
- * hands back for the replay is made by a device-to-host DMA into pinned memory
- * while the block is scanned.  Every page of the block must be readable: a
- * fault inside the runtime's copy cannot be caught, so a libyara caller first
- * touches each page inside its YR_TRYCATCH (integration/yr_gpu_scanner.c).
+ * The same at link rate: the block is copied into the slot's pinned host
+ * buffer by several threads at once (the caller's and a small pool; the
+ * buffer may be reused on return) and moved to the device by plain DMA, with
+ * no second host pass in the runtime's pageable staging.  The pinned copy is
+ * what yr_amd_pipeline_next hands back for the replay.  Every page of the
+ * block must be readable: a fault in a helper thread cannot unwind through
+ * the caller's YR_TRYCATCH, so a libyara caller first touches each page
+ * inside it (integration/yr_gpu_scanner.c).
  */
 int yr_amd_pipeline_submit_dma(
     yr_amd_pipeline* pipeline,

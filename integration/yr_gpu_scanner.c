@@ -517,12 +517,11 @@ static int _pipeline_block(
     YR_MEMORY_BLOCK* block)
 {
   int result = ERROR_SUCCESS;
-  /* The block goes to the GPU straight from the caller's buffer
-   * (yr_amd_pipeline_submit_dma: no host copy by the CPU; the copy the replay
-   * reads comes back by DMA), and that H2D reads the buffer inside the HIP
-   * runtime, where a fault cannot be unwound.  So every page is touched
-   * first, inside the trycatch: a block that faults (a truncated mapping)
-   * yields ERROR_COULD_NOT_MAP_FILE as scanner.c:493-496 does. */
+  /* The block is copied into the pipeline's pinned buffer by several threads
+   * at once (yr_amd_pipeline_submit_dma), and a fault in a helper thread
+   * cannot be unwound through this thread's trycatch.  So every page is
+   * touched first, inside the trycatch: a block that faults (a truncated
+   * mapping) yields ERROR_COULD_NOT_MAP_FILE as scanner.c:493-496 does. */
   YR_TRYCATCH(
       !(scanner->flags & SCAN_FLAGS_NO_TRYCATCH),
       {

@@ -15,18 +15,21 @@
 // caller's thread (a fault on an mmap'ed block unwinds through the caller's
 // YR_TRYCATCH), then the worker's H2D reads that copy: two host passes over
 // every byte (the memcpy and the runtime's pageable staging), ~23 GB/s.
-// yr_amd_pipeline_submit_dma instead copies the caller's bytes to the slot's
-// device buffer directly (hipMemcpy from pageable memory in the caller's
-// thread, returning once the bytes are on the device -- the caller's buffer is
-// free again), and the worker makes the host copy the replay reads with a
-// device-to-host DMA into pinned memory, concurrent with the scan: no CPU
-// copy at all, H2D and D2H on the two directions of the link.  The caller
-// must have made every page of the block readable (the shim touches each
-// page inside its YR_TRYCATCH first, as for its direct blocks).
+// yr_amd_pipeline_submit_dma instead copies the caller's bytes into the slot's
+// PINNED host buffer with several threads at once (the caller's thread and a
+// small pool: one host pass at the machine's memory bandwidth, not one
+// core's), returns -- the caller's buffer is free again -- and the worker moves
+// the pinned copy to the device with a plain DMA (no runtime staging), then
+// scans it; the pinned copy is what the replay reads.  Helper threads cannot
+// unwind a fault through the caller's YR_TRYCATCH, so the caller must have
+// made every page of the block readable first (the shim touches each page
+// inside its YR_TRYCATCH, as for its direct blocks).
 #include <hip/hip_runtime.h>
 #include <stdlib.h>
 #include <string.h>
 
+#include <algorithm>
+#include <atomic>
 #include <condition_variable>
 #include <mutex>
 #include <new>
@@ -64,6 +67,77 @@ struct Slot {
   std::vector<yr_amd_verify_rec> h_recs;
 };
 
+// A parallel memcpy: persistent helper threads plus the calling thread take
+// 4 MiB chunks of one copy job from an atomic counter.
+class CopyPool {
+ public:
+  explicit CopyPool(unsigned n) {
+    for (unsigned i = 0; i < n; ++i) th_.emplace_back([this] { loop(); });
+  }
+  ~CopyPool() {
+    {
+      std::lock_guard<std::mutex> lk(mu_);
+      stop_ = true;
+    }
+    cv_.notify_all();
+    for (std::thread& t : th_) t.join();
+  }
+  void copy(uint8_t* dst, const uint8_t* src, size_t size) {
+    if (size < 2 * kChunk || th_.empty()) {
+      memcpy(dst, src, size);
+      return;
+    }
+    {
+      std::lock_guard<std::mutex> lk(mu_);
+      dst_ = dst;
+      src_ = src;
+      size_ = size;
+      next_.store(0);
+      done_ = 0;
+      ++gen_;
+    }
+    cv_.notify_all();
+    work();
+    std::unique_lock<std::mutex> lk(mu_);
+    done_cv_.wait(lk, [&] { return done_ == size_; });
+  }
+
+ private:
+  static constexpr size_t kChunk = 4u << 20;
+  void work() {   // take chunks until the job is exhausted
+    for (;;) {
+      const size_t off = next_.fetch_add(kChunk);
+      if (off >= size_) return;
+      const size_t n = std::min(kChunk, size_ - off);
+      memcpy(dst_ + off, src_ + off, n);
+      std::lock_guard<std::mutex> lk(mu_);
+      done_ += n;
+      if (done_ == size_) done_cv_.notify_all();
+    }
+  }
+  void loop() {
+    uint64_t seen = 0;
+    std::unique_lock<std::mutex> lk(mu_);
+    for (;;) {
+      cv_.wait(lk, [&] { return stop_ || gen_ != seen; });
+      if (stop_) return;
+      seen = gen_;
+      lk.unlock();
+      work();
+      lk.lock();
+    }
+  }
+  std::vector<std::thread> th_;
+  std::mutex mu_;
+  std::condition_variable cv_, done_cv_;
+  uint8_t* dst_ = nullptr;
+  const uint8_t* src_ = nullptr;
+  size_t size_ = 0, done_ = 0;
+  std::atomic<size_t> next_{0};
+  uint64_t gen_ = 0;
+  bool stop_ = false;
+};
+
 }  // namespace
 
 struct yr_amd_pipeline {
@@ -75,19 +149,21 @@ struct yr_amd_pipeline {
   bool stop = false;
   std::mutex mu;
   std::condition_variable cv;
+  CopyPool* copier = nullptr;   // submit_dma's parallel host copy (created on first use)
 };
 
 namespace {
 
-// A submit_dma block on the worker: the host copy streams back (D2H into the
-// pinned buffer) while the block is scanned and pre-verified on the device.
+// A submit_dma block on the worker: the pinned host copy goes to the device
+// by DMA, then the block is scanned and pre-verified there.
 int run_dma(Slot& s, const yr_amd_verify_rec** recs, uint64_t* n) {
   *recs = nullptr;
   *n = 0;
   if (hipSetDevice(s.device) != hipSuccess) return YR_AMD_INTERNAL_FATAL_ERROR;
-  if (s.size > 0 && hipMemcpyAsync(s.h_pinned, s.d_buf, s.size, hipMemcpyDeviceToHost,
-                                   s.copy_stream) != hipSuccess)
-    return YR_AMD_INTERNAL_FATAL_ERROR;
+  if (s.size > 0 && (hipMemcpyAsync(s.d_buf, s.h_pinned, s.size, hipMemcpyHostToDevice,
+                                    s.copy_stream) != hipSuccess ||
+                     hipStreamSynchronize(s.copy_stream) != hipSuccess))
+    return YR_AMD_COULD_NOT_MAP_FILE;
   int r = yr_amd_scan_device(s.scanner, s.d_buf, s.size, 0, s.size);
   if (!r) r = yr_amd_scan_device_result(s.scanner, nullptr, nullptr, nullptr);
   const yr_amd_verify_rec* d_rec = nullptr;
@@ -99,7 +175,6 @@ int run_dma(Slot& s, const yr_amd_verify_rec** recs, uint64_t* n) {
                              hipMemcpyDeviceToHost) != hipSuccess)
       r = YR_AMD_INTERNAL_FATAL_ERROR;
   }
-  if (hipStreamSynchronize(s.copy_stream) != hipSuccess && !r) r = YR_AMD_INTERNAL_FATAL_ERROR;
   if (r) return r;
   *recs = s.h_recs.data();
   *n = cnt;
@@ -156,6 +231,7 @@ int yr_amd_pipeline_destroy(yr_amd_pipeline* p) {
     if (s.d_buf) (void)hipFree(s.d_buf);
     if (s.h_pinned) (void)hipHostFree(s.h_pinned);
   }
+  delete p->copier;
   delete p;
   return YR_AMD_SUCCESS;
 }
@@ -255,10 +331,16 @@ int yr_amd_pipeline_submit_dma(yr_amd_pipeline* p, const uint8_t* data, size_t s
     }
     s.h_cap = need;
   }
-  // H2D straight from the caller's (pageable) buffer; when it returns the
-  // bytes are on the device and the caller may reuse its buffer
-  if (size > 0 && hipMemcpy(s.d_buf, data, size, hipMemcpyHostToDevice) != hipSuccess)
-    return YR_AMD_COULD_NOT_MAP_FILE;
+  // the caller's bytes into the pinned copy, several threads at once; when
+  // it returns the caller may reuse its buffer (the worker DMAs the copy)
+  if (size > 0) {
+    if (p->copier == nullptr) {
+      const unsigned hw = std::thread::hardware_concurrency();
+      p->copier = new (std::nothrow) CopyPool(std::min(7u, hw > 1 ? hw / 2 : 0u));
+      if (p->copier == nullptr) return YR_AMD_INSUFFICIENT_MEMORY;
+    }
+    p->copier->copy(s.h_pinned, data, size);
+  }
   {
     std::lock_guard<std::mutex> lk(p->mu);
     s.dma = true;

@@ -630,10 +630,43 @@ __device__ int general_re_reachable(const uint8_t* __restrict__ code, uint32_t l
 // in the block or the staged window: true (the interpreter decides).  The
 // guard's 4 + span bytes come from four LDS dwords of the staged window and
 // byte shifts; every j is one AND and one compare.
+#ifndef YAMD_GUARD_DIRECT
+#define YAMD_GUARD_DIRECT 0
+#endif
 __device__ bool guard_ok(const VerifyParams& p, const uint8_t* d, uint64_t offset, bool backwards,
                          uint32_t bs, DevGuard g, uint32_t lds) {
   const uint32_t base = bs & 15u, span = bs >> 4, L = base + span + 4;
   if (backwards ? offset < L : p.size - offset < L) return true;
+#if YAMD_GUARD_DIRECT
+  {
+    // The guard's span + 4 <= 12 bytes straight into registers: three aligned
+    // 8-byte loads from the 8-byte boundary below the region (24 bytes, at
+    // most 7 of them before it) -- no 48-byte window staged through LDS.  Dense
+    // candidate streams (1-byte atoms: a call every ~128 bytes) read about
+    // half the bytes this way.
+    const uint64_t r0 = backwards ? offset - L : offset + base;
+    const uint64_t a8 = r0 & ~7ull;
+    if (a8 >= p.win_lo && a8 + 24 <= p.win_hi) {   // region: span + 4 <= 12 bytes from r0
+      const uint2* q = reinterpret_cast<const uint2*>(p.data + a8);
+      const uint2 q0 = q[0], q1 = q[1], q2 = q[2];
+      const uint32_t sh = (uint32_t)(r0 - a8), k = sh >> 2, bsh = sh & 3u;
+      // region dwords from dword k of (q0.x, q0.y, q1.x, q1.y, q2.x, q2.y)
+      const uint32_t B0 = k ? q0.y : q0.x, B1 = k ? q1.x : q0.y, B2 = k ? q1.y : q1.x;
+      const uint32_t B3 = k ? q2.x : q1.y;
+      const uint32_t W[3] = {__builtin_amdgcn_alignbyte(B1, B0, bsh),
+                             __builtin_amdgcn_alignbyte(B2, B1, bsh),
+                             __builtin_amdgcn_alignbyte(B3, B2, bsh)};
+      bool hit = false;
+#pragma unroll
+      for (uint32_t t = 0; t <= 8; ++t) {
+        const uint32_t r = (t & 3) == 0 ? W[t >> 2]
+                                        : __builtin_amdgcn_alignbyte(W[(t >> 2) + 1], W[t >> 2], t & 3);
+        hit |= t <= span && (r & g.m) == g.v;
+      }
+      return hit;
+    }
+  }
+#endif
   const ByteWindow w = stage_window(p, d, backwards, lds);
   if (w.lo == nullptr) return true;
   const int32_t rel0 = (int32_t)(d - w.lo);
