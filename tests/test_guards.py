@@ -18,7 +18,7 @@ import pytest
 from yara_amd import _lib
 
 ANY, LIT, MASKED, CLASS, MATCH, NOTLIT, MASKEDNOT = 0xA0, 0xA2, 0xA4, 0xA5, 0xAD, 0xAE, 0xAF
-WORDB, REPANY, SPLITA, JUMP = 0xB2, 0xB5, 0xC0, 0xC2
+WORDB, REPANYG, REPANY, SPLITA, JUMP = 0xB2, 0xB4, 0xB5, 0xC0, 0xC2
 
 
 def guard(code, skip=0, backwards=False, general=False, nocase=False):
@@ -114,15 +114,34 @@ def random_fast_program(r):
     return bytes(code), bytes(inp)
 
 
+def as_greedy(code):
+    """The program with its REPEAT_ANY_UNGREEDY opcodes made greedy."""
+    out, ip = bytearray(code), 0
+    size = {ANY: 1, LIT: 2, NOTLIT: 2, MASKED: 3, MASKEDNOT: 3, REPANY: 5, MATCH: 1}
+    while ip < len(code):
+        if code[ip] == REPANY:
+            out[ip] = REPANYG
+        ip += size[code[ip]]
+    return bytes(out)
+
+
+@pytest.mark.parametrize("general", [False, True], ids=["fast", "general"])
 @pytest.mark.parametrize("seed", range(8))
-def test_fast_guards_never_reject_a_match(seed):
+def test_fast_guards_never_reject_a_match(seed, general):
+    """Also as yr_re_exec programs (general): on a linear program they accept a
+    subset of what the fast model accepts (their ANY / REPEAT_ANY refuse 0x0A
+    without DOT_ALL), so a guard that passes every fast match is sound for
+    them; REPEAT_ANY_GREEDY enumerates the same counts."""
     r = random.Random(seed)
     guarded = rejected = 0
     for _ in range(400):
         code, inp = random_fast_program(r)
         backwards = r.random() < 0.5
         skip = r.randint(0, 4)
-        g = guard(code, skip=skip, backwards=backwards)
+        g = guard(code, skip=skip, backwards=backwards, general=general)
+        if general and r.random() < 0.5:
+            greedy = as_greedy(code)
+            assert guard(greedy, skip=skip, backwards=backwards, general=True) == g
         if g is None:
             continue
         guarded += 1
@@ -168,6 +187,15 @@ def test_general_guard_follows_jumps_and_stops_at_splits():
     cls = bytes([CLASS, 0] + [0xFF] * 32)
     prog = bytes([WORDB]) + cls + bytes([LIT, 0x41, LIT, 0x42, MATCH])
     assert guard(prog, general=True) == (0x00FFFF00, 0x00424100, 0)
+    # past the first REPEAT_ANY: { 5F ?? 62 61 ( 31 | ... ) [0-4] 3E }-like forward
+    # program from the atom 5F (JUMP over dead code): 3E at distance 1 + j, j <= 4
+    fwd = bytes([LIT, 0x5F, JUMP, 9, 0, LIT, 0x61, LIT, 0x62, LIT, 0x31,
+                 REPANY, 0, 0, 4, 0, LIT, 0x3E, MATCH])
+    assert guard(fwd, skip=1, general=True) == (0x000000FF, 0x0000003E, 1 | 4 << 4)
+    assert guard(bytes([REPANYG]) + fwd[12:], general=True) == (0xFF, 0x3E, 0 | 4 << 4)
+    # a second repeat ends the tail
+    two = bytes([LIT, 1, REPANY, 0, 0, 2, 0, REPANY, 1, 0, 3, 0, LIT, 2, MATCH])
+    assert guard(two, skip=1, general=True) is None
     # a SPLIT first: more than one fiber, no guard
     assert guard(bytes([SPLITA, 0, 6, 0, LIT, 0x41, LIT, 0x42, MATCH]), general=True) is None
     # nocase literals compare through the host's case folding: untested

@@ -748,9 +748,17 @@ bool fast_guard(const uint8_t* c, uint32_t len, uint32_t skip, bool backwards, D
 // through the host's case folding: their literals are left untested.
 bool general_guard(const uint8_t* c, uint32_t len, uint32_t skip, bool backwards, bool nocase,
                    DevGuard& g, uint8_t& bs) {
-  std::vector<GuardPos> head;
+  // head: the single fiber's consumed positions from the start; tail: those
+  // right after its first REPEAT_ANY {mn, mx} (re.c:1810-1821: the fiber
+  // forks over every repetition count, each fork consuming mn..mx bytes
+  // and then the same opcodes -- the tail lies at distance head + mn + j,
+  // j <= mx - mn, as for a fast program's REPEAT_ANY_UNGREEDY)
+  std::vector<GuardPos> head, tail;
+  uint32_t mn = 0, mx = 0;
+  bool repeat = false;
   uint32_t n = 0;
   for (int steps = 0; steps < 256 && n < len && head.size() < 20; ++steps) {
+    std::vector<GuardPos>& run = repeat ? tail : head;
     const uint8_t op = c[n];
     const uint32_t sz = re_op_size(op);
     if (sz == 0 || n + sz > len) break;
@@ -765,20 +773,30 @@ bool general_guard(const uint8_t* c, uint32_t len, uint32_t skip, bool backwards
       n += sz;   // zero width
       continue;
     }
+    if (op == kOpRepeatAnyGreedy || op == kOpRepeatAnyUngreedy) {
+      if (repeat) break;        // a second repeat: the tail's distance is no longer fixed
+      mn = re_u16(c + n + 1);
+      mx = re_u16(c + n + 3);
+      if (mn > mx) break;
+      repeat = true;
+      n += sz;
+      continue;
+    }
     if (op == kOpLiteral) {
-      head.push_back(nocase ? GuardPos{0, 0} : GuardPos{0xFF, c[n + 1]});
+      run.push_back(nocase ? GuardPos{0, 0} : GuardPos{0xFF, c[n + 1]});
     } else if (op == kOpMaskedLiteral) {
-      head.push_back(nocase ? GuardPos{0, 0} : GuardPos{c[n + 2], c[n + 1]});
+      run.push_back(nocase ? GuardPos{0, 0} : GuardPos{c[n + 2], c[n + 1]});
     } else if (op == kOpAny || op == kOpClass || op == kOpNotLiteral || op == kOpMaskedNotLiteral ||
                op == kOpWordChar || op == kOpNonWordChar || op == kOpSpace || op == kOpNonSpace ||
                op == kOpDigit || op == kOpNonDigit) {
-      head.push_back({0, 0});   // consumes one byte, not tested here
+      run.push_back({0, 0});    // consumes one byte, not tested here
     } else {
-      break;                    // MATCH, SPLIT, REPEAT*: the single fiber ends
+      break;                    // MATCH, SPLIT, REPEAT_START/END: the single fiber ends
     }
     n += sz;
+    if (repeat && tail.size() >= 4) break;
   }
-  return pick_guard(head, {}, false, 0, 0, skip, backwards, g, bs);
+  return pick_guard(head, tail, repeat, mn, mx, skip, backwards, g, bs);
 }
 }  // namespace
 

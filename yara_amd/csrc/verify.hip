@@ -49,14 +49,30 @@ __device__ __forceinline__ bool node_bucket_get(const uint4& b, uint32_t key, ui
                              // read only, 6 = 4 without the data read
 #endif
 
-__device__ __forceinline__ uint32_t node_head(const VerifyParams& p, uint64_t i) {
+// The 8 block bytes [a, a + 8) around a candidate that node_head loads anyway
+// (a = (i - 4) & ~3: at least the 4 bytes before i and byte i itself), kept
+// for the guards (guard_ok): most calls of a dense rule set are decided by a
+// guard whose tested bytes lie there, with no further memory access.
+struct Near {
+  uint64_t a;   // block position of byte 0; kNoNear: not loaded
+  uint64_t v;   // the 8 bytes, little endian
+};
+constexpr uint64_t kNoNear = ~0ull;
+#ifndef YAMD_GUARD_REG
+#define YAMD_GUARD_REG 0
+#endif
+
+__device__ __forceinline__ uint32_t node_head(const VerifyParams& p, uint64_t i, Near& near) {
   const uint32_t n = i < 4 ? (uint32_t)i : 4u;
   uint32_t w = 0;   // data[i-n .. i), oldest byte lowest, at the top (bytes i-4.. i-1)
   const uint64_t a = (i - 4) & ~3ull;   // p.data is 16-byte aligned
+  near.a = kNoNear;
   if (i >= 4 && a >= p.win_lo && a + 8 <= p.win_hi) {
     // one 8-byte load (4 byte loads per lane cost 2-3x the time: the random
     // reads of the candidates' neighbourhoods are the count pass's largest item)
     const uint2 v = *reinterpret_cast<const uint2*>(p.data + a);
+    near.a = a;
+    near.v = (uint64_t)v.x | ((uint64_t)v.y << 32);
     w = __builtin_amdgcn_alignbyte(v.y, v.x, (uint32_t)(i - 4 - a));
   } else {
 #pragma unroll
@@ -634,9 +650,26 @@ __device__ int general_re_reachable(const uint8_t* __restrict__ code, uint32_t l
 #define YAMD_GUARD_DIRECT 0
 #endif
 __device__ bool guard_ok(const VerifyParams& p, const uint8_t* d, uint64_t offset, bool backwards,
-                         uint32_t bs, DevGuard g, uint32_t lds) {
+                         uint32_t bs, DevGuard g, uint32_t lds, const Near& near) {
   const uint32_t base = bs & 15u, span = bs >> 4, L = base + span + 4;
   if (backwards ? offset < L : p.size - offset < L) return true;
+#if YAMD_GUARD_REG
+  if (near.a != kNoNear) {
+    // every tested byte (a nonzero mask byte, for every j <= span) inside the
+    // 8 bytes node_head loaded: decide from registers
+    const uint64_t r0 = backwards ? offset - L : offset + base;
+    const uint32_t bmin = (uint32_t)__builtin_ctz(g.m) >> 3, bmax = (31u - (uint32_t)__builtin_clz(g.m)) >> 3;
+    if (r0 + bmin >= near.a && r0 + span + bmax < near.a + 8) {
+      bool hit = false;
+      for (uint32_t q = 0; q <= span; ++q) {
+        const int64_t dq = (int64_t)(r0 + q) - (int64_t)near.a;   // in [-3, 7]
+        const uint32_t x = (uint32_t)(dq >= 0 ? near.v >> (8 * dq) : near.v << (-8 * dq));
+        hit |= (x & g.m) == g.v;
+      }
+      return hit;
+    }
+  }
+#endif
 #if YAMD_GUARD_DIRECT
   {
     // The guard's span + 4 <= 12 bytes straight into registers: three aligned
@@ -697,7 +730,7 @@ __device__ bool guard_ok(const VerifyParams& p, const uint8_t* d, uint64_t offse
 // return), a zero-length forward match needs a backward program, and with a
 // backward program its MATCHes are the only way to _yr_scan_match_callback.
 __device__ bool re_call_matters(const VerifyParams& p, const DevPoolRec& e, uint32_t flags,
-                                uint64_t offset, uint32_t lds, uint32_t codebuf) {
+                                uint64_t offset, uint32_t lds, uint32_t codebuf, const Near& near) {
   if (YAMD_VERIFY_DIAG == 2) return true;
   if (!p.re_on) return true;
   const DevRe r = e.re;
@@ -709,9 +742,9 @@ __device__ bool re_call_matters(const VerifyParams& p, const DevPoolRec& e, uint
     if (!(flags & kStrAscii) || (flags & (kStrWide | kStrBase64Any))) return true;
     // the guards first: most calls are atom hits whose next bytes already
     // rule the program out (no code staging, no interpretation)
-    if (e.fguard.m != 0 && !guard_ok(p, d, offset, false, e.fguard_bs, e.fguard, lds)) return false;
+    if (e.fguard.m != 0 && !guard_ok(p, d, offset, false, e.fguard_bs, e.fguard, lds, near)) return false;
     if (r.bwd_len > 0 && e.bguard.m != 0 &&
-        !guard_ok(p, d, offset, true, e.bguard_bs, e.bguard, lds))
+        !guard_ok(p, d, offset, true, e.bguard_bs, e.bguard, lds, near))
       return false;
     // forward and backward programs are contiguous in the blob (the shim and
     // yarc.cpp lay them out so): stage both at once when they fit
@@ -736,14 +769,14 @@ __device__ bool re_call_matters(const VerifyParams& p, const DevPoolRec& e, uint
   // running the search (and without any fiber to run out of).
   for (int w = 0; w < 2; ++w) {
     if (w == 0 ? !try_ascii : !try_wide) continue;
-    if (w == 0 && e.fguard.m != 0 && !guard_ok(p, d, offset, false, e.fguard_bs, e.fguard, lds))
+    if (w == 0 && e.fguard.m != 0 && !guard_ok(p, d, offset, false, e.fguard_bs, e.fguard, lds, near))
       continue;
     const int f = general_re_reachable(fwd, r.fwd_len, d, p.size - offset, offset, false, w == 1,
                                        nocase, dotall, p.lowercase);
     if (f == kPathUnknown) return true;
     if (f == kPathDead) continue;
     if (r.bwd_len == 0) return true;
-    if (w == 0 && e.bguard.m != 0 && !guard_ok(p, d, offset, true, e.bguard_bs, e.bguard, lds))
+    if (w == 0 && e.bguard.m != 0 && !guard_ok(p, d, offset, true, e.bguard_bs, e.bguard, lds, near))
       continue;
     const int b = general_re_reachable(bwd, r.bwd_len, d, p.size - offset, offset, true, w == 1,
                                        nocase, dotall, p.lowercase);
@@ -756,7 +789,7 @@ __device__ bool re_call_matters(const VerifyParams& p, const DevPoolRec& e, uint
 // have an effect?  false only where the reference provably returns without
 // touching the context.
 __device__ bool call_matters(const VerifyParams& p, const DevPoolRec& st, uint64_t offset,
-                             uint32_t lds, uint32_t codebuf) {
+                             uint32_t lds, uint32_t codebuf, const Near& near) {
   if (YAMD_VERIFY_DIAG == 1) return false;
   // scan.c:1013: data_size - offset <= 0 (size_t) <=> offset == size
   if (offset >= p.size) return false;
@@ -778,7 +811,7 @@ __device__ bool call_matters(const VerifyParams& p, const DevPoolRec& st, uint64
         min<uint64_t>(p.size, offset + max<uint64_t>((uint64_t)kReScanLimit, 2ull * st.length + 2));
     if (need_lo < p.win_lo || need_hi > p.win_hi) return true;
   }
-  if (!(st.flags & kStrLiteral)) return re_call_matters(p, st, st.flags, offset, lds, codebuf);
+  if (!(st.flags & kStrLiteral)) return re_call_matters(p, st, st.flags, offset, lds, codebuf, near);
   if (st.flags & kStrUnmodelled) return true;            // conservative
   // _yr_scan_verify_literal_match, scan.c:907-972
   const uint8_t* d = p.data + offset;
@@ -835,7 +868,9 @@ __device__ __forceinline__ void verify_one(const VerifyParams& p, uint64_t c, ui
   if (!PASS && YAMD_VERIFY_DIAG == 3) {   // profiling: candidate positions only
     p.counts[c] = 0; p.keep[c] = 0; p.heads[c] = (uint32_t)i; count = 0; return;
   }
-  if (!PASS) head = node_head(p, i);
+  Near near;
+  near.a = kNoNear;
+  if (!PASS) head = node_head(p, i, near);
   if (!PASS && YAMD_VERIFY_DIAG >= 4) {   // profiling: + the state's list head
     p.counts[c] = 0; p.keep[c] = 0; p.heads[c] = head; count = 0; return;
   }
@@ -849,7 +884,7 @@ __device__ __forceinline__ void verify_one(const VerifyParams& p, uint64_t c, ui
     const uint32_t bt = e.backtrack;
     bool kept, count_only = false;
     if (decide) {
-      kept = bt <= i && call_matters(p, e, i - bt, lds, codebuf);
+      kept = bt <= i && call_matters(p, e, i - bt, lds, codebuf, near);
       // YR_PROFILING_ENABLED: yr_scan_verify_match counts atom_matches for
       // every call past its early returns (scan.c:1013-1027, :1083), effect or
       // not -- a dropped call past them becomes a count-only record, which the
