@@ -183,6 +183,10 @@ constexpr uint32_t kNoHit = 0xFFFFFFFFu;
 // Kernel variant: the product kernel for rule sets whose 1-byte keys are tested
 // byte by byte in stage 1 (byte_keys_any below) instead of in the filter.
 constexpr int kModeByteKeys = 20;
+// Kernel variant: the product kernel for rule sets with 1-byte keys whose
+// other keys rarely pass the filter (FlatTables::byte_direct): no ring, every
+// tile's candidates go straight to the segment output (direct_step below).
+constexpr int kModeByteDirect = 23;
 // Kernel variant: the product kernel for the even-position filter
 // (internal.h kFilterEven: rule sets whose keys are all 4 bytes long).
 constexpr int kModeEven = 21;
@@ -311,6 +315,43 @@ __device__ __forceinline__ uint32_t byte_keys_mask(const uint32_t (&S)[6], const
     }
   }
   return m;
+}
+
+// The byte-key flags of the lane's 16 bytes for the direct kernel: bit
+// 8n + 7 - d set iff lane byte 4d + n equals a 1-byte key (key_flag_byte).
+// Per dword x and key v (replicated): y = ((x ^ v) & 0x7F7F7F7F) + 0x7F7F7F7F
+// has bit 7 of byte n clear iff the low 7 bits of that byte of x ^ v are zero,
+// so ~y & ~(x ^ v) has it set iff the byte equals the key (one v_bitop3 on y,
+// x and the scalar v).  Exact per byte (no carry between bytes); 3
+// instructions per dword for the first key, 4 for each further one; the
+// other bits are don't-care until the merge.
+__device__ __forceinline__ uint32_t byte_key_flags(const uint32_t (&S)[6], const ScanParams& p) {
+  uint32_t a[4];
+  {
+    const uint32_t v = (p.byte_keys & 0xFFu) * 0x01010101u;   // n_byte_keys >= 1
+#pragma unroll
+    for (int d = 0; d < 4; ++d) {
+      const uint32_t y = ((S[1 + d] ^ v) & 0x7F7F7F7Fu) + 0x7F7F7F7Fu;
+      a[d] = ~y & ~(S[1 + d] ^ v);
+    }
+  }
+  for (uint32_t k = 1; k < p.n_byte_keys; ++k) {   // wave-uniform
+    const uint32_t v = ((p.byte_keys >> (8 * k)) & 0xFFu) * 0x01010101u;
+#pragma unroll
+    for (int d = 0; d < 4; ++d) {
+      const uint32_t y = ((S[1 + d] ^ v) & 0x7F7F7F7Fu) + 0x7F7F7F7Fu;
+      a[d] |= ~y & ~(S[1 + d] ^ v);
+    }
+  }
+  // merge: bit 7 of each byte from a[0], bit 6 from a[1], 5 from a[2], 4 from a[3]
+  uint32_t u = (a[0] & 0x80808080u) | ((a[1] >> 1) & ~0x80808080u);
+  u = (u & 0xC0C0C0C0u) | ((a[2] >> 2) & ~0xC0C0C0C0u);
+  u = (u & 0xE0E0E0E0u) | ((a[3] >> 3) & ~0xE0E0E0E0u);
+  return u & 0xF0F0F0F0u;
+}
+// Lane byte of flag bit b of byte_key_flags: b = 8n + 7 - d <=> byte 4d + n.
+__device__ __forceinline__ uint32_t key_flag_byte(uint32_t b) {
+  return ((~b & 7u) << 2) | (b >> 3);
 }
 
 // Kernel variants whose drains defer their first-level loads (WaveQueue).
@@ -733,6 +774,84 @@ __device__ __forceinline__ void issue_first_level(const ScanParams& p, WaveQueue
   }
 }
 
+// A tile of the direct byte-key kernel (kModeByteDirect).  The positions whose
+// last byte is a 1-byte key are certain candidates (1/256 of random input per
+// key: tens of millions per 4 GiB); the filter covers the other keys and
+// passes in only a few per cent of tiles.  So a tile whose lanes pass no
+// filter test emits its key positions straight to the segment output, in
+// order, when no lane holds more than two (wave_inclusive_scan-free: lane L's
+// slot = found + #lanes below L with >= 1 + #lanes below L with 2); any other
+// tile (filter passes, three or more key bytes in a lane, the ragged tail, a
+// full output slot range) takes direct_tile_general.
+template <bool TAIL>
+__device__ __forceinline__ void direct_tile_general(const ScanParams& p, WaveQueue& q, SegState& st,
+                                                    const uint32_t (&S)[6], uint32_t f,
+                                                    uint32_t lane_off, uint32_t lane) {
+  uint32_t cand = byte_keys_mask(S, p);   // bit j <=> lane byte j is a 1-byte key
+  uint32_t lim_mask = 0xFFFFu;
+  if constexpr (TAIL) {
+    const uint32_t lim = lane_off >= st.seg_len ? 0u : st.seg_len - lane_off;
+    lim_mask = lim >= 16u ? 0xFFFFu : (1u << lim) - 1u;
+  }
+  if (__ballot(f != 0u) != 0) {
+    // the other filter hits: exact check in place (one round trip), through
+    // the lane's ring slot for the windows (window4)
+    uint32_t unc = 0;
+    if (f != 0u) unc = dense_mask(stage1<0, false>(S, lane)) & ~cand & lim_mask;
+    if (__ballot(unc != 0u) != 0) {
+      const uint32_t ent = q.ring + lane * (kQueueEntryWords * 4);
+      if (unc != 0u) {
+        lds_store2(ent, S[1], S[2]);
+        lds_store2(ent + 8, S[3], S[4]);
+        lds_store2(ent + 16, S[0], 0u);
+      }
+      __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+      while (unc != 0u) {
+        const uint32_t j = (uint32_t)__builtin_ctz(unc);
+        unc &= unc - 1u;
+        if (exact_check(window4(ent, j), st.seg_start + lane_off + j + 1, p)) cand |= 1u << j;
+      }
+    }
+  }
+  cand &= lim_mask;
+  const uint32_t c = __popc(cand);
+  append_hits(p, cand, c, wave_inclusive_scan(c), lane_off, st.out, st.found);
+}
+
+template <bool TAIL>
+__device__ __forceinline__ void direct_step(const ScanParams& p, WaveQueue& q, SegState& st,
+                                            const uint32_t (&S)[6], uint32_t tile_off,
+                                            uint32_t lane) {
+  const uint32_t f = stage1<0, true>(S, lane);   // bit 0: a position of the lane passes
+  const uint32_t mt = byte_key_flags(S, p);
+  const uint32_t lane_off = tile_off + lane * kBytesPerLane;
+  if (!TAIL && __ballot(f != 0u) == 0) {
+    const uint64_t one = __ballot(mt != 0u);
+    if (one == 0) return;
+    const uint32_t m2 = mt & (mt - 1u);   // the lane's flags past its first
+    const uint64_t two = __ballot(m2 != 0u);
+    const uint32_t total = (uint32_t)__popcll(one) + (uint32_t)__popcll(two);
+    if ((two == 0 || __ballot((m2 & (m2 - 1u)) != 0u) == 0) && st.found + total <= p.seg_cap) {
+      uint32_t idx = __builtin_amdgcn_mbcnt_hi((uint32_t)(one >> 32),
+                                               __builtin_amdgcn_mbcnt_lo((uint32_t)one, st.found));
+      const uint32_t j1 = key_flag_byte((uint32_t)__builtin_ctz(mt | 0x80000000u));
+      if (two == 0) {
+        if (mt != 0u) st.out[idx] = lane_off + j1;
+      } else {
+        idx = __builtin_amdgcn_mbcnt_hi((uint32_t)(two >> 32),
+                                        __builtin_amdgcn_mbcnt_lo((uint32_t)two, idx));
+        const uint32_t j2 = key_flag_byte((uint32_t)__builtin_ctz(m2 | 0x80000000u));
+        const bool has2 = m2 != 0u;
+        if (mt != 0u) st.out[idx] = lane_off + (has2 ? min(j1, j2) : j1);
+        if (has2) st.out[idx + 1] = lane_off + max(j1, j2);
+      }
+      st.found += total;
+      return;
+    }
+  }
+  direct_tile_general<TAIL>(p, q, st, S, f, lane_off, lane);
+}
+
 // One 1 KiB tile: stage-1 filter over its 1024 byte positions, then the ordered
 // append of the hits to the wave ring.
 template <int MODE, bool TAIL>
@@ -740,6 +859,10 @@ __device__ __forceinline__ void tile_step(const ScanParams& p, WaveQueue& q, Seg
                                           uint4 cur, uint32_t tile_off, uint32_t lane) {
   uint32_t S[6];
   tile_context(st, cur, S);
+  if constexpr (MODE == kModeByteDirect) {
+    direct_step<TAIL>(p, q, st, S, tile_off, lane);
+    return;
+  }
   uint32_t any = stage1<MODE == kModeByteKeys ? 0 : MODE, true>(S, lane);
   if constexpr (MODE == kModeByteKeys) any |= byte_keys_any(S, p);
   if constexpr (kDeferFl<MODE>)
@@ -991,7 +1114,10 @@ hipError_t launch_scan(const ScanParams& p, int grid, hipStream_t s, int mode) {
     case 12: hipLaunchKernelGGL(scan_segments_kernel<12>, dim3(grid), dim3(kWGThreads), lds, s, p); break;
 #endif
     default:
-      if (p.n_byte_keys != 0)
+      if (p.n_byte_keys != 0 && p.byte_direct != 0)
+        hipLaunchKernelGGL(scan_segments_kernel<kModeByteDirect>, dim3(grid), dim3(kWGThreads),
+                           lds, s, p);
+      else if (p.n_byte_keys != 0)
         hipLaunchKernelGGL(scan_segments_kernel<kModeByteKeys>, dim3(grid), dim3(kWGThreads), lds,
                            s, p);
       else if (p.filter_mode == kFilterEven)
@@ -1031,6 +1157,7 @@ hipError_t configure_scan_kernel() {
   hipError_t e = hipSuccess;
   for (const void* k : {(const void*)scan_segments_kernel<0>,
                         (const void*)scan_segments_kernel<kModeByteKeys>,
+                        (const void*)scan_segments_kernel<kModeByteDirect>,
                         (const void*)scan_segments_kernel<kModeEven>,
                         (const void*)scan_segments_kernel<kModeEvenHash>,
 #if YAMD_DIAG

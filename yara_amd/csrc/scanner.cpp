@@ -484,6 +484,7 @@ int yr_amd_scan_window(yr_amd_scanner* s, const uint8_t* d_window, uint64_t wind
   p.len_mask = t->flat.len_mask;
   p.byte_keys = t->flat.byte_keys;
   p.n_byte_keys = t->flat.n_byte_keys;
+  p.byte_direct = t->flat.byte_direct;
   p.filter_mode = t->flat.filter_mode;
   p.n_segments = n_segments;
   p.seg_bytes = seg_bytes;
