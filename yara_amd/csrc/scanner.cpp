@@ -932,7 +932,7 @@ int yr_amd_verify_device(yr_amd_scanner* s, uint64_t data_base, const yr_amd_ver
     if (v.data == nullptr) return YR_AMD_INVALID_ARGUMENT;
     int r = grow(s->d_vcount, s->vcount_cap, v.count);
     if (!r) r = grow(s->d_vkeep, s->vkeep_cap, 2 * v.count);
-    if (!r) r = grow(s->d_vblock, s->vblock_cap, verify_blocks(v.count));
+    if (!r) r = grow(s->d_vblock, s->vblock_cap, verify_blocks(v.count) + 1);
     // record space before the count is known (one per 16 candidates, capped;
     // the buffer is kept, so mostly a scanner's first calls outgrow it): the
     // write pass is queued behind the count pass with no host round trip in

@@ -96,8 +96,9 @@ struct VerifyParams {
                               // entry of the candidate's list is kept (t < 31); bit 31 =
                               // the list is longer, pass 1 decides again
   uint32_t* heads;            // [count] the candidate's match-list head M[state] (pass 0)
-  uint64_t* block_off;        // [verify_blocks(count)] pass 0: records per 256-candidate
-                              // block; then (launch_block_offsets) exclusive offsets
+  uint64_t* block_off;        // [verify_blocks(count) + 1] pass 0: records per 256-candidate
+                              // block; then (launch_block_offsets) exclusive offsets and
+                              // the total
   VerifyRec* out;             // records (pass 1)
   uint64_t out_cap;           // records that fit in out; pass 1 drops the rest (the
                               // host re-runs it when the total turns out larger)

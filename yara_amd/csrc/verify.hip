@@ -968,6 +968,9 @@ __global__ __launch_bounds__(256) void verify_kernel(VerifyParams p) {
     if (threadIdx.x == 0) p.block_off[blockIdx.x] = total;
     return;
   }
+  // a block without records (block_offsets_kernel: one entry past the last
+  // block) reads nothing more -- most blocks of a dense rule set
+  if (p.block_off[blockIdx.x + 1] == p.block_off[blockIdx.x]) return;
   const uint32_t keep = in ? p.keep[c] : 0u;
   n = keep == 0 ? 0u : p.counts[c];
   const uint32_t pre = block_exclusive_scan(n, wsum, total);
@@ -976,7 +979,7 @@ __global__ __launch_bounds__(256) void verify_kernel(VerifyParams p) {
 }
 
 // Exclusive scan, in place, of the per-block record counts (one workgroup),
-// and their total.
+// and their total (also into block_off[n_blocks]).
 __global__ __launch_bounds__(1024) void block_offsets_kernel(uint64_t* block_off, uint64_t n_blocks,
                                                              uint64_t* total) {
   __shared__ uint64_t part[1024];
@@ -999,7 +1002,10 @@ __global__ __launch_bounds__(1024) void block_offsets_kernel(uint64_t* block_off
     block_off[i] = run;
     run += c;
   }
-  if (t == 1023) *total = part[1023];
+  if (t == 1023) {
+    block_off[n_blocks] = part[1023];   // (verify_kernel<1>: block b's count = next - own)
+    *total = part[1023];
+  }
 }
 
 hipError_t launch_verify(const VerifyParams& p, int pass, hipStream_t s) {
