@@ -16,7 +16,7 @@ import json, sys
 d = json.load(sys.stdin); m = d['modes']['product']
 print('median %.4f ms  min %.4f  candidates %d' % (m['median_ms'], m['min_ms'], m['candidates']))"
       rc=${PIPESTATUS[0]}
-      [ $rc -ne 0 ] && exit $rc
+      if [ $rc -ne 0 ]; then exit $rc; fi
     done
   done
 done

@@ -778,15 +778,36 @@ __device__ __forceinline__ void issue_first_level(const ScanParams& p, WaveQueue
 // last byte is a 1-byte key are certain candidates (1/256 of random input per
 // key: tens of millions per 4 GiB); the filter covers the other keys and
 // passes in only a few per cent of tiles.  So a tile whose lanes pass no
-// filter test emits its key positions straight to the segment output, in
-// order, when no lane holds more than two (wave_inclusive_scan-free: lane L's
-// slot = found + #lanes below L with >= 1 + #lanes below L with 2); any other
-// tile (filter passes, three or more key bytes in a lane, the ragged tail, a
-// full output slot range) takes direct_tile_general.
+// filter test emits its key positions, in order, to the wave's output buffer
+// (direct_flush) when no lane holds more than two (wave_inclusive_scan-free:
+// lane L's slot = count + #lanes below L with >= 1 + #lanes below L with 2); any other
+// tile (filter passes, three or more key bytes in a lane, the ragged tail)
+// takes direct_tile_general.
+// The direct kernel's output goes through a per-wave LDS buffer (the ring's
+// space: kDirectBuf offsets) and out to the segment output in coalesced runs:
+// a global store per tile would make the next tile's input wait for its
+// write acknowledgement (loads and stores share vmcnt on gfx950).
+constexpr uint32_t kDirectBuf = kQueueCap * kQueueEntryWords;   // 384
+__device__ __forceinline__ void lds_store1(uint32_t addr, uint32_t x) {
+  *reinterpret_cast<__attribute__((address_space(3))) uint32_t*>((uintptr_t)addr) = x;
+}
+__device__ __forceinline__ void direct_flush(const ScanParams& p, WaveQueue& q, SegState& st,
+                                             uint32_t lane) {
+  __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+  for (uint32_t k = lane; k < q.count; k += kWave) {
+    const uint32_t idx = st.found + k;
+    if (idx < p.seg_cap) st.out[idx] = lds_load<uint32_t>(q.ring + 4 * k);
+  }
+  st.found += q.count;
+  q.count = 0;
+  __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+}
+
 template <bool TAIL>
 __device__ __forceinline__ void direct_tile_general(const ScanParams& p, WaveQueue& q, SegState& st,
                                                     const uint32_t (&S)[6], uint32_t f,
                                                     uint32_t lane_off, uint32_t lane) {
+  if (q.count != 0) direct_flush(p, q, st, lane);   // (in order; frees the ring for the windows)
   uint32_t cand = byte_keys_mask(S, p);   // bit j <=> lane byte j is a 1-byte key
   uint32_t lim_mask = 0xFFFFu;
   if constexpr (TAIL) {
@@ -831,21 +852,22 @@ __device__ __forceinline__ void direct_step(const ScanParams& p, WaveQueue& q, S
     const uint32_t m2 = mt & (mt - 1u);   // the lane's flags past its first
     const uint64_t two = __ballot(m2 != 0u);
     const uint32_t total = (uint32_t)__popcll(one) + (uint32_t)__popcll(two);
-    if ((two == 0 || __ballot((m2 & (m2 - 1u)) != 0u) == 0) && st.found + total <= p.seg_cap) {
+    if (two == 0 || __ballot((m2 & (m2 - 1u)) != 0u) == 0) {
+      if (q.count + total > kDirectBuf) direct_flush(p, q, st, lane);
       uint32_t idx = __builtin_amdgcn_mbcnt_hi((uint32_t)(one >> 32),
-                                               __builtin_amdgcn_mbcnt_lo((uint32_t)one, st.found));
+                                               __builtin_amdgcn_mbcnt_lo((uint32_t)one, q.count));
       const uint32_t j1 = key_flag_byte((uint32_t)__builtin_ctz(mt | 0x80000000u));
       if (two == 0) {
-        if (mt != 0u) st.out[idx] = lane_off + j1;
+        if (mt != 0u) lds_store1(q.ring + 4 * idx, lane_off + j1);
       } else {
         idx = __builtin_amdgcn_mbcnt_hi((uint32_t)(two >> 32),
                                         __builtin_amdgcn_mbcnt_lo((uint32_t)two, idx));
         const uint32_t j2 = key_flag_byte((uint32_t)__builtin_ctz(m2 | 0x80000000u));
         const bool has2 = m2 != 0u;
-        if (mt != 0u) st.out[idx] = lane_off + (has2 ? min(j1, j2) : j1);
-        if (has2) st.out[idx + 1] = lane_off + max(j1, j2);
+        if (mt != 0u) lds_store1(q.ring + 4 * idx, lane_off + (has2 ? min(j1, j2) : j1));
+        if (has2) lds_store1(q.ring + 4 * idx + 4, lane_off + max(j1, j2));
       }
-      st.found += total;
+      q.count += total;
       return;
     }
   }
@@ -940,7 +962,11 @@ __device__ __forceinline__ void scan_segment(const ScanParams& p, WaveQueue& q, 
     tile_step<MODE, true>(p, q, st, load_tile(base, n_full * kTile, lane, avail), n_full * kTile,
                           lane);
   // everything queued to the segment's output, in order
-  if (q.count != 0) drain<MODE>(p, q, lane, st.seg_start, st.seg_len, st.out, st.found);
+  if constexpr (MODE == kModeByteDirect) {
+    if (q.count != 0) direct_flush(p, q, st, lane);
+  } else if (q.count != 0) {
+    drain<MODE>(p, q, lane, st.seg_start, st.seg_len, st.out, st.found);
+  }
   if constexpr (kDeferFl<MODE>)
     if (q.defer) drain_complete<MODE>(p, q, lane, st.seg_start, st.out, st.found);
   if (q.pend_n != 0) flush_pending<MODE>(p, q, lane, st.seg_start, st.out, st.found);
