@@ -150,6 +150,8 @@ struct yr_amd_scanner {
   size_t vcount_cap = 0;
   uint32_t* d_vkeep = nullptr;    // pre-verification keep masks + states (2 x count)
   size_t vkeep_cap = 0;
+  uint32_t* d_vheavy = nullptr;   // triage: undecided-list count + candidates (1 + count)
+  size_t vheavy_cap = 0;
   uint64_t* d_vblock = nullptr;   // per-256-candidate record counts -> offsets
   size_t vblock_cap = 0;
   VerifyRec* d_vrec = nullptr;
@@ -371,7 +373,7 @@ int yr_amd_scanner_destroy(yr_amd_scanner* s) {
                   (void*)s->d_seg_offset,
                   (void*)s->d_seg_out, (void*)s->d_positions, (void*)s->d_summary,
                   (void*)s->d_vcount, (void*)s->d_vkeep, (void*)s->d_vblock, (void*)s->d_vrec,
-                  (void*)s->d_seg_base, (void*)s->d_seg_next})
+                  (void*)s->d_vheavy, (void*)s->d_seg_base, (void*)s->d_seg_next})
     if (p) (void)hipFree(p);
   if (s->h_summary) (void)hipHostFree(s->h_summary);
   if (s->ev_begin) (void)hipEventDestroy(s->ev_begin);
@@ -945,9 +947,22 @@ int yr_amd_verify_device(yr_amd_scanner* s, uint64_t data_base, const yr_amd_ver
     v.block_off = s->d_vblock;
     v.out = s->d_vrec;
     v.out_cap = s->vrec_cap;
+    // long streams (the 1-byte atoms of regexp / hex sets): the triage pass
+    // instead of the count pass (verify.h launch_verify_triage)
+    // (YAMD_TRIAGE_MIN: another threshold, for tests and A/B measurements)
+    const char* tmin = diag_env("YAMD_TRIAGE_MIN");
+    const bool triage =
+        v.count >= (tmin ? strtoull(tmin, nullptr, 10) : kVerifyTriageMin) && !v.profile;
+    if (triage) {
+      r = grow(s->d_vheavy, s->vheavy_cap, v.count + 1);
+      if (r) return r;
+      v.heavy_n = s->d_vheavy;
+      v.heavy = s->d_vheavy + 1;
+      HIP_TRY(hipMemsetAsync(v.heavy_n, 0, sizeof(uint32_t), s->stream));
+    }
     // count pass -> block offsets (total straight into the host-mapped
     // summary) -> write pass, then one wait
-    HIP_TRY(launch_verify(v, 0, s->stream));
+    HIP_TRY(triage ? launch_verify_triage(v, s->stream) : launch_verify(v, 0, s->stream));
     HIP_TRY(launch_block_offsets(s->d_vblock, v.count, s->d_hsum, s->stream));
     HIP_TRY(launch_verify(v, 1, s->stream));
     HIP_TRY(hipStreamSynchronize(s->stream));

@@ -959,23 +959,171 @@ __global__ __launch_bounds__(256) void verify_kernel(VerifyParams p) {
   // (the low 32 bits of a flat LDS address are the LDS offset)
   const uint32_t lds = (uint32_t)(uintptr_t)(win + threadIdx.x * kWinBytes);
   const uint32_t codebuf = (uint32_t)(uintptr_t)(code + threadIdx.x * kCodeBytes);
-  const uint64_t c = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  const bool in = c < p.count;
   uint32_t n = 0, total = 0;
   if (!PASS) {
-    if (in) verify_one<0>(p, c, lds, codebuf, 0, 0, 0, n);
+    const uint64_t c = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (c < p.count) verify_one<0>(p, c, lds, codebuf, 0, 0, 0, n);
     (void)block_exclusive_scan(n, wsum, total);
     if (threadIdx.x == 0) p.block_off[blockIdx.x] = total;
     return;
   }
-  // a block without records (block_offsets_kernel: one entry past the last
-  // block) reads nothing more -- most blocks of a dense rule set
-  if (p.block_off[blockIdx.x + 1] == p.block_off[blockIdx.x]) return;
-  const uint32_t keep = in ? p.keep[c] : 0u;
-  n = keep == 0 ? 0u : p.counts[c];
-  const uint32_t pre = block_exclusive_scan(n, wsum, total);
-  if (total == 0 || keep == 0) return;
-  verify_one<1>(p, c, lds, codebuf, keep, p.heads[c], p.block_off[blockIdx.x] + pre, n);
+  // pass 1: persistent blocks over the 256-candidate groups; a group without
+  // records (block_offsets_kernel: one entry past the last group) reads
+  // nothing more -- most groups of a dense rule set
+  const uint64_t groups = (p.count + 255) / 256;
+  for (uint64_t g = blockIdx.x; g < groups; g += gridDim.x) {
+    if (p.block_off[g + 1] == p.block_off[g]) continue;
+    const uint64_t c = g * 256 + threadIdx.x;
+    const uint32_t keep = c < p.count ? p.keep[c] : 0u;
+    n = keep == 0 ? 0u : p.counts[c];
+    const uint32_t pre = block_exclusive_scan(n, wsum, total);
+    if (keep != 0) verify_one<1>(p, c, lds, codebuf, keep, p.heads[c], p.block_off[g] + pre, n);
+    __syncthreads();   // (wsum is rewritten by the next group)
+  }
+}
+
+// ---------------------------------------------------------------------------
+// Triage (long candidate streams: the 1-byte atoms of regexp / hex sets give a
+// candidate every ~128 bytes).  Most of their calls are decided by a guard,
+// whose bytes come straight from three aligned 8-byte loads -- no LDS window,
+// no program staging -- so one kernel without LDS decides those lists at full
+// occupancy and hands the few others to verify_heavy_kernel.
+// ---------------------------------------------------------------------------
+// guard_ok without a staged window: true when the region is not all inside
+// the bytes present (the full decision then runs).
+__device__ __forceinline__ bool guard_direct(const VerifyParams& p, uint64_t offset, bool backwards,
+                                             uint32_t bs, DevGuard g) {
+  const uint32_t base = bs & 15u, span = bs >> 4, L = base + span + 4;
+  if (backwards ? offset < L : p.size - offset < L) return true;
+  const uint64_t r0 = backwards ? offset - L : offset + base;   // region: span + 4 <= 12 bytes
+  const uint64_t a8 = r0 & ~7ull;
+  if (a8 < p.win_lo || a8 + 24 > p.win_hi) return true;
+  const uint2* q = reinterpret_cast<const uint2*>(p.data + a8);
+  const uint2 q0 = q[0], q1 = q[1], q2 = q[2];
+  const uint32_t sh = (uint32_t)(r0 - a8), k = sh >> 2, bsh = sh & 3u;
+  const uint32_t B0 = k ? q0.y : q0.x, B1 = k ? q1.x : q0.y, B2 = k ? q1.y : q1.x;
+  const uint32_t B3 = k ? q2.x : q1.y;
+  const uint32_t W[3] = {__builtin_amdgcn_alignbyte(B1, B0, bsh),
+                         __builtin_amdgcn_alignbyte(B2, B1, bsh),
+                         __builtin_amdgcn_alignbyte(B3, B2, bsh)};
+  bool hit = false;
+#pragma unroll
+  for (uint32_t t = 0; t <= 8; ++t) {
+    const uint32_t r = (t & 3) == 0 ? W[t >> 2]
+                                    : __builtin_amdgcn_alignbyte(W[(t >> 2) + 1], W[t >> 2], t & 3);
+    hit |= t <= span && (r & g.m) == g.v;
+  }
+  return hit;
+}
+
+// One call of the triage: 0 = no effect, 1 = kept, 2 = needs call_matters.
+// Each 0 / 1 is call_matters' own answer (its early returns and guard tests,
+// in its order).
+__device__ __forceinline__ uint32_t triage_call(const VerifyParams& p, const DevPoolRec& e,
+                                                uint64_t i) {
+  const uint32_t bt = e.backtrack;
+  if (bt > i) return 0;   // scanner.c:107: not called
+  const uint64_t offset = i - bt;
+  if (offset >= p.size) return 0;
+  if ((e.flags & kStrFixedOffset) && e.fixed_offset != (int64_t)(p.data_base + offset)) return 0;
+  if ((e.flags & (kStrLiteral | kStrFitsInAtom)) == (kStrLiteral | kStrFitsInAtom) &&
+      !(e.flags & (kStrUnmodelled | kStrFullWord)))
+    return bt != 0 ? 1u : 0u;
+  if (p.win_lo != 0 || p.win_hi != p.size) {
+    const uint64_t need_lo = offset - min<uint64_t>(offset, (uint64_t)kReScanLimit);
+    const uint64_t need_hi =
+        min<uint64_t>(p.size, offset + max<uint64_t>((uint64_t)kReScanLimit, 2ull * e.length + 2));
+    if (need_lo < p.win_lo || need_hi > p.win_hi) return 1;
+  }
+  if (e.flags & kStrLiteral) return (e.flags & kStrUnmodelled) ? 1u : 2u;
+  if (!p.re_on || e.re.fwd_len == 0) return 1;
+  const bool has_bwd = e.re.bwd_len > 0;
+  if (e.flags & kStrFastRegexp) {
+    if (!(e.flags & kStrAscii) || (e.flags & (kStrWide | kStrBase64Any))) return 1;
+  } else {
+    // yr_re_exec strings: a wide attempt is never ruled out here
+    if ((e.flags & kStrWide) && !(e.flags & kStrBase64Any)) return 2;
+    if (!(e.flags & (kStrAscii | kStrBase64Any))) return 0;   // no attempt runs
+  }
+  // the ascii attempt: dead if either direction's guard fails
+  if (e.fguard.m != 0 && !guard_direct(p, offset, false, e.fguard_bs, e.fguard)) return 0;
+  if (has_bwd && e.bguard.m != 0 && !guard_direct(p, offset, true, e.bguard_bs, e.bguard)) return 0;
+  return 2;
+}
+
+// One candidate of the triage: true = its list needs the full decision
+// (nothing written); else keep / counts / heads as verify_one<0> writes them
+// and its record count in n.
+__device__ __forceinline__ bool triage_one(const VerifyParams& p, uint64_t c, uint32_t& n) {
+  const uint64_t i = p.all ? p.all_first + c : p.positions[c];
+  Near near;
+  const uint32_t head = node_head(p, i, near);
+  uint32_t t = 0, mask = 0;
+  n = 0;
+  for (uint32_t k = head; k != 0; ++t) {
+    const DevPoolRec e = p.pool[k - 1];
+    const uint32_t d = triage_call(p, e, i);
+    k = e.next;
+    if (d == 2) return true;
+    if (d == 1) {
+      if (t < 31) mask |= 1u << t;
+      ++n;
+    }
+  }
+  p.keep[c] = n == 0 ? 0u : (t > 31 ? kKeepOverflow : mask);
+  if (n != 0) {
+    p.counts[c] = n;
+    p.heads[c] = head;
+  }
+  return false;
+}
+
+// Persistent blocks over the 256-candidate groups of verify_kernel: each
+// group's triaged record count into block_off; the undecided candidates onto
+// the heavy list (one atomic per wave).
+__global__ __launch_bounds__(256) void verify_triage_kernel(VerifyParams p) {
+  __shared__ uint32_t wsum[4];
+  const uint64_t groups = (p.count + 255) / 256;
+  const uint32_t lane = threadIdx.x & 63u;
+  for (uint64_t g = blockIdx.x; g < groups; g += gridDim.x) {
+    const uint64_t c = g * 256 + threadIdx.x;
+    uint32_t n = 0;
+    bool heavy = false;
+    if (c < p.count) heavy = triage_one(p, c, n);
+    const uint64_t hm = __ballot(heavy);
+    if (hm != 0) {
+      const uint32_t leader = (uint32_t)__builtin_ctzll(hm);
+      uint32_t at = 0;
+      if (lane == leader) at = atomicAdd(p.heavy_n, (uint32_t)__popcll(hm));
+      at = __shfl(at, (int)leader, 64);
+      if (heavy)
+        p.heavy[at + __builtin_amdgcn_mbcnt_hi((uint32_t)(hm >> 32),
+                                               __builtin_amdgcn_mbcnt_lo((uint32_t)hm, 0u))] =
+            (uint32_t)c;
+    }
+    uint32_t total;
+    (void)block_exclusive_scan(heavy ? 0u : n, wsum, total);
+    if (threadIdx.x == 0) p.block_off[g] = total;
+    __syncthreads();   // (wsum is rewritten by the next group)
+  }
+}
+
+// The heavy list, decided as verify_kernel<0> decides (staged windows, regexp
+// search); each record count is added to its group's.
+__global__ __launch_bounds__(256) void verify_heavy_kernel(VerifyParams p) {
+  __shared__ __attribute__((aligned(16))) uint8_t win[256 * kWinBytes];
+  __shared__ __attribute__((aligned(16))) uint8_t code[256 * kCodeBytes];
+  const uint32_t lds = (uint32_t)(uintptr_t)(win + threadIdx.x * kWinBytes);
+  const uint32_t codebuf = (uint32_t)(uintptr_t)(code + threadIdx.x * kCodeBytes);
+  const uint32_t nh = *p.heavy_n;
+  for (uint64_t h = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; h < nh;
+       h += (uint64_t)gridDim.x * blockDim.x) {
+    const uint32_t c = p.heavy[h];
+    uint32_t n = 0;
+    verify_one<0>(p, c, lds, codebuf, 0, 0, 0, n);
+    if (n != 0) atomicAdd(reinterpret_cast<unsigned long long*>(p.block_off + (c >> 8)),
+                          (unsigned long long)n);
+  }
 }
 
 // Exclusive scan, in place, of the per-block record counts (one workgroup),
@@ -987,6 +1135,7 @@ __global__ __launch_bounds__(1024) void block_offsets_kernel(uint64_t* block_off
   const uint64_t per = (n_blocks + 1023) / 1024;
   const uint64_t lo = min(t * per, n_blocks), hi = min(lo + per, n_blocks);
   uint64_t s = 0;
+#pragma unroll 16
   for (uint64_t i = lo; i < hi; ++i) s += block_off[i];
   part[t] = s;
   __syncthreads();
@@ -997,6 +1146,7 @@ __global__ __launch_bounds__(1024) void block_offsets_kernel(uint64_t* block_off
     __syncthreads();
   }
   uint64_t run = part[t] - s;
+#pragma unroll 16
   for (uint64_t i = lo; i < hi; ++i) {
     const uint64_t c = block_off[i];
     block_off[i] = run;
@@ -1008,13 +1158,25 @@ __global__ __launch_bounds__(1024) void block_offsets_kernel(uint64_t* block_off
   }
 }
 
+// Grid of the persistent kernels: 8 blocks of 256 per CU of the MI355X.
+constexpr uint64_t kPersistentBlocks = 256 * 8;
+
 hipError_t launch_verify(const VerifyParams& p, int pass, hipStream_t s) {
   if (p.count == 0) return hipSuccess;
   const uint64_t blocks = (p.count + 255) / 256;
   if (pass == 0)
     hipLaunchKernelGGL(verify_kernel<0>, dim3((uint32_t)blocks), dim3(256), 0, s, p);
   else
-    hipLaunchKernelGGL(verify_kernel<1>, dim3((uint32_t)blocks), dim3(256), 0, s, p);
+    hipLaunchKernelGGL(verify_kernel<1>, dim3((uint32_t)std::min<uint64_t>(blocks, kPersistentBlocks)),
+                       dim3(256), 0, s, p);
+  return hipGetLastError();
+}
+
+hipError_t launch_verify_triage(const VerifyParams& p, hipStream_t s) {
+  if (p.count == 0) return hipSuccess;
+  const uint32_t blocks = (uint32_t)std::min<uint64_t>((p.count + 255) / 256, kPersistentBlocks);
+  hipLaunchKernelGGL(verify_triage_kernel, dim3(blocks), dim3(256), 0, s, p);
+  hipLaunchKernelGGL(verify_heavy_kernel, dim3(blocks), dim3(256), 0, s, p);
   return hipGetLastError();
 }
 
