@@ -194,6 +194,11 @@ constexpr int kModeEven = 21;
 constexpr int kModeEvenHash = 22;
 template <int MODE>
 constexpr bool kEven = MODE == kModeEven || MODE == kModeEvenHash;
+// Profiling ablations of the byte-key kernel (diagnostic builds): 24 = the 1-byte
+// keys detected but not appended (the ring holds the filter hits only), 25 =
+// not even detected.  Both on a 1-byte-key rule set; output wrong by construction.
+template <int MODE>
+constexpr bool kByteKeyAblation = MODE == 24 || MODE == 25;
 // A pending entry's offset with this bit set is a certain candidate (its last
 // byte is a 1-byte key): no bucket probe.  (Segment offsets are < 2^20.)
 constexpr uint32_t kConfirmed = 0x80000000u;
@@ -376,7 +381,8 @@ template <int MODE>
 constexpr bool kHoldFl = YAMD_HOLD_FL && !kEven<MODE>;
 template <int MODE>
 constexpr bool kDeferFl =
-    YAMD_DEFER_FL && (MODE == 0 || MODE == 12 || MODE == kModeByteKeys || kEven<MODE>);
+    YAMD_DEFER_FL &&
+    (MODE == 0 || MODE == 12 || MODE == kModeByteKeys || kEven<MODE> || kByteKeyAblation<MODE>);
 
 // Consume a deferred drain's first-level words: the lanes' hits that pass go,
 // in order, to the pending list.
@@ -465,7 +471,7 @@ __device__ __forceinline__ void drain(const ScanParams& p, WaveQueue& q, uint32_
       return;
     }
   }
-  if ((MODE == 0 || MODE == kModeByteKeys) && (p.len_mask & 6u) != 0u) {
+  if ((MODE == 0 || MODE == kModeByteKeys || kByteKeyAblation<MODE>) && (p.len_mask & 6u) != 0u) {
     maybe = m;   // 1-/2-byte keys: no first level, every hit goes to the buckets
   } else {
     while (m) {
@@ -885,8 +891,9 @@ __device__ __forceinline__ void tile_step(const ScanParams& p, WaveQueue& q, Seg
     direct_step<TAIL>(p, q, st, S, tile_off, lane);
     return;
   }
-  uint32_t any = stage1<MODE == kModeByteKeys ? 0 : MODE, true>(S, lane);
+  uint32_t any = stage1<(MODE == kModeByteKeys || kByteKeyAblation<MODE>) ? 0 : MODE, true>(S, lane);
   if constexpr (MODE == kModeByteKeys) any |= byte_keys_any(S, p);
+  if constexpr (MODE == 24) asm volatile("" ::"v"(byte_keys_any(S, p)));
   if constexpr (kDeferFl<MODE>)
     if (q.defer) drain_complete<MODE>(p, q, lane, st.seg_start, st.out, st.found);
   ring_append<MODE, TAIL>(p, q, st, S, any, tile_off, lane);
@@ -1138,6 +1145,8 @@ hipError_t launch_scan(const ScanParams& p, int grid, hipStream_t s, int mode) {
     case 10: hipLaunchKernelGGL(scan_segments_kernel<10>, dim3(grid), dim3(kWGThreads), lds, s, p); break;
     case 11: hipLaunchKernelGGL(scan_segments_kernel<11>, dim3(grid), dim3(kWGThreads), lds, s, p); break;
     case 12: hipLaunchKernelGGL(scan_segments_kernel<12>, dim3(grid), dim3(kWGThreads), lds, s, p); break;
+    case 24: hipLaunchKernelGGL(scan_segments_kernel<24>, dim3(grid), dim3(kWGThreads), lds, s, p); break;
+    case 25: hipLaunchKernelGGL(scan_segments_kernel<25>, dim3(grid), dim3(kWGThreads), lds, s, p); break;
 #endif
     default:
       if (p.n_byte_keys != 0 && p.byte_direct != 0)
@@ -1194,6 +1203,7 @@ hipError_t configure_scan_kernel() {
                         (const void*)scan_segments_kernel<8>, (const void*)scan_segments_kernel<9>,
                         (const void*)scan_segments_kernel<10>, (const void*)scan_segments_kernel<11>,
                         (const void*)scan_segments_kernel<12>,
+                        (const void*)scan_segments_kernel<24>, (const void*)scan_segments_kernel<25>,
 #endif
                        }) {
     hipError_t r = hipFuncSetAttribute(k, hipFuncAttributeMaxDynamicSharedMemorySize, lds);

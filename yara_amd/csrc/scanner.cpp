@@ -401,7 +401,8 @@ int yr_amd_scanner_set_timing(yr_amd_scanner* s, int enable) {
 // ablations of the scan kernel (tools/ablate.py).  Any mode other than 0
 // produces wrong results.
 int yr_amd__diag_kernel_mode(yr_amd_scanner* s, int mode) {
-  if (s == nullptr || mode < 0 || mode > 12) return YR_AMD_INVALID_ARGUMENT;
+  if (s == nullptr || mode < 0 || (mode > 12 && mode != 24 && mode != 25))
+    return YR_AMD_INVALID_ARGUMENT;
   s->diag_mode = mode;
   return YR_AMD_SUCCESS;
 }
