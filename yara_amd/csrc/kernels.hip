@@ -811,8 +811,16 @@ __device__ __forceinline__ void direct_flush(const ScanParams& p, WaveQueue& q, 
 
 template <bool TAIL>
 __device__ __forceinline__ void direct_tile_general(const ScanParams& p, WaveQueue& q, SegState& st,
-                                                    const uint32_t (&S)[6], uint32_t f,
+                                                    const uint32_t (&S0)[6], uint32_t f,
                                                     uint32_t lane_off, uint32_t lane) {
+  // (a laundered copy of the context: nothing this rare path computes from it
+  // can be hoisted into the common path, where it would cost every tile)
+  uint32_t S[6];
+#pragma unroll
+  for (int k = 0; k < 6; ++k) {
+    S[k] = S0[k];
+    asm volatile("" : "+v"(S[k]));
+  }
   if (q.count != 0) direct_flush(p, q, st, lane);   // (in order; frees the ring for the windows)
   uint32_t cand = byte_keys_mask(S, p);   // bit j <=> lane byte j is a 1-byte key
   uint32_t lim_mask = 0xFFFFu;
