@@ -634,7 +634,11 @@ int yr_amd_tables_set_strings(yr_amd_tables* t, const uint32_t* pool_string, uin
   int r = YR_AMD_SUCCESS;
   if (!r) r = upload(t->d_nodes, f.nodes.data(), f.nodes.size());
   if (!r) r = upload(t->d_pool, t->h_pool.data(), t->h_pool.size());
-  if (!r) r = upload(t->d_str_bytes, bytes, n_bytes);
+  // (32 zero bytes past the blob: the triage reads 24 bytes from the 8-byte
+  // boundary below a string, verify.hip bytes16)
+  std::vector<uint8_t> blob((size_t)n_bytes + 32, 0);
+  if (n_bytes > 0) memcpy(blob.data(), bytes, (size_t)n_bytes);
+  if (!r) r = upload(t->d_str_bytes, blob.data(), blob.size());
   if (!r) r = upload(t->d_lowercase, lowercase, 256);
   if (r) return r;   // partial uploads are freed with the tables
   t->h_pool_string.assign(pool_string, pool_string + n_pool);

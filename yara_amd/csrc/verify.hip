@@ -1016,6 +1016,47 @@ __device__ __forceinline__ bool guard_direct(const VerifyParams& p, uint64_t off
   return hit;
 }
 
+// The 16 bytes at base + off, from three aligned 8-byte loads at the 8-byte
+// boundary below (24 bytes from there must be readable).
+__device__ __forceinline__ uint4 bytes16(const uint8_t* base, uint64_t off) {
+  const uint64_t a8 = off & ~7ull;
+  const uint2* q = reinterpret_cast<const uint2*>(base + a8);
+  const uint2 q0 = q[0], q1 = q[1], q2 = q[2];
+  const uint32_t sh = (uint32_t)(off - a8), k = sh >> 2, bsh = sh & 3u;
+  const uint32_t B0 = k ? q0.y : q0.x, B1 = k ? q1.x : q0.y, B2 = k ? q1.y : q1.x;
+  const uint32_t B3 = k ? q2.x : q1.y, B4 = k ? q2.y : q2.x;
+  return make_uint4(__builtin_amdgcn_alignbyte(B1, B0, bsh), __builtin_amdgcn_alignbyte(B2, B1, bsh),
+                    __builtin_amdgcn_alignbyte(B3, B2, bsh), __builtin_amdgcn_alignbyte(B4, B3, bsh));
+}
+
+// A plain ascii literal of up to 16 bytes (no wide / nocase / xor form), as
+// call_matters decides it (cmp_ascii, then the FULL_WORD test), with the
+// compared bytes from bytes16; 2 where the 24 bytes are not all present.
+__device__ __forceinline__ uint32_t triage_literal(const VerifyParams& p, const DevPoolRec& e,
+                                                   uint64_t offset) {
+  const uint32_t n = e.length;
+  if ((e.flags & (kStrWide | kStrNoCase | kStrXor)) || !(e.flags & kStrAscii) || n == 0 || n > 16)
+    return 2;
+  if (p.size - offset < n) return 0;   // cmp_ascii: avail < n, and no other form
+  const uint64_t a8 = offset & ~7ull;
+  if (a8 < p.win_lo || a8 + 24 > p.win_hi) return 2;
+  const uint4 D = bytes16(p.data, offset);
+  const uint4 S = bytes16(p.str_bytes, e.bytes_off);
+  auto m = [n](uint32_t d) {   // the compared bytes of dword d
+    return n >= 4 * d + 4 ? 0xFFFFFFFFu : n <= 4 * d ? 0u : (1u << (8 * (n - 4 * d))) - 1u;
+  };
+  const uint32_t diff = ((D.x ^ S.x) & m(0)) | ((D.y ^ S.y) & m(1)) | ((D.z ^ S.z) & m(2)) |
+                        ((D.w ^ S.w) & m(3));
+  if (diff != 0) return 0;   // scan.c:974-975
+  if (!(e.flags & kStrFullWord)) return 1;
+  auto alnum = [](uint8_t c) {
+    return (c >= 0x30 && c <= 0x39) || (c >= 0x41 && c <= 0x5a) || (c >= 0x61 && c <= 0x7a);
+  };
+  if (offset >= 1 && alnum(p.data[offset - 1])) return 0;   // scan.c:672-694
+  if (offset + n < p.size && alnum(p.data[offset + n])) return 0;
+  return 1;
+}
+
 // One call of the triage: 0 = no effect, 1 = kept, 2 = needs call_matters.
 // Each 0 / 1 is call_matters' own answer (its early returns and guard tests,
 // in its order).
@@ -1035,7 +1076,7 @@ __device__ __forceinline__ uint32_t triage_call(const VerifyParams& p, const Dev
         min<uint64_t>(p.size, offset + max<uint64_t>((uint64_t)kReScanLimit, 2ull * e.length + 2));
     if (need_lo < p.win_lo || need_hi > p.win_hi) return 1;
   }
-  if (e.flags & kStrLiteral) return (e.flags & kStrUnmodelled) ? 1u : 2u;
+  if (e.flags & kStrLiteral) return (e.flags & kStrUnmodelled) ? 1u : triage_literal(p, e, offset);
   if (!p.re_on || e.re.fwd_len == 0) return 1;
   const bool has_bwd = e.re.bwd_len > 0;
   if (e.flags & kStrFastRegexp) {
