@@ -152,7 +152,9 @@ struct yr_amd_scanner {
   size_t vkeep_cap = 0;
   uint32_t* d_vheavy = nullptr;   // triage: undecided-list count + candidates (1 + count)
   size_t vheavy_cap = 0;
-  uint64_t* d_vblock = nullptr;   // per-256-candidate record counts -> offsets
+  uint64_t* d_vblock = nullptr;   // per-group (64 candidates) record counts -> offsets
+  uint64_t* d_vchunk = nullptr;   // per-chunk (1024 groups) offsets
+  size_t vchunk_cap = 0;
   size_t vblock_cap = 0;
   VerifyRec* d_vrec = nullptr;
   size_t vrec_cap = 0;
@@ -373,7 +375,8 @@ int yr_amd_scanner_destroy(yr_amd_scanner* s) {
                   (void*)s->d_seg_offset,
                   (void*)s->d_seg_out, (void*)s->d_positions, (void*)s->d_summary,
                   (void*)s->d_vcount, (void*)s->d_vkeep, (void*)s->d_vblock, (void*)s->d_vrec,
-                  (void*)s->d_vheavy, (void*)s->d_seg_base, (void*)s->d_seg_next})
+                  (void*)s->d_vheavy, (void*)s->d_vchunk, (void*)s->d_seg_base,
+                  (void*)s->d_seg_next})
     if (p) (void)hipFree(p);
   if (s->h_summary) (void)hipHostFree(s->h_summary);
   if (s->ev_begin) (void)hipEventDestroy(s->ev_begin);
@@ -939,7 +942,8 @@ int yr_amd_verify_device(yr_amd_scanner* s, uint64_t data_base, const yr_amd_ver
     if (v.data == nullptr) return YR_AMD_INVALID_ARGUMENT;
     int r = grow(s->d_vcount, s->vcount_cap, v.count);
     if (!r) r = grow(s->d_vkeep, s->vkeep_cap, 2 * v.count);
-    if (!r) r = grow(s->d_vblock, s->vblock_cap, verify_blocks(v.count) + 1);
+    if (!r) r = grow(s->d_vblock, s->vblock_cap, verify_groups(v.count) + 1);
+    if (!r) r = grow(s->d_vchunk, s->vchunk_cap, verify_chunks(v.count) + 1);
     // record space before the count is known (one per 16 candidates, capped;
     // the buffer is kept, so mostly a scanner's first calls outgrow it): the
     // write pass is queued behind the count pass with no host round trip in
@@ -950,6 +954,7 @@ int yr_amd_verify_device(yr_amd_scanner* s, uint64_t data_base, const yr_amd_ver
     v.keep = s->d_vkeep;
     v.heads = s->d_vkeep + v.count;
     v.block_off = s->d_vblock;
+    v.chunk_off = s->d_vchunk;
     v.out = s->d_vrec;
     v.out_cap = s->vrec_cap;
     // long streams (the 1-byte atoms of regexp / hex sets): the triage pass
@@ -968,7 +973,7 @@ int yr_amd_verify_device(yr_amd_scanner* s, uint64_t data_base, const yr_amd_ver
     // count pass -> block offsets (total straight into the host-mapped
     // summary) -> write pass, then one wait
     HIP_TRY(triage ? launch_verify_triage(v, s->stream) : launch_verify(v, 0, s->stream));
-    HIP_TRY(launch_block_offsets(s->d_vblock, v.count, s->d_hsum, s->stream));
+    HIP_TRY(launch_block_offsets(s->d_vblock, s->d_vchunk, v.count, s->d_hsum, s->stream));
     HIP_TRY(launch_verify(v, 1, s->stream));
     HIP_TRY(hipStreamSynchronize(s->stream));
     total = s->h_summary[0];

@@ -96,9 +96,10 @@ struct VerifyParams {
                               // entry of the candidate's list is kept (t < 31); bit 31 =
                               // the list is longer, pass 1 decides again
   uint32_t* heads;            // [count] the candidate's match-list head M[state] (pass 0)
-  uint64_t* block_off;        // [verify_blocks(count) + 1] pass 0: records per 256-candidate
-                              // block; then (launch_block_offsets) exclusive offsets and
-                              // the total
+  uint64_t* block_off;        // [verify_groups(count) + 1] pass 0: records per group of
+                              // kGroup candidates; then (launch_block_offsets) exclusive
+                              // offsets within the group's chunk of kChunkGroups
+  uint64_t* chunk_off;        // [verify_chunks(count) + 1] the chunks' exclusive offsets, total
   uint32_t* heavy;            // triage (launch_verify_triage): the candidates whose lists need
   uint32_t* heavy_n;          //   the full decision, in no order, and their number
   VerifyRec* out;             // records (pass 1)
@@ -113,8 +114,11 @@ hipError_t launch_verify(const VerifyParams& p, int pass, hipStream_t s);
 // does.  Needs heavy / heavy_n (zeroed count) and not profile.
 hipError_t launch_verify_triage(const VerifyParams& p, hipStream_t s);
 constexpr uint64_t kVerifyTriageMin = 1u << 20;   // candidates (scanner.cpp)
-hipError_t launch_block_offsets(uint64_t* block_off, uint64_t count, uint64_t* total,
-                                hipStream_t s);
-uint64_t verify_blocks(uint64_t count);
+hipError_t launch_block_offsets(uint64_t* block_off, uint64_t* chunk_off, uint64_t count,
+                                uint64_t* total, hipStream_t s);
+constexpr uint64_t kGroup = 64;           // candidates per group (one wave)
+constexpr uint64_t kChunkGroups = 1024;   // groups per chunk of the offsets scan
+uint64_t verify_groups(uint64_t count);
+uint64_t verify_chunks(uint64_t count);
 
 }  // namespace yamd

@@ -924,61 +924,62 @@ __device__ __forceinline__ void verify_one(const VerifyParams& p, uint64_t c, ui
   count = n;
 }
 
-// Exclusive scan of one value per thread over a 256-thread block (wave
-// shuffles, one barrier); `total` = the block's sum.
-__device__ __forceinline__ uint32_t block_exclusive_scan(uint32_t v, uint32_t* wsum,
-                                                         uint32_t& total) {
-  const uint32_t lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+// Candidates are decided in groups of 64, one wave each: block_off[g] = the
+// group's record count, then (launch_block_offsets) its exclusive offset
+// within its chunk of kChunkGroups groups, chunk_off[] the chunks' offsets --
+// no barrier anywhere, so a wave never waits for another's longest list.
+__device__ __forceinline__ uint64_t group_offset(const VerifyParams& p, uint64_t g) {
+  return p.chunk_off[g / kChunkGroups] + p.block_off[g];
+}
+__device__ __forceinline__ uint32_t wave_sum(uint32_t v) {
+#pragma unroll
+  for (int d = 32; d >= 1; d >>= 1) v += __shfl_xor(v, d, 64);
+  return v;
+}
+__device__ __forceinline__ uint32_t wave_exclusive(uint32_t v) {
+  const uint32_t lane = threadIdx.x & 63u;
   uint32_t inc = v;
+#pragma unroll
   for (int d = 1; d < 64; d <<= 1) {
     const uint32_t u = __shfl_up(inc, d, 64);
     if (lane >= (uint32_t)d) inc += u;
   }
-  if (lane == 63) wsum[w] = inc;
-  __syncthreads();
-  uint32_t before = 0;
-  total = 0;
-#pragma unroll
-  for (uint32_t k = 0; k < 4; ++k) {
-    const uint32_t x = wsum[k];
-    if (k < w) before += x;
-    total += x;
-  }
-  return before + inc - v;
+  return inc - v;
+}
+__device__ __forceinline__ uint32_t wave_in_block() {
+  return __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
 }
 
-// PASS 0: every candidate of the block is decided; the block's record count
-// goes to block_off[block].  (launch_block_offsets turns those into exclusive
-// offsets.)  PASS 1: each block scans its candidates' counts, adds its block
-// offset and writes the records; candidates without records return at once.
+// PASS 0: one candidate per lane; each wave's record count goes to its group.
+// PASS 1: persistent waves over the groups: a group without records reads
+// nothing more (most groups of a dense rule set); the others scan their
+// candidates' counts and write the records from the group's offset on.
 template <int PASS>
 __global__ __launch_bounds__(256) void verify_kernel(VerifyParams p) {
   __shared__ __attribute__((aligned(16))) uint8_t win[256 * kWinBytes];
   __shared__ __attribute__((aligned(16))) uint8_t code[256 * kCodeBytes];
-  __shared__ uint32_t wsum[4];
   // (the low 32 bits of a flat LDS address are the LDS offset)
   const uint32_t lds = (uint32_t)(uintptr_t)(win + threadIdx.x * kWinBytes);
   const uint32_t codebuf = (uint32_t)(uintptr_t)(code + threadIdx.x * kCodeBytes);
-  uint32_t n = 0, total = 0;
+  const uint64_t groups = (p.count + kGroup - 1) / kGroup;
   if (!PASS) {
     const uint64_t c = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    uint32_t n = 0;
     if (c < p.count) verify_one<0>(p, c, lds, codebuf, 0, 0, 0, n);
-    (void)block_exclusive_scan(n, wsum, total);
-    if (threadIdx.x == 0) p.block_off[blockIdx.x] = total;
+    const uint32_t sum = wave_sum(n);
+    if ((threadIdx.x & 63u) == 0 && c / kGroup < groups) p.block_off[c / kGroup] = sum;
     return;
   }
-  // pass 1: persistent blocks over the 256-candidate groups; a group without
-  // records (block_offsets_kernel: one entry past the last group) reads
-  // nothing more -- most groups of a dense rule set
-  const uint64_t groups = (p.count + 255) / 256;
-  for (uint64_t g = blockIdx.x; g < groups; g += gridDim.x) {
-    if (p.block_off[g + 1] == p.block_off[g]) continue;
-    const uint64_t c = g * 256 + threadIdx.x;
+  const uint64_t waves = (uint64_t)gridDim.x * (blockDim.x / 64);
+  for (uint64_t g = (uint64_t)blockIdx.x * (blockDim.x / 64) + wave_in_block(); g < groups;
+       g += waves) {
+    const uint64_t o = group_offset(p, g);
+    if (group_offset(p, g + 1) == o) continue;
+    const uint64_t c = g * kGroup + (threadIdx.x & 63u);
     const uint32_t keep = c < p.count ? p.keep[c] : 0u;
-    n = keep == 0 ? 0u : p.counts[c];
-    const uint32_t pre = block_exclusive_scan(n, wsum, total);
-    if (keep != 0) verify_one<1>(p, c, lds, codebuf, keep, p.heads[c], p.block_off[g] + pre, n);
-    __syncthreads();   // (wsum is rewritten by the next group)
+    uint32_t n = keep == 0 ? 0u : p.counts[c];
+    const uint32_t pre = wave_exclusive(n);
+    if (keep != 0) verify_one<1>(p, c, lds, codebuf, keep, p.heads[c], o + pre, n);
   }
 }
 
@@ -1119,15 +1120,15 @@ __device__ __forceinline__ bool triage_one(const VerifyParams& p, uint64_t c, ui
   return false;
 }
 
-// Persistent blocks over the 256-candidate groups of verify_kernel: each
-// group's triaged record count into block_off; the undecided candidates onto
-// the heavy list (one atomic per wave).
+// Persistent waves over the groups: each group's triaged record count into
+// block_off; the undecided candidates onto the heavy list (one atomic per wave).
 __global__ __launch_bounds__(256) void verify_triage_kernel(VerifyParams p) {
-  __shared__ uint32_t wsum[4];
-  const uint64_t groups = (p.count + 255) / 256;
+  const uint64_t groups = (p.count + kGroup - 1) / kGroup;
   const uint32_t lane = threadIdx.x & 63u;
-  for (uint64_t g = blockIdx.x; g < groups; g += gridDim.x) {
-    const uint64_t c = g * 256 + threadIdx.x;
+  const uint64_t waves = (uint64_t)gridDim.x * (blockDim.x / 64);
+  for (uint64_t g = (uint64_t)blockIdx.x * (blockDim.x / 64) + wave_in_block(); g < groups;
+       g += waves) {
+    const uint64_t c = g * kGroup + lane;
     uint32_t n = 0;
     bool heavy = false;
     if (c < p.count) heavy = triage_one(p, c, n);
@@ -1142,10 +1143,8 @@ __global__ __launch_bounds__(256) void verify_triage_kernel(VerifyParams p) {
                                                __builtin_amdgcn_mbcnt_lo((uint32_t)hm, 0u))] =
             (uint32_t)c;
     }
-    uint32_t total;
-    (void)block_exclusive_scan(heavy ? 0u : n, wsum, total);
-    if (threadIdx.x == 0) p.block_off[g] = total;
-    __syncthreads();   // (wsum is rewritten by the next group)
+    const uint32_t sum = wave_sum(heavy ? 0u : n);
+    if (lane == 0) p.block_off[g] = sum;
   }
 }
 
@@ -1162,13 +1161,45 @@ __global__ __launch_bounds__(256) void verify_heavy_kernel(VerifyParams p) {
     const uint32_t c = p.heavy[h];
     uint32_t n = 0;
     verify_one<0>(p, c, lds, codebuf, 0, 0, 0, n);
-    if (n != 0) atomicAdd(reinterpret_cast<unsigned long long*>(p.block_off + (c >> 8)),
+    if (n != 0) atomicAdd(reinterpret_cast<unsigned long long*>(p.block_off + c / kGroup),
                           (unsigned long long)n);
   }
 }
 
-// Exclusive scan, in place, of the per-block record counts (one workgroup),
-// and their total (also into block_off[n_blocks]).
+// Offsets, step 1: one 1024-thread block per chunk of kChunkGroups groups --
+// the chunk's exclusive scan in place (entry `groups`, past the last group,
+// counts 0) and its total into chunk_off[chunk].
+__global__ __launch_bounds__(1024) void group_scan_kernel(uint64_t* block_off, uint64_t groups,
+                                                          uint64_t* chunk_off) {
+  __shared__ uint64_t wsum[16];
+  const uint32_t lane = threadIdx.x & 63u, w = threadIdx.x >> 6;
+  const uint64_t i = (uint64_t)blockIdx.x * kChunkGroups + threadIdx.x;
+  const uint64_t v = i < groups ? block_off[i] : 0;
+  uint64_t inc = v;
+#pragma unroll
+  for (int d = 1; d < 64; d <<= 1) {
+    const uint64_t u = __shfl_up(inc, d, 64);
+    if (lane >= (uint32_t)d) inc += u;
+  }
+  if (lane == 63) wsum[w] = inc;
+  __syncthreads();
+  if (w == 0) {
+    const uint64_t x = lane < 16 ? wsum[lane] : 0;
+    uint64_t y = x;
+#pragma unroll
+    for (int d = 1; d < 16; d <<= 1) {
+      const uint64_t u = __shfl_up(y, d, 64);
+      if (lane >= (uint32_t)d) y += u;
+    }
+    if (lane < 16) wsum[lane] = y - x;
+    if (lane == 15) chunk_off[blockIdx.x] = y;
+  }
+  __syncthreads();
+  if (i <= groups) block_off[i] = wsum[w] + inc - v;
+}
+
+// Offsets, step 2 (one workgroup): exclusive scan, in place, of the chunk
+// totals, and their sum (into chunk_off[n] and *total).
 __global__ __launch_bounds__(1024) void block_offsets_kernel(uint64_t* block_off, uint64_t n_blocks,
                                                              uint64_t* total) {
   __shared__ uint64_t part[1024];
@@ -1194,41 +1225,59 @@ __global__ __launch_bounds__(1024) void block_offsets_kernel(uint64_t* block_off
     run += c;
   }
   if (t == 1023) {
-    block_off[n_blocks] = part[1023];   // (verify_kernel<1>: block b's count = next - own)
+    block_off[n_blocks] = part[1023];
     *total = part[1023];
   }
 }
 
-// Grid of the persistent kernels: 8 blocks of 256 per CU of the MI355X.
-constexpr uint64_t kPersistentBlocks = 256 * 8;
+// Grid of the persistent kernels: as many 256-thread blocks as the device
+// keeps resident (a second wave of blocks would finish late).
+static uint32_t resident_blocks(const void* kernel) {
+  int dev = 0, cus = 0, per = 0;
+  if (hipGetDevice(&dev) != hipSuccess ||
+      hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess ||
+      hipOccupancyMaxActiveBlocksPerMultiprocessor(&per, kernel, 256, 0) != hipSuccess)
+    return 256;
+  return (uint32_t)std::max(1, cus * std::max(1, per));
+}
 
 hipError_t launch_verify(const VerifyParams& p, int pass, hipStream_t s) {
   if (p.count == 0) return hipSuccess;
-  const uint64_t blocks = (p.count + 255) / 256;
-  if (pass == 0)
-    hipLaunchKernelGGL(verify_kernel<0>, dim3((uint32_t)blocks), dim3(256), 0, s, p);
-  else
-    hipLaunchKernelGGL(verify_kernel<1>, dim3((uint32_t)std::min<uint64_t>(blocks, kPersistentBlocks)),
-                       dim3(256), 0, s, p);
+  if (pass == 0) {
+    hipLaunchKernelGGL(verify_kernel<0>, dim3((uint32_t)((p.count + 255) / 256)), dim3(256), 0, s, p);
+  } else {
+    const uint64_t waves = verify_groups(p.count);
+    const uint32_t blocks = (uint32_t)std::min<uint64_t>(
+        (waves + 3) / 4, resident_blocks((const void*)verify_kernel<1>));
+    hipLaunchKernelGGL(verify_kernel<1>, dim3(blocks), dim3(256), 0, s, p);
+  }
   return hipGetLastError();
 }
 
 hipError_t launch_verify_triage(const VerifyParams& p, hipStream_t s) {
   if (p.count == 0) return hipSuccess;
-  const uint32_t blocks = (uint32_t)std::min<uint64_t>((p.count + 255) / 256, kPersistentBlocks);
-  hipLaunchKernelGGL(verify_triage_kernel, dim3(blocks), dim3(256), 0, s, p);
-  hipLaunchKernelGGL(verify_heavy_kernel, dim3(blocks), dim3(256), 0, s, p);
+  const uint64_t waves = verify_groups(p.count);
+  const uint32_t tb = (uint32_t)std::min<uint64_t>(
+      (waves + 3) / 4, resident_blocks((const void*)verify_triage_kernel));
+  hipLaunchKernelGGL(verify_triage_kernel, dim3(tb), dim3(256), 0, s, p);
+  const uint32_t hb = (uint32_t)std::min<uint64_t>(
+      (p.count + 255) / 256, resident_blocks((const void*)verify_heavy_kernel));
+  hipLaunchKernelGGL(verify_heavy_kernel, dim3(hb), dim3(256), 0, s, p);
   return hipGetLastError();
 }
 
-hipError_t launch_block_offsets(uint64_t* block_off, uint64_t count, uint64_t* total,
-                                hipStream_t s) {
-  const uint64_t blocks = verify_blocks(count);
-  if (blocks == 0) return hipMemsetAsync(total, 0, sizeof(uint64_t), s);
-  hipLaunchKernelGGL(block_offsets_kernel, dim3(1), dim3(1024), 0, s, block_off, blocks, total);
+hipError_t launch_block_offsets(uint64_t* block_off, uint64_t* chunk_off, uint64_t count,
+                                uint64_t* total, hipStream_t s) {
+  const uint64_t groups = verify_groups(count);
+  if (groups == 0) return hipMemsetAsync(total, 0, sizeof(uint64_t), s);
+  const uint64_t chunks = verify_chunks(count);
+  hipLaunchKernelGGL(group_scan_kernel, dim3((uint32_t)chunks), dim3(1024), 0, s, block_off, groups,
+                     chunk_off);
+  hipLaunchKernelGGL(block_offsets_kernel, dim3(1), dim3(1024), 0, s, chunk_off, chunks, total);
   return hipGetLastError();
 }
 
-uint64_t verify_blocks(uint64_t count) { return (count + 255) / 256; }
+uint64_t verify_groups(uint64_t count) { return (count + kGroup - 1) / kGroup; }
+uint64_t verify_chunks(uint64_t count) { return (verify_groups(count) + 1 + kChunkGroups - 1) / kChunkGroups; }
 
 }  // namespace yamd
