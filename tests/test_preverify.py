@@ -214,47 +214,3 @@ def test_profiling_count_only_records(case):
     assert np.array_equal(r["offset"], off[want])
     assert np.array_equal(r["pool_index"] & 0x7FFFFFFF, idx[want])
     assert np.array_equal(co, ~keep[want])
-
-
-@pytest.mark.gpu
-def test_triage_pass_equals_count_pass():
-    """Long candidate streams take the triage pass (verify.h
-    launch_verify_triage: guards and early returns decided without LDS, the
-    other lists by the full pass).  With the diagnostic build's threshold at 0
-    every golden case goes that way (one child process): device records equal
-    the golden stream filtered by the oracle, as for the count pass above; and
-    the root-accepting set (every position a candidate) gives the same records
-    both ways."""
-    from conftest import run_diag_child
-    code = (
-        "import numpy as np, yara_amd, oracle\n"
-        "from conftest import case_arrays, case_data, tables_npz\n"
-        "from test_preverify import CASES, FULL, _expected\n"
-        "from test_gpu_parity import blocks\n"
-        "n = 0\n"
-        "for case in FULL:\n"
-        "  rec = CASES[case]; arr = case_arrays(case); data = case_data(rec)\n"
-        "  z, keep, off, idx, base = _expected(rec, arr, data)\n"
-        "  sc = yara_amd.Scanner(yara_amd.Tables.from_npz(tables_npz(rec['rules']), device=0, strings=True))\n"
-        "  if rec['block']:\n"
-        "    rs = [sc.verify_calls(data[b:b + k], data_base=b) for b, k in blocks(rec['size'], rec['block'], rec['overlap'])]\n"
-        "    g_off = np.concatenate([r['offset'] for r in rs]); g_idx = np.concatenate([r['pool_index'] for r in rs])\n"
-        "  else:\n"
-        "    r = sc.verify_calls(data); g_off, g_idx = r['offset'], r['pool_index']\n"
-        "  assert np.array_equal(g_off, off[keep]) and np.array_equal(g_idx, idx[keep]), case\n"
-        "  n += 1\n"
-        "print('triage ok', n)\n")
-    out = run_diag_child(code, env={"YAMD_TRIAGE_MIN": "0"}, timeout=600)
-    assert "triage ok %d" % len(FULL) in out
-    code = (
-        "import numpy as np, yara_amd, oracle, os\n"
-        "from conftest import tables_npz\n"
-        "data = oracle.xorshift((1 << 20) + 5, 9)\n"
-        "outs = []\n"
-        "for m in ('0', '1000000000'):\n"
-        "  os.environ['YAMD_TRIAGE_MIN'] = m\n"
-        "  r = yara_amd.Scanner(yara_amd.Tables.from_npz(tables_npz('root'), device=0, strings=True)).verify_calls(data)\n"
-        "  outs.append(r)\n"
-        "assert len(outs[0]) > 0 and np.array_equal(outs[0], outs[1])\n"
-        "print('root ok', len(outs[0]))\n")
-    assert "root ok" in run_diag_child(code, timeout=300)

@@ -34,9 +34,6 @@ constexpr int kTile = kWave * kBytesPerLane;        // 1024 B
 constexpr uint32_t kSegment = 1u << 20;   // max segment: 1 MiB (ring entries hold offset/16 in 16 bits)
 constexpr uint32_t kSegmentTarget = kSegment;   // preferred segment size (scanner.cpp)
 constexpr uint32_t kMaxByteKeys = 4;   // 1-byte keys tested in stage 1 (more: filter)
-// the direct byte-key kernel when at most this fraction of random tiles has a
-// filter pass (tables.cpp)
-constexpr double kByteDirectMaxTiles = 0.25;
 constexpr int kWavesPerWG = 16;
 constexpr int kWGThreads = kWave * kWavesPerWG;     // 1024
 
@@ -186,7 +183,6 @@ struct ScanParams {
                             // seg_out + seg_base[s] (exact-size rerun after an overflow)
   uint32_t byte_keys;       // FlatTables::byte_keys / n_byte_keys (stage-1 byte test)
   uint32_t n_byte_keys;
-  uint32_t byte_direct;     // FlatTables::byte_direct: the direct byte-key kernel
   uint32_t filter_mode;     // kFilterPair / kFilterEven / kFilterEvenHash (FlatTables)
   uint32_t* seg_next;       // null: wave w takes segments w, w + waves, ...; else each wave
                             // takes its first segment by index and the next ones from this

@@ -178,15 +178,25 @@ struct WaveQueue {
   // loads (0 = none), the loaded word
   uint32_t wa, oa, ia, da;
   uint32_t wb, ob, ib, db;
+  // (YAMD_STORE_SLOT) the last flush's output store, per lane: byte offset in
+  // the segment's output (kNoStore: none) and value; issued at the tile step's
+  // fixed store point (store_slot)
+  uint32_t so_off, so_val;
+  bool so_pending;  // wave-uniform
 };
+// Output stores at one fixed point of every tile step (one buffer store per
+// tile, lanes without data out of the buffer's range, so the hardware drops
+// them): the wait for the next input tile then never waits for a store
+// (gfx950 counts loads and stores in one vmcnt, in order; a store issued on
+// some paths only makes the compiler's merged wait cover it).
+#ifndef YAMD_STORE_SLOT
+#define YAMD_STORE_SLOT 0
+#endif
+constexpr uint32_t kNoStore = 0x7FFFFFF0u;
 constexpr uint32_t kNoHit = 0xFFFFFFFFu;
 // Kernel variant: the product kernel for rule sets whose 1-byte keys are tested
 // byte by byte in stage 1 (byte_keys_any below) instead of in the filter.
 constexpr int kModeByteKeys = 20;
-// Kernel variant: the product kernel for rule sets with 1-byte keys whose
-// other keys rarely pass the filter (FlatTables::byte_direct): no ring, every
-// tile's candidates go straight to the segment output (direct_step below).
-constexpr int kModeByteDirect = 23;
 // Kernel variant: the product kernel for the even-position filter
 // (internal.h kFilterEven: rule sets whose keys are all 4 bytes long).
 constexpr int kModeEven = 21;
@@ -229,13 +239,34 @@ __device__ __forceinline__ void flush_pending(const ScanParams& p, WaveQueue& q,
     keep = MODE == 12 ? true : exact_check(e.x, seg_start + off + 1, p);   // 12: ablation
   }
   const uint64_t b = __ballot(keep);
+#if YAMD_STORE_SLOT
+  if (q.so_pending && q.so_off != kNoStore) out[q.so_off / 4] = q.so_val;   // (a second flush in one step)
+  const uint32_t idx = found + __builtin_amdgcn_mbcnt_hi((uint32_t)(b >> 32),
+                                                         __builtin_amdgcn_mbcnt_lo((uint32_t)b, 0u));
+  q.so_off = keep && idx < p.seg_cap ? idx * 4u : kNoStore;
+  q.so_val = off;
+  q.so_pending = true;
+#else
   if (keep) {
     const uint32_t idx = found + __builtin_amdgcn_mbcnt_hi((uint32_t)(b >> 32),
                                                            __builtin_amdgcn_mbcnt_lo((uint32_t)b, 0u));
     if (idx < p.seg_cap) out[idx] = off;
   }
+#endif
   found += (uint32_t)__popcll(b);
   q.pend_n = 0;
+}
+
+// The fixed store point of a tile step (YAMD_STORE_SLOT): the pending output
+// store, or a dropped one.
+__device__ __forceinline__ void store_slot(const ScanParams& p, WaveQueue& q, uint32_t* out) {
+#if YAMD_STORE_SLOT
+  const __amdgpu_buffer_rsrc_t r =
+      __builtin_amdgcn_make_buffer_rsrc(out, (short)0, (int)(p.seg_cap * 4u), 0x00020000);
+  __builtin_amdgcn_raw_buffer_store_b32(q.so_val, r, q.so_off, 0, 0);
+  q.so_off = kNoStore;
+  q.so_pending = false;
+#endif
 }
 
 // Append hits (bit j of `keep` = lane byte j at segment offset off0 + j) to
@@ -320,43 +351,6 @@ __device__ __forceinline__ uint32_t byte_keys_mask(const uint32_t (&S)[6], const
     }
   }
   return m;
-}
-
-// The byte-key flags of the lane's 16 bytes for the direct kernel: bit
-// 8n + 7 - d set iff lane byte 4d + n equals a 1-byte key (key_flag_byte).
-// Per dword x and key v (replicated): y = ((x ^ v) & 0x7F7F7F7F) + 0x7F7F7F7F
-// has bit 7 of byte n clear iff the low 7 bits of that byte of x ^ v are zero,
-// so ~y & ~(x ^ v) has it set iff the byte equals the key (one v_bitop3 on y,
-// x and the scalar v).  Exact per byte (no carry between bytes); 3
-// instructions per dword for the first key, 4 for each further one; the
-// other bits are don't-care until the merge.
-__device__ __forceinline__ uint32_t byte_key_flags(const uint32_t (&S)[6], const ScanParams& p) {
-  uint32_t a[4];
-  {
-    const uint32_t v = (p.byte_keys & 0xFFu) * 0x01010101u;   // n_byte_keys >= 1
-#pragma unroll
-    for (int d = 0; d < 4; ++d) {
-      const uint32_t y = ((S[1 + d] ^ v) & 0x7F7F7F7Fu) + 0x7F7F7F7Fu;
-      a[d] = ~y & ~(S[1 + d] ^ v);
-    }
-  }
-  for (uint32_t k = 1; k < p.n_byte_keys; ++k) {   // wave-uniform
-    const uint32_t v = ((p.byte_keys >> (8 * k)) & 0xFFu) * 0x01010101u;
-#pragma unroll
-    for (int d = 0; d < 4; ++d) {
-      const uint32_t y = ((S[1 + d] ^ v) & 0x7F7F7F7Fu) + 0x7F7F7F7Fu;
-      a[d] |= ~y & ~(S[1 + d] ^ v);
-    }
-  }
-  // merge: bit 7 of each byte from a[0], bit 6 from a[1], 5 from a[2], 4 from a[3]
-  uint32_t u = (a[0] & 0x80808080u) | ((a[1] >> 1) & ~0x80808080u);
-  u = (u & 0xC0C0C0C0u) | ((a[2] >> 2) & ~0xC0C0C0C0u);
-  u = (u & 0xE0E0E0E0u) | ((a[3] >> 3) & ~0xE0E0E0E0u);
-  return u & 0xF0F0F0F0u;
-}
-// Lane byte of flag bit b of byte_key_flags: b = 8n + 7 - d <=> byte 4d + n.
-__device__ __forceinline__ uint32_t key_flag_byte(uint32_t b) {
-  return ((~b & 7u) << 2) | (b >> 3);
 }
 
 // Kernel variants whose drains defer their first-level loads (WaveQueue).
@@ -780,114 +774,6 @@ __device__ __forceinline__ void issue_first_level(const ScanParams& p, WaveQueue
   }
 }
 
-// A tile of the direct byte-key kernel (kModeByteDirect).  The positions whose
-// last byte is a 1-byte key are certain candidates (1/256 of random input per
-// key: tens of millions per 4 GiB); the filter covers the other keys and
-// passes in only a few per cent of tiles.  So a tile whose lanes pass no
-// filter test emits its key positions, in order, to the wave's output buffer
-// (direct_flush) when no lane holds more than two (wave_inclusive_scan-free:
-// lane L's slot = count + #lanes below L with >= 1 + #lanes below L with 2); any other
-// tile (filter passes, three or more key bytes in a lane, the ragged tail)
-// takes direct_tile_general.
-// The direct kernel's output goes through a per-wave LDS buffer (the ring's
-// space: kDirectBuf offsets) and out to the segment output in coalesced runs:
-// a global store per tile would make the next tile's input wait for its
-// write acknowledgement (loads and stores share vmcnt on gfx950).
-constexpr uint32_t kDirectBuf = kQueueCap * kQueueEntryWords;   // 384
-__device__ __forceinline__ void lds_store1(uint32_t addr, uint32_t x) {
-  *reinterpret_cast<__attribute__((address_space(3))) uint32_t*>((uintptr_t)addr) = x;
-}
-__device__ __forceinline__ void direct_flush(const ScanParams& p, WaveQueue& q, SegState& st,
-                                             uint32_t lane) {
-  __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
-  for (uint32_t k = lane; k < q.count; k += kWave) {
-    const uint32_t idx = st.found + k;
-    if (idx < p.seg_cap) st.out[idx] = lds_load<uint32_t>(q.ring + 4 * k);
-  }
-  st.found += q.count;
-  q.count = 0;
-  __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
-}
-
-template <bool TAIL>
-__device__ __forceinline__ void direct_tile_general(const ScanParams& p, WaveQueue& q, SegState& st,
-                                                    const uint32_t (&S0)[6], uint32_t f,
-                                                    uint32_t lane_off, uint32_t lane) {
-  // (a laundered copy of the context: nothing this rare path computes from it
-  // can be hoisted into the common path, where it would cost every tile)
-  uint32_t S[6];
-#pragma unroll
-  for (int k = 0; k < 6; ++k) {
-    S[k] = S0[k];
-    asm volatile("" : "+v"(S[k]));
-  }
-  if (q.count != 0) direct_flush(p, q, st, lane);   // (in order; frees the ring for the windows)
-  uint32_t cand = byte_keys_mask(S, p);   // bit j <=> lane byte j is a 1-byte key
-  uint32_t lim_mask = 0xFFFFu;
-  if constexpr (TAIL) {
-    const uint32_t lim = lane_off >= st.seg_len ? 0u : st.seg_len - lane_off;
-    lim_mask = lim >= 16u ? 0xFFFFu : (1u << lim) - 1u;
-  }
-  if (__ballot(f != 0u) != 0) {
-    // the other filter hits: exact check in place (one round trip), through
-    // the lane's ring slot for the windows (window4)
-    uint32_t unc = 0;
-    if (f != 0u) unc = dense_mask(stage1<0, false>(S, lane)) & ~cand & lim_mask;
-    if (__ballot(unc != 0u) != 0) {
-      const uint32_t ent = q.ring + lane * (kQueueEntryWords * 4);
-      if (unc != 0u) {
-        lds_store2(ent, S[1], S[2]);
-        lds_store2(ent + 8, S[3], S[4]);
-        lds_store2(ent + 16, S[0], 0u);
-      }
-      __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
-      while (unc != 0u) {
-        const uint32_t j = (uint32_t)__builtin_ctz(unc);
-        unc &= unc - 1u;
-        if (exact_check(window4(ent, j), st.seg_start + lane_off + j + 1, p)) cand |= 1u << j;
-      }
-    }
-  }
-  cand &= lim_mask;
-  const uint32_t c = __popc(cand);
-  append_hits(p, cand, c, wave_inclusive_scan(c), lane_off, st.out, st.found);
-}
-
-template <bool TAIL>
-__device__ __forceinline__ void direct_step(const ScanParams& p, WaveQueue& q, SegState& st,
-                                            const uint32_t (&S)[6], uint32_t tile_off,
-                                            uint32_t lane) {
-  const uint32_t f = stage1<0, true>(S, lane);   // bit 0: a position of the lane passes
-  const uint32_t mt = byte_key_flags(S, p);
-  const uint32_t lane_off = tile_off + lane * kBytesPerLane;
-  if (!TAIL && __ballot(f != 0u) == 0) {
-    const uint64_t one = __ballot(mt != 0u);
-    if (one == 0) return;
-    const uint32_t m2 = mt & (mt - 1u);   // the lane's flags past its first
-    const uint64_t two = __ballot(m2 != 0u);
-    const uint32_t total = (uint32_t)__popcll(one) + (uint32_t)__popcll(two);
-    if (two == 0 || __ballot((m2 & (m2 - 1u)) != 0u) == 0) {
-      if (q.count + total > kDirectBuf) direct_flush(p, q, st, lane);
-      uint32_t idx = __builtin_amdgcn_mbcnt_hi((uint32_t)(one >> 32),
-                                               __builtin_amdgcn_mbcnt_lo((uint32_t)one, q.count));
-      const uint32_t j1 = key_flag_byte((uint32_t)__builtin_ctz(mt | 0x80000000u));
-      if (two == 0) {
-        if (mt != 0u) lds_store1(q.ring + 4 * idx, lane_off + j1);
-      } else {
-        idx = __builtin_amdgcn_mbcnt_hi((uint32_t)(two >> 32),
-                                        __builtin_amdgcn_mbcnt_lo((uint32_t)two, idx));
-        const uint32_t j2 = key_flag_byte((uint32_t)__builtin_ctz(m2 | 0x80000000u));
-        const bool has2 = m2 != 0u;
-        if (mt != 0u) lds_store1(q.ring + 4 * idx, lane_off + (has2 ? min(j1, j2) : j1));
-        if (has2) lds_store1(q.ring + 4 * idx + 4, lane_off + max(j1, j2));
-      }
-      q.count += total;
-      return;
-    }
-  }
-  direct_tile_general<TAIL>(p, q, st, S, f, lane_off, lane);
-}
-
 // One 1 KiB tile: stage-1 filter over its 1024 byte positions, then the ordered
 // append of the hits to the wave ring.
 template <int MODE, bool TAIL>
@@ -895,10 +781,6 @@ __device__ __forceinline__ void tile_step(const ScanParams& p, WaveQueue& q, Seg
                                           uint4 cur, uint32_t tile_off, uint32_t lane) {
   uint32_t S[6];
   tile_context(st, cur, S);
-  if constexpr (MODE == kModeByteDirect) {
-    direct_step<TAIL>(p, q, st, S, tile_off, lane);
-    return;
-  }
   uint32_t any = stage1<(MODE == kModeByteKeys || kByteKeyAblation<MODE>) ? 0 : MODE, true>(S, lane);
   if constexpr (MODE == kModeByteKeys) any |= byte_keys_any(S, p);
   if constexpr (MODE == 24) asm volatile("" ::"v"(byte_keys_any(S, p)));
@@ -906,6 +788,7 @@ __device__ __forceinline__ void tile_step(const ScanParams& p, WaveQueue& q, Seg
     if (q.defer) drain_complete<MODE>(p, q, lane, st.seg_start, st.out, st.found);
   ring_append<MODE, TAIL>(p, q, st, S, any, tile_off, lane);
   issue_first_level<MODE>(p, q);
+  store_slot(p, q, st.out);
 }
 
 // Stream one segment [seg_start, seg_start + seg_len) of the block: full tiles
@@ -952,6 +835,9 @@ __device__ __forceinline__ void scan_segment(const ScanParams& p, WaveQueue& q, 
   q.da = q.db = 0u;
   q.wa = q.wb = 0u;
   q.oa = q.ob = kNoHit;
+  q.so_off = kNoStore;
+  q.so_val = 0u;
+  q.so_pending = false;
 
   const uint32_t n_full = st.seg_len / kTile;            // tiles needing no mask / bounds
   if (n_full > 0) {
@@ -977,14 +863,13 @@ __device__ __forceinline__ void scan_segment(const ScanParams& p, WaveQueue& q, 
     tile_step<MODE, true>(p, q, st, load_tile(base, n_full * kTile, lane, avail), n_full * kTile,
                           lane);
   // everything queued to the segment's output, in order
-  if constexpr (MODE == kModeByteDirect) {
-    if (q.count != 0) direct_flush(p, q, st, lane);
-  } else if (q.count != 0) {
-    drain<MODE>(p, q, lane, st.seg_start, st.seg_len, st.out, st.found);
-  }
+  if (q.count != 0) drain<MODE>(p, q, lane, st.seg_start, st.seg_len, st.out, st.found);
   if constexpr (kDeferFl<MODE>)
     if (q.defer) drain_complete<MODE>(p, q, lane, st.seg_start, st.out, st.found);
   if (q.pend_n != 0) flush_pending<MODE>(p, q, lane, st.seg_start, st.out, st.found);
+#if YAMD_STORE_SLOT
+  if (q.so_pending && q.so_off != kNoStore) st.out[q.so_off / 4] = q.so_val;
+#endif
   if (lane == 0) p.seg_count[seg] = st.found;
 }
 
@@ -1157,10 +1042,7 @@ hipError_t launch_scan(const ScanParams& p, int grid, hipStream_t s, int mode) {
     case 25: hipLaunchKernelGGL(scan_segments_kernel<25>, dim3(grid), dim3(kWGThreads), lds, s, p); break;
 #endif
     default:
-      if (p.n_byte_keys != 0 && p.byte_direct != 0)
-        hipLaunchKernelGGL(scan_segments_kernel<kModeByteDirect>, dim3(grid), dim3(kWGThreads),
-                           lds, s, p);
-      else if (p.n_byte_keys != 0)
+      if (p.n_byte_keys != 0)
         hipLaunchKernelGGL(scan_segments_kernel<kModeByteKeys>, dim3(grid), dim3(kWGThreads), lds,
                            s, p);
       else if (p.filter_mode == kFilterEven)
@@ -1200,7 +1082,6 @@ hipError_t configure_scan_kernel() {
   hipError_t e = hipSuccess;
   for (const void* k : {(const void*)scan_segments_kernel<0>,
                         (const void*)scan_segments_kernel<kModeByteKeys>,
-                        (const void*)scan_segments_kernel<kModeByteDirect>,
                         (const void*)scan_segments_kernel<kModeEven>,
                         (const void*)scan_segments_kernel<kModeEvenHash>,
 #if YAMD_DIAG

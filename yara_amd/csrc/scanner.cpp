@@ -150,8 +150,6 @@ struct yr_amd_scanner {
   size_t vcount_cap = 0;
   uint32_t* d_vkeep = nullptr;    // pre-verification keep masks + states (2 x count)
   size_t vkeep_cap = 0;
-  uint32_t* d_vheavy = nullptr;   // triage: undecided-list count + candidates (1 + count)
-  size_t vheavy_cap = 0;
   uint64_t* d_vblock = nullptr;   // per-group (64 candidates) record counts -> offsets
   uint64_t* d_vchunk = nullptr;   // per-chunk (1024 groups) offsets
   size_t vchunk_cap = 0;
@@ -375,7 +373,7 @@ int yr_amd_scanner_destroy(yr_amd_scanner* s) {
                   (void*)s->d_seg_offset,
                   (void*)s->d_seg_out, (void*)s->d_positions, (void*)s->d_summary,
                   (void*)s->d_vcount, (void*)s->d_vkeep, (void*)s->d_vblock, (void*)s->d_vrec,
-                  (void*)s->d_vheavy, (void*)s->d_vchunk, (void*)s->d_seg_base,
+                  (void*)s->d_vchunk, (void*)s->d_seg_base,
                   (void*)s->d_seg_next})
     if (p) (void)hipFree(p);
   if (s->h_summary) (void)hipHostFree(s->h_summary);
@@ -490,7 +488,6 @@ int yr_amd_scan_window(yr_amd_scanner* s, const uint8_t* d_window, uint64_t wind
   p.len_mask = t->flat.len_mask;
   p.byte_keys = t->flat.byte_keys;
   p.n_byte_keys = t->flat.n_byte_keys;
-  p.byte_direct = t->flat.byte_direct;
   p.filter_mode = t->flat.filter_mode;
   p.n_segments = n_segments;
   p.seg_bytes = seg_bytes;
@@ -637,11 +634,7 @@ int yr_amd_tables_set_strings(yr_amd_tables* t, const uint32_t* pool_string, uin
   int r = YR_AMD_SUCCESS;
   if (!r) r = upload(t->d_nodes, f.nodes.data(), f.nodes.size());
   if (!r) r = upload(t->d_pool, t->h_pool.data(), t->h_pool.size());
-  // (32 zero bytes past the blob: the triage reads 24 bytes from the 8-byte
-  // boundary below a string, verify.hip bytes16)
-  std::vector<uint8_t> blob((size_t)n_bytes + 32, 0);
-  if (n_bytes > 0) memcpy(blob.data(), bytes, (size_t)n_bytes);
-  if (!r) r = upload(t->d_str_bytes, blob.data(), blob.size());
+  if (!r) r = upload(t->d_str_bytes, bytes, n_bytes);
   if (!r) r = upload(t->d_lowercase, lowercase, 256);
   if (r) return r;   // partial uploads are freed with the tables
   t->h_pool_string.assign(pool_string, pool_string + n_pool);
@@ -957,22 +950,9 @@ int yr_amd_verify_device(yr_amd_scanner* s, uint64_t data_base, const yr_amd_ver
     v.chunk_off = s->d_vchunk;
     v.out = s->d_vrec;
     v.out_cap = s->vrec_cap;
-    // long streams (the 1-byte atoms of regexp / hex sets): the triage pass
-    // instead of the count pass (verify.h launch_verify_triage)
-    // (YAMD_TRIAGE_MIN: another threshold, for tests and A/B measurements)
-    const char* tmin = diag_env("YAMD_TRIAGE_MIN");
-    const bool triage =
-        v.count >= (tmin ? strtoull(tmin, nullptr, 10) : kVerifyTriageMin) && !v.profile;
-    if (triage) {
-      r = grow(s->d_vheavy, s->vheavy_cap, v.count + 1);
-      if (r) return r;
-      v.heavy_n = s->d_vheavy;
-      v.heavy = s->d_vheavy + 1;
-      HIP_TRY(hipMemsetAsync(v.heavy_n, 0, sizeof(uint32_t), s->stream));
-    }
     // count pass -> block offsets (total straight into the host-mapped
     // summary) -> write pass, then one wait
-    HIP_TRY(triage ? launch_verify_triage(v, s->stream) : launch_verify(v, 0, s->stream));
+    HIP_TRY(launch_verify(v, 0, s->stream));
     HIP_TRY(launch_block_offsets(s->d_vblock, s->d_vchunk, v.count, s->d_hsum, s->stream));
     HIP_TRY(launch_verify(v, 1, s->stream));
     HIP_TRY(hipStreamSynchronize(s->stream));

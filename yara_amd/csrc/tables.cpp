@@ -19,7 +19,6 @@
 //    open-addressed hash table for the second stage.
 #include "tables.h"
 
-#include <math.h>
 #include <stdlib.h>
 #include <string.h>
 
@@ -311,20 +310,6 @@ int flatten_tables(const uint32_t* T, const uint32_t* M, uint32_t n_slots,
     }
   }
   for (uint32_t w : out.filter) out.filter_set_bits += (uint32_t)__builtin_popcount(w);
-  // With 1-byte keys in stage 1: the direct kernel (no ring; a tile with a
-  // filter pass is checked in place, one round trip) unless the other keys
-  // pass in more than kByteDirectMaxTiles of random tiles.  A random window
-  // passes the pair filter with probability sum over blocks of |lo| x |hi|
-  // / 2^24 in either role; a tile tests 1,024.  (YAMD_BYTE_DIRECT = 0 / 1
-  // forces the choice: A/B measurements.)
-  if (out.n_byte_keys != 0) {
-    uint64_t pass = 0;
-    for (uint32_t b = 0; b < kFilterWords / 2; ++b)
-      pass += (uint64_t)__builtin_popcount(out.filter[2 * b]) * __builtin_popcount(out.filter[2 * b + 1]);
-    const double per_tile = 1.0 - pow(1.0 - (double)pass / 16777216.0, (double)kTile);
-    const char* e = diag_env("YAMD_BYTE_DIRECT");
-    out.byte_direct = e ? (uint32_t)(atoi(e) != 0) : (uint32_t)(per_tile <= kByteDirectMaxTiles);
-  }
 
   // 3b. exact key sets: bitmaps for 1-2 byte keys, two-choice bucketed
   //     hash tables for 3-4 byte keys

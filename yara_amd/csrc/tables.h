@@ -41,9 +41,6 @@ struct FlatTables {
   // being inserted into the window filter (each would fill it with 65,536
   // windows): up to kMaxByteKeys key bytes, packed low byte first
   uint32_t byte_keys = 0, n_byte_keys = 0;
-  // the direct byte-key kernel (kernels.hip kModeByteDirect): set when the
-  // filter's other keys pass in few tiles of random input (tables.cpp)
-  uint32_t byte_direct = 0;
 
   // accepting trie nodes -> match-list head M[slot], by the node's string
   // (pre-verification: the walk's state at a candidate is its longest

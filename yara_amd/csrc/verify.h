@@ -100,20 +100,12 @@ struct VerifyParams {
                               // kGroup candidates; then (launch_block_offsets) exclusive
                               // offsets within the group's chunk of kChunkGroups
   uint64_t* chunk_off;        // [verify_chunks(count) + 1] the chunks' exclusive offsets, total
-  uint32_t* heavy;            // triage (launch_verify_triage): the candidates whose lists need
-  uint32_t* heavy_n;          //   the full decision, in no order, and their number
   VerifyRec* out;             // records (pass 1)
   uint64_t out_cap;           // records that fit in out; pass 1 drops the rest (the
                               // host re-runs it when the total turns out larger)
 };
 
 hipError_t launch_verify(const VerifyParams& p, int pass, hipStream_t s);
-// Pass 0 for long candidate streams: a triage kernel (no LDS, full occupancy)
-// decides every list whose calls need no window staging or regexp search and
-// collects the other candidates, which a second kernel decides as pass 0
-// does.  Needs heavy / heavy_n (zeroed count) and not profile.
-hipError_t launch_verify_triage(const VerifyParams& p, hipStream_t s);
-constexpr uint64_t kVerifyTriageMin = 1u << 20;   // candidates (scanner.cpp)
 hipError_t launch_block_offsets(uint64_t* block_off, uint64_t* chunk_off, uint64_t count,
                                 uint64_t* total, hipStream_t s);
 constexpr uint64_t kGroup = 64;           // candidates per group (one wave)

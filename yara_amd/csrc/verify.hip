@@ -983,189 +983,6 @@ __global__ __launch_bounds__(256) void verify_kernel(VerifyParams p) {
   }
 }
 
-// ---------------------------------------------------------------------------
-// Triage (long candidate streams: the 1-byte atoms of regexp / hex sets give a
-// candidate every ~128 bytes).  Most of their calls are decided by a guard,
-// whose bytes come straight from three aligned 8-byte loads -- no LDS window,
-// no program staging -- so one kernel without LDS decides those lists at full
-// occupancy and hands the few others to verify_heavy_kernel.
-// ---------------------------------------------------------------------------
-// guard_ok without a staged window: true when the region is not all inside
-// the bytes present (the full decision then runs).
-__device__ __forceinline__ bool guard_direct(const VerifyParams& p, uint64_t offset, bool backwards,
-                                             uint32_t bs, DevGuard g) {
-  const uint32_t base = bs & 15u, span = bs >> 4, L = base + span + 4;
-  if (backwards ? offset < L : p.size - offset < L) return true;
-  const uint64_t r0 = backwards ? offset - L : offset + base;   // region: span + 4 <= 12 bytes
-  const uint64_t a8 = r0 & ~7ull;
-  if (a8 < p.win_lo || a8 + 24 > p.win_hi) return true;
-  const uint2* q = reinterpret_cast<const uint2*>(p.data + a8);
-  const uint2 q0 = q[0], q1 = q[1], q2 = q[2];
-  const uint32_t sh = (uint32_t)(r0 - a8), k = sh >> 2, bsh = sh & 3u;
-  const uint32_t B0 = k ? q0.y : q0.x, B1 = k ? q1.x : q0.y, B2 = k ? q1.y : q1.x;
-  const uint32_t B3 = k ? q2.x : q1.y;
-  const uint32_t W[3] = {__builtin_amdgcn_alignbyte(B1, B0, bsh),
-                         __builtin_amdgcn_alignbyte(B2, B1, bsh),
-                         __builtin_amdgcn_alignbyte(B3, B2, bsh)};
-  bool hit = false;
-#pragma unroll
-  for (uint32_t t = 0; t <= 8; ++t) {
-    const uint32_t r = (t & 3) == 0 ? W[t >> 2]
-                                    : __builtin_amdgcn_alignbyte(W[(t >> 2) + 1], W[t >> 2], t & 3);
-    hit |= t <= span && (r & g.m) == g.v;
-  }
-  return hit;
-}
-
-// The 16 bytes at base + off, from three aligned 8-byte loads at the 8-byte
-// boundary below (24 bytes from there must be readable).
-__device__ __forceinline__ uint4 bytes16(const uint8_t* base, uint64_t off) {
-  const uint64_t a8 = off & ~7ull;
-  const uint2* q = reinterpret_cast<const uint2*>(base + a8);
-  const uint2 q0 = q[0], q1 = q[1], q2 = q[2];
-  const uint32_t sh = (uint32_t)(off - a8), k = sh >> 2, bsh = sh & 3u;
-  const uint32_t B0 = k ? q0.y : q0.x, B1 = k ? q1.x : q0.y, B2 = k ? q1.y : q1.x;
-  const uint32_t B3 = k ? q2.x : q1.y, B4 = k ? q2.y : q2.x;
-  return make_uint4(__builtin_amdgcn_alignbyte(B1, B0, bsh), __builtin_amdgcn_alignbyte(B2, B1, bsh),
-                    __builtin_amdgcn_alignbyte(B3, B2, bsh), __builtin_amdgcn_alignbyte(B4, B3, bsh));
-}
-
-// A plain ascii literal of up to 16 bytes (no wide / nocase / xor form), as
-// call_matters decides it (cmp_ascii, then the FULL_WORD test), with the
-// compared bytes from bytes16; 2 where the 24 bytes are not all present.
-__device__ __forceinline__ uint32_t triage_literal(const VerifyParams& p, const DevPoolRec& e,
-                                                   uint64_t offset) {
-  const uint32_t n = e.length;
-  if ((e.flags & (kStrWide | kStrNoCase | kStrXor)) || !(e.flags & kStrAscii) || n == 0 || n > 16)
-    return 2;
-  if (p.size - offset < n) return 0;   // cmp_ascii: avail < n, and no other form
-  const uint64_t a8 = offset & ~7ull;
-  if (a8 < p.win_lo || a8 + 24 > p.win_hi) return 2;
-  const uint4 D = bytes16(p.data, offset);
-  const uint4 S = bytes16(p.str_bytes, e.bytes_off);
-  auto m = [n](uint32_t d) {   // the compared bytes of dword d
-    return n >= 4 * d + 4 ? 0xFFFFFFFFu : n <= 4 * d ? 0u : (1u << (8 * (n - 4 * d))) - 1u;
-  };
-  const uint32_t diff = ((D.x ^ S.x) & m(0)) | ((D.y ^ S.y) & m(1)) | ((D.z ^ S.z) & m(2)) |
-                        ((D.w ^ S.w) & m(3));
-  if (diff != 0) return 0;   // scan.c:974-975
-  if (!(e.flags & kStrFullWord)) return 1;
-  auto alnum = [](uint8_t c) {
-    return (c >= 0x30 && c <= 0x39) || (c >= 0x41 && c <= 0x5a) || (c >= 0x61 && c <= 0x7a);
-  };
-  if (offset >= 1 && alnum(p.data[offset - 1])) return 0;   // scan.c:672-694
-  if (offset + n < p.size && alnum(p.data[offset + n])) return 0;
-  return 1;
-}
-
-// One call of the triage: 0 = no effect, 1 = kept, 2 = needs call_matters.
-// Each 0 / 1 is call_matters' own answer (its early returns and guard tests,
-// in its order).
-__device__ __forceinline__ uint32_t triage_call(const VerifyParams& p, const DevPoolRec& e,
-                                                uint64_t i) {
-  const uint32_t bt = e.backtrack;
-  if (bt > i) return 0;   // scanner.c:107: not called
-  const uint64_t offset = i - bt;
-  if (offset >= p.size) return 0;
-  if ((e.flags & kStrFixedOffset) && e.fixed_offset != (int64_t)(p.data_base + offset)) return 0;
-  if ((e.flags & (kStrLiteral | kStrFitsInAtom)) == (kStrLiteral | kStrFitsInAtom) &&
-      !(e.flags & (kStrUnmodelled | kStrFullWord)))
-    return bt != 0 ? 1u : 0u;
-  if (p.win_lo != 0 || p.win_hi != p.size) {
-    const uint64_t need_lo = offset - min<uint64_t>(offset, (uint64_t)kReScanLimit);
-    const uint64_t need_hi =
-        min<uint64_t>(p.size, offset + max<uint64_t>((uint64_t)kReScanLimit, 2ull * e.length + 2));
-    if (need_lo < p.win_lo || need_hi > p.win_hi) return 1;
-  }
-  if (e.flags & kStrLiteral) return (e.flags & kStrUnmodelled) ? 1u : triage_literal(p, e, offset);
-  if (!p.re_on || e.re.fwd_len == 0) return 1;
-  const bool has_bwd = e.re.bwd_len > 0;
-  if (e.flags & kStrFastRegexp) {
-    if (!(e.flags & kStrAscii) || (e.flags & (kStrWide | kStrBase64Any))) return 1;
-  } else {
-    // yr_re_exec strings: a wide attempt is never ruled out here
-    if ((e.flags & kStrWide) && !(e.flags & kStrBase64Any)) return 2;
-    if (!(e.flags & (kStrAscii | kStrBase64Any))) return 0;   // no attempt runs
-  }
-  // the ascii attempt: dead if either direction's guard fails
-  if (e.fguard.m != 0 && !guard_direct(p, offset, false, e.fguard_bs, e.fguard)) return 0;
-  if (has_bwd && e.bguard.m != 0 && !guard_direct(p, offset, true, e.bguard_bs, e.bguard)) return 0;
-  return 2;
-}
-
-// One candidate of the triage: true = its list needs the full decision
-// (nothing written); else keep / counts / heads as verify_one<0> writes them
-// and its record count in n.
-__device__ __forceinline__ bool triage_one(const VerifyParams& p, uint64_t c, uint32_t& n) {
-  const uint64_t i = p.all ? p.all_first + c : p.positions[c];
-  Near near;
-  const uint32_t head = node_head(p, i, near);
-  uint32_t t = 0, mask = 0;
-  n = 0;
-  for (uint32_t k = head; k != 0; ++t) {
-    const DevPoolRec e = p.pool[k - 1];
-    const uint32_t d = triage_call(p, e, i);
-    k = e.next;
-    if (d == 2) return true;
-    if (d == 1) {
-      if (t < 31) mask |= 1u << t;
-      ++n;
-    }
-  }
-  p.keep[c] = n == 0 ? 0u : (t > 31 ? kKeepOverflow : mask);
-  if (n != 0) {
-    p.counts[c] = n;
-    p.heads[c] = head;
-  }
-  return false;
-}
-
-// Persistent waves over the groups: each group's triaged record count into
-// block_off; the undecided candidates onto the heavy list (one atomic per wave).
-__global__ __launch_bounds__(256) void verify_triage_kernel(VerifyParams p) {
-  const uint64_t groups = (p.count + kGroup - 1) / kGroup;
-  const uint32_t lane = threadIdx.x & 63u;
-  const uint64_t waves = (uint64_t)gridDim.x * (blockDim.x / 64);
-  for (uint64_t g = (uint64_t)blockIdx.x * (blockDim.x / 64) + wave_in_block(); g < groups;
-       g += waves) {
-    const uint64_t c = g * kGroup + lane;
-    uint32_t n = 0;
-    bool heavy = false;
-    if (c < p.count) heavy = triage_one(p, c, n);
-    const uint64_t hm = __ballot(heavy);
-    if (hm != 0) {
-      const uint32_t leader = (uint32_t)__builtin_ctzll(hm);
-      uint32_t at = 0;
-      if (lane == leader) at = atomicAdd(p.heavy_n, (uint32_t)__popcll(hm));
-      at = __shfl(at, (int)leader, 64);
-      if (heavy)
-        p.heavy[at + __builtin_amdgcn_mbcnt_hi((uint32_t)(hm >> 32),
-                                               __builtin_amdgcn_mbcnt_lo((uint32_t)hm, 0u))] =
-            (uint32_t)c;
-    }
-    const uint32_t sum = wave_sum(heavy ? 0u : n);
-    if (lane == 0) p.block_off[g] = sum;
-  }
-}
-
-// The heavy list, decided as verify_kernel<0> decides (staged windows, regexp
-// search); each record count is added to its group's.
-__global__ __launch_bounds__(256) void verify_heavy_kernel(VerifyParams p) {
-  __shared__ __attribute__((aligned(16))) uint8_t win[256 * kWinBytes];
-  __shared__ __attribute__((aligned(16))) uint8_t code[256 * kCodeBytes];
-  const uint32_t lds = (uint32_t)(uintptr_t)(win + threadIdx.x * kWinBytes);
-  const uint32_t codebuf = (uint32_t)(uintptr_t)(code + threadIdx.x * kCodeBytes);
-  const uint32_t nh = *p.heavy_n;
-  for (uint64_t h = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; h < nh;
-       h += (uint64_t)gridDim.x * blockDim.x) {
-    const uint32_t c = p.heavy[h];
-    uint32_t n = 0;
-    verify_one<0>(p, c, lds, codebuf, 0, 0, 0, n);
-    if (n != 0) atomicAdd(reinterpret_cast<unsigned long long*>(p.block_off + c / kGroup),
-                          (unsigned long long)n);
-  }
-}
-
 // Offsets, step 1: one 1024-thread block per chunk of kChunkGroups groups --
 // the chunk's exclusive scan in place (entry `groups`, past the last group,
 // counts 0) and its total into chunk_off[chunk].
@@ -1251,18 +1068,6 @@ hipError_t launch_verify(const VerifyParams& p, int pass, hipStream_t s) {
         (waves + 3) / 4, resident_blocks((const void*)verify_kernel<1>));
     hipLaunchKernelGGL(verify_kernel<1>, dim3(blocks), dim3(256), 0, s, p);
   }
-  return hipGetLastError();
-}
-
-hipError_t launch_verify_triage(const VerifyParams& p, hipStream_t s) {
-  if (p.count == 0) return hipSuccess;
-  const uint64_t waves = verify_groups(p.count);
-  const uint32_t tb = (uint32_t)std::min<uint64_t>(
-      (waves + 3) / 4, resident_blocks((const void*)verify_triage_kernel));
-  hipLaunchKernelGGL(verify_triage_kernel, dim3(tb), dim3(256), 0, s, p);
-  const uint32_t hb = (uint32_t)std::min<uint64_t>(
-      (p.count + 255) / 256, resident_blocks((const void*)verify_heavy_kernel));
-  hipLaunchKernelGGL(verify_heavy_kernel, dim3(hb), dim3(256), 0, s, p);
   return hipGetLastError();
 }
 
