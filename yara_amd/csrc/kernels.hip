@@ -261,8 +261,11 @@ __device__ __forceinline__ void flush_pending(const ScanParams& p, WaveQueue& q,
 // store, or a dropped one.
 __device__ __forceinline__ void store_slot(const ScanParams& p, WaveQueue& q, uint32_t* out) {
 #if YAMD_STORE_SLOT
-  const __amdgpu_buffer_rsrc_t r =
-      __builtin_amdgcn_make_buffer_rsrc(out, (short)0, (int)(p.seg_cap * 4u), 0x00020000);
+  // (num_records <= kNoStore, so kNoStore is out of range even for the exact-size
+  // rerun's unlimited capacity)
+  const uint64_t bytes = 4ull * p.seg_cap;
+  const __amdgpu_buffer_rsrc_t r = __builtin_amdgcn_make_buffer_rsrc(
+      out, (short)0, (int)(bytes < kNoStore ? bytes : kNoStore), 0x00020000);
   __builtin_amdgcn_raw_buffer_store_b32(q.so_val, r, q.so_off, 0, 0);
   q.so_off = kNoStore;
   q.so_pending = false;
