@@ -375,6 +375,33 @@ def test_byte_key_sets_dense_and_mixed():
                 np.testing.assert_array_equal(got, oracle.candidates(ref_t, d), err_msg=(rules, n))
 
 
+@pytest.mark.slow
+def test_verify_refuses_more_than_2_32_candidates():
+    """yr_amd_verify_device refuses a candidate stream longer than
+    YR_AMD_VERIFY_MAX_CANDIDATES (2^32: records carry 32-bit candidate indices)
+    before allocating anything, and the libyara shim replays such blocks on the
+    host instead (integration/yr_gpu_scanner.c, the same limit).  A zero-filled
+    block of 2^32 + 16 bytes under a rule set with the 1-byte key 00 makes
+    every position a candidate: the scan gives all 2^32 + 16 of them, the
+    pre-verification returns INVALID_ARGUMENT, and the scanner stays usable."""
+    torch = _torch()
+    n = (1 << 32) + 16
+    if torch.cuda.mem_get_info()[0] < 80 << 30:
+        pytest.skip("needs ~80 GiB of free HBM (positions of 2^32 candidates)")
+    d = torch.zeros(n + 16, dtype=torch.uint8, device="cuda")
+    sc = yara_amd.Scanner(yara_amd.Tables.from_npz(tables_npz("bytekeys"), device=0, strings=True))
+    sc.scan_device(d.data_ptr(), n)
+    ptr, cnt, allp = sc.device_result()
+    assert not allp and cnt == n
+    with pytest.raises(yara_amd.YaraAmdError) as e:
+        sc.verify_device(0)
+    assert e.value.code == yara_amd.INVALID_ARGUMENT
+    del d
+    torch.cuda.empty_cache()
+    small = oracle.xorshift(1 << 20, 3)
+    assert len(sc.verify_calls(small)) > 0
+
+
 def test_block_larger_than_4gib():
     """A single 8 GiB block (past 32-bit byte offsets: 8,192 segments, positions
     above 2^32): its candidates up to 4 GiB equal the golden C_4G stream (the

@@ -178,21 +178,7 @@ struct WaveQueue {
   // loads (0 = none), the loaded word
   uint32_t wa, oa, ia, da;
   uint32_t wb, ob, ib, db;
-  // (YAMD_STORE_SLOT) the last flush's output store, per lane: byte offset in
-  // the segment's output (kNoStore: none) and value; issued at the tile step's
-  // fixed store point (store_slot)
-  uint32_t so_off, so_val;
-  bool so_pending;  // wave-uniform
 };
-// Output stores at one fixed point of every tile step (one buffer store per
-// tile, lanes without data out of the buffer's range, so the hardware drops
-// them): the wait for the next input tile then never waits for a store
-// (gfx950 counts loads and stores in one vmcnt, in order; a store issued on
-// some paths only makes the compiler's merged wait cover it).
-#ifndef YAMD_STORE_SLOT
-#define YAMD_STORE_SLOT 0
-#endif
-constexpr uint32_t kNoStore = 0x7FFFFFF0u;
 constexpr uint32_t kNoHit = 0xFFFFFFFFu;
 // Kernel variant: the product kernel for rule sets whose 1-byte keys are tested
 // byte by byte in stage 1 (byte_keys_any below) instead of in the filter.
@@ -239,37 +225,13 @@ __device__ __forceinline__ void flush_pending(const ScanParams& p, WaveQueue& q,
     keep = MODE == 12 ? true : exact_check(e.x, seg_start + off + 1, p);   // 12: ablation
   }
   const uint64_t b = __ballot(keep);
-#if YAMD_STORE_SLOT
-  if (q.so_pending && q.so_off != kNoStore) out[q.so_off / 4] = q.so_val;   // (a second flush in one step)
-  const uint32_t idx = found + __builtin_amdgcn_mbcnt_hi((uint32_t)(b >> 32),
-                                                         __builtin_amdgcn_mbcnt_lo((uint32_t)b, 0u));
-  q.so_off = keep && idx < p.seg_cap ? idx * 4u : kNoStore;
-  q.so_val = off;
-  q.so_pending = true;
-#else
   if (keep) {
     const uint32_t idx = found + __builtin_amdgcn_mbcnt_hi((uint32_t)(b >> 32),
                                                            __builtin_amdgcn_mbcnt_lo((uint32_t)b, 0u));
     if (idx < p.seg_cap) out[idx] = off;
   }
-#endif
   found += (uint32_t)__popcll(b);
   q.pend_n = 0;
-}
-
-// The fixed store point of a tile step (YAMD_STORE_SLOT): the pending output
-// store, or a dropped one.
-__device__ __forceinline__ void store_slot(const ScanParams& p, WaveQueue& q, uint32_t* out) {
-#if YAMD_STORE_SLOT
-  // (num_records <= kNoStore, so kNoStore is out of range even for the exact-size
-  // rerun's unlimited capacity)
-  const uint64_t bytes = 4ull * p.seg_cap;
-  const __amdgpu_buffer_rsrc_t r = __builtin_amdgcn_make_buffer_rsrc(
-      out, (short)0, (int)(bytes < kNoStore ? bytes : kNoStore), 0x00020000);
-  __builtin_amdgcn_raw_buffer_store_b32(q.so_val, r, q.so_off, 0, 0);
-  q.so_off = kNoStore;
-  q.so_pending = false;
-#endif
 }
 
 // Append hits (bit j of `keep` = lane byte j at segment offset off0 + j) to
@@ -791,7 +753,6 @@ __device__ __forceinline__ void tile_step(const ScanParams& p, WaveQueue& q, Seg
     if (q.defer) drain_complete<MODE>(p, q, lane, st.seg_start, st.out, st.found);
   ring_append<MODE, TAIL>(p, q, st, S, any, tile_off, lane);
   issue_first_level<MODE>(p, q);
-  store_slot(p, q, st.out);
 }
 
 // Stream one segment [seg_start, seg_start + seg_len) of the block: full tiles
@@ -838,9 +799,6 @@ __device__ __forceinline__ void scan_segment(const ScanParams& p, WaveQueue& q, 
   q.da = q.db = 0u;
   q.wa = q.wb = 0u;
   q.oa = q.ob = kNoHit;
-  q.so_off = kNoStore;
-  q.so_val = 0u;
-  q.so_pending = false;
 
   const uint32_t n_full = st.seg_len / kTile;            // tiles needing no mask / bounds
   if (n_full > 0) {
@@ -870,9 +828,6 @@ __device__ __forceinline__ void scan_segment(const ScanParams& p, WaveQueue& q, 
   if constexpr (kDeferFl<MODE>)
     if (q.defer) drain_complete<MODE>(p, q, lane, st.seg_start, st.out, st.found);
   if (q.pend_n != 0) flush_pending<MODE>(p, q, lane, st.seg_start, st.out, st.found);
-#if YAMD_STORE_SLOT
-  if (q.so_pending && q.so_off != kNoStore) st.out[q.so_off / 4] = q.so_val;
-#endif
   if (lane == 0) p.seg_count[seg] = st.found;
 }
 
