@@ -954,18 +954,8 @@ __device__ __forceinline__ uint32_t wave_in_block() {
 // PASS 1: persistent waves over the groups: a group without records reads
 // nothing more (most groups of a dense rule set); the others scan their
 // candidates' counts and write the records from the group's offset on.
-// Build switch YAMD_VERIFY_WAVES=N: ask the register allocator for N waves per
-// SIMD (the kernels' 84-93 VGPRs allow 5; the LDS, 24.6 KB a block, allows 6).
-#ifndef YAMD_VERIFY_WAVES
-#define YAMD_VERIFY_WAVES 0
-#endif
-#if YAMD_VERIFY_WAVES
-#define YAMD_VERIFY_OCC __attribute__((amdgpu_waves_per_eu(YAMD_VERIFY_WAVES, 8)))
-#else
-#define YAMD_VERIFY_OCC
-#endif
 template <int PASS>
-__global__ __launch_bounds__(256) YAMD_VERIFY_OCC void verify_kernel(VerifyParams p) {
+__global__ __launch_bounds__(256) void verify_kernel(VerifyParams p) {
   __shared__ __attribute__((aligned(16))) uint8_t win[256 * kWinBytes];
   __shared__ __attribute__((aligned(16))) uint8_t code[256 * kCodeBytes];
   // (the low 32 bits of a flat LDS address are the LDS offset)
