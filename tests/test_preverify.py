@@ -214,3 +214,35 @@ def test_profiling_count_only_records(case):
     assert np.array_equal(r["offset"], off[want])
     assert np.array_equal(r["pool_index"] & 0x7FFFFFFF, idx[want])
     assert np.array_equal(co, ~keep[want])
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("tail", [0, 1, 2, 5, 15, 16, 17, 1000])
+def test_scan_side_guard_flags(tail):
+    """1-byte keys whose list is one regexp call decided by its forward guard
+    (rx's `[` and `]`: the guard tests the key and the next byte, C3) are
+    decided in the scan kernel's drain (kernels.hip key_dead) and skipped by the
+    count pass.  Random bytes with `[` / `]` planted at every lane byte, half of
+    them followed by C3 (the guard passes, the call is searched), and the block
+    cut `tail` bytes after a planted key (regions past the block end are never
+    flagged): the device records equal the oracle's kept calls."""
+    import yara_amd
+    from conftest import ref_tables
+    z = np.load(tables_npz("rx"))
+    n = (1 << 20) + 77
+    data = oracle.xorshift(n, 61).copy()
+    k = 0
+    for off in range(5, n - 64, 37):
+        data[off] = (0x5B, 0x5D)[k & 1]
+        if k % 2 == 0:
+            data[off + 1] = 0xC3
+        k += 1
+    cut = (n - 200) + tail
+    data[n - 200] = 0x5B
+    data = np.ascontiguousarray(data[:cut])
+    P, K = oracle.walk_verify(ref_tables("rx"), data)
+    keep = oracle.literal_effect(z, P, K, data)
+    r = yara_amd.Scanner(yara_amd.Tables.from_npz(tables_npz("rx"), device=0, strings=True)).verify_calls(data)
+    off = P.astype(np.uint64) - z["pool_backtrack"][K].astype(np.uint64)
+    np.testing.assert_array_equal(r["offset"], off[keep])
+    np.testing.assert_array_equal(r["pool_index"], K[keep])

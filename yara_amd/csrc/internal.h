@@ -163,6 +163,12 @@ constexpr uint32_t kNodeL2 = 256;
 constexpr uint32_t kNodeZero4 = 256 + 65536;
 constexpr uint32_t kNodeHeadWords = kNodeZero4 + 4;   // (keeps the buckets 16-B aligned)
 
+// Bits of the candidate outputs: a segment output entry with kDeadOut is a
+// certain candidate whose calls the drain proved dead (its flag goes to
+// ScanParams::dead); a pending entry's offset carries it as kPendDead.
+constexpr uint32_t kDeadOut = 0x80000000u;
+constexpr uint32_t kPendDead = 0x40000000u;
+
 struct ScanParams {
   const uint8_t* data;      // block base in HBM (16-byte aligned)
   uint64_t block_size;      // bytes in the block
@@ -183,6 +189,13 @@ struct ScanParams {
                             // seg_out + seg_base[s] (exact-size rerun after an overflow)
   uint32_t byte_keys;       // FlatTables::byte_keys / n_byte_keys (stage-1 byte test)
   uint32_t n_byte_keys;
+  // Per 1-byte key k: the guard that decides every call of the key's match
+  // list from the bytes next to it (scanner.cpp key_dead_guards): m, v and info
+  // = valid | region start relative to the key byte (int8) << 8 | span << 16 |
+  // region end relative to the position (int8) << 24; info 0 = none
+  uint32_t kd_m[4], kd_v[4], kd_info[4];
+  uint8_t* dead;            // null, or per output candidate 1 = no call of its list can
+                            // have an effect (written by the compaction)
   uint32_t filter_mode;     // kFilterPair / kFilterEven / kFilterEvenHash (FlatTables)
   uint32_t* seg_next;       // null: wave w takes segments w, w + waves, ...; else each wave
                             // takes its first segment by index and the next ones from this

@@ -215,10 +215,11 @@ __device__ __forceinline__ void flush_pending(const ScanParams& p, WaveQueue& q,
     u32x2 e = {0u, 0u};
     if (lane < q.pend_n) e = lds_load<u32x2>(q.pend + 8 * lane);
     const bool conf = (e.y & kConfirmed) != 0u;
-    off = e.y & ~kConfirmed;
+    off = e.y & ~(kConfirmed | kPendDead);
     const bool probe = lane < q.pend_n && !conf;
     keep = lane < q.pend_n && conf;
     if (__ballot(probe) != 0 && probe) keep = exact_check(e.x, seg_start + off + 1, p);
+    if (e.y & kPendDead) off |= kDeadOut;   // (a certain candidate: kept either way)
   } else if (lane < q.pend_n) {
     const u32x2 e = lds_load<u32x2>(q.pend + 8 * lane);
     off = e.y;
@@ -343,6 +344,32 @@ constexpr bool kDeferFl =
     YAMD_DEFER_FL &&
     (MODE == 0 || MODE == 12 || MODE == kModeByteKeys || kEven<MODE> || kByteKeyAblation<MODE>);
 
+// Does some call of a certain candidate's list possibly have an effect?  For a
+// 1-byte key whose list is decided by one guard on the bytes right after it
+// (ScanParams::kd_*, scanner.cpp key_dead_guards), the drain tests that guard
+// on the ring entry (lane byte j is the key): false only if the guard's whole
+// region lies in the entry and inside the block and no shift passes -- then
+// pre-verification skips the candidate without reading the input.
+__device__ __forceinline__ bool key_dead(const ScanParams& p, uint32_t ent, uint32_t j, uint32_t key,
+                                         uint64_t pos) {
+  uint32_t info = 0, m = 0, v = 0;
+#pragma unroll
+  for (uint32_t k = 0; k < kMaxByteKeys; ++k) {
+    const bool is = k < p.n_byte_keys && key == ((p.byte_keys >> (8 * k)) & 0xFFu);
+    info = is ? p.kd_info[k] : info;
+    m = is ? p.kd_m[k] : m;
+    v = is ? p.kd_v[k] : v;
+  }
+  if (!(info & 1u)) return false;
+  const int32_t rs = (int32_t)j + (int32_t)(int8_t)(info >> 8);
+  const uint32_t span = (info >> 16) & 15u;
+  const int64_t end = (int64_t)pos + (int8_t)(info >> 24);
+  if (rs < 0 || rs + (int32_t)span + 4 > kBytesPerLane || end > (int64_t)p.block_size) return false;
+  bool hit = false;
+  for (uint32_t jj = 0; jj <= span; ++jj) hit |= (window4(ent, (uint32_t)rs + jj + 3) & m) == v;
+  return !hit;
+}
+
 // Consume a deferred drain's first-level words: the lanes' hits that pass go,
 // in order, to the pending list.
 template <int MODE>
@@ -466,8 +493,15 @@ __device__ __forceinline__ void drain(const ScanParams& p, WaveQueue& q, uint32_
     while (maybe != 0u && idx < base + kWave) {
       const uint32_t j = (uint32_t)__builtin_ctz(maybe);
       maybe &= maybe - 1;
-      lds_store2(q.pend + 8 * (idx - base), window4(ent, j),
-                 (off0 + j) | (MODE == kModeByteKeys && ((kmask >> j) & 1u) ? kConfirmed : 0u));
+      const uint32_t w = window4(ent, j);
+      uint32_t y = off0 + j;
+      if constexpr (MODE == kModeByteKeys) {
+        if ((kmask >> j) & 1u) {
+          y |= kConfirmed;
+          if (p.dead != nullptr && key_dead(p, ent, j, w >> 24, seg_start + off0 + j + 1)) y |= kPendDead;
+        }
+      }
+      lds_store2(q.pend + 8 * (idx - base), w, y);
       ++idx;
     }
     if (end <= base + kWave) {
@@ -927,7 +961,8 @@ __global__ __launch_bounds__(256) void seg_scatter_kernel(const uint32_t* seg_co
                                                           const uint64_t* seg_base,
                                                           const uint64_t* seg_offset, uint32_t cap,
                                                           uint64_t byte_begin, uint32_t seg_bytes,
-                                                          uint32_t n_segments, uint64_t* positions) {
+                                                          uint32_t n_segments, uint64_t* positions,
+                                                          uint8_t* dead) {
   // one wave per segment (segments hold tens to hundreds of candidates)
   const uint32_t seg = blockIdx.x * (blockDim.x / kWave) + threadIdx.x / kWave;
   if (seg >= n_segments) return;
@@ -935,7 +970,11 @@ __global__ __launch_bounds__(256) void seg_scatter_kernel(const uint32_t* seg_co
   const uint64_t base = byte_begin + (uint64_t)seg * seg_bytes + 1;  // position = byte + 1
   const uint32_t* src = seg_out + (seg_base ? seg_base[seg] : (size_t)seg * cap);
   uint64_t* dst = positions + seg_offset[seg];
-  for (uint32_t i = threadIdx.x % kWave; i < c; i += kWave) dst[i] = base + src[i];
+  for (uint32_t i = threadIdx.x % kWave; i < c; i += kWave) {
+    const uint32_t e = src[i];
+    dst[i] = base + (e & ~kDeadOut);
+    if (dead != nullptr) dead[seg_offset[seg] + i] = (uint8_t)(e >> 31);
+  }
 }
 
 // ---------------------------------------------------------------------------
@@ -1023,7 +1062,7 @@ hipError_t launch_compact(const ScanParams& p, uint64_t* seg_offset, uint64_t* s
   } else {
     hipLaunchKernelGGL(seg_scatter_kernel, dim3((p.n_segments + 3) / 4), dim3(256), 0, s,
                        p.seg_count, p.seg_out, p.seg_base, seg_offset, p.seg_cap, p.byte_begin,
-                       p.seg_bytes, p.n_segments, positions);
+                       p.seg_bytes, p.n_segments, positions, p.dead);
   }
   return hipGetLastError();
 }

@@ -86,6 +86,9 @@ struct yr_amd_tables {
   // on-device literal pre-verification (yr_amd_tables_set_strings)
   bool has_strings = false;
   bool profile = false;               // yr_amd_tables_set_profiling
+  // per 1-byte key: the guard that decides its list in the scan (ScanParams kd_*)
+  uint32_t kd_m[4] = {0, 0, 0, 0}, kd_v[4] = {0, 0, 0, 0}, kd_info[4] = {0, 0, 0, 0};
+  bool kd_any = false;
   uint32_t* d_nodes = nullptr;        // accepting nodes by string (FlatTables::nodes)
   DevPoolRec* d_pool = nullptr;       // per pool entry: link, backtrack, string, programs
   uint8_t* d_str_bytes = nullptr;
@@ -109,6 +112,8 @@ struct yr_amd_scanner {
   uint32_t* d_seg_out = nullptr;
   size_t seg_out_cap = 0;               // entries
   uint64_t* d_positions = nullptr;
+  uint8_t* d_dead = nullptr;            // per candidate: the scan proved its calls dead
+  size_t dead_cap = 0;
   size_t positions_cap = 0;             // entries
   uint64_t* h_summary = nullptr;        // pinned, coherent: {total, max per segment}
   uint64_t* d_hsum = nullptr;           // h_summary mapped for the device: the offsets
@@ -230,9 +235,11 @@ int run_scan(yr_amd_scanner* s) {
   // output is sized for the clipped worst case (every segment at capacity),
   // so the host synchronises once, in yr_amd_scan_device_result
   const ScanParams& p = s->last;
-  int r = grow(s->d_positions, s->positions_cap,
-               p.seg_base ? s->rerun_total : (size_t)p.n_segments * p.seg_cap);
+  const size_t out_cap = p.seg_base ? s->rerun_total : (size_t)p.n_segments * p.seg_cap;
+  int r = grow(s->d_positions, s->positions_cap, out_cap);
+  if (!r && s->tables->kd_any) r = grow(s->d_dead, s->dead_cap, out_cap);
   if (r) return r;
+  s->last.dead = s->tables->kd_any ? s->d_dead : nullptr;
   if (s->timing) HIP_TRY(hipEventRecord(s->ev_begin, s->stream));
   HIP_TRY(launch_scan(p, s->last_grid, s->stream, s->diag_mode));
   if (s->timing) {
@@ -371,7 +378,8 @@ int yr_amd_scanner_destroy(yr_amd_scanner* s) {
   if (s->stream) (void)hipStreamSynchronize(s->stream);
   for (void* p : {(void*)s->d_block, (void*)s->d_seg_count,
                   (void*)s->d_seg_offset,
-                  (void*)s->d_seg_out, (void*)s->d_positions, (void*)s->d_summary,
+                  (void*)s->d_seg_out, (void*)s->d_positions, (void*)s->d_dead,
+                  (void*)s->d_summary,
                   (void*)s->d_vcount, (void*)s->d_vkeep, (void*)s->d_vblock, (void*)s->d_vrec,
                   (void*)s->d_vchunk, (void*)s->d_seg_base,
                   (void*)s->d_seg_next})
@@ -449,6 +457,7 @@ int yr_amd_scan_window(yr_amd_scanner* s, const uint8_t* d_window, uint64_t wind
   s->last.byte_end = byte_end;
   s->last_all = t->flat.root_accepting;
   s->last_empty = s->last_all || byte_end == byte_begin;
+  s->last.dead = nullptr;
   if (s->last_empty) return YR_AMD_SUCCESS;
   if (d_window == nullptr) return YR_AMD_INVALID_ARGUMENT;
   HIP_TRY(hipSetDevice(t->device));
@@ -488,6 +497,11 @@ int yr_amd_scan_window(yr_amd_scanner* s, const uint8_t* d_window, uint64_t wind
   p.len_mask = t->flat.len_mask;
   p.byte_keys = t->flat.byte_keys;
   p.n_byte_keys = t->flat.n_byte_keys;
+  for (int k = 0; k < 4; ++k) {
+    p.kd_m[k] = t->kd_m[k];
+    p.kd_v[k] = t->kd_v[k];
+    p.kd_info[k] = t->kd_info[k];
+  }
   p.filter_mode = t->flat.filter_mode;
   p.n_segments = n_segments;
   p.seg_bytes = seg_bytes;
@@ -804,6 +818,47 @@ bool general_guard(const uint8_t* c, uint32_t len, uint32_t skip, bool backwards
 }
 }  // namespace
 
+namespace {
+// The 1-byte keys whose calls the scan kernel can decide (kernels.hip
+// key_dead): the key's state is always its own node (no trie node of depth >= 2
+// ends with it, so no longer suffix is a state), its list is one regexp call,
+// and that call is dropped by call_matters whenever its forward guard fails
+// (re_call_matters: a FAST ascii program, or a yr_re_exec one with only the
+// ascii attempt).  The drain tests the guard when its region lies in the
+// key's lane; the count pass then skips the candidate.  (YR_AC_MATCH offsets:
+// the call's offset is position - backtrack, the guard's region starts `base`
+// bytes after it.)
+void key_dead_guards(yr_amd_tables* t) {
+  const FlatTables& f = t->flat;
+  t->kd_any = false;
+  for (int k = 0; k < 4; ++k) t->kd_m[k] = t->kd_v[k] = t->kd_info[k] = 0;
+  if (f.root_accepting || t->h_pool.empty() || diag_env("YAMD_NO_KEY_DEAD") != nullptr) return;
+  for (uint32_t k = 0; k < f.n_byte_keys && k < 4; ++k) {
+    const uint32_t b = (f.byte_keys >> (8 * k)) & 0xFFu;
+    if ((f.deep_last[b >> 5] >> (b & 31)) & 1u) continue;
+    const uint32_t head = f.nodes[kNodeL1 + b];
+    if (head == 0 || head > t->h_pool.size()) continue;
+    const DevPoolRec& e = t->h_pool[head - 1];
+    const uint32_t fl = e.flags;
+    if (e.next != 0 || (fl & kStrLiteral) || e.re.fwd_len == 0 || e.fguard.m == 0) continue;
+    if (fl & kStrFastRegexp) {
+      if (!(fl & kStrAscii) || (fl & (kStrWide | kStrBase64Any))) continue;
+    } else if (((fl & kStrWide) && !(fl & kStrBase64Any)) || !(fl & (kStrAscii | kStrBase64Any))) {
+      continue;
+    }
+    const int base = e.fguard_bs & 15, span = e.fguard_bs >> 4;
+    const int rs = base + 1 - (int)e.backtrack;          // region start - key byte
+    const int end = base + span + 4 - (int)e.backtrack;  // region end - position
+    if (rs < -128 || rs > 127 || end < -128 || end > 127) continue;
+    t->kd_m[k] = e.fguard.m;
+    t->kd_v[k] = e.fguard.v;
+    t->kd_info[k] = 1u | ((uint32_t)(uint8_t)(int8_t)rs << 8) | ((uint32_t)span << 16) |
+                    ((uint32_t)(uint8_t)(int8_t)end << 24);
+    t->kd_any = true;
+  }
+}
+}  // namespace
+
 // Not declared in include/yara_amd.h: the guard compiler on one program, for
 // the CPU tests (tests/test_guards.py).  Returns 1 and the guard (verify.h
 // DevGuard: m, v, base | span << 4) if the program has one, else 0.
@@ -887,6 +942,7 @@ int yr_amd_tables_set_re_code(yr_amd_tables* t, uint32_t n_pool, const uint32_t*
   if (n_pool > 0 && hipMemcpy(t->d_pool, t->h_pool.data(), n_pool * sizeof(DevPoolRec),
                               hipMemcpyHostToDevice) != hipSuccess)
     return YR_AMD_INTERNAL_FATAL_ERROR;
+  key_dead_guards(t);
   return YR_AMD_SUCCESS;
 }
 
@@ -911,6 +967,8 @@ int yr_amd_verify_device(yr_amd_scanner* s, uint64_t data_base, const yr_amd_ver
   } else {
     v.positions = s->d_positions;
     v.count = s->last_count;
+    // (profiling needs every call past the early returns: no skipping)
+    v.dead = t->profile ? nullptr : L.dead;
   }
   const FlatTables& f = t->flat;
   v.nodes = t->d_nodes;

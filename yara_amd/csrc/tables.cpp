@@ -212,6 +212,11 @@ int flatten_tables(const uint32_t* T, const uint32_t* M, uint32_t n_slots,
     if (M[n.slot] != 0) out.accepting++;
   }
   out.root_accepting = M[0] != 0;
+  for (const Node& n : nodes) {
+    if (n.depth < 2) continue;
+    const uint32_t last = (n.bytes >> (8 * (n.depth - 1))) & 0xFFu;
+    out.deep_last[last >> 5] |= 1u << (last & 31);
+  }
 
   // accepting nodes by string (pre-verification, internal.h kNode*)
   {

@@ -41,6 +41,9 @@ struct FlatTables {
   // being inserted into the window filter (each would fill it with 65,536
   // windows): up to kMaxByteKeys key bytes, packed low byte first
   uint32_t byte_keys = 0, n_byte_keys = 0;
+  // bit b set: some trie node of depth >= 2 ends with byte b (so a position
+  // whose last byte is the 1-byte key b may have a deeper state than b's node)
+  uint32_t deep_last[8] = {0, 0, 0, 0, 0, 0, 0, 0};
 
   // accepting trie nodes -> match-list head M[slot], by the node's string
   // (pre-verification: the walk's state at a candidate is its longest

@@ -78,6 +78,8 @@ struct VerifyParams {
   uint64_t win_lo, win_hi;    // the bytes of the block present in HBM (yr_amd_scan_window)
   uint64_t data_base;         // YR_MEMORY_BLOCK.base (fixed-offset strings)
   const uint64_t* positions;  // ascending candidates (unused when all)
+  const uint8_t* dead;        // null, or per candidate 1 = the scan proved no call of its
+                              // list can have an effect (ScanParams::dead)
   uint64_t count;             // candidates (size + 1 when all)
   int all;                    // every position of a range is a candidate:
   uint64_t all_first;         //   i = all_first + c

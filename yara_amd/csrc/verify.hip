@@ -864,6 +864,13 @@ template <int PASS>
 __device__ __forceinline__ void verify_one(const VerifyParams& p, uint64_t c, uint32_t lds,
                                            uint32_t codebuf, uint32_t keep, uint32_t head,
                                            uint64_t o, uint32_t& count) {
+  if (!PASS && p.dead != nullptr && p.dead[c]) {
+    // the scan's drain already ran this candidate's one guard on the bytes it
+    // held (kernels.hip key_dead): nothing to read
+    p.keep[c] = 0;
+    count = 0;
+    return;
+  }
   const uint64_t i = p.all ? p.all_first + c : p.positions[c];
   if (!PASS && YAMD_VERIFY_DIAG == 3) {   // profiling: candidate positions only
     p.counts[c] = 0; p.keep[c] = 0; p.heads[c] = (uint32_t)i; count = 0; return;
