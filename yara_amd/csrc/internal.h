@@ -191,9 +191,13 @@ struct ScanParams {
   uint32_t n_byte_keys;
   // Per 1-byte key k: the guard that decides every call of the key's match
   // list from the bytes next to it (scanner.cpp key_dead_guards): m, v and info
-  // = valid | region start relative to the key byte (int8) << 8 | span << 16 |
-  // region end relative to the position (int8) << 24; info 0 = none
+  // = valid | has-exclusions << 1 | region start relative to the key byte
+  // (int8) << 8 | span << 16 | region end relative to the position (int8) << 24;
+  // info 0 = none
   uint32_t kd_m[4], kd_v[4], kd_info[4];
+  // with info bit 1: the bytes before the key (up to 8, repeated to fill) after
+  // which a deeper state ends at the key -- such candidates are not decided
+  uint32_t kd_x0[4], kd_x1[4];
   uint8_t* dead;            // null, or per output candidate 1 = no call of its list can
                             // have an effect (written by the compaction)
   uint32_t filter_mode;     // kFilterPair / kFilterEven / kFilterEvenHash (FlatTables)

@@ -350,17 +350,26 @@ constexpr bool kDeferFl =
 // on the ring entry (lane byte j is the key): false only if the guard's whole
 // region lies in the entry and inside the block and no shift passes -- then
 // pre-verification skips the candidate without reading the input.
-__device__ __forceinline__ bool key_dead(const ScanParams& p, uint32_t ent, uint32_t j, uint32_t key,
+__device__ __forceinline__ bool key_dead(const ScanParams& p, uint32_t ent, uint32_t j, uint32_t w_prev,
                                          uint64_t pos) {
-  uint32_t info = 0, m = 0, v = 0;
+  const uint32_t key = w_prev >> 24;
+  uint32_t info = 0, m = 0, v = 0, x0 = 0, x1 = 0;
 #pragma unroll
   for (uint32_t k = 0; k < kMaxByteKeys; ++k) {
     const bool is = k < p.n_byte_keys && key == ((p.byte_keys >> (8 * k)) & 0xFFu);
     info = is ? p.kd_info[k] : info;
     m = is ? p.kd_m[k] : m;
     v = is ? p.kd_v[k] : v;
+    x0 = is ? p.kd_x0[k] : x0;
+    x1 = is ? p.kd_x1[k] : x1;
   }
   if (!(info & 1u)) return false;
+  if (info & 2u) {
+    // the byte before the key (window byte 2) among the exclusions: zero-byte test
+    const uint32_t pv = (w_prev >> 16 & 0xFFu) * 0x01010101u;
+    const uint32_t a = pv ^ x0, b = pv ^ x1;
+    if ((((a - 0x01010101u) & ~a) | ((b - 0x01010101u) & ~b)) & 0x80808080u) return false;
+  }
   const int32_t rs = (int32_t)j + (int32_t)(int8_t)(info >> 8);
   const uint32_t span = (info >> 16) & 15u;
   const int64_t end = (int64_t)pos + (int8_t)(info >> 24);
@@ -498,7 +507,7 @@ __device__ __forceinline__ void drain(const ScanParams& p, WaveQueue& q, uint32_
       if constexpr (MODE == kModeByteKeys) {
         if ((kmask >> j) & 1u) {
           y |= kConfirmed;
-          if (p.dead != nullptr && key_dead(p, ent, j, w >> 24, seg_start + off0 + j + 1)) y |= kPendDead;
+          if (p.dead != nullptr && key_dead(p, ent, j, w, seg_start + off0 + j + 1)) y |= kPendDead;
         }
       }
       lds_store2(q.pend + 8 * (idx - base), w, y);

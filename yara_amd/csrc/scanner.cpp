@@ -88,6 +88,7 @@ struct yr_amd_tables {
   bool profile = false;               // yr_amd_tables_set_profiling
   // per 1-byte key: the guard that decides its list in the scan (ScanParams kd_*)
   uint32_t kd_m[4] = {0, 0, 0, 0}, kd_v[4] = {0, 0, 0, 0}, kd_info[4] = {0, 0, 0, 0};
+  uint32_t kd_x0[4] = {0, 0, 0, 0}, kd_x1[4] = {0, 0, 0, 0};
   bool kd_any = false;
   uint32_t* d_nodes = nullptr;        // accepting nodes by string (FlatTables::nodes)
   DevPoolRec* d_pool = nullptr;       // per pool entry: link, backtrack, string, programs
@@ -501,6 +502,8 @@ int yr_amd_scan_window(yr_amd_scanner* s, const uint8_t* d_window, uint64_t wind
     p.kd_m[k] = t->kd_m[k];
     p.kd_v[k] = t->kd_v[k];
     p.kd_info[k] = t->kd_info[k];
+    p.kd_x0[k] = t->kd_x0[k];
+    p.kd_x1[k] = t->kd_x1[k];
   }
   p.filter_mode = t->flat.filter_mode;
   p.n_segments = n_segments;
@@ -820,8 +823,10 @@ bool general_guard(const uint8_t* c, uint32_t len, uint32_t skip, bool backwards
 
 namespace {
 // The 1-byte keys whose calls the scan kernel can decide (kernels.hip
-// key_dead): the key's state is always its own node (no trie node of depth >= 2
-// ends with it, so no longer suffix is a state), its list is one regexp call,
+// key_dead): the key's state is its own node unless the byte before it is one
+// of at most 8 bytes x with a trie node of depth >= 2 ending in x, key (any
+// deeper state has such a suffix; those candidates are left undecided), its
+// list is one regexp call,
 // and that call is dropped by call_matters whenever its forward guard fails
 // (re_call_matters: a FAST ascii program, or a yr_re_exec one with only the
 // ascii attempt).  The drain tests the guard when its region lies in the
@@ -831,11 +836,21 @@ namespace {
 void key_dead_guards(yr_amd_tables* t) {
   const FlatTables& f = t->flat;
   t->kd_any = false;
-  for (int k = 0; k < 4; ++k) t->kd_m[k] = t->kd_v[k] = t->kd_info[k] = 0;
+  for (int k = 0; k < 4; ++k) t->kd_m[k] = t->kd_v[k] = t->kd_info[k] = t->kd_x0[k] = t->kd_x1[k] = 0;
   if (f.root_accepting || t->h_pool.empty() || diag_env("YAMD_NO_KEY_DEAD") != nullptr) return;
   for (uint32_t k = 0; k < f.n_byte_keys && k < 4; ++k) {
     const uint32_t b = (f.byte_keys >> (8 * k)) & 0xFFu;
-    if ((f.deep_last[b >> 5] >> (b & 31)) & 1u) continue;
+    uint8_t xs[8];
+    uint32_t nx = 0;
+    bool too_many = false;
+    if ((f.deep_last[b >> 5] >> (b & 31)) & 1u) {
+      for (uint32_t x = 0; x < 256; ++x) {
+        if (!((f.deep_pair[b * 8 + (x >> 5)] >> (x & 31)) & 1u)) continue;
+        if (nx == 8) { too_many = true; break; }
+        xs[nx++] = (uint8_t)x;
+      }
+    }
+    if (too_many) continue;
     const uint32_t head = f.nodes[kNodeL1 + b];
     if (head == 0 || head > t->h_pool.size()) continue;
     const DevPoolRec& e = t->h_pool[head - 1];
@@ -852,8 +867,12 @@ void key_dead_guards(yr_amd_tables* t) {
     if (rs < -128 || rs > 127 || end < -128 || end > 127) continue;
     t->kd_m[k] = e.fguard.m;
     t->kd_v[k] = e.fguard.v;
-    t->kd_info[k] = 1u | ((uint32_t)(uint8_t)(int8_t)rs << 8) | ((uint32_t)span << 16) |
-                    ((uint32_t)(uint8_t)(int8_t)end << 24);
+    t->kd_info[k] = 1u | (nx ? 2u : 0u) | ((uint32_t)(uint8_t)(int8_t)rs << 8) |
+                    ((uint32_t)span << 16) | ((uint32_t)(uint8_t)(int8_t)end << 24);
+    for (uint32_t q = 0; q < 8 && nx; ++q) {   // the exclusions, the first repeated to fill
+      const uint32_t x = xs[q < nx ? q : 0];
+      (q < 4 ? t->kd_x0[k] : t->kd_x1[k]) |= x << (8 * (q & 3));
+    }
     t->kd_any = true;
   }
 }

@@ -212,10 +212,13 @@ int flatten_tables(const uint32_t* T, const uint32_t* M, uint32_t n_slots,
     if (M[n.slot] != 0) out.accepting++;
   }
   out.root_accepting = M[0] != 0;
+  out.deep_pair.assign(256 * 8, 0u);
   for (const Node& n : nodes) {
     if (n.depth < 2) continue;
     const uint32_t last = (n.bytes >> (8 * (n.depth - 1))) & 0xFFu;
+    const uint32_t prev = (n.bytes >> (8 * (n.depth - 2))) & 0xFFu;
     out.deep_last[last >> 5] |= 1u << (last & 31);
+    out.deep_pair[last * 8 + (prev >> 5)] |= 1u << (prev & 31);
   }
 
   // accepting nodes by string (pre-verification, internal.h kNode*)

@@ -44,6 +44,9 @@ struct FlatTables {
   // bit b set: some trie node of depth >= 2 ends with byte b (so a position
   // whose last byte is the 1-byte key b may have a deeper state than b's node)
   uint32_t deep_last[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+  // bit x of row b (8 words a row): some trie node of depth >= 2 ends with the
+  // bytes x, b -- such a position's state may be that node instead of b's
+  std::vector<uint32_t> deep_pair;   // 256 x 8
 
   // accepting trie nodes -> match-list head M[slot], by the node's string
   // (pre-verification: the walk's state at a candidate is its longest
