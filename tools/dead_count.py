@@ -1,0 +1,15 @@
+import ctypes, os, sys
+sys.path.insert(0, os.getcwd())
+os.environ["YARA_AMD_LIB"] = os.path.join(os.getcwd(), "yara_amd/_diag/libyara_amd.so")
+import torch, yara_amd
+from yara_amd import _lib
+L = _lib.lib(); f = L.yr_amd__diag_dead_count; f.restype = ctypes.c_int64; f.argtypes = [ctypes.c_void_p]
+for rules, gib in (("rx", 1), ("fuzz0", 1)):
+    n = gib << 30
+    buf = torch.empty(n + 16, dtype=torch.uint8, device="cuda")
+    yara_amd.fill_xorshift64(buf.data_ptr(), n, 1)
+    t = yara_amd.Tables.from_npz(os.path.join("tests/golden/tables", rules + ".npz"), device=0, strings=True)
+    sc = yara_amd.Scanner(t)
+    for _ in range(2):
+        sc.scan_device(buf.data_ptr(), n); _, cnt, _ = sc.device_result()
+        print(rules, "candidates", cnt, "dead", f(sc._h), flush=True)

@@ -199,7 +199,8 @@ struct ScanParams {
   // which a deeper state ends at the key -- such candidates are not decided
   uint32_t kd_x0[4], kd_x1[4];
   uint8_t* dead;            // null, or per output candidate 1 = no call of its list can
-                            // have an effect (written by the compaction)
+                            // have an effect (written by the compaction), and
+  uint32_t* live;           // [0] = count, then the other candidates' indices (any order)
   uint32_t filter_mode;     // kFilterPair / kFilterEven / kFilterEvenHash (FlatTables)
   uint32_t* seg_next;       // null: wave w takes segments w, w + waves, ...; else each wave
                             // takes its first segment by index and the next ones from this

@@ -971,7 +971,7 @@ __global__ __launch_bounds__(256) void seg_scatter_kernel(const uint32_t* seg_co
                                                           const uint64_t* seg_offset, uint32_t cap,
                                                           uint64_t byte_begin, uint32_t seg_bytes,
                                                           uint32_t n_segments, uint64_t* positions,
-                                                          uint8_t* dead) {
+                                                          uint8_t* dead, uint32_t* live) {
   // one wave per segment (segments hold tens to hundreds of candidates)
   const uint32_t seg = blockIdx.x * (blockDim.x / kWave) + threadIdx.x / kWave;
   if (seg >= n_segments) return;
@@ -979,10 +979,24 @@ __global__ __launch_bounds__(256) void seg_scatter_kernel(const uint32_t* seg_co
   const uint64_t base = byte_begin + (uint64_t)seg * seg_bytes + 1;  // position = byte + 1
   const uint32_t* src = seg_out + (seg_base ? seg_base[seg] : (size_t)seg * cap);
   uint64_t* dst = positions + seg_offset[seg];
-  for (uint32_t i = threadIdx.x % kWave; i < c; i += kWave) {
-    const uint32_t e = src[i];
-    dst[i] = base + (e & ~kDeadOut);
-    if (dead != nullptr) dead[seg_offset[seg] + i] = (uint8_t)(e >> 31);
+  const uint32_t lane = threadIdx.x % kWave;
+  for (uint32_t i0 = 0; i0 < c; i0 += kWave) {   // (wave-uniform trips: the ballot below)
+    const uint32_t i = i0 + lane;
+    const uint32_t e = i < c ? src[i] : kDeadOut;
+    if (i < c) dst[i] = base + (e & ~kDeadOut);
+    if (dead == nullptr) continue;
+    if (i < c) dead[seg_offset[seg] + i] = (uint8_t)(e >> 31);
+    // the undecided candidates onto the live list (one atomic per wave)
+    const uint64_t lm = __ballot((e & kDeadOut) == 0u);
+    if (lm == 0) continue;
+    const uint32_t leader = (uint32_t)__builtin_ctzll(lm);
+    uint32_t at = 0;
+    if (lane == leader) at = atomicAdd(live, (uint32_t)__popcll(lm));
+    at = __shfl(at, (int)leader, kWave);
+    if ((e & kDeadOut) == 0u)
+      live[1 + at + __builtin_amdgcn_mbcnt_hi((uint32_t)(lm >> 32),
+                                              __builtin_amdgcn_mbcnt_lo((uint32_t)lm, 0u))] =
+          (uint32_t)(seg_offset[seg] + i);
   }
 }
 
@@ -1071,7 +1085,7 @@ hipError_t launch_compact(const ScanParams& p, uint64_t* seg_offset, uint64_t* s
   } else {
     hipLaunchKernelGGL(seg_scatter_kernel, dim3((p.n_segments + 3) / 4), dim3(256), 0, s,
                        p.seg_count, p.seg_out, p.seg_base, seg_offset, p.seg_cap, p.byte_begin,
-                       p.seg_bytes, p.n_segments, positions, p.dead);
+                       p.seg_bytes, p.n_segments, positions, p.dead, p.live);
   }
   return hipGetLastError();
 }

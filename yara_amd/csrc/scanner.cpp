@@ -115,6 +115,8 @@ struct yr_amd_scanner {
   uint64_t* d_positions = nullptr;
   uint8_t* d_dead = nullptr;            // per candidate: the scan proved its calls dead
   size_t dead_cap = 0;
+  uint32_t* d_live = nullptr;           // [0] count, then the other candidates (ScanParams::live)
+  size_t live_cap = 0;
   size_t positions_cap = 0;             // entries
   uint64_t* h_summary = nullptr;        // pinned, coherent: {total, max per segment}
   uint64_t* d_hsum = nullptr;           // h_summary mapped for the device: the offsets
@@ -239,8 +241,10 @@ int run_scan(yr_amd_scanner* s) {
   const size_t out_cap = p.seg_base ? s->rerun_total : (size_t)p.n_segments * p.seg_cap;
   int r = grow(s->d_positions, s->positions_cap, out_cap);
   if (!r && s->tables->kd_any) r = grow(s->d_dead, s->dead_cap, out_cap);
+  if (!r && s->tables->kd_any) r = grow(s->d_live, s->live_cap, out_cap + 1);
   if (r) return r;
   s->last.dead = s->tables->kd_any ? s->d_dead : nullptr;
+  s->last.live = s->tables->kd_any ? s->d_live : nullptr;
   if (s->timing) HIP_TRY(hipEventRecord(s->ev_begin, s->stream));
   HIP_TRY(launch_scan(p, s->last_grid, s->stream, s->diag_mode));
   if (s->timing) {
@@ -248,6 +252,7 @@ int run_scan(yr_amd_scanner* s) {
     s->ev_valid = true;
   }
   HIP_TRY(launch_compact(p, s->d_seg_offset, s->d_hsum, nullptr, false, s->stream));
+  if (p.live != nullptr) HIP_TRY(hipMemsetAsync(p.live, 0, sizeof(uint32_t), s->stream));
   HIP_TRY(launch_compact(p, s->d_seg_offset, s->d_hsum, s->d_positions, true, s->stream));
   HIP_TRY(hipEventRecord(s->ev_done, s->stream));
   return YR_AMD_SUCCESS;
@@ -379,7 +384,7 @@ int yr_amd_scanner_destroy(yr_amd_scanner* s) {
   if (s->stream) (void)hipStreamSynchronize(s->stream);
   for (void* p : {(void*)s->d_block, (void*)s->d_seg_count,
                   (void*)s->d_seg_offset,
-                  (void*)s->d_seg_out, (void*)s->d_positions, (void*)s->d_dead,
+                  (void*)s->d_seg_out, (void*)s->d_positions, (void*)s->d_dead, (void*)s->d_live,
                   (void*)s->d_summary,
                   (void*)s->d_vcount, (void*)s->d_vkeep, (void*)s->d_vblock, (void*)s->d_vrec,
                   (void*)s->d_vchunk, (void*)s->d_seg_base,
@@ -410,6 +415,16 @@ int yr_amd_scanner_set_timing(yr_amd_scanner* s, int enable) {
 // Diagnostic builds only (not declared in include/yara_amd.h): profiling
 // ablations of the scan kernel (tools/ablate.py).  Any mode other than 0
 // produces wrong results.
+// Candidates of the last scan that the drain proved dead (ScanParams::dead).
+int64_t yr_amd__diag_dead_count(yr_amd_scanner* s) {
+  if (s == nullptr || s->last.dead == nullptr || s->last_count == 0) return -1;
+  std::vector<uint8_t> h(s->last_count);
+  if (hipMemcpy(h.data(), s->last.dead, h.size(), hipMemcpyDeviceToHost) != hipSuccess) return -2;
+  int64_t n = 0;
+  for (uint8_t x : h) n += x != 0;
+  return n;
+}
+
 int yr_amd__diag_kernel_mode(yr_amd_scanner* s, int mode) {
   if (s == nullptr || mode < 0 || (mode > 12 && mode != 24 && mode != 25))
     return YR_AMD_INVALID_ARGUMENT;
@@ -459,6 +474,7 @@ int yr_amd_scan_window(yr_amd_scanner* s, const uint8_t* d_window, uint64_t wind
   s->last_all = t->flat.root_accepting;
   s->last_empty = s->last_all || byte_end == byte_begin;
   s->last.dead = nullptr;
+  s->last.live = nullptr;
   if (s->last_empty) return YR_AMD_SUCCESS;
   if (d_window == nullptr) return YR_AMD_INVALID_ARGUMENT;
   HIP_TRY(hipSetDevice(t->device));
@@ -988,6 +1004,7 @@ int yr_amd_verify_device(yr_amd_scanner* s, uint64_t data_base, const yr_amd_ver
     v.count = s->last_count;
     // (profiling needs every call past the early returns: no skipping)
     v.dead = t->profile ? nullptr : L.dead;
+    v.live = t->profile ? nullptr : L.live;
   }
   const FlatTables& f = t->flat;
   v.nodes = t->d_nodes;
@@ -1029,7 +1046,15 @@ int yr_amd_verify_device(yr_amd_scanner* s, uint64_t data_base, const yr_amd_ver
     v.out_cap = s->vrec_cap;
     // count pass -> block offsets (total straight into the host-mapped
     // summary) -> write pass, then one wait
-    HIP_TRY(launch_verify(v, 0, s->stream));
+    if (v.live != nullptr) {
+      // the scan's live list: only its candidates are decided, their record
+      // counts added to the groups' (zeroed here)
+      HIP_TRY(hipMemsetAsync(v.block_off, 0, (verify_groups(v.count) + 1) * sizeof(uint64_t),
+                             s->stream));
+      HIP_TRY(launch_verify_live(v, s->stream));
+    } else {
+      HIP_TRY(launch_verify(v, 0, s->stream));
+    }
     HIP_TRY(launch_block_offsets(s->d_vblock, s->d_vchunk, v.count, s->d_hsum, s->stream));
     HIP_TRY(launch_verify(v, 1, s->stream));
     HIP_TRY(hipStreamSynchronize(s->stream));

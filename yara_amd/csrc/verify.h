@@ -79,7 +79,8 @@ struct VerifyParams {
   uint64_t data_base;         // YR_MEMORY_BLOCK.base (fixed-offset strings)
   const uint64_t* positions;  // ascending candidates (unused when all)
   const uint8_t* dead;        // null, or per candidate 1 = the scan proved no call of its
-                              // list can have an effect (ScanParams::dead)
+                              // list can have an effect (ScanParams::dead), and
+  const uint32_t* live;       // [0] = count, then the other candidates' indices
   uint64_t count;             // candidates (size + 1 when all)
   int all;                    // every position of a range is a candidate:
   uint64_t all_first;         //   i = all_first + c
@@ -108,6 +109,9 @@ struct VerifyParams {
 };
 
 hipError_t launch_verify(const VerifyParams& p, int pass, hipStream_t s);
+// Pass 0 over the scan's live list (p.live; block_off zeroed): the dead
+// candidates keep nothing and are never read.
+hipError_t launch_verify_live(const VerifyParams& p, hipStream_t s);
 hipError_t launch_block_offsets(uint64_t* block_off, uint64_t* chunk_off, uint64_t count,
                                 uint64_t* total, hipStream_t s);
 constexpr uint64_t kGroup = 64;           // candidates per group (one wave)

@@ -983,10 +983,29 @@ __global__ __launch_bounds__(256) void verify_kernel(VerifyParams p) {
     const uint64_t o = group_offset(p, g);
     if (group_offset(p, g + 1) == o) continue;
     const uint64_t c = g * kGroup + (threadIdx.x & 63u);
-    const uint32_t keep = c < p.count ? p.keep[c] : 0u;
+    const uint32_t keep =
+        c < p.count && (p.dead == nullptr || p.dead[c] == 0) ? p.keep[c] : 0u;
     uint32_t n = keep == 0 ? 0u : p.counts[c];
     const uint32_t pre = wave_exclusive(n);
     if (keep != 0) verify_one<1>(p, c, lds, codebuf, keep, p.heads[c], o + pre, n);
+  }
+}
+
+// Pass 0 over the live list (persistent blocks): each live candidate decided
+// as verify_kernel<0> does, its record count added to its group's.
+__global__ __launch_bounds__(256) void verify_live_kernel(VerifyParams p) {
+  __shared__ __attribute__((aligned(16))) uint8_t win[256 * kWinBytes];
+  __shared__ __attribute__((aligned(16))) uint8_t code[256 * kCodeBytes];
+  const uint32_t lds = (uint32_t)(uintptr_t)(win + threadIdx.x * kWinBytes);
+  const uint32_t codebuf = (uint32_t)(uintptr_t)(code + threadIdx.x * kCodeBytes);
+  const uint32_t n_live = p.live[0];
+  for (uint64_t h = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; h < n_live;
+       h += (uint64_t)gridDim.x * blockDim.x) {
+    const uint32_t c = p.live[1 + h];
+    uint32_t n = 0;
+    verify_one<0>(p, c, lds, codebuf, 0, 0, 0, n);
+    if (n != 0) atomicAdd(reinterpret_cast<unsigned long long*>(p.block_off + c / kGroup),
+                          (unsigned long long)n);
   }
 }
 
@@ -1075,6 +1094,14 @@ hipError_t launch_verify(const VerifyParams& p, int pass, hipStream_t s) {
         (waves + 3) / 4, resident_blocks((const void*)verify_kernel<1>));
     hipLaunchKernelGGL(verify_kernel<1>, dim3(blocks), dim3(256), 0, s, p);
   }
+  return hipGetLastError();
+}
+
+hipError_t launch_verify_live(const VerifyParams& p, hipStream_t s) {
+  if (p.count == 0) return hipSuccess;
+  const uint32_t blocks = (uint32_t)std::min<uint64_t>(
+      (p.count + 255) / 256, resident_blocks((const void*)verify_live_kernel));
+  hipLaunchKernelGGL(verify_live_kernel, dim3(blocks), dim3(256), 0, s, p);
   return hipGetLastError();
 }
 
