@@ -192,8 +192,8 @@ struct ScanParams {
   // Per 1-byte key k: the guard that decides every call of the key's match
   // list from the bytes next to it (scanner.cpp key_dead_guards): m, v and info
   // = valid | has-exclusions << 1 | region start relative to the key byte
-  // (int8) << 8 | span << 16 | region end relative to the position (int8) << 24;
-  // info 0 = none
+  // (int8) << 8 | span << 16 | last tested byte of the 4 << 20 | region end
+  // relative to the position (int8) << 24; info 0 = none
   uint32_t kd_m[4], kd_v[4], kd_info[4];
   // with info bit 1: the bytes before the key (up to 8, repeated to fill) after
   // which a deeper state ends at the key -- such candidates are not decided

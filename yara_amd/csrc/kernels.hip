@@ -370,12 +370,21 @@ __device__ __forceinline__ bool key_dead(const ScanParams& p, uint32_t ent, uint
     const uint32_t a = pv ^ x0, b = pv ^ x1;
     if ((((a - 0x01010101u) & ~a) | ((b - 0x01010101u) & ~b)) & 0x80808080u) return false;
   }
+  // the tested bytes of shift jj: region bytes jj + t for the t with mask byte
+  // t set, t <= tmax (info bits 20..21); they must all lie in the lane
   const int32_t rs = (int32_t)j + (int32_t)(int8_t)(info >> 8);
-  const uint32_t span = (info >> 16) & 15u;
+  const uint32_t span = (info >> 16) & 15u, tmax = (info >> 20) & 3u;
   const int64_t end = (int64_t)pos + (int8_t)(info >> 24);
-  if (rs < 0 || rs + (int32_t)span + 4 > kBytesPerLane || end > (int64_t)p.block_size) return false;
+  if (rs < 0 || rs + (int32_t)(span + tmax) >= kBytesPerLane || end > (int64_t)p.block_size)
+    return false;
   bool hit = false;
-  for (uint32_t jj = 0; jj <= span; ++jj) hit |= (window4(ent, (uint32_t)rs + jj + 3) & m) == v;
+  for (uint32_t jj = 0; jj <= span; ++jj) {
+    // the 4 bytes from rs + jj, or those ending at the lane's last byte shifted
+    // down (bytes past it are untested)
+    const uint32_t e = min((uint32_t)rs + jj + 3, (uint32_t)kBytesPerLane - 1);
+    const uint32_t x = window4(ent, e) >> (8 * ((uint32_t)rs + jj + 3 - e));
+    hit |= (x & m) == v;
+  }
   return !hit;
 }
 

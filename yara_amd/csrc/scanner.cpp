@@ -883,8 +883,9 @@ void key_dead_guards(yr_amd_tables* t) {
     if (rs < -128 || rs > 127 || end < -128 || end > 127) continue;
     t->kd_m[k] = e.fguard.m;
     t->kd_v[k] = e.fguard.v;
+    const uint32_t tmax = (31u - (uint32_t)__builtin_clz(e.fguard.m)) >> 3;   // last tested byte
     t->kd_info[k] = 1u | (nx ? 2u : 0u) | ((uint32_t)(uint8_t)(int8_t)rs << 8) |
-                    ((uint32_t)span << 16) | ((uint32_t)(uint8_t)(int8_t)end << 24);
+                    ((uint32_t)span << 16) | (tmax << 20) | ((uint32_t)(uint8_t)(int8_t)end << 24);
     for (uint32_t q = 0; q < 8 && nx; ++q) {   // the exclusions, the first repeated to fill
       const uint32_t x = xs[q < nx ? q : 0];
       (q < 4 ? t->kd_x0[k] : t->kd_x1[k]) |= x << (8 * (q & 3));
