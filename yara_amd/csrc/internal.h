@@ -163,11 +163,18 @@ constexpr uint32_t kNodeL2 = 256;
 constexpr uint32_t kNodeZero4 = 256 + 65536;
 constexpr uint32_t kNodeHeadWords = kNodeZero4 + 4;   // (keeps the buckets 16-B aligned)
 
-// Bits of the candidate outputs: a segment output entry with kDeadOut is a
-// certain candidate whose calls the drain proved dead (its flag goes to
-// ScanParams::dead); a pending entry's offset carries it as kPendDead.
-constexpr uint32_t kDeadOut = 0x80000000u;
-constexpr uint32_t kPendDead = 0x40000000u;
+// The class the byte-key drain gives a certain candidate (kernels.hip
+// key_class; ScanParams::dead holds it per candidate): 0 = undecided, 1 = no
+// call of its list can have an effect, 2 | k << 2 = every call of 1-byte key
+// k's list is kept (ScanParams::kd_n / kd_head).  A segment output entry
+// carries it in bits kOutClassShift.., a pending entry's offset in bits
+// kPendClassShift..; segment offsets are below 2^20.
+constexpr uint32_t kOutClassShift = 28;
+constexpr uint32_t kOutOffsetMask = (1u << kOutClassShift) - 1u;
+constexpr uint32_t kPendClassShift = 24;
+constexpr uint32_t kPendOffsetMask = (1u << kPendClassShift) - 1u;
+constexpr uint32_t kClassDead = 1u;
+constexpr uint32_t kClassKept = 2u;
 
 struct ScanParams {
   const uint8_t* data;      // block base in HBM (16-byte aligned)
@@ -191,15 +198,19 @@ struct ScanParams {
   uint32_t n_byte_keys;
   // Per 1-byte key k: the guard that decides every call of the key's match
   // list from the bytes next to it (scanner.cpp key_dead_guards): m, v and info
-  // = valid | has-exclusions << 1 | region start relative to the key byte
+  // = valid | has-exclusions << 1 | kept-list << 2 | region start relative to the key byte
   // (int8) << 8 | span << 16 | last tested byte of the 4 << 20 | region end
   // relative to the position (int8) << 24; info 0 = none
   uint32_t kd_m[4], kd_v[4], kd_info[4];
   // with info bit 1: the bytes before the key (up to 8, repeated to fill) after
   // which a deeper state ends at the key -- such candidates are not decided
   uint32_t kd_x0[4], kd_x1[4];
-  uint8_t* dead;            // null, or per output candidate 1 = no call of its list can
-                            // have an effect (written by the compaction), and
+  // with info bit 2 ("kept" keys: every call of the list is kept whatever the
+  // bytes): the list's length and head, and the smallest position at which
+  // every call is made (the largest backtrack, scanner.c:107)
+  uint32_t kd_n[4], kd_head[4], kd_min_pos[4];
+  uint8_t* dead;            // null, or per output candidate its class (key_class;
+                            // written by the compaction), and
   uint32_t* live;           // [0] = count, then the other candidates' indices (any order)
   uint32_t filter_mode;     // kFilterPair / kFilterEven / kFilterEvenHash (FlatTables)
   uint32_t* seg_next;       // null: wave w takes segments w, w + waves, ...; else each wave

@@ -215,11 +215,11 @@ __device__ __forceinline__ void flush_pending(const ScanParams& p, WaveQueue& q,
     u32x2 e = {0u, 0u};
     if (lane < q.pend_n) e = lds_load<u32x2>(q.pend + 8 * lane);
     const bool conf = (e.y & kConfirmed) != 0u;
-    off = e.y & ~(kConfirmed | kPendDead);
+    off = e.y & kPendOffsetMask;
     const bool probe = lane < q.pend_n && !conf;
     keep = lane < q.pend_n && conf;
     if (__ballot(probe) != 0 && probe) keep = exact_check(e.x, seg_start + off + 1, p);
-    if (e.y & kPendDead) off |= kDeadOut;   // (a certain candidate: kept either way)
+    off |= ((e.y & ~kConfirmed) >> kPendClassShift) << kOutClassShift;   // (certain: kept either way)
   } else if (lane < q.pend_n) {
     const u32x2 e = lds_load<u32x2>(q.pend + 8 * lane);
     off = e.y;
@@ -344,16 +344,18 @@ constexpr bool kDeferFl =
     YAMD_DEFER_FL &&
     (MODE == 0 || MODE == 12 || MODE == kModeByteKeys || kEven<MODE> || kByteKeyAblation<MODE>);
 
-// Does some call of a certain candidate's list possibly have an effect?  For a
-// 1-byte key whose list is decided by one guard on the bytes right after it
-// (ScanParams::kd_*, scanner.cpp key_dead_guards), the drain tests that guard
-// on the ring entry (lane byte j is the key): false only if the guard's whole
-// region lies in the entry and inside the block and no shift passes -- then
-// pre-verification skips the candidate without reading the input.
-__device__ __forceinline__ bool key_dead(const ScanParams& p, uint32_t ent, uint32_t j, uint32_t w_prev,
-                                         uint64_t pos) {
+// The class of a certain candidate (internal.h kClass*): for a 1-byte key whose
+// state is its own node (ScanParams::kd_*, scanner.cpp key_classes), either
+// every call of the list is kept whatever the bytes ("kept" keys: plain
+// literals that fit in the atom), or the list is one call decided by a guard
+// on the bytes after the key, which the drain tests on the ring entry (lane
+// byte j is the key): dead only if every tested byte lies in the lane and
+// inside the block and no shift passes.  Pre-verification then never reads
+// the input for the candidate.
+__device__ __forceinline__ uint32_t key_class(const ScanParams& p, uint32_t ent, uint32_t j,
+                                              uint32_t w_prev, uint64_t pos) {
   const uint32_t key = w_prev >> 24;
-  uint32_t info = 0, m = 0, v = 0, x0 = 0, x1 = 0;
+  uint32_t info = 0, m = 0, v = 0, x0 = 0, x1 = 0, kidx = 0, min_pos = 0;
 #pragma unroll
   for (uint32_t k = 0; k < kMaxByteKeys; ++k) {
     const bool is = k < p.n_byte_keys && key == ((p.byte_keys >> (8 * k)) & 0xFFu);
@@ -362,21 +364,24 @@ __device__ __forceinline__ bool key_dead(const ScanParams& p, uint32_t ent, uint
     v = is ? p.kd_v[k] : v;
     x0 = is ? p.kd_x0[k] : x0;
     x1 = is ? p.kd_x1[k] : x1;
+    min_pos = is ? p.kd_min_pos[k] : min_pos;
+    kidx = is ? k : kidx;
   }
-  if (!(info & 1u)) return false;
+  if (!(info & 1u)) return 0;
   if (info & 2u) {
     // the byte before the key (window byte 2) among the exclusions: zero-byte test
     const uint32_t pv = (w_prev >> 16 & 0xFFu) * 0x01010101u;
     const uint32_t a = pv ^ x0, b = pv ^ x1;
-    if ((((a - 0x01010101u) & ~a) | ((b - 0x01010101u) & ~b)) & 0x80808080u) return false;
+    if ((((a - 0x01010101u) & ~a) | ((b - 0x01010101u) & ~b)) & 0x80808080u) return 0;
   }
+  if (info & 4u) return pos >= min_pos ? (kClassKept | kidx << 2) : 0u;
   // the tested bytes of shift jj: region bytes jj + t for the t with mask byte
   // t set, t <= tmax (info bits 20..21); they must all lie in the lane
   const int32_t rs = (int32_t)j + (int32_t)(int8_t)(info >> 8);
   const uint32_t span = (info >> 16) & 15u, tmax = (info >> 20) & 3u;
   const int64_t end = (int64_t)pos + (int8_t)(info >> 24);
   if (rs < 0 || rs + (int32_t)(span + tmax) >= kBytesPerLane || end > (int64_t)p.block_size)
-    return false;
+    return 0;
   bool hit = false;
   for (uint32_t jj = 0; jj <= span; ++jj) {
     // the 4 bytes from rs + jj, or those ending at the lane's last byte shifted
@@ -385,7 +390,7 @@ __device__ __forceinline__ bool key_dead(const ScanParams& p, uint32_t ent, uint
     const uint32_t x = window4(ent, e) >> (8 * ((uint32_t)rs + jj + 3 - e));
     hit |= (x & m) == v;
   }
-  return !hit;
+  return hit ? 0u : kClassDead;
 }
 
 // Consume a deferred drain's first-level words: the lanes' hits that pass go,
@@ -516,7 +521,7 @@ __device__ __forceinline__ void drain(const ScanParams& p, WaveQueue& q, uint32_
       if constexpr (MODE == kModeByteKeys) {
         if ((kmask >> j) & 1u) {
           y |= kConfirmed;
-          if (p.dead != nullptr && key_dead(p, ent, j, w, seg_start + off0 + j + 1)) y |= kPendDead;
+          if (p.dead != nullptr) y |= key_class(p, ent, j, w, seg_start + off0 + j + 1) << kPendClassShift;
         }
       }
       lds_store2(q.pend + 8 * (idx - base), w, y);
@@ -991,18 +996,19 @@ __global__ __launch_bounds__(256) void seg_scatter_kernel(const uint32_t* seg_co
   const uint32_t lane = threadIdx.x % kWave;
   for (uint32_t i0 = 0; i0 < c; i0 += kWave) {   // (wave-uniform trips: the ballot below)
     const uint32_t i = i0 + lane;
-    const uint32_t e = i < c ? src[i] : kDeadOut;
-    if (i < c) dst[i] = base + (e & ~kDeadOut);
+    const uint32_t e = i < c ? src[i] : kClassDead << kOutClassShift;
+    const uint32_t cls = e >> kOutClassShift;
+    if (i < c) dst[i] = base + (e & kOutOffsetMask);
     if (dead == nullptr) continue;
-    if (i < c) dead[seg_offset[seg] + i] = (uint8_t)(e >> 31);
+    if (i < c) dead[seg_offset[seg] + i] = (uint8_t)cls;
     // the undecided candidates onto the live list (one atomic per wave)
-    const uint64_t lm = __ballot((e & kDeadOut) == 0u);
+    const uint64_t lm = __ballot(cls == 0u);
     if (lm == 0) continue;
     const uint32_t leader = (uint32_t)__builtin_ctzll(lm);
     uint32_t at = 0;
     if (lane == leader) at = atomicAdd(live, (uint32_t)__popcll(lm));
     at = __shfl(at, (int)leader, kWave);
-    if ((e & kDeadOut) == 0u)
+    if (cls == 0u)
       live[1 + at + __builtin_amdgcn_mbcnt_hi((uint32_t)(lm >> 32),
                                               __builtin_amdgcn_mbcnt_lo((uint32_t)lm, 0u))] =
           (uint32_t)(seg_offset[seg] + i);

@@ -89,6 +89,7 @@ struct yr_amd_tables {
   // per 1-byte key: the guard that decides its list in the scan (ScanParams kd_*)
   uint32_t kd_m[4] = {0, 0, 0, 0}, kd_v[4] = {0, 0, 0, 0}, kd_info[4] = {0, 0, 0, 0};
   uint32_t kd_x0[4] = {0, 0, 0, 0}, kd_x1[4] = {0, 0, 0, 0};
+  uint32_t kd_n[4] = {0, 0, 0, 0}, kd_head[4] = {0, 0, 0, 0}, kd_min_pos[4] = {0, 0, 0, 0};
   bool kd_any = false;
   uint32_t* d_nodes = nullptr;        // accepting nodes by string (FlatTables::nodes)
   DevPoolRec* d_pool = nullptr;       // per pool entry: link, backtrack, string, programs
@@ -520,6 +521,9 @@ int yr_amd_scan_window(yr_amd_scanner* s, const uint8_t* d_window, uint64_t wind
     p.kd_info[k] = t->kd_info[k];
     p.kd_x0[k] = t->kd_x0[k];
     p.kd_x1[k] = t->kd_x1[k];
+    p.kd_n[k] = t->kd_n[k];
+    p.kd_head[k] = t->kd_head[k];
+    p.kd_min_pos[k] = t->kd_min_pos[k];
   }
   p.filter_mode = t->flat.filter_mode;
   p.n_segments = n_segments;
@@ -633,6 +637,10 @@ int upload(T*& d, const T* h, size_t n) {
 }  // namespace
 }  // extern "C++"
 
+namespace {
+void key_classes(yr_amd_tables* t);
+}
+
 int yr_amd_tables_set_strings(yr_amd_tables* t, const uint32_t* pool_string, uint32_t n_pool,
                               const yr_amd_string* strings, uint32_t n_strings,
                               const uint8_t* bytes, uint64_t n_bytes, const uint8_t* lowercase) {
@@ -679,6 +687,7 @@ int yr_amd_tables_set_strings(yr_amd_tables* t, const uint32_t* pool_string, uin
     t->max_str_bytes = std::max<uint64_t>(t->max_str_bytes, 2ull * strings[k].length + 2);
   }
   t->has_strings = true;
+  key_classes(t);   // (again with the guards once regexp programs are attached)
   return YR_AMD_SUCCESS;
 }
 
@@ -838,22 +847,28 @@ bool general_guard(const uint8_t* c, uint32_t len, uint32_t skip, bool backwards
 }  // namespace
 
 namespace {
-// The 1-byte keys whose calls the scan kernel can decide (kernels.hip
-// key_dead): the key's state is its own node unless the byte before it is one
-// of at most 8 bytes x with a trie node of depth >= 2 ending in x, key (any
-// deeper state has such a suffix; those candidates are left undecided), its
-// list is one regexp call,
-// and that call is dropped by call_matters whenever its forward guard fails
-// (re_call_matters: a FAST ascii program, or a yr_re_exec one with only the
-// ascii attempt).  The drain tests the guard when its region lies in the
-// key's lane; the count pass then skips the candidate.  (YR_AC_MATCH offsets:
-// the call's offset is position - backtrack, the guard's region starts `base`
-// bytes after it.)
-void key_dead_guards(yr_amd_tables* t) {
+// The 1-byte keys whose calls the scan kernel can classify (kernels.hip
+// key_class).  The key's state is its own node unless the byte before it is
+// one of at most 8 bytes x with a trie node of depth >= 2 ending in x, key (a
+// deeper state has such a suffix; those candidates stay undecided).  Then
+// either
+//  * "kept": every call of the node's list is kept whatever the bytes --
+//    plain literals that fit in the atom (call_matters: backtrack != 0, no
+//    FULL_WORD / base64 / fixed offset), made at every position from the
+//    largest backtrack on (scanner.c:107) -- or
+//  * the list is one regexp call that call_matters drops whenever its forward
+//    guard fails (a FAST ascii program, or a yr_re_exec one with only the
+//    ascii attempt); the drain tests the guard when its tested bytes lie in
+//    the key's lane.  (YR_AC_MATCH offsets: the call's offset is position -
+//    backtrack, the guard's region starts `base` bytes after it.)
+// Pre-verification then never reads the input for such candidates.
+void key_classes(yr_amd_tables* t) {
   const FlatTables& f = t->flat;
   t->kd_any = false;
-  for (int k = 0; k < 4; ++k) t->kd_m[k] = t->kd_v[k] = t->kd_info[k] = t->kd_x0[k] = t->kd_x1[k] = 0;
-  if (f.root_accepting || t->h_pool.empty() || diag_env("YAMD_NO_KEY_DEAD") != nullptr) return;
+  for (int k = 0; k < 4; ++k)
+    t->kd_m[k] = t->kd_v[k] = t->kd_info[k] = t->kd_x0[k] = t->kd_x1[k] = t->kd_n[k] =
+        t->kd_head[k] = t->kd_min_pos[k] = 0;
+  if (f.root_accepting || t->h_pool.empty() || diag_env("YAMD_NO_KEY_CLASSES") != nullptr) return;
   for (uint32_t k = 0; k < f.n_byte_keys && k < 4; ++k) {
     const uint32_t b = (f.byte_keys >> (8 * k)) & 0xFFu;
     uint8_t xs[8];
@@ -869,23 +884,43 @@ void key_dead_guards(yr_amd_tables* t) {
     if (too_many) continue;
     const uint32_t head = f.nodes[kNodeL1 + b];
     if (head == 0 || head > t->h_pool.size()) continue;
-    const DevPoolRec& e = t->h_pool[head - 1];
-    const uint32_t fl = e.flags;
-    if (e.next != 0 || (fl & kStrLiteral) || e.re.fwd_len == 0 || e.fguard.m == 0) continue;
-    if (fl & kStrFastRegexp) {
-      if (!(fl & kStrAscii) || (fl & (kStrWide | kStrBase64Any))) continue;
-    } else if (((fl & kStrWide) && !(fl & kStrBase64Any)) || !(fl & (kStrAscii | kStrBase64Any))) {
-      continue;
+    uint32_t info = 0;
+    // "kept": every entry a plain fits-in-atom literal (call_matters' early
+    // decision), at most 30 of them (pass 1's keep mask)
+    uint32_t n = 0, max_bt = 0;
+    bool kept = true;
+    for (uint32_t q = head; q != 0 && kept; q = t->h_pool[q - 1].next) {
+      const DevPoolRec& e = t->h_pool[q - 1];
+      kept = (e.flags & (kStrLiteral | kStrFitsInAtom)) == (kStrLiteral | kStrFitsInAtom) &&
+             !(e.flags & (kStrUnmodelled | kStrFullWord | kStrFixedOffset)) && e.backtrack != 0 &&
+             ++n <= 30;
+      max_bt = std::max<uint32_t>(max_bt, e.backtrack);
     }
-    const int base = e.fguard_bs & 15, span = e.fguard_bs >> 4;
-    const int rs = base + 1 - (int)e.backtrack;          // region start - key byte
-    const int end = base + span + 4 - (int)e.backtrack;  // region end - position
-    if (rs < -128 || rs > 127 || end < -128 || end > 127) continue;
-    t->kd_m[k] = e.fguard.m;
-    t->kd_v[k] = e.fguard.v;
-    const uint32_t tmax = (31u - (uint32_t)__builtin_clz(e.fguard.m)) >> 3;   // last tested byte
-    t->kd_info[k] = 1u | (nx ? 2u : 0u) | ((uint32_t)(uint8_t)(int8_t)rs << 8) |
-                    ((uint32_t)span << 16) | (tmax << 20) | ((uint32_t)(uint8_t)(int8_t)end << 24);
+    if (kept && n > 0) {
+      info = 1u | 4u;
+      t->kd_n[k] = n;
+      t->kd_head[k] = head;
+      t->kd_min_pos[k] = max_bt;
+    } else {
+      const DevPoolRec& e = t->h_pool[head - 1];
+      const uint32_t fl = e.flags;
+      if (e.next != 0 || (fl & kStrLiteral) || e.re.fwd_len == 0 || e.fguard.m == 0) continue;
+      if (fl & kStrFastRegexp) {
+        if (!(fl & kStrAscii) || (fl & (kStrWide | kStrBase64Any))) continue;
+      } else if (((fl & kStrWide) && !(fl & kStrBase64Any)) || !(fl & (kStrAscii | kStrBase64Any))) {
+        continue;
+      }
+      const int base = e.fguard_bs & 15, span = e.fguard_bs >> 4;
+      const int rs = base + 1 - (int)e.backtrack;          // region start - key byte
+      const int end = base + span + 4 - (int)e.backtrack;  // region end - position
+      if (rs < -128 || rs > 127 || end < -128 || end > 127) continue;
+      t->kd_m[k] = e.fguard.m;
+      t->kd_v[k] = e.fguard.v;
+      const uint32_t tmax = (31u - (uint32_t)__builtin_clz(e.fguard.m)) >> 3;   // last tested byte
+      info = 1u | ((uint32_t)(uint8_t)(int8_t)rs << 8) | ((uint32_t)span << 16) | (tmax << 20) |
+             ((uint32_t)(uint8_t)(int8_t)end << 24);
+    }
+    t->kd_info[k] = info | (nx ? 2u : 0u);
     for (uint32_t q = 0; q < 8 && nx; ++q) {   // the exclusions, the first repeated to fill
       const uint32_t x = xs[q < nx ? q : 0];
       (q < 4 ? t->kd_x0[k] : t->kd_x1[k]) |= x << (8 * (q & 3));
@@ -978,7 +1013,7 @@ int yr_amd_tables_set_re_code(yr_amd_tables* t, uint32_t n_pool, const uint32_t*
   if (n_pool > 0 && hipMemcpy(t->d_pool, t->h_pool.data(), n_pool * sizeof(DevPoolRec),
                               hipMemcpyHostToDevice) != hipSuccess)
     return YR_AMD_INTERNAL_FATAL_ERROR;
-  key_dead_guards(t);
+  key_classes(t);
   return YR_AMD_SUCCESS;
 }
 
@@ -1006,6 +1041,10 @@ int yr_amd_verify_device(yr_amd_scanner* s, uint64_t data_base, const yr_amd_ver
     // (profiling needs every call past the early returns: no skipping)
     v.dead = t->profile ? nullptr : L.dead;
     v.live = t->profile ? nullptr : L.live;
+    for (int k = 0; k < 4; ++k) {
+      v.kd_n[k] = L.kd_n[k];
+      v.kd_head[k] = L.kd_head[k];
+    }
   }
   const FlatTables& f = t->flat;
   v.nodes = t->d_nodes;
@@ -1056,7 +1095,9 @@ int yr_amd_verify_device(yr_amd_scanner* s, uint64_t data_base, const yr_amd_ver
     } else {
       HIP_TRY(launch_verify(v, 0, s->stream));
     }
-    HIP_TRY(launch_block_offsets(s->d_vblock, s->d_vchunk, v.count, s->d_hsum, s->stream));
+    KeptLists kept{{v.kd_n[0], v.kd_n[1], v.kd_n[2], v.kd_n[3]}};
+    HIP_TRY(launch_block_offsets(s->d_vblock, s->d_vchunk, v.count, s->d_hsum, v.dead, kept,
+                                 s->stream));
     HIP_TRY(launch_verify(v, 1, s->stream));
     HIP_TRY(hipStreamSynchronize(s->stream));
     total = s->h_summary[0];

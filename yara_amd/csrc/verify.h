@@ -81,6 +81,7 @@ struct VerifyParams {
   const uint8_t* dead;        // null, or per candidate 1 = the scan proved no call of its
                               // list can have an effect (ScanParams::dead), and
   const uint32_t* live;       // [0] = count, then the other candidates' indices
+  uint32_t kd_n[4], kd_head[4];   // the "kept" keys' list lengths and heads (ScanParams)
   uint64_t count;             // candidates (size + 1 when all)
   int all;                    // every position of a range is a candidate:
   uint64_t all_first;         //   i = all_first + c
@@ -112,8 +113,14 @@ hipError_t launch_verify(const VerifyParams& p, int pass, hipStream_t s);
 // Pass 0 over the scan's live list (p.live; block_off zeroed): the dead
 // candidates keep nothing and are never read.
 hipError_t launch_verify_live(const VerifyParams& p, hipStream_t s);
+// The "kept" keys' list lengths (the class byte's key index): their records
+// count into the group totals without pass 0.
+struct KeptLists {
+  uint32_t n[4];
+};
 hipError_t launch_block_offsets(uint64_t* block_off, uint64_t* chunk_off, uint64_t count,
-                                uint64_t* total, hipStream_t s);
+                                uint64_t* total, const uint8_t* cls, const KeptLists& kept,
+                                hipStream_t s);
 constexpr uint64_t kGroup = 64;           // candidates per group (one wave)
 constexpr uint64_t kChunkGroups = 1024;   // groups per chunk of the offsets scan
 uint64_t verify_groups(uint64_t count);

@@ -864,9 +864,9 @@ template <int PASS>
 __device__ __forceinline__ void verify_one(const VerifyParams& p, uint64_t c, uint32_t lds,
                                            uint32_t codebuf, uint32_t keep, uint32_t head,
                                            uint64_t o, uint32_t& count) {
-  if (!PASS && p.dead != nullptr && p.dead[c]) {
+  if (!PASS && p.dead != nullptr && (p.dead[c] & kClassDead)) {
     // the scan's drain already ran this candidate's one guard on the bytes it
-    // held (kernels.hip key_dead): nothing to read
+    // held (kernels.hip key_class): nothing to read
     p.keep[c] = 0;
     count = 0;
     return;
@@ -983,11 +983,23 @@ __global__ __launch_bounds__(256) void verify_kernel(VerifyParams p) {
     const uint64_t o = group_offset(p, g);
     if (group_offset(p, g + 1) == o) continue;
     const uint64_t c = g * kGroup + (threadIdx.x & 63u);
-    const uint32_t keep =
-        c < p.count && (p.dead == nullptr || p.dead[c] == 0) ? p.keep[c] : 0u;
-    uint32_t n = keep == 0 ? 0u : p.counts[c];
+    // the scan's class (kernels.hip key_class): dead -- nothing; kept -- every
+    // call of the key's list; else pass 0's decisions
+    const uint32_t cls = c < p.count && p.dead != nullptr ? p.dead[c] : 0u;
+    uint32_t keep = 0, n = 0, head = 0;
+    if (cls & kClassKept) {
+      n = p.kd_n[(cls >> 2) & 3u];
+      keep = (1u << n) - 1u;
+      head = p.kd_head[(cls >> 2) & 3u];
+    } else if (c < p.count && !(cls & kClassDead)) {
+      keep = p.keep[c];
+      if (keep != 0) {
+        n = p.counts[c];
+        head = p.heads[c];
+      }
+    }
     const uint32_t pre = wave_exclusive(n);
-    if (keep != 0) verify_one<1>(p, c, lds, codebuf, keep, p.heads[c], o + pre, n);
+    if (keep != 0) verify_one<1>(p, c, lds, codebuf, keep, head, o + pre, n);
   }
 }
 
@@ -1013,11 +1025,37 @@ __global__ __launch_bounds__(256) void verify_live_kernel(VerifyParams p) {
 // the chunk's exclusive scan in place (entry `groups`, past the last group,
 // counts 0) and its total into chunk_off[chunk].
 __global__ __launch_bounds__(1024) void group_scan_kernel(uint64_t* block_off, uint64_t groups,
-                                                          uint64_t* chunk_off) {
+                                                          uint64_t* chunk_off, const uint8_t* cls,
+                                                          uint64_t count, KeptLists kept) {
   __shared__ uint64_t wsum[16];
   const uint32_t lane = threadIdx.x & 63u, w = threadIdx.x >> 6;
   const uint64_t i = (uint64_t)blockIdx.x * kChunkGroups + threadIdx.x;
-  const uint64_t v = i < groups ? block_off[i] : 0;
+  uint64_t v = i < groups ? block_off[i] : 0;
+  if (cls != nullptr && i < groups) {
+    // + the records of the group's "kept" candidates (their calls are the
+    // key's whole list; pass 0 never saw them)
+    const uint64_t c0 = i * kGroup, c1 = min(c0 + kGroup, count);
+    auto add = [&](uint32_t word) {   // four class bytes
+#pragma unroll
+      for (int b = 0; b < 4; ++b) {
+        const uint32_t x = (word >> (8 * b)) & 0xFFu;
+        v += (x & kClassKept) ? kept.n[(x >> 2) & 3u] : 0u;
+      }
+    };
+    if (c1 - c0 == kGroup) {   // a whole group: four 16-byte loads
+      const uint4* q = reinterpret_cast<const uint4*>(cls + c0);
+#pragma unroll
+      for (int k = 0; k < 4; ++k) {
+        const uint4 u = q[k];
+        add(u.x);
+        add(u.y);
+        add(u.z);
+        add(u.w);
+      }
+    } else {
+      for (uint64_t c = c0; c < c1; ++c) add(cls[c]);
+    }
+  }
   uint64_t inc = v;
 #pragma unroll
   for (int d = 1; d < 64; d <<= 1) {
@@ -1106,12 +1144,13 @@ hipError_t launch_verify_live(const VerifyParams& p, hipStream_t s) {
 }
 
 hipError_t launch_block_offsets(uint64_t* block_off, uint64_t* chunk_off, uint64_t count,
-                                uint64_t* total, hipStream_t s) {
+                                uint64_t* total, const uint8_t* cls, const KeptLists& kept,
+                                hipStream_t s) {
   const uint64_t groups = verify_groups(count);
   if (groups == 0) return hipMemsetAsync(total, 0, sizeof(uint64_t), s);
   const uint64_t chunks = verify_chunks(count);
   hipLaunchKernelGGL(group_scan_kernel, dim3((uint32_t)chunks), dim3(1024), 0, s, block_off, groups,
-                     chunk_off);
+                     chunk_off, cls, count, kept);
   hipLaunchKernelGGL(block_offsets_kernel, dim3(1), dim3(1024), 0, s, chunk_off, chunks, total);
   return hipGetLastError();
 }
