@@ -1,3 +1,7 @@
+"""Candidates of a 1 GiB scan that the byte-key drain classified (kernels.hip
+key_class: dead or kept), counted through the diagnostic build's
+yr_amd__diag_dead_count.  GPU box:  python tools/dead_count.py
+"""
 import ctypes, os, sys
 sys.path.insert(0, os.getcwd())
 os.environ["YARA_AMD_LIB"] = os.path.join(os.getcwd(), "yara_amd/_diag/libyara_amd.so")
