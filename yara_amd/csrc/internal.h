@@ -163,16 +163,19 @@ constexpr uint32_t kNodeL2 = 256;
 constexpr uint32_t kNodeZero4 = 256 + 65536;
 constexpr uint32_t kNodeHeadWords = kNodeZero4 + 4;   // (keeps the buckets 16-B aligned)
 
-// The class the byte-key drain gives a certain candidate (kernels.hip
-// key_class; ScanParams::dead holds it per candidate): 0 = undecided, 1 = no
+// The class of a certain candidate (kernels.hip key_class, decided in the
+// compaction; ScanParams::dead holds it per candidate): 0 = undecided, 1 = no
 // call of its list can have an effect, 2 | k << 2 = every call of 1-byte key
-// k's list is kept (ScanParams::kd_n / kd_head).  A segment output entry
-// carries it in bits kOutClassShift.., a pending entry's offset in bits
-// kPendClassShift..; segment offsets are below 2^20.
-constexpr uint32_t kOutClassShift = 28;
-constexpr uint32_t kOutOffsetMask = (1u << kOutClassShift) - 1u;
-constexpr uint32_t kPendClassShift = 24;
-constexpr uint32_t kPendOffsetMask = (1u << kPendClassShift) - 1u;
+// k's list is kept (ScanParams::kd_n / kd_head).  The scan marks a certain
+// candidate's segment output entry with kOutCertain and the position of its
+// key in the four bytes it stores beside it (ScanParams::seg_x) in bits
+// kOutKeyShift..; a pending entry carries that position in bits
+// kPendKeyShift..; segment offsets are below 2^20.
+constexpr uint32_t kOutCertain = 0x40000000u;
+constexpr uint32_t kOutKeyShift = 28;
+constexpr uint32_t kOutOffsetMask = (1u << 20) - 1u;
+constexpr uint32_t kPendKeyShift = 24;
+constexpr uint32_t kPendOffsetMask = (1u << 20) - 1u;
 constexpr uint32_t kClassDead = 1u;
 constexpr uint32_t kClassKept = 2u;
 
@@ -209,6 +212,8 @@ struct ScanParams {
   // bytes): the list's length and head, and the smallest position at which
   // every call is made (the largest backtrack, scanner.c:107)
   uint32_t kd_n[4], kd_head[4], kd_min_pos[4];
+  uint32_t* seg_x;          // null, or beside seg_out: a certain candidate's four bytes
+                            // (the one before its key, the key, the two after)
   uint8_t* dead;            // null, or per output candidate its class (key_class;
                             // written by the compaction), and
   uint32_t* live;           // [0] = count, then the other candidates' indices (any order)

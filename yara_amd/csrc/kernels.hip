@@ -201,6 +201,48 @@ constexpr uint32_t kConfirmed = 0x80000000u;
 static_assert(kSegment <= kConfirmed, "segment offsets must leave the confirmed bit free");
 static_assert(kQueueCap == kWave, "a drain takes the whole ring, one entry per lane");
 
+// The class of a certain candidate (internal.h kClass*), one lane per pending
+// entry in the flush.  For a 1-byte key whose state is its own node
+// (ScanParams::kd_*, scanner.cpp key_classes) either every call of the list is
+// kept whatever the bytes ("kept" keys: plain literals that fit in the atom),
+// or the list is one call decided by a guard on the bytes next to the key.  x
+// = the four bytes the drain kept for the candidate, the key at byte kp >= 1
+// (the byte before it at kp - 1): the guard is decided only if every byte it
+// tests lies in x and the block.  Pre-verification then never reads the input
+// for the candidate.
+__device__ __forceinline__ uint32_t key_class(const ScanParams& p, uint32_t x, uint32_t kp,
+                                              uint64_t pos) {
+  const uint32_t key = (x >> (8 * kp)) & 0xFFu, prev = (x >> (8 * kp - 8)) & 0xFFu;
+  uint32_t info = 0, m = 0, v = 0, x0 = 0, x1 = 0, kidx = 0, min_pos = 0;
+#pragma unroll
+  for (uint32_t k = 0; k < kMaxByteKeys; ++k) {
+    const bool is = k < p.n_byte_keys && key == ((p.byte_keys >> (8 * k)) & 0xFFu);
+    info = is ? p.kd_info[k] : info;
+    m = is ? p.kd_m[k] : m;
+    v = is ? p.kd_v[k] : v;
+    x0 = is ? p.kd_x0[k] : x0;
+    x1 = is ? p.kd_x1[k] : x1;
+    min_pos = is ? p.kd_min_pos[k] : min_pos;
+    kidx = is ? k : kidx;
+  }
+  if (!(info & 1u)) return 0;
+  if (info & 2u) {
+    // the byte before the key among the exclusions: zero-byte test
+    const uint32_t pv = prev * 0x01010101u;
+    const uint32_t a = pv ^ x0, b = pv ^ x1;
+    if ((((a - 0x01010101u) & ~a) | ((b - 0x01010101u) & ~b)) & 0x80808080u) return 0;
+  }
+  if (info & 4u) return pos >= min_pos ? (kClassKept | kidx << 2) : 0u;
+  // shift jj tests x bytes s0 + jj + t for the t <= tmax with mask byte t set
+  const int32_t s0 = (int32_t)kp + (int32_t)(int8_t)(info >> 8);
+  const uint32_t span = (info >> 16) & 15u, tmax = (info >> 20) & 3u;
+  const int64_t end = (int64_t)pos + (int8_t)(info >> 24);
+  if (s0 < 0 || s0 + (int32_t)(span + tmax) > 3 || end > (int64_t)p.block_size) return 0;
+  bool hit = false;
+  for (uint32_t jj = 0; jj <= span; ++jj) hit |= ((x >> (8 * ((uint32_t)s0 + jj))) & m) == v;
+  return hit ? 0u : kClassDead;
+}
+
 // Bucket-probe every pending hit (one lane each) and append the survivors,
 // in order, to the segment's output.
 template <int MODE>
@@ -208,7 +250,7 @@ __device__ __forceinline__ void flush_pending(const ScanParams& p, WaveQueue& q,
                                               uint64_t seg_start, uint32_t* out, uint32_t& found) {
   __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
   bool keep = false;
-  uint32_t off = 0;
+  uint32_t off = 0, xv = 0;
   if constexpr (MODE == kModeByteKeys) {
     // confirmed entries need no probe; a flush of nothing else makes no
     // memory round trip at all
@@ -219,7 +261,9 @@ __device__ __forceinline__ void flush_pending(const ScanParams& p, WaveQueue& q,
     const bool probe = lane < q.pend_n && !conf;
     keep = lane < q.pend_n && conf;
     if (__ballot(probe) != 0 && probe) keep = exact_check(e.x, seg_start + off + 1, p);
-    off |= ((e.y & ~kConfirmed) >> kPendClassShift) << kOutClassShift;   // (certain: kept either way)
+    xv = e.x;
+    if (p.seg_x != nullptr && conf)   // (its four bytes and its key's place for key_class)
+      off |= kOutCertain | (e.y >> kPendKeyShift & 3u) << kOutKeyShift;
   } else if (lane < q.pend_n) {
     const u32x2 e = lds_load<u32x2>(q.pend + 8 * lane);
     off = e.y;
@@ -229,7 +273,10 @@ __device__ __forceinline__ void flush_pending(const ScanParams& p, WaveQueue& q,
   if (keep) {
     const uint32_t idx = found + __builtin_amdgcn_mbcnt_hi((uint32_t)(b >> 32),
                                                            __builtin_amdgcn_mbcnt_lo((uint32_t)b, 0u));
-    if (idx < p.seg_cap) out[idx] = off;
+    if (idx < p.seg_cap) {
+      out[idx] = off;
+      if (MODE == kModeByteKeys && p.seg_x != nullptr) p.seg_x[(out - p.seg_out) + idx] = xv;
+    }
   }
   found += (uint32_t)__popcll(b);
   q.pend_n = 0;
@@ -343,55 +390,6 @@ template <int MODE>
 constexpr bool kDeferFl =
     YAMD_DEFER_FL &&
     (MODE == 0 || MODE == 12 || MODE == kModeByteKeys || kEven<MODE> || kByteKeyAblation<MODE>);
-
-// The class of a certain candidate (internal.h kClass*): for a 1-byte key whose
-// state is its own node (ScanParams::kd_*, scanner.cpp key_classes), either
-// every call of the list is kept whatever the bytes ("kept" keys: plain
-// literals that fit in the atom), or the list is one call decided by a guard
-// on the bytes after the key, which the drain tests on the ring entry (lane
-// byte j is the key): dead only if every tested byte lies in the lane and
-// inside the block and no shift passes.  Pre-verification then never reads
-// the input for the candidate.
-__device__ __forceinline__ uint32_t key_class(const ScanParams& p, uint32_t ent, uint32_t j,
-                                              uint32_t w_prev, uint64_t pos) {
-  const uint32_t key = w_prev >> 24;
-  uint32_t info = 0, m = 0, v = 0, x0 = 0, x1 = 0, kidx = 0, min_pos = 0;
-#pragma unroll
-  for (uint32_t k = 0; k < kMaxByteKeys; ++k) {
-    const bool is = k < p.n_byte_keys && key == ((p.byte_keys >> (8 * k)) & 0xFFu);
-    info = is ? p.kd_info[k] : info;
-    m = is ? p.kd_m[k] : m;
-    v = is ? p.kd_v[k] : v;
-    x0 = is ? p.kd_x0[k] : x0;
-    x1 = is ? p.kd_x1[k] : x1;
-    min_pos = is ? p.kd_min_pos[k] : min_pos;
-    kidx = is ? k : kidx;
-  }
-  if (!(info & 1u)) return 0;
-  if (info & 2u) {
-    // the byte before the key (window byte 2) among the exclusions: zero-byte test
-    const uint32_t pv = (w_prev >> 16 & 0xFFu) * 0x01010101u;
-    const uint32_t a = pv ^ x0, b = pv ^ x1;
-    if ((((a - 0x01010101u) & ~a) | ((b - 0x01010101u) & ~b)) & 0x80808080u) return 0;
-  }
-  if (info & 4u) return pos >= min_pos ? (kClassKept | kidx << 2) : 0u;
-  // the tested bytes of shift jj: region bytes jj + t for the t with mask byte
-  // t set, t <= tmax (info bits 20..21); they must all lie in the lane
-  const int32_t rs = (int32_t)j + (int32_t)(int8_t)(info >> 8);
-  const uint32_t span = (info >> 16) & 15u, tmax = (info >> 20) & 3u;
-  const int64_t end = (int64_t)pos + (int8_t)(info >> 24);
-  if (rs < 0 || rs + (int32_t)(span + tmax) >= kBytesPerLane || end > (int64_t)p.block_size)
-    return 0;
-  bool hit = false;
-  for (uint32_t jj = 0; jj <= span; ++jj) {
-    // the 4 bytes from rs + jj, or those ending at the lane's last byte shifted
-    // down (bytes past it are untested)
-    const uint32_t e = min((uint32_t)rs + jj + 3, (uint32_t)kBytesPerLane - 1);
-    const uint32_t x = window4(ent, e) >> (8 * ((uint32_t)rs + jj + 3 - e));
-    hit |= (x & m) == v;
-  }
-  return hit ? 0u : kClassDead;
-}
 
 // Consume a deferred drain's first-level words: the lanes' hits that pass go,
 // in order, to the pending list.
@@ -516,15 +514,20 @@ __device__ __forceinline__ void drain(const ScanParams& p, WaveQueue& q, uint32_
     while (maybe != 0u && idx < base + kWave) {
       const uint32_t j = (uint32_t)__builtin_ctz(maybe);
       maybe &= maybe - 1;
-      const uint32_t w = window4(ent, j);
-      uint32_t y = off0 + j;
+      uint32_t y = off0 + j, e = j;
       if constexpr (MODE == kModeByteKeys) {
         if ((kmask >> j) & 1u) {
+          // a certain candidate needs no window for the exact check: keep the
+          // byte before it, itself and the two after (key_class), the key at
+          // byte kp of them
           y |= kConfirmed;
-          if (p.dead != nullptr) y |= key_class(p, ent, j, w, seg_start + off0 + j + 1) << kPendClassShift;
+          if (p.seg_x != nullptr) {
+            e = min(j + 2, (uint32_t)kBytesPerLane - 1);
+            y |= (j + 3 - e) << kPendKeyShift;
+          }
         }
       }
-      lds_store2(q.pend + 8 * (idx - base), w, y);
+      lds_store2(q.pend + 8 * (idx - base), window4(ent, e), y);
       ++idx;
     }
     if (end <= base + kWave) {
@@ -979,38 +982,37 @@ __global__ __launch_bounds__(1024) void seg_offsets_kernel(const uint32_t* seg_c
   }
 }
 
-__global__ __launch_bounds__(256) void seg_scatter_kernel(const uint32_t* seg_count,
-                                                          const uint32_t* seg_out,
-                                                          const uint64_t* seg_base,
-                                                          const uint64_t* seg_offset, uint32_t cap,
-                                                          uint64_t byte_begin, uint32_t seg_bytes,
-                                                          uint32_t n_segments, uint64_t* positions,
-                                                          uint8_t* dead, uint32_t* live) {
+__global__ __launch_bounds__(256) void seg_scatter_kernel(ScanParams p, const uint64_t* seg_offset,
+                                                          uint64_t* positions) {
   // one wave per segment (segments hold tens to hundreds of candidates)
   const uint32_t seg = blockIdx.x * (blockDim.x / kWave) + threadIdx.x / kWave;
-  if (seg >= n_segments) return;
-  const uint32_t c = min(seg_count[seg], cap);
-  const uint64_t base = byte_begin + (uint64_t)seg * seg_bytes + 1;  // position = byte + 1
-  const uint32_t* src = seg_out + (seg_base ? seg_base[seg] : (size_t)seg * cap);
+  if (seg >= p.n_segments) return;
+  const uint32_t c = min(p.seg_count[seg], p.seg_cap);
+  const uint64_t base = p.byte_begin + (uint64_t)seg * p.seg_bytes + 1;  // position = byte + 1
+  const size_t at0 = p.seg_base ? p.seg_base[seg] : (size_t)seg * p.seg_cap;
+  const uint32_t* src = p.seg_out + at0;
   uint64_t* dst = positions + seg_offset[seg];
   const uint32_t lane = threadIdx.x % kWave;
   for (uint32_t i0 = 0; i0 < c; i0 += kWave) {   // (wave-uniform trips: the ballot below)
     const uint32_t i = i0 + lane;
-    const uint32_t e = i < c ? src[i] : kClassDead << kOutClassShift;
-    const uint32_t cls = e >> kOutClassShift;
-    if (i < c) dst[i] = base + (e & kOutOffsetMask);
-    if (dead == nullptr) continue;
-    if (i < c) dead[seg_offset[seg] + i] = (uint8_t)cls;
+    const uint32_t e = i < c ? src[i] : 0u;
+    const uint64_t pos = base + (e & kOutOffsetMask);
+    if (i < c) dst[i] = pos;
+    if (p.dead == nullptr) continue;
+    // the certain candidates' classes from the bytes the scan kept beside them
+    uint32_t cls = i < c ? 0u : kClassDead;
+    if (i < c && (e & kOutCertain)) cls = key_class(p, p.seg_x[at0 + i], e >> kOutKeyShift & 3u, pos);
+    if (i < c) p.dead[seg_offset[seg] + i] = (uint8_t)cls;
     // the undecided candidates onto the live list (one atomic per wave)
     const uint64_t lm = __ballot(cls == 0u);
     if (lm == 0) continue;
     const uint32_t leader = (uint32_t)__builtin_ctzll(lm);
     uint32_t at = 0;
-    if (lane == leader) at = atomicAdd(live, (uint32_t)__popcll(lm));
+    if (lane == leader) at = atomicAdd(p.live, (uint32_t)__popcll(lm));
     at = __shfl(at, (int)leader, kWave);
     if (cls == 0u)
-      live[1 + at + __builtin_amdgcn_mbcnt_hi((uint32_t)(lm >> 32),
-                                              __builtin_amdgcn_mbcnt_lo((uint32_t)lm, 0u))] =
+      p.live[1 + at + __builtin_amdgcn_mbcnt_hi((uint32_t)(lm >> 32),
+                                                __builtin_amdgcn_mbcnt_lo((uint32_t)lm, 0u))] =
           (uint32_t)(seg_offset[seg] + i);
   }
 }
@@ -1098,9 +1100,8 @@ hipError_t launch_compact(const ScanParams& p, uint64_t* seg_offset, uint64_t* s
     hipLaunchKernelGGL(seg_offsets_kernel, dim3(1), dim3(1024), 0, s, p.seg_count, p.n_segments,
                        p.seg_cap, seg_offset, summary);
   } else {
-    hipLaunchKernelGGL(seg_scatter_kernel, dim3((p.n_segments + 3) / 4), dim3(256), 0, s,
-                       p.seg_count, p.seg_out, p.seg_base, seg_offset, p.seg_cap, p.byte_begin,
-                       p.seg_bytes, p.n_segments, positions, p.dead, p.live);
+    hipLaunchKernelGGL(seg_scatter_kernel, dim3((p.n_segments + 3) / 4), dim3(256), 0, s, p,
+                       (const uint64_t*)seg_offset, positions);
   }
   return hipGetLastError();
 }

@@ -118,6 +118,8 @@ struct yr_amd_scanner {
   size_t dead_cap = 0;
   uint32_t* d_live = nullptr;           // [0] count, then the other candidates (ScanParams::live)
   size_t live_cap = 0;
+  uint32_t* d_seg_x = nullptr;          // beside the segment outputs (ScanParams::seg_x)
+  size_t seg_x_cap = 0;
   size_t positions_cap = 0;             // entries
   uint64_t* h_summary = nullptr;        // pinned, coherent: {total, max per segment}
   uint64_t* d_hsum = nullptr;           // h_summary mapped for the device: the offsets
@@ -243,9 +245,11 @@ int run_scan(yr_amd_scanner* s) {
   int r = grow(s->d_positions, s->positions_cap, out_cap);
   if (!r && s->tables->kd_any) r = grow(s->d_dead, s->dead_cap, out_cap);
   if (!r && s->tables->kd_any) r = grow(s->d_live, s->live_cap, out_cap + 1);
+  if (!r && s->tables->kd_any) r = grow(s->d_seg_x, s->seg_x_cap, out_cap);
   if (r) return r;
   s->last.dead = s->tables->kd_any ? s->d_dead : nullptr;
   s->last.live = s->tables->kd_any ? s->d_live : nullptr;
+  s->last.seg_x = s->tables->kd_any ? s->d_seg_x : nullptr;
   if (s->timing) HIP_TRY(hipEventRecord(s->ev_begin, s->stream));
   HIP_TRY(launch_scan(p, s->last_grid, s->stream, s->diag_mode));
   if (s->timing) {
@@ -386,6 +390,7 @@ int yr_amd_scanner_destroy(yr_amd_scanner* s) {
   for (void* p : {(void*)s->d_block, (void*)s->d_seg_count,
                   (void*)s->d_seg_offset,
                   (void*)s->d_seg_out, (void*)s->d_positions, (void*)s->d_dead, (void*)s->d_live,
+                  (void*)s->d_seg_x,
                   (void*)s->d_summary,
                   (void*)s->d_vcount, (void*)s->d_vkeep, (void*)s->d_vblock, (void*)s->d_vrec,
                   (void*)s->d_vchunk, (void*)s->d_seg_base,
@@ -476,6 +481,7 @@ int yr_amd_scan_window(yr_amd_scanner* s, const uint8_t* d_window, uint64_t wind
   s->last_empty = s->last_all || byte_end == byte_begin;
   s->last.dead = nullptr;
   s->last.live = nullptr;
+  s->last.seg_x = nullptr;
   if (s->last_empty) return YR_AMD_SUCCESS;
   if (d_window == nullptr) return YR_AMD_INVALID_ARGUMENT;
   HIP_TRY(hipSetDevice(t->device));
