@@ -521,10 +521,8 @@ __device__ __forceinline__ void drain(const ScanParams& p, WaveQueue& q, uint32_
           // byte before it, itself and the two after (key_class), the key at
           // byte kp of them
           y |= kConfirmed;
-          if (p.seg_x != nullptr) {
-            e = min(j + 2, (uint32_t)kBytesPerLane - 1);
-            y |= (j + 3 - e) << kPendKeyShift;
-          }
+          e = min(j + 2, (uint32_t)kBytesPerLane - 1);
+          y |= (j + 3 - e) << kPendKeyShift;
         }
       }
       lds_store2(q.pend + 8 * (idx - base), window4(ent, e), y);

@@ -864,9 +864,10 @@ namespace {
 //    largest backtrack on (scanner.c:107) -- or
 //  * the list is one regexp call that call_matters drops whenever its forward
 //    guard fails (a FAST ascii program, or a yr_re_exec one with only the
-//    ascii attempt); the drain tests the guard when its tested bytes lie in
-//    the key's lane.  (YR_AC_MATCH offsets: the call's offset is position -
-//    backtrack, the guard's region starts `base` bytes after it.)
+//    ascii attempt) and whose tested bytes fit the four bytes the scan keeps
+//    beside a certain candidate (the one before the key, the key, two after);
+//    the compaction tests it.  (YR_AC_MATCH offsets: the call's offset is
+//    position - backtrack, the guard's region starts `base` bytes after it.)
 // Pre-verification then never reads the input for such candidates.
 void key_classes(yr_amd_tables* t) {
   const FlatTables& f = t->flat;
@@ -919,10 +920,13 @@ void key_classes(yr_amd_tables* t) {
       const int base = e.fguard_bs & 15, span = e.fguard_bs >> 4;
       const int rs = base + 1 - (int)e.backtrack;          // region start - key byte
       const int end = base + span + 4 - (int)e.backtrack;  // region end - position
-      if (rs < -128 || rs > 127 || end < -128 || end > 127) continue;
+      const uint32_t tmax = (31u - (uint32_t)__builtin_clz(e.fguard.m)) >> 3;   // last tested byte
+      // every tested byte must fit the four the scan keeps (the byte before
+      // the key, the key, the two after: kernels.hip key_class) for some place
+      // of the key among them
+      if (rs < -3 || rs + span + (int)tmax > 2 || end < -128 || end > 127) continue;
       t->kd_m[k] = e.fguard.m;
       t->kd_v[k] = e.fguard.v;
-      const uint32_t tmax = (31u - (uint32_t)__builtin_clz(e.fguard.m)) >> 3;   // last tested byte
       info = 1u | ((uint32_t)(uint8_t)(int8_t)rs << 8) | ((uint32_t)span << 16) | (tmax << 20) |
              ((uint32_t)(uint8_t)(int8_t)end << 24);
     }
