@@ -507,10 +507,12 @@ int yr_amd_tables_set_profiling(yr_amd_tables* tables, int enable);
  * Kernel timing (measurement support): when enabled, the scanner records HIP
  * events around its scan kernel on its own stream; yr_amd_scanner_kernel_ms
  * returns the duration of the last scan kernel launch (after the scan result
- * was collected).
+ * was collected), yr_amd_scanner_scan_ms that of the scan and its compaction
+ * into the position list (the candidate classes included).
  */
 int yr_amd_scanner_set_timing(yr_amd_scanner* scanner, int enable);
 int yr_amd_scanner_kernel_ms(yr_amd_scanner* scanner, float* ms);
+int yr_amd_scanner_scan_ms(yr_amd_scanner* scanner, float* ms);
 
 /*
  * Benchmark/test utility (not part of the libyara path): fill a device buffer

@@ -221,8 +221,8 @@ def test_profiling_count_only_records(case):
 def test_scan_side_guard_flags(tail):
     """1-byte keys whose list is one regexp call decided by its forward guard
     (rx's `[` and `]`: the guard tests the key and the next byte, C3) are
-    decided in the scan kernel's drain (kernels.hip key_dead) and skipped by the
-    count pass.  Random bytes with `[` / `]` planted at every lane byte, half of
+    decided from the bytes the scan keeps beside them (kernels.hip key_class,
+    in the compaction) and skipped by pre-verification.  Random bytes with `[` / `]` planted at every lane byte, half of
     them followed by C3 (the guard passes, the call is searched), and the block
     cut `tail` bytes after a planted key (regions past the block end are never
     flagged): the device records equal the oracle's kept calls."""
@@ -243,6 +243,37 @@ def test_scan_side_guard_flags(tail):
     P, K = oracle.walk_verify(ref_tables("rx"), data)
     keep = oracle.literal_effect(z, P, K, data)
     r = yara_amd.Scanner(yara_amd.Tables.from_npz(tables_npz("rx"), device=0, strings=True)).verify_calls(data)
+    off = P.astype(np.uint64) - z["pool_backtrack"][K].astype(np.uint64)
+    np.testing.assert_array_equal(r["offset"], off[keep])
+    np.testing.assert_array_equal(r["pool_index"], K[keep])
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("tail", [0, 1, 3, 5, 6, 7, 16, 1000])
+def test_scan_side_guard_after_key(tail):
+    """fuzz0's one 1-byte key (`d`, the hex string { 64 ( .. ) [0-4] 3E }) is
+    decided by a guard over the five bytes after it: the scan keeps the bytes
+    after the key instead of the one before (scanner.cpp key_classes picks the
+    place per table), and near a lane's end or the block's end the candidate
+    stays undecided.  `d` planted at every lane byte with `>` 1..7 bytes after
+    it (the guard passes for 1..5) and the block cut `tail` bytes after a key:
+    the device records equal the oracle's kept calls."""
+    import yara_amd
+    from conftest import ref_tables
+    z = np.load(tables_npz("fuzz0"))
+    n = (1 << 20) + 77
+    data = oracle.xorshift(n, 67).copy()
+    k = 0
+    for off in range(5, n - 64, 37):
+        data[off] = 0x64
+        data[off + 1 + k % 7] = 0x3E
+        k += 1
+    cut = (n - 200) + tail
+    data[n - 200] = 0x64
+    data = np.ascontiguousarray(data[:cut])
+    P, K = oracle.walk_verify(ref_tables("fuzz0"), data)
+    keep = oracle.literal_effect(z, P, K, data)
+    r = yara_amd.Scanner(yara_amd.Tables.from_npz(tables_npz("fuzz0"), device=0, strings=True)).verify_calls(data)
     off = P.astype(np.uint64) - z["pool_backtrack"][K].astype(np.uint64)
     np.testing.assert_array_equal(r["offset"], off[keep])
     np.testing.assert_array_equal(r["pool_index"], K[keep])

@@ -17,3 +17,13 @@ for rules, gib in (("rx", 1), ("fuzz0", 1)):
     for _ in range(2):
         sc.scan_device(buf.data_ptr(), n); _, cnt, _ = sc.device_result()
         print(rules, "candidates", cnt, "dead", f(sc._h), flush=True)
+
+# the key classes of every golden table with 1-byte keys (yr_amd__diag_key_classes)
+g = L.yr_amd__diag_key_classes; g.argtypes = [ctypes.c_void_p, ctypes.POINTER(ctypes.c_uint32)]
+for name in sorted(os.listdir("tests/golden/tables")):
+    t = yara_amd.Tables.from_npz(os.path.join("tests/golden/tables", name), device=0, strings=True)
+    o = (ctypes.c_uint32 * 15)()
+    g(t._h, o)
+    if o[2]:
+        print(name[:-4], "kx_end", o[0], "keys", [hex(o[1] >> (8 * k) & 255) for k in range(o[2])],
+              "info", [hex(x) for x in o[3:7]], "m", [hex(x) for x in o[7:11]], "v", [hex(x) for x in o[11:15]], flush=True)

@@ -58,14 +58,18 @@ def main():
             rec.update({"kernel_ms": 0.0, "candidates": n + 1})
         else:
             sc.set_timing(True)
-            ks, cnt = [], 0
+            ks, ss, cnt = [], [], 0
             for _ in range(a.reps):
                 sc.scan_device(buf.data_ptr(), n)
                 cnt = sc.device_result()[1]
                 ks.append(sc.kernel_ms())
+                ss.append(sc.scan_ms())
             sc.set_timing(False)
             k = statistics.median(ks)
-            rec.update({"kernel_ms": round(k, 4), "GB/s": round(n / (k * 1e-3) / 1e9, 1),
+            # scan_ms: the scan kernel and its compaction (the position list and
+            # the candidate classes)
+            rec.update({"kernel_ms": round(k, 4), "scan_ms": round(statistics.median(ss), 4),
+                        "GB/s": round(n / (k * 1e-3) / 1e9, 1),
                         "frac": round(n / (k * 1e-3) / 1e9 / HBM_PEAK_GBS, 4),
                         "candidates": int(cnt)})
         rec.update({"root_accepting": bool(info["root_accepting"]),

@@ -296,6 +296,12 @@ class Scanner:
         _lib.check("yr_amd_scanner_kernel_ms", _lib.lib().yr_amd_scanner_kernel_ms(self._h, ctypes.byref(ms)))
         return ms.value
 
+    def scan_ms(self) -> float:
+        """Duration of the last scan and its compaction (HIP events on the scan stream)."""
+        ms = ctypes.c_float()
+        _lib.check("yr_amd_scanner_scan_ms", _lib.lib().yr_amd_scanner_scan_ms(self._h, ctypes.byref(ms)))
+        return ms.value
+
     def close(self):
         if getattr(self, "_h", None):
             _lib.lib().yr_amd_scanner_destroy(self._h)

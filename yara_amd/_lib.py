@@ -84,6 +84,7 @@ PROTOTYPES = {
     "yr_amd_fill_xorshift64": (_int, [_vp, ctypes.c_uint64, ctypes.c_uint64, ctypes.c_uint64, _vp]),
     "yr_amd_scanner_set_timing": (_int, [_vp, _int]),
     "yr_amd_scanner_kernel_ms": (_int, [_vp, ctypes.POINTER(ctypes.c_float)]),
+    "yr_amd_scanner_scan_ms": (_int, [_vp, ctypes.POINTER(ctypes.c_float)]),
     "yr_amd_version": (ctypes.c_char_p, []),
     "yr_amd_tables_set_strings": (_int, [_vp, _u32p, ctypes.c_uint32, ctypes.POINTER(String),
                                          ctypes.c_uint32, _u8p, ctypes.c_uint64, _u8p]),

@@ -166,16 +166,15 @@ constexpr uint32_t kNodeHeadWords = kNodeZero4 + 4;   // (keeps the buckets 16-B
 // The class of a certain candidate (kernels.hip key_class, decided in the
 // compaction; ScanParams::dead holds it per candidate): 0 = undecided, 1 = no
 // call of its list can have an effect, 2 | k << 2 = every call of 1-byte key
-// k's list is kept (ScanParams::kd_n / kd_head).  The scan marks a certain
-// candidate's segment output entry with kOutCertain and the position of its
-// key in the four bytes it stores beside it (ScanParams::seg_x) in bits
-// kOutKeyShift..; a pending entry carries that position in bits
-// kPendKeyShift..; segment offsets are below 2^20.
-constexpr uint32_t kOutCertain = 0x40000000u;
+// k's list is kept (ScanParams::kd_n / kd_head).  The scan keeps five bytes
+// next to a certain candidate's key: four in ScanParams::seg_x, and its
+// segment output entry (offset below 2^20, the bits of its pending entry)
+// holds kOutCertain, the fifth byte in bits kOutByteShift.. and the key's
+// place among the five + 1 (0: just before them) in bits kOutKeyShift..
+constexpr uint32_t kOutCertain = 0x80000000u;
+constexpr uint32_t kOutByteShift = 20;
 constexpr uint32_t kOutKeyShift = 28;
 constexpr uint32_t kOutOffsetMask = (1u << 20) - 1u;
-constexpr uint32_t kPendKeyShift = 24;
-constexpr uint32_t kPendOffsetMask = (1u << 20) - 1u;
 constexpr uint32_t kClassDead = 1u;
 constexpr uint32_t kClassKept = 2u;
 
@@ -212,8 +211,9 @@ struct ScanParams {
   // bytes): the list's length and head, and the smallest position at which
   // every call is made (the largest backtrack, scanner.c:107)
   uint32_t kd_n[4], kd_head[4], kd_min_pos[4];
-  uint32_t* seg_x;          // null, or beside seg_out: a certain candidate's four bytes
-                            // (the one before its key, the key, the two after)
+  uint32_t* seg_x;          // null, or beside seg_out: a certain candidate's first four
+                            // bytes (lane bytes s .. s + 3, s = min(key + kx_end - 3, 11))
+  uint32_t kx_end;          // 2..4 (scanner.cpp key_classes)
   uint8_t* dead;            // null, or per output candidate its class (key_class;
                             // written by the compaction), and
   uint32_t* live;           // [0] = count, then the other candidates' indices (any order)

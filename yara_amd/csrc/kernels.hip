@@ -197,22 +197,23 @@ template <int MODE>
 constexpr bool kByteKeyAblation = MODE == 24 || MODE == 25;
 // A pending entry's offset with this bit set is a certain candidate (its last
 // byte is a 1-byte key): no bucket probe.  (Segment offsets are < 2^20.)
-constexpr uint32_t kConfirmed = 0x80000000u;
-static_assert(kSegment <= kConfirmed, "segment offsets must leave the confirmed bit free");
+constexpr uint32_t kConfirmed = kOutCertain;   // (a pending entry becomes the output entry)
+static_assert(kSegment <= kOutOffsetMask + 1u, "segment offsets must leave the top bits free");
 static_assert(kQueueCap == kWave, "a drain takes the whole ring, one entry per lane");
 
-// The class of a certain candidate (internal.h kClass*), one lane per pending
-// entry in the flush.  For a 1-byte key whose state is its own node
+// The class of a certain candidate (internal.h kClass*), one lane per output
+// entry in the compaction.  For a 1-byte key whose state is its own node
 // (ScanParams::kd_*, scanner.cpp key_classes) either every call of the list is
 // kept whatever the bytes ("kept" keys: plain literals that fit in the atom),
-// or the list is one call decided by a guard on the bytes next to the key.  x
-// = the four bytes the drain kept for the candidate, the key at byte kp >= 1
-// (the byte before it at kp - 1): the guard is decided only if every byte it
-// tests lies in x and the block.  Pre-verification then never reads the input
-// for the candidate.
-__device__ __forceinline__ uint32_t key_class(const ScanParams& p, uint32_t x, uint32_t kp,
+// or the list is one call decided by a guard on the bytes next to the key.  w
+// = the five bytes the scan kept for the candidate, the key at byte kp of them
+// (-1: just before them; then the table has one 1-byte key): the byte before
+// the key and the guard are decided only if every byte they test lies in w and
+// the block.  Pre-verification then never reads the input for the candidate.
+__device__ __forceinline__ uint32_t key_class(const ScanParams& p, uint64_t w, int32_t kp,
                                               uint64_t pos) {
-  const uint32_t key = (x >> (8 * kp)) & 0xFFu, prev = (x >> (8 * kp - 8)) & 0xFFu;
+  if (kp < 0 && p.n_byte_keys != 1) return 0;
+  const uint32_t key = kp < 0 ? (p.byte_keys & 0xFFu) : (uint32_t)(w >> (8 * kp)) & 0xFFu;
   uint32_t info = 0, m = 0, v = 0, x0 = 0, x1 = 0, kidx = 0, min_pos = 0;
 #pragma unroll
   for (uint32_t k = 0; k < kMaxByteKeys; ++k) {
@@ -228,18 +229,19 @@ __device__ __forceinline__ uint32_t key_class(const ScanParams& p, uint32_t x, u
   if (!(info & 1u)) return 0;
   if (info & 2u) {
     // the byte before the key among the exclusions: zero-byte test
-    const uint32_t pv = prev * 0x01010101u;
+    if (kp < 1) return 0;
+    const uint32_t pv = ((uint32_t)(w >> (8 * kp - 8)) & 0xFFu) * 0x01010101u;
     const uint32_t a = pv ^ x0, b = pv ^ x1;
     if ((((a - 0x01010101u) & ~a) | ((b - 0x01010101u) & ~b)) & 0x80808080u) return 0;
   }
   if (info & 4u) return pos >= min_pos ? (kClassKept | kidx << 2) : 0u;
-  // shift jj tests x bytes s0 + jj + t for the t <= tmax with mask byte t set
-  const int32_t s0 = (int32_t)kp + (int32_t)(int8_t)(info >> 8);
+  // shift jj tests w bytes s0 + jj + t for the t <= tmax with mask byte t set
+  const int32_t s0 = kp + (int32_t)(int8_t)(info >> 8);
   const uint32_t span = (info >> 16) & 15u, tmax = (info >> 20) & 3u;
   const int64_t end = (int64_t)pos + (int8_t)(info >> 24);
-  if (s0 < 0 || s0 + (int32_t)(span + tmax) > 3 || end > (int64_t)p.block_size) return 0;
+  if (s0 < 0 || s0 + (int32_t)(span + tmax) > 4 || end > (int64_t)p.block_size) return 0;
   bool hit = false;
-  for (uint32_t jj = 0; jj <= span; ++jj) hit |= ((x >> (8 * ((uint32_t)s0 + jj))) & m) == v;
+  for (uint32_t jj = 0; jj <= span; ++jj) hit |= ((uint32_t)(w >> (8 * ((uint32_t)s0 + jj))) & m) == v;
   return hit ? 0u : kClassDead;
 }
 
@@ -257,13 +259,11 @@ __device__ __forceinline__ void flush_pending(const ScanParams& p, WaveQueue& q,
     u32x2 e = {0u, 0u};
     if (lane < q.pend_n) e = lds_load<u32x2>(q.pend + 8 * lane);
     const bool conf = (e.y & kConfirmed) != 0u;
-    off = e.y & kPendOffsetMask;
+    off = e.y;   // (a certain entry's bits for key_class with it)
     const bool probe = lane < q.pend_n && !conf;
     keep = lane < q.pend_n && conf;
     if (__ballot(probe) != 0 && probe) keep = exact_check(e.x, seg_start + off + 1, p);
     xv = e.x;
-    if (p.seg_x != nullptr && conf)   // (its four bytes and its key's place for key_class)
-      off |= kOutCertain | (e.y >> kPendKeyShift & 3u) << kOutKeyShift;
   } else if (lane < q.pend_n) {
     const u32x2 e = lds_load<u32x2>(q.pend + 8 * lane);
     off = e.y;
@@ -517,12 +517,12 @@ __device__ __forceinline__ void drain(const ScanParams& p, WaveQueue& q, uint32_
       uint32_t y = off0 + j, e = j;
       if constexpr (MODE == kModeByteKeys) {
         if ((kmask >> j) & 1u) {
-          // a certain candidate needs no window for the exact check: keep the
-          // byte before it, itself and the two after (key_class), the key at
-          // byte kp of them
-          y |= kConfirmed;
-          e = min(j + 2, (uint32_t)kBytesPerLane - 1);
-          y |= (j + 3 - e) << kPendKeyShift;
+          // a certain candidate needs no window for the exact check: keep
+          // five bytes next to it for key_class, lane bytes e - 3 .. e + 1
+          // (e = min(j + kx_end, 14)), the key at place j + 3 - e of them
+          e = min(j + p.kx_end, (uint32_t)kBytesPerLane - 2);
+          y |= kConfirmed | (uint32_t)lds_load<uint8_t>(ent + e + 1) << kOutByteShift |
+               (j + 4 - e) << kOutKeyShift;
         }
       }
       lds_store2(q.pend + 8 * (idx - base), window4(ent, e), y);
@@ -980,38 +980,70 @@ __global__ __launch_bounds__(1024) void seg_offsets_kernel(const uint32_t* seg_c
   }
 }
 
-__global__ __launch_bounds__(256) void seg_scatter_kernel(ScanParams p, const uint64_t* seg_offset,
-                                                          uint64_t* positions) {
-  // one wave per segment (segments hold tens to hundreds of candidates)
-  const uint32_t seg = blockIdx.x * (blockDim.x / kWave) + threadIdx.x / kWave;
-  if (seg >= p.n_segments) return;
+constexpr uint32_t kScatterWaves = 8;   // waves per segment in the scatter
+
+__global__ __launch_bounds__(kScatterWaves * kWave) void seg_scatter_kernel(
+    ScanParams p, const uint64_t* seg_offset, uint64_t* positions) {
+  // one block per segment (segments hold up to ~10^4 candidates), its waves
+  // interleaved 64 candidates apart
+  __shared__ uint32_t wlive[kScatterWaves + 1];
+  const uint32_t seg = blockIdx.x;
   const uint32_t c = min(p.seg_count[seg], p.seg_cap);
   const uint64_t base = p.byte_begin + (uint64_t)seg * p.seg_bytes + 1;  // position = byte + 1
   const size_t at0 = p.seg_base ? p.seg_base[seg] : (size_t)seg * p.seg_cap;
   const uint32_t* src = p.seg_out + at0;
-  uint64_t* dst = positions + seg_offset[seg];
-  const uint32_t lane = threadIdx.x % kWave;
-  for (uint32_t i0 = 0; i0 < c; i0 += kWave) {   // (wave-uniform trips: the ballot below)
+  const uint64_t first = seg_offset[seg];
+  uint64_t* dst = positions + first;
+  const uint32_t lane = threadIdx.x % kWave, w = threadIdx.x / kWave;
+  constexpr uint32_t kStride = kScatterWaves * kWave;
+  uint32_t n_live = 0;
+  // (latency-bound: a few hundred candidates per wave; the loads of an
+  // iteration issue together and unrolled iterations overlap)
+#pragma unroll 4
+  for (uint32_t i0 = w * kWave; i0 < c; i0 += kStride) {   // (wave-uniform trips: the ballot)
     const uint32_t i = i0 + lane;
     const uint32_t e = i < c ? src[i] : 0u;
     const uint64_t pos = base + (e & kOutOffsetMask);
     if (i < c) dst[i] = pos;
     if (p.dead == nullptr) continue;
     // the certain candidates' classes from the bytes the scan kept beside them
+    const uint32_t x = i < c ? p.seg_x[at0 + i] : 0u;
     uint32_t cls = i < c ? 0u : kClassDead;
-    if (i < c && (e & kOutCertain)) cls = key_class(p, p.seg_x[at0 + i], e >> kOutKeyShift & 3u, pos);
-    if (i < c) p.dead[seg_offset[seg] + i] = (uint8_t)cls;
-    // the undecided candidates onto the live list (one atomic per wave)
-    const uint64_t lm = __ballot(cls == 0u);
-    if (lm == 0) continue;
-    const uint32_t leader = (uint32_t)__builtin_ctzll(lm);
-    uint32_t at = 0;
-    if (lane == leader) at = atomicAdd(p.live, (uint32_t)__popcll(lm));
-    at = __shfl(at, (int)leader, kWave);
-    if (cls == 0u)
-      p.live[1 + at + __builtin_amdgcn_mbcnt_hi((uint32_t)(lm >> 32),
-                                                __builtin_amdgcn_mbcnt_lo((uint32_t)lm, 0u))] =
-          (uint32_t)(seg_offset[seg] + i);
+    if (i < c && (e & kOutCertain))
+      cls = key_class(p, x | (uint64_t)(e >> kOutByteShift & 0xFFu) << 32,
+                      (int32_t)(e >> kOutKeyShift & 7u) - 1, pos);
+    if (i < c) p.dead[first + i] = (uint8_t)cls;
+    n_live += (uint32_t)__popcll(__ballot(cls == 0u));
+  }
+  if (p.dead == nullptr) return;
+  // the undecided candidates onto the live list: one atomic per segment (one
+  // per 64 candidates, serialised on the counter, took 1.2 ms for 34 M
+  // candidates), then each lane reads its own class bytes back
+  if (lane == 0) wlive[w] = n_live;
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    uint32_t run = 0;
+    for (uint32_t k = 0; k < kScatterWaves; ++k) {
+      const uint32_t n = wlive[k];
+      wlive[k] = run;
+      run += n;
+    }
+    wlive[kScatterWaves] = run ? atomicAdd(p.live, run) + 1 : 0u;
+  }
+  __syncthreads();
+  if (n_live == 0) return;
+  uint32_t at = wlive[kScatterWaves] + wlive[w];
+  const uint8_t* cl = p.dead + first;
+#pragma unroll 4
+  for (uint32_t i0 = w * kWave; i0 < c; i0 += kStride) {
+    const uint32_t i = i0 + lane;
+    const bool live = i < c && cl[i] == 0u;
+    const uint64_t lm = __ballot(live);
+    if (live)
+      p.live[at + __builtin_amdgcn_mbcnt_hi((uint32_t)(lm >> 32),
+                                            __builtin_amdgcn_mbcnt_lo((uint32_t)lm, 0u))] =
+          (uint32_t)(first + i);
+    at += (uint32_t)__popcll(lm);
   }
 }
 
@@ -1098,7 +1130,7 @@ hipError_t launch_compact(const ScanParams& p, uint64_t* seg_offset, uint64_t* s
     hipLaunchKernelGGL(seg_offsets_kernel, dim3(1), dim3(1024), 0, s, p.seg_count, p.n_segments,
                        p.seg_cap, seg_offset, summary);
   } else {
-    hipLaunchKernelGGL(seg_scatter_kernel, dim3((p.n_segments + 3) / 4), dim3(256), 0, s, p,
+    hipLaunchKernelGGL(seg_scatter_kernel, dim3(p.n_segments), dim3(kScatterWaves * kWave), 0, s, p,
                        (const uint64_t*)seg_offset, positions);
   }
   return hipGetLastError();

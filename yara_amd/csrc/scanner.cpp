@@ -91,6 +91,7 @@ struct yr_amd_tables {
   uint32_t kd_x0[4] = {0, 0, 0, 0}, kd_x1[4] = {0, 0, 0, 0};
   uint32_t kd_n[4] = {0, 0, 0, 0}, kd_head[4] = {0, 0, 0, 0}, kd_min_pos[4] = {0, 0, 0, 0};
   bool kd_any = false;
+  uint32_t kx_end = 2;                // ScanParams::kx_end
   uint32_t* d_nodes = nullptr;        // accepting nodes by string (FlatTables::nodes)
   DevPoolRec* d_pool = nullptr;       // per pool entry: link, backtrack, string, programs
   uint8_t* d_str_bytes = nullptr;
@@ -139,7 +140,7 @@ struct yr_amd_scanner {
 
   // optional kernel timing (HIP events on the scan stream)
   bool timing = false;
-  hipEvent_t ev_begin = nullptr, ev_end = nullptr;
+  hipEvent_t ev_begin = nullptr, ev_end = nullptr, ev_compact = nullptr;
   // recorded behind a scan's result copy: yr_amd_scan_device_result waits for
   // this scan only, so scanners sharing a stream can have the next scan queued
   hipEvent_t ev_done = nullptr;
@@ -259,6 +260,7 @@ int run_scan(yr_amd_scanner* s) {
   HIP_TRY(launch_compact(p, s->d_seg_offset, s->d_hsum, nullptr, false, s->stream));
   if (p.live != nullptr) HIP_TRY(hipMemsetAsync(p.live, 0, sizeof(uint32_t), s->stream));
   HIP_TRY(launch_compact(p, s->d_seg_offset, s->d_hsum, s->d_positions, true, s->stream));
+  if (s->timing) HIP_TRY(hipEventRecord(s->ev_compact, s->stream));
   HIP_TRY(hipEventRecord(s->ev_done, s->stream));
   return YR_AMD_SUCCESS;
 }
@@ -399,6 +401,7 @@ int yr_amd_scanner_destroy(yr_amd_scanner* s) {
   if (s->h_summary) (void)hipHostFree(s->h_summary);
   if (s->ev_begin) (void)hipEventDestroy(s->ev_begin);
   if (s->ev_end) (void)hipEventDestroy(s->ev_end);
+  if (s->ev_compact) (void)hipEventDestroy(s->ev_compact);
   if (s->ev_done) (void)hipEventDestroy(s->ev_done);
   if (s->own_stream && s->stream) (void)hipStreamDestroy(s->stream);
   delete s;
@@ -411,6 +414,7 @@ int yr_amd_scanner_set_timing(yr_amd_scanner* s, int enable) {
     HIP_TRY(hipSetDevice(s->tables->device));
     HIP_TRY(hipEventCreate(&s->ev_begin));
     HIP_TRY(hipEventCreate(&s->ev_end));
+    HIP_TRY(hipEventCreate(&s->ev_compact));
   }
   s->timing = enable != 0;
   s->ev_valid = false;
@@ -431,6 +435,17 @@ int64_t yr_amd__diag_dead_count(yr_amd_scanner* s) {
   return n;
 }
 
+// The key classes of a table (key_classes): out[0] = kx_end, [1] = the
+// 1-byte keys, [2] = their count, [3..6] = kd_info, [7..10] = kd_m, [11..14] = kd_v.
+int yr_amd__diag_key_classes(const yr_amd_tables* t, uint32_t* out) {
+  if (t == nullptr || out == nullptr) return YR_AMD_INVALID_ARGUMENT;
+  out[0] = t->kx_end;
+  out[1] = t->flat.byte_keys;
+  out[2] = t->flat.n_byte_keys;
+  for (int k = 0; k < 4; ++k) out[3 + k] = t->kd_info[k], out[7 + k] = t->kd_m[k], out[11 + k] = t->kd_v[k];
+  return YR_AMD_SUCCESS;
+}
+
 int yr_amd__diag_kernel_mode(yr_amd_scanner* s, int mode) {
   if (s == nullptr || mode < 0 || (mode > 12 && mode != 24 && mode != 25))
     return YR_AMD_INVALID_ARGUMENT;
@@ -443,6 +458,13 @@ int yr_amd_scanner_kernel_ms(yr_amd_scanner* s, float* ms) {
   if (s == nullptr || ms == nullptr || !s->ev_valid) return YR_AMD_INVALID_ARGUMENT;
   HIP_TRY(hipEventSynchronize(s->ev_end));
   HIP_TRY(hipEventElapsedTime(ms, s->ev_begin, s->ev_end));
+  return YR_AMD_SUCCESS;
+}
+
+int yr_amd_scanner_scan_ms(yr_amd_scanner* s, float* ms) {
+  if (s == nullptr || ms == nullptr || !s->ev_valid) return YR_AMD_INVALID_ARGUMENT;
+  HIP_TRY(hipEventSynchronize(s->ev_compact));
+  HIP_TRY(hipEventElapsedTime(ms, s->ev_begin, s->ev_compact));
   return YR_AMD_SUCCESS;
 }
 
@@ -521,6 +543,7 @@ int yr_amd_scan_window(yr_amd_scanner* s, const uint8_t* d_window, uint64_t wind
   p.len_mask = t->flat.len_mask;
   p.byte_keys = t->flat.byte_keys;
   p.n_byte_keys = t->flat.n_byte_keys;
+  p.kx_end = t->kx_end;
   for (int k = 0; k < 4; ++k) {
     p.kd_m[k] = t->kd_m[k];
     p.kd_v[k] = t->kd_v[k];
@@ -872,26 +895,38 @@ namespace {
 void key_classes(yr_amd_tables* t) {
   const FlatTables& f = t->flat;
   t->kd_any = false;
+  t->kx_end = 2;
   for (int k = 0; k < 4; ++k)
     t->kd_m[k] = t->kd_v[k] = t->kd_info[k] = t->kd_x0[k] = t->kd_x1[k] = t->kd_n[k] =
         t->kd_head[k] = t->kd_min_pos[k] = 0;
   if (f.root_accepting || t->h_pool.empty() || diag_env("YAMD_NO_KEY_CLASSES") != nullptr) return;
-  for (uint32_t k = 0; k < f.n_byte_keys && k < 4; ++k) {
+  // Per key the class it can have, then the five bytes the scan keeps beside
+  // its certain candidates (kernels.hip key_class): lane bytes key - kp ..
+  // key - kp + 4 for one kp in {1, 0, -1} per table (kx_end = 3 - kp), the one
+  // under which the most keys are decided.
+  struct Desc {
+    bool ok = false, kept = false;
+    uint32_t nx = 0, xs0 = 0, xs1 = 0, m = 0, v = 0, n = 0, head = 0, min_pos = 0;
+    int rs = 0, span = 0, tmax = 0, end = 0;
+  } d[4];
+  const uint32_t nk = std::min<uint32_t>(f.n_byte_keys, 4);
+  for (uint32_t k = 0; k < nk; ++k) {
     const uint32_t b = (f.byte_keys >> (8 * k)) & 0xFFu;
-    uint8_t xs[8];
-    uint32_t nx = 0;
+    Desc& o = d[k];
     bool too_many = false;
     if ((f.deep_last[b >> 5] >> (b & 31)) & 1u) {
       for (uint32_t x = 0; x < 256; ++x) {
         if (!((f.deep_pair[b * 8 + (x >> 5)] >> (x & 31)) & 1u)) continue;
-        if (nx == 8) { too_many = true; break; }
-        xs[nx++] = (uint8_t)x;
+        if (o.nx == 8) { too_many = true; break; }
+        (o.nx < 4 ? o.xs0 : o.xs1) |= x << (8 * (o.nx & 3));
+        ++o.nx;
       }
     }
     if (too_many) continue;
+    for (uint32_t q = o.nx; q < 8 && o.nx; ++q)   // the first exclusion repeated to fill
+      (q < 4 ? o.xs0 : o.xs1) |= (o.xs0 & 0xFFu) << (8 * (q & 3));
     const uint32_t head = f.nodes[kNodeL1 + b];
     if (head == 0 || head > t->h_pool.size()) continue;
-    uint32_t info = 0;
     // "kept": every entry a plain fits-in-atom literal (call_matters' early
     // decision), at most 30 of them (pass 1's keep mask)
     uint32_t n = 0, max_bt = 0;
@@ -904,37 +939,62 @@ void key_classes(yr_amd_tables* t) {
       max_bt = std::max<uint32_t>(max_bt, e.backtrack);
     }
     if (kept && n > 0) {
-      info = 1u | 4u;
-      t->kd_n[k] = n;
-      t->kd_head[k] = head;
-      t->kd_min_pos[k] = max_bt;
+      o.ok = o.kept = true;
+      o.n = n;
+      o.head = head;
+      o.min_pos = max_bt;
+      continue;
+    }
+    const DevPoolRec& e = t->h_pool[head - 1];
+    const uint32_t fl = e.flags;
+    if (e.next != 0 || (fl & kStrLiteral) || e.re.fwd_len == 0 || e.fguard.m == 0) continue;
+    if (fl & kStrFastRegexp) {
+      if (!(fl & kStrAscii) || (fl & (kStrWide | kStrBase64Any))) continue;
+    } else if (((fl & kStrWide) && !(fl & kStrBase64Any)) || !(fl & (kStrAscii | kStrBase64Any))) {
+      continue;
+    }
+    const int base = e.fguard_bs & 15, span = e.fguard_bs >> 4;
+    o.rs = base + 1 - (int)e.backtrack;           // region start - key byte
+    o.end = base + span + 4 - (int)e.backtrack;   // region end - position
+    o.span = span;
+    o.tmax = (31 - __builtin_clz(e.fguard.m)) >> 3;   // last tested byte of the 4
+    if (o.end < -128 || o.end > 127) continue;
+    o.m = e.fguard.m;
+    o.v = e.fguard.v;
+    o.ok = true;
+  }
+  // a key is decided at place kp if its identity, the byte before it (with
+  // exclusions) and every byte its guard tests lie in the five
+  auto fits = [&](const Desc& o, int kp) {
+    if (!o.ok || (kp < 0 && nk != 1) || (o.nx && kp < 1)) return false;
+    return o.kept || (kp + o.rs >= 0 && kp + o.rs + o.span + o.tmax <= 4);
+  };
+  int best_kp = 1, best = 0;
+  for (int kp = 1; kp >= -1; --kp) {
+    int c = 0;
+    for (uint32_t k = 0; k < nk; ++k) c += fits(d[k], kp);
+    if (c > best) best = c, best_kp = kp;
+  }
+  if (best == 0) return;
+  t->kx_end = (uint32_t)(3 - best_kp);
+  for (uint32_t k = 0; k < nk; ++k) {
+    const Desc& o = d[k];
+    if (!fits(o, best_kp)) continue;
+    uint32_t info = 1u | (o.nx ? 2u : 0u);
+    if (o.kept) {
+      info |= 4u;
+      t->kd_n[k] = o.n;
+      t->kd_head[k] = o.head;
+      t->kd_min_pos[k] = o.min_pos;
     } else {
-      const DevPoolRec& e = t->h_pool[head - 1];
-      const uint32_t fl = e.flags;
-      if (e.next != 0 || (fl & kStrLiteral) || e.re.fwd_len == 0 || e.fguard.m == 0) continue;
-      if (fl & kStrFastRegexp) {
-        if (!(fl & kStrAscii) || (fl & (kStrWide | kStrBase64Any))) continue;
-      } else if (((fl & kStrWide) && !(fl & kStrBase64Any)) || !(fl & (kStrAscii | kStrBase64Any))) {
-        continue;
-      }
-      const int base = e.fguard_bs & 15, span = e.fguard_bs >> 4;
-      const int rs = base + 1 - (int)e.backtrack;          // region start - key byte
-      const int end = base + span + 4 - (int)e.backtrack;  // region end - position
-      const uint32_t tmax = (31u - (uint32_t)__builtin_clz(e.fguard.m)) >> 3;   // last tested byte
-      // every tested byte must fit the four the scan keeps (the byte before
-      // the key, the key, the two after: kernels.hip key_class) for some place
-      // of the key among them
-      if (rs < -3 || rs + span + (int)tmax > 2 || end < -128 || end > 127) continue;
-      t->kd_m[k] = e.fguard.m;
-      t->kd_v[k] = e.fguard.v;
-      info = 1u | ((uint32_t)(uint8_t)(int8_t)rs << 8) | ((uint32_t)span << 16) | (tmax << 20) |
-             ((uint32_t)(uint8_t)(int8_t)end << 24);
+      t->kd_m[k] = o.m;
+      t->kd_v[k] = o.v;
+      info |= ((uint32_t)(uint8_t)(int8_t)o.rs << 8) | ((uint32_t)o.span << 16) |
+              ((uint32_t)o.tmax << 20) | ((uint32_t)(uint8_t)(int8_t)o.end << 24);
     }
-    t->kd_info[k] = info | (nx ? 2u : 0u);
-    for (uint32_t q = 0; q < 8 && nx; ++q) {   // the exclusions, the first repeated to fill
-      const uint32_t x = xs[q < nx ? q : 0];
-      (q < 4 ? t->kd_x0[k] : t->kd_x1[k]) |= x << (8 * (q & 3));
-    }
+    t->kd_info[k] = info;
+    t->kd_x0[k] = o.xs0;
+    t->kd_x1[k] = o.xs1;
     t->kd_any = true;
   }
 }
