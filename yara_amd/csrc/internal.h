@@ -169,11 +169,13 @@ constexpr uint32_t kNodeHeadWords = kNodeZero4 + 4;   // (keeps the buckets 16-B
 // k's list is kept (ScanParams::kd_n / kd_head).  The scan keeps five bytes
 // next to a certain candidate's key: four in ScanParams::seg_x, and its
 // segment output entry (offset below 2^20, the bits of its pending entry)
-// holds kOutCertain, the fifth byte in bits kOutByteShift.. and the key's
-// place among the five + 1 (0: just before them) in bits kOutKeyShift..
-constexpr uint32_t kOutCertain = 0x80000000u;
+// holds the fifth byte in bits kOutByteShift.., the key's place among the five
+// + 2 (1: just before them; 0: not a certain candidate) in bits
+// kOutKeyShift.., and with ScanParams::kx_deep kOutDeep: the byte before the
+// key is one of key 0's exclusions (kd_x0 / kd_x1).
 constexpr uint32_t kOutByteShift = 20;
 constexpr uint32_t kOutKeyShift = 28;
+constexpr uint32_t kOutDeep = 0x80000000u;
 constexpr uint32_t kOutOffsetMask = (1u << 20) - 1u;
 constexpr uint32_t kClassDead = 1u;
 constexpr uint32_t kClassKept = 2u;
@@ -214,6 +216,7 @@ struct ScanParams {
   uint32_t* seg_x;          // null, or beside seg_out: a certain candidate's first four
                             // bytes (lane bytes s .. s + 3, s = min(key + kx_end - 3, 11))
   uint32_t kx_end;          // 2..4 (scanner.cpp key_classes)
+  uint32_t kx_deep;         // 1: the scan tests the byte before the key (one 1-byte key)
   uint8_t* dead;            // null, or per output candidate its class (key_class;
                             // written by the compaction), and
   uint32_t* live;           // [0] = count, then the other candidates' indices (any order)

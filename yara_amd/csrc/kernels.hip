@@ -197,8 +197,15 @@ template <int MODE>
 constexpr bool kByteKeyAblation = MODE == 24 || MODE == 25;
 // A pending entry's offset with this bit set is a certain candidate (its last
 // byte is a 1-byte key): no bucket probe.  (Segment offsets are < 2^20.)
-constexpr uint32_t kConfirmed = kOutCertain;   // (a pending entry becomes the output entry)
+// a pending entry becomes the output entry: certain iff its key place is set
+constexpr uint32_t kCertainMask = 7u << kOutKeyShift;
 static_assert(kSegment <= kOutOffsetMask + 1u, "segment offsets must leave the top bits free");
+
+// b one of the (up to 8, repeated to fill) bytes of x0, x1: zero-byte test
+__device__ __forceinline__ bool excluded(uint32_t b, uint32_t x0, uint32_t x1) {
+  const uint32_t pv = b * 0x01010101u, a = pv ^ x0, c = pv ^ x1;
+  return ((((a - 0x01010101u) & ~a) | ((c - 0x01010101u) & ~c)) & 0x80808080u) != 0u;
+}
 static_assert(kQueueCap == kWave, "a drain takes the whole ring, one entry per lane");
 
 // The class of a certain candidate (internal.h kClass*), one lane per output
@@ -208,10 +215,11 @@ static_assert(kQueueCap == kWave, "a drain takes the whole ring, one entry per l
 // or the list is one call decided by a guard on the bytes next to the key.  w
 // = the five bytes the scan kept for the candidate, the key at byte kp of them
 // (-1: just before them; then the table has one 1-byte key): the byte before
-// the key and the guard are decided only if every byte they test lies in w and
-// the block.  Pre-verification then never reads the input for the candidate.
+// the key (or the scan's test of it, deep) and the guard are decided only if
+// every byte they test lies in w and the block.  Pre-verification then never
+// reads the input for the candidate.
 __device__ __forceinline__ uint32_t key_class(const ScanParams& p, uint64_t w, int32_t kp,
-                                              uint64_t pos) {
+                                              bool deep, uint64_t pos) {
   if (kp < 0 && p.n_byte_keys != 1) return 0;
   const uint32_t key = kp < 0 ? (p.byte_keys & 0xFFu) : (uint32_t)(w >> (8 * kp)) & 0xFFu;
   uint32_t info = 0, m = 0, v = 0, x0 = 0, x1 = 0, kidx = 0, min_pos = 0;
@@ -227,12 +235,12 @@ __device__ __forceinline__ uint32_t key_class(const ScanParams& p, uint64_t w, i
     kidx = is ? k : kidx;
   }
   if (!(info & 1u)) return 0;
-  if (info & 2u) {
-    // the byte before the key among the exclusions: zero-byte test
-    if (kp < 1) return 0;
-    const uint32_t pv = ((uint32_t)(w >> (8 * kp - 8)) & 0xFFu) * 0x01010101u;
-    const uint32_t a = pv ^ x0, b = pv ^ x1;
-    if ((((a - 0x01010101u) & ~a) | ((b - 0x01010101u) & ~b)) & 0x80808080u) return 0;
+  if (info & 2u) {   // the byte before the key among the exclusions: a deeper state
+    if (kp >= 1) {
+      if (excluded((uint32_t)(w >> (8 * kp - 8)) & 0xFFu, x0, x1)) return 0;
+    } else if (!p.kx_deep || deep) {
+      return 0;
+    }
   }
   if (info & 4u) return pos >= min_pos ? (kClassKept | kidx << 2) : 0u;
   // shift jj tests w bytes s0 + jj + t for the t <= tmax with mask byte t set
@@ -258,7 +266,7 @@ __device__ __forceinline__ void flush_pending(const ScanParams& p, WaveQueue& q,
     // memory round trip at all
     u32x2 e = {0u, 0u};
     if (lane < q.pend_n) e = lds_load<u32x2>(q.pend + 8 * lane);
-    const bool conf = (e.y & kConfirmed) != 0u;
+    const bool conf = (e.y & kCertainMask) != 0u;
     off = e.y;   // (a certain entry's bits for key_class with it)
     const bool probe = lane < q.pend_n && !conf;
     keep = lane < q.pend_n && conf;
@@ -521,8 +529,11 @@ __device__ __forceinline__ void drain(const ScanParams& p, WaveQueue& q, uint32_
           // five bytes next to it for key_class, lane bytes e - 3 .. e + 1
           // (e = min(j + kx_end, 14)), the key at place j + 3 - e of them
           e = min(j + p.kx_end, (uint32_t)kBytesPerLane - 2);
-          y |= kConfirmed | (uint32_t)lds_load<uint8_t>(ent + e + 1) << kOutByteShift |
-               (j + 4 - e) << kOutKeyShift;
+          y |= (uint32_t)lds_load<uint8_t>(ent + e + 1) << kOutByteShift | (j + 5 - e) << kOutKeyShift;
+          if (p.kx_deep != 0u) {   // (the byte before the key, bytes -4..-1 at 16..19)
+            const uint32_t b = lds_load<uint8_t>(ent + (j != 0u ? j - 1u : 19u));
+            if (excluded(b, p.kd_x0[0], p.kd_x1[0])) y |= kOutDeep;
+          }
         }
       }
       lds_store2(q.pend + 8 * (idx - base), window4(ent, e), y);
@@ -1009,9 +1020,9 @@ __global__ __launch_bounds__(kScatterWaves * kWave) void seg_scatter_kernel(
     // the certain candidates' classes from the bytes the scan kept beside them
     const uint32_t x = i < c ? p.seg_x[at0 + i] : 0u;
     uint32_t cls = i < c ? 0u : kClassDead;
-    if (i < c && (e & kOutCertain))
+    if (i < c && (e & kCertainMask) != 0u)
       cls = key_class(p, x | (uint64_t)(e >> kOutByteShift & 0xFFu) << 32,
-                      (int32_t)(e >> kOutKeyShift & 7u) - 1, pos);
+                      (int32_t)(e >> kOutKeyShift & 7u) - 2, (e & kOutDeep) != 0u, pos);
     if (i < c) p.dead[first + i] = (uint8_t)cls;
     n_live += (uint32_t)__popcll(__ballot(cls == 0u));
   }

@@ -91,7 +91,7 @@ struct yr_amd_tables {
   uint32_t kd_x0[4] = {0, 0, 0, 0}, kd_x1[4] = {0, 0, 0, 0};
   uint32_t kd_n[4] = {0, 0, 0, 0}, kd_head[4] = {0, 0, 0, 0}, kd_min_pos[4] = {0, 0, 0, 0};
   bool kd_any = false;
-  uint32_t kx_end = 2;                // ScanParams::kx_end
+  uint32_t kx_end = 2, kx_deep = 0;   // ScanParams::kx_end / kx_deep
   uint32_t* d_nodes = nullptr;        // accepting nodes by string (FlatTables::nodes)
   DevPoolRec* d_pool = nullptr;       // per pool entry: link, backtrack, string, programs
   uint8_t* d_str_bytes = nullptr;
@@ -544,6 +544,7 @@ int yr_amd_scan_window(yr_amd_scanner* s, const uint8_t* d_window, uint64_t wind
   p.byte_keys = t->flat.byte_keys;
   p.n_byte_keys = t->flat.n_byte_keys;
   p.kx_end = t->kx_end;
+  p.kx_deep = t->kx_deep;
   for (int k = 0; k < 4; ++k) {
     p.kd_m[k] = t->kd_m[k];
     p.kd_v[k] = t->kd_v[k];
@@ -896,6 +897,7 @@ void key_classes(yr_amd_tables* t) {
   const FlatTables& f = t->flat;
   t->kd_any = false;
   t->kx_end = 2;
+  t->kx_deep = 0;
   for (int k = 0; k < 4; ++k)
     t->kd_m[k] = t->kd_v[k] = t->kd_info[k] = t->kd_x0[k] = t->kd_x1[k] = t->kd_n[k] =
         t->kd_head[k] = t->kd_min_pos[k] = 0;
@@ -903,7 +905,9 @@ void key_classes(yr_amd_tables* t) {
   // Per key the class it can have, then the five bytes the scan keeps beside
   // its certain candidates (kernels.hip key_class): lane bytes key - kp ..
   // key - kp + 4 for one kp in {1, 0, -1} per table (kx_end = 3 - kp), the one
-  // under which the most keys are decided.
+  // under which the most keys are decided.  With one 1-byte key the scan can
+  // also test the byte before it against the key's exclusions (kx_deep), so
+  // the five bytes may all lie after the key.
   struct Desc {
     bool ok = false, kept = false;
     uint32_t nx = 0, xs0 = 0, xs1 = 0, m = 0, v = 0, n = 0, head = 0, min_pos = 0;
@@ -964,9 +968,10 @@ void key_classes(yr_amd_tables* t) {
     o.ok = true;
   }
   // a key is decided at place kp if its identity, the byte before it (with
-  // exclusions) and every byte its guard tests lie in the five
+  // exclusions; or the scan's test of it) and every byte its guard tests lie
+  // in the five
   auto fits = [&](const Desc& o, int kp) {
-    if (!o.ok || (kp < 0 && nk != 1) || (o.nx && kp < 1)) return false;
+    if (!o.ok || (kp < 0 && nk != 1) || (o.nx && kp < 1 && nk != 1)) return false;
     return o.kept || (kp + o.rs >= 0 && kp + o.rs + o.span + o.tmax <= 4);
   };
   int best_kp = 1, best = 0;
@@ -977,6 +982,7 @@ void key_classes(yr_amd_tables* t) {
   }
   if (best == 0) return;
   t->kx_end = (uint32_t)(3 - best_kp);
+  t->kx_deep = best_kp < 1 && nk == 1 && d[0].nx > 0 ? 1u : 0u;
   for (uint32_t k = 0; k < nk; ++k) {
     const Desc& o = d[k];
     if (!fits(o, best_kp)) continue;
