@@ -130,6 +130,46 @@ def test_device_verify_after_sharded_device_scan():
 
 
 @pytest.mark.gpu
+@pytest.mark.parametrize("rules,pre,key,after", [
+    ("rx", b"\xe8\x11\x22\x33\x44", 0x5B, b"\xc3"),   # { E8 ?? ?? ?? ?? ( 5B | 5D ) C3 }
+    ("fuzz0", b"\x64", 0x5F, b"\x00\x3e")])               # { 64 ( .. | 5F | .. ) [0-4] 3E }
+@pytest.mark.parametrize("split", [1, 2, 3, 4])
+def test_range_scan_keeps_candidates_decided_past_its_end(rules, pre, key, after, split):
+    """A byte range scan of a device-resident block reads nothing past the
+    range's end (zeros fill its last lane), so a 1-byte key whose guard bytes lie
+    beyond it stays undecided (kernels.hip key_class tests the range end, not
+    the block's): the range [0, cut) ends 5 bytes into a lane, keys planted
+    `split` bytes before the cut with their guard's bytes after it; the range's
+    records equal the whole-block host path's up to the cut, planted matches
+    included."""
+    import torch
+    import yara_amd
+    from yara_amd._hip import memcpy
+    n = (1 << 20) + 77
+    data = oracle.xorshift(n, 71).copy()
+    cut = ((n // 2) & ~15) + 5
+    data[cut - split - len(pre):cut - split] = np.frombuffer(pre, np.uint8)
+    data[cut - split] = key
+    data[cut - split + 1:cut - split + 1 + len(after)] = np.frombuffer(after, np.uint8)
+    tab = yara_amd.Tables.from_npz(tables_npz(rules), device=0, strings=True)
+    sc = yara_amd.Scanner(tab)
+    want = sc.verify_calls(data)
+    want = want[want["offset"] < cut]   # (a record's offset: its key's byte)
+    assert np.isin(cut - split, want["offset"])
+    d = torch.from_numpy(data.copy()).cuda()
+    sc.scan_device(d.data_ptr(), n, 0, cut)
+    sc.device_result()
+    p, m = sc.verify_device(0)
+    got = np.zeros(m, dtype=yara_amd._lib.VERIFY_REC_DTYPE)
+    if m:
+        h = torch.empty(m * 16, dtype=torch.uint8, device="cuda")
+        memcpy(h.data_ptr(), p, m * 16, 3)
+        got = np.frombuffer(h.cpu().numpy().tobytes(), dtype=yara_amd._lib.VERIFY_REC_DTYPE)
+    assert np.array_equal(got["offset"], want["offset"])
+    assert np.array_equal(got["pool_index"], want["pool_index"])
+
+
+@pytest.mark.gpu
 def test_preverify_requires_strings():
     import yara_amd
     tab = yara_amd.Tables.from_npz(tables_npz("lit"), device=0)

@@ -216,7 +216,7 @@ static_assert(kQueueCap == kWave, "a drain takes the whole ring, one entry per l
 // = the five bytes the scan kept for the candidate, the key at byte kp of them
 // (-1: just before them; then the table has one 1-byte key): the byte before
 // the key (or the scan's test of it, deep) and the guard are decided only if
-// every byte they test lies in w and the block.  Pre-verification then never
+// every byte they test lies in w and the scanned range.  Pre-verification then never
 // reads the input for the candidate.
 __device__ __forceinline__ uint32_t key_class(const ScanParams& p, uint64_t w, int32_t kp,
                                               bool deep, uint64_t pos) {
@@ -246,8 +246,9 @@ __device__ __forceinline__ uint32_t key_class(const ScanParams& p, uint64_t w, i
   // shift jj tests w bytes s0 + jj + t for the t <= tmax with mask byte t set
   const int32_t s0 = kp + (int32_t)(int8_t)(info >> 8);
   const uint32_t span = (info >> 16) & 15u, tmax = (info >> 20) & 3u;
+  // (the scan read nothing past byte_end: a range of a larger block has zeros there)
   const int64_t end = (int64_t)pos + (int8_t)(info >> 24);
-  if (s0 < 0 || s0 + (int32_t)(span + tmax) > 4 || end > (int64_t)p.block_size) return 0;
+  if (s0 < 0 || s0 + (int32_t)(span + tmax) > 4 || end > (int64_t)p.byte_end) return 0;
   bool hit = false;
   for (uint32_t jj = 0; jj <= span; ++jj) hit |= ((uint32_t)(w >> (8 * ((uint32_t)s0 + jj))) & m) == v;
   return hit ? 0u : kClassDead;
