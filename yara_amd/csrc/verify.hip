@@ -957,12 +957,36 @@ __device__ __forceinline__ uint32_t wave_in_block() {
   return __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
 }
 
+// Pass 1 of one group with records (o = its first record's index).
+__device__ __forceinline__ void verify_group(const VerifyParams& p, uint64_t g, uint64_t o,
+                                             uint32_t lds, uint32_t codebuf) {
+  const uint64_t c = g * kGroup + (threadIdx.x & 63u);
+  // the scan's class (kernels.hip key_class): dead -- nothing; kept -- every
+  // call of the key's list; else pass 0's decisions
+  const uint32_t cls = c < p.count && p.dead != nullptr ? p.dead[c] : 0u;
+  uint32_t keep = 0, n = 0, head = 0;
+  if (cls & kClassKept) {
+    n = p.kd_n[(cls >> 2) & 3u];
+    keep = (1u << n) - 1u;
+    head = p.kd_head[(cls >> 2) & 3u];
+  } else if (c < p.count && !(cls & kClassDead)) {
+    keep = p.keep[c];
+    if (keep != 0) {
+      n = p.counts[c];
+      head = p.heads[c];
+    }
+  }
+  const uint32_t pre = wave_exclusive(n);
+  if (keep != 0) verify_one<1>(p, c, lds, codebuf, keep, head, o + pre, n);
+}
+
 // PASS 0: one candidate per lane; each wave's record count goes to its group.
-// PASS 1: persistent waves over the groups: a group without records reads
-// nothing more (most groups of a dense rule set); the others scan their
-// candidates' counts and write the records from the group's offset on.
+// PASS 1: persistent waves over the groups, 64 tested at once for records;
+// the groups with some scan their candidates' counts and write the records
+// from the group's offset on.
 template <int PASS>
-__global__ __launch_bounds__(256) void verify_kernel(VerifyParams p) {
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(5))) void verify_kernel(
+    VerifyParams p) {   // (5 waves per SIMD: the LDS allows them, and pass 1 fits 96 VGPRs)
   __shared__ __attribute__((aligned(16))) uint8_t win[256 * kWinBytes];
   __shared__ __attribute__((aligned(16))) uint8_t code[256 * kCodeBytes];
   // (the low 32 bits of a flat LDS address are the LDS offset)
@@ -977,29 +1001,22 @@ __global__ __launch_bounds__(256) void verify_kernel(VerifyParams p) {
     if ((threadIdx.x & 63u) == 0 && c / kGroup < groups) p.block_off[c / kGroup] = sum;
     return;
   }
+  // wave w takes groups w, w + waves, ...; it tests 64 of them for records at
+  // once (one lane each: a group without records reads nothing more -- most of
+  // a dense rule set's, e.g. rx: 539 records from 525,000 groups), then runs
+  // the groups that have some
   const uint64_t waves = (uint64_t)gridDim.x * (blockDim.x / 64);
-  for (uint64_t g = (uint64_t)blockIdx.x * (blockDim.x / 64) + wave_in_block(); g < groups;
-       g += waves) {
-    const uint64_t o = group_offset(p, g);
-    if (group_offset(p, g + 1) == o) continue;
-    const uint64_t c = g * kGroup + (threadIdx.x & 63u);
-    // the scan's class (kernels.hip key_class): dead -- nothing; kept -- every
-    // call of the key's list; else pass 0's decisions
-    const uint32_t cls = c < p.count && p.dead != nullptr ? p.dead[c] : 0u;
-    uint32_t keep = 0, n = 0, head = 0;
-    if (cls & kClassKept) {
-      n = p.kd_n[(cls >> 2) & 3u];
-      keep = (1u << n) - 1u;
-      head = p.kd_head[(cls >> 2) & 3u];
-    } else if (c < p.count && !(cls & kClassDead)) {
-      keep = p.keep[c];
-      if (keep != 0) {
-        n = p.counts[c];
-        head = p.heads[c];
-      }
+  const uint32_t lane = threadIdx.x & 63u;
+  for (uint64_t g0 = (uint64_t)blockIdx.x * (blockDim.x / 64) + wave_in_block(); g0 < groups;
+       g0 += waves * 64) {
+    const uint64_t gl = g0 + lane * waves;
+    const bool has = gl < groups && group_offset(p, gl + 1) != group_offset(p, gl);
+    // (the group's offset loaded again, wave-uniform: a VGPR pair held across
+    // the loop costs the kernel a wave per SIMD)
+    for (uint64_t m = __ballot(has); m != 0; m &= m - 1) {
+      const uint64_t g = g0 + (uint64_t)__builtin_ctzll(m) * waves;
+      verify_group(p, g, group_offset(p, g), lds, codebuf);
     }
-    const uint32_t pre = wave_exclusive(n);
-    if (keep != 0) verify_one<1>(p, c, lds, codebuf, keep, head, o + pre, n);
   }
 }
 
