@@ -217,6 +217,8 @@ struct ScanParams {
                             // bytes (lane bytes s .. s + 3, s = min(key + kx_end - 3, 11))
   uint32_t kx_end;          // 2..4 (scanner.cpp key_classes)
   uint32_t kx_deep;         // 1: the scan tests the byte before the key (one 1-byte key)
+  uint32_t kx_next;         // 1: guard-decided keys -- the byte-key kernel that keeps the
+                            // next lane's first two bytes in each ring entry (kernels.hip)
   uint8_t* dead;            // null, or per output candidate its class (key_class;
                             // written by the compaction), and
   uint32_t* live;           // [0] = count, then the other candidates' indices (any order)

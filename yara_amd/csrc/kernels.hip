@@ -183,6 +183,12 @@ constexpr uint32_t kNoHit = 0xFFFFFFFFu;
 // Kernel variant: the product kernel for rule sets whose 1-byte keys are tested
 // byte by byte in stage 1 (byte_keys_any below) instead of in the filter.
 constexpr int kModeByteKeys = 20;
+// ... and the same with the next lane's first two bytes in each ring entry, for
+// the five bytes kept beside certain candidates near a lane's end (tables with
+// guard-decided 1-byte keys: ScanParams::kx_next)
+constexpr int kModeByteKeysNext = 23;
+template <int MODE>
+constexpr bool kByteKeys = MODE == kModeByteKeys || MODE == kModeByteKeysNext;
 // Kernel variant: the product kernel for the even-position filter
 // (internal.h kFilterEven: rule sets whose keys are all 4 bytes long).
 constexpr int kModeEven = 21;
@@ -262,7 +268,7 @@ __device__ __forceinline__ void flush_pending(const ScanParams& p, WaveQueue& q,
   __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
   bool keep = false;
   uint32_t off = 0, xv = 0;
-  if constexpr (MODE == kModeByteKeys) {
+  if constexpr (kByteKeys<MODE>) {
     // confirmed entries need no probe; a flush of nothing else makes no
     // memory round trip at all
     u32x2 e = {0u, 0u};
@@ -284,7 +290,7 @@ __device__ __forceinline__ void flush_pending(const ScanParams& p, WaveQueue& q,
                                                            __builtin_amdgcn_mbcnt_lo((uint32_t)b, 0u));
     if (idx < p.seg_cap) {
       out[idx] = off;
-      if (MODE == kModeByteKeys && p.seg_x != nullptr) p.seg_x[(out - p.seg_out) + idx] = xv;
+      if (kByteKeys<MODE> && p.seg_x != nullptr) p.seg_x[(out - p.seg_out) + idx] = xv;
     }
   }
   found += (uint32_t)__popcll(b);
@@ -398,7 +404,7 @@ constexpr bool kHoldFl = YAMD_HOLD_FL && !kEven<MODE>;
 template <int MODE>
 constexpr bool kDeferFl =
     YAMD_DEFER_FL &&
-    (MODE == 0 || MODE == 12 || MODE == kModeByteKeys || kEven<MODE> || kByteKeyAblation<MODE>);
+    (MODE == 0 || MODE == 12 || kByteKeys<MODE> || kEven<MODE> || kByteKeyAblation<MODE>);
 
 // Consume a deferred drain's first-level words: the lanes' hits that pass go,
 // in order, to the pending list.
@@ -456,7 +462,7 @@ __device__ __forceinline__ void drain(const ScanParams& p, WaveQueue& q, uint32_
     off0 = (e45.y & 0xFFFFu) * kBytesPerLane;
     if constexpr (kEven<MODE>) m = even_mask<MODE == kModeEvenHash>(S);
     else m = dense_mask(stage1<0, false>(S, lane));
-    if constexpr (MODE == kModeByteKeys) {
+    if constexpr (kByteKeys<MODE>) {
       kmask = byte_keys_mask(S, p);
       m |= kmask;
     }
@@ -487,7 +493,7 @@ __device__ __forceinline__ void drain(const ScanParams& p, WaveQueue& q, uint32_
       return;
     }
   }
-  if ((MODE == 0 || MODE == kModeByteKeys || kByteKeyAblation<MODE>) && (p.len_mask & 6u) != 0u) {
+  if ((MODE == 0 || kByteKeys<MODE> || kByteKeyAblation<MODE>) && (p.len_mask & 6u) != 0u) {
     maybe = m;   // 1-/2-byte keys: no first level, every hit goes to the buckets
   } else {
     while (m) {
@@ -523,21 +529,34 @@ __device__ __forceinline__ void drain(const ScanParams& p, WaveQueue& q, uint32_
     while (maybe != 0u && idx < base + kWave) {
       const uint32_t j = (uint32_t)__builtin_ctz(maybe);
       maybe &= maybe - 1;
-      uint32_t y = off0 + j, e = j;
-      if constexpr (MODE == kModeByteKeys) {
-        if ((kmask >> j) & 1u) {
-          // a certain candidate needs no window for the exact check: keep
-          // five bytes next to it for key_class, lane bytes e - 3 .. e + 1
-          // (e = min(j + kx_end, 14)), the key at place j + 3 - e of them
-          e = min(j + p.kx_end, (uint32_t)kBytesPerLane - 2);
-          y |= (uint32_t)lds_load<uint8_t>(ent + e + 1) << kOutByteShift | (j + 5 - e) << kOutKeyShift;
-          if (p.kx_deep != 0u) {   // (the byte before the key, bytes -4..-1 at 16..19)
-            const uint32_t b = lds_load<uint8_t>(ent + (j != 0u ? j - 1u : 19u));
-            if (excluded(b, p.kd_x0[0], p.kd_x1[0])) y |= kOutDeep;
-          }
+      uint32_t y = off0 + j, x;
+      if (kByteKeys<MODE> && ((kmask >> j) & 1u)) {
+        // a certain candidate needs no window for the exact check: keep five
+        // bytes next to it for key_class, lane bytes e - 3 .. e + 1, the key at
+        // place j + 3 - e of them: e = min(j + kx_end, 16), where bytes 16
+        // and 17 are the next lane's first two (ring entry bytes 22, 23; not in
+        // the entry of a tile's last lane: e <= 14 there)
+        const uint32_t li = lds_load<uint32_t>(ent + 20);
+        const uint32_t e =
+            min(j + p.kx_end, MODE == kModeByteKeysNext && (li & (kWave - 1)) != kWave - 1 ? 16u : 14u);
+        uint32_t b5;
+        if (e <= 14u) {
+          x = window4(ent, e);
+          b5 = lds_load<uint8_t>(ent + e + 1);
+        } else {   // lane bytes 12..17
+          const uint64_t w6 = lds_load<uint32_t>(ent + 12) | (uint64_t)(li >> 16) << 32;
+          x = (uint32_t)(w6 >> (8 * (e - 15u)));
+          b5 = (uint32_t)(w6 >> (8 * (e - 11u))) & 0xFFu;
         }
+        y |= b5 << kOutByteShift | (j + 5 - e) << kOutKeyShift;
+        if (p.kx_deep != 0u) {   // (the byte before the key, bytes -4..-1 at 16..19)
+          const uint32_t b = lds_load<uint8_t>(ent + (j != 0u ? j - 1u : 19u));
+          if (excluded(b, p.kd_x0[0], p.kd_x1[0])) y |= kOutDeep;
+        }
+      } else {
+        x = window4(ent, j);
       }
-      lds_store2(q.pend + 8 * (idx - base), window4(ent, e), y);
+      lds_store2(q.pend + 8 * (idx - base), x, y);
       ++idx;
     }
     if (end <= base + kWave) {
@@ -756,7 +775,8 @@ __device__ __forceinline__ void ring_append(const ScanParams& p, WaveQueue& q, S
       } else {
         lds_store2(ent, S[1], S[2]);
         lds_store2(ent + 8, S[3], S[4]);
-        lds_store2(ent + 16, S[0], (tile_off >> 4) + lane);
+        // (byte-key kernel: the next lane's first two bytes in the top half)
+        lds_store2(ent + 16, S[0], (tile_off >> 4) + lane | (MODE == kModeByteKeysNext ? S[5] << 16 : 0u));
       }
     }
     q.count += n;
@@ -816,8 +836,11 @@ __device__ __forceinline__ void tile_step(const ScanParams& p, WaveQueue& q, Seg
                                           uint4 cur, uint32_t tile_off, uint32_t lane) {
   uint32_t S[6];
   tile_context(st, cur, S);
-  uint32_t any = stage1<(MODE == kModeByteKeys || kByteKeyAblation<MODE>) ? 0 : MODE, true>(S, lane);
-  if constexpr (MODE == kModeByteKeys) any |= byte_keys_any(S, p);
+  // the next lane's first dword (wave_shl:1; lane 63: 0), for the five bytes
+  // kept beside a certain candidate near the lane's end (drain)
+  if constexpr (MODE == kModeByteKeysNext) S[5] = __builtin_amdgcn_mov_dpp(cur.x, 0x130, 0xF, 0xF, true);
+  uint32_t any = stage1<(kByteKeys<MODE> || kByteKeyAblation<MODE>) ? 0 : MODE, true>(S, lane);
+  if constexpr (kByteKeys<MODE>) any |= byte_keys_any(S, p);
   if constexpr (MODE == 24) asm volatile("" ::"v"(byte_keys_any(S, p)));
   if constexpr (kDeferFl<MODE>)
     if (q.defer) drain_complete<MODE>(p, q, lane, st.seg_start, st.out, st.found);
@@ -1121,7 +1144,10 @@ hipError_t launch_scan(const ScanParams& p, int grid, hipStream_t s, int mode) {
     case 25: hipLaunchKernelGGL(scan_segments_kernel<25>, dim3(grid), dim3(kWGThreads), lds, s, p); break;
 #endif
     default:
-      if (p.n_byte_keys != 0)
+      if (p.n_byte_keys != 0 && p.kx_next != 0)
+        hipLaunchKernelGGL(scan_segments_kernel<kModeByteKeysNext>, dim3(grid), dim3(kWGThreads),
+                           lds, s, p);
+      else if (p.n_byte_keys != 0)
         hipLaunchKernelGGL(scan_segments_kernel<kModeByteKeys>, dim3(grid), dim3(kWGThreads), lds,
                            s, p);
       else if (p.filter_mode == kFilterEven)
@@ -1160,6 +1186,7 @@ hipError_t configure_scan_kernel() {
   hipError_t e = hipSuccess;
   for (const void* k : {(const void*)scan_segments_kernel<0>,
                         (const void*)scan_segments_kernel<kModeByteKeys>,
+                        (const void*)scan_segments_kernel<kModeByteKeysNext>,
                         (const void*)scan_segments_kernel<kModeEven>,
                         (const void*)scan_segments_kernel<kModeEvenHash>,
 #if YAMD_DIAG

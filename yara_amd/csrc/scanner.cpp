@@ -91,7 +91,7 @@ struct yr_amd_tables {
   uint32_t kd_x0[4] = {0, 0, 0, 0}, kd_x1[4] = {0, 0, 0, 0};
   uint32_t kd_n[4] = {0, 0, 0, 0}, kd_head[4] = {0, 0, 0, 0}, kd_min_pos[4] = {0, 0, 0, 0};
   bool kd_any = false;
-  uint32_t kx_end = 2, kx_deep = 0;   // ScanParams::kx_end / kx_deep
+  uint32_t kx_end = 2, kx_deep = 0, kx_next = 0;   // ScanParams::kx_end / kx_deep / kx_next
   uint32_t* d_nodes = nullptr;        // accepting nodes by string (FlatTables::nodes)
   DevPoolRec* d_pool = nullptr;       // per pool entry: link, backtrack, string, programs
   uint8_t* d_str_bytes = nullptr;
@@ -545,6 +545,7 @@ int yr_amd_scan_window(yr_amd_scanner* s, const uint8_t* d_window, uint64_t wind
   p.n_byte_keys = t->flat.n_byte_keys;
   p.kx_end = t->kx_end;
   p.kx_deep = t->kx_deep;
+  p.kx_next = t->kx_next;
   for (int k = 0; k < 4; ++k) {
     p.kd_m[k] = t->kd_m[k];
     p.kd_v[k] = t->kd_v[k];
@@ -898,6 +899,7 @@ void key_classes(yr_amd_tables* t) {
   t->kd_any = false;
   t->kx_end = 2;
   t->kx_deep = 0;
+  t->kx_next = 0;
   for (int k = 0; k < 4; ++k)
     t->kd_m[k] = t->kd_v[k] = t->kd_info[k] = t->kd_x0[k] = t->kd_x1[k] = t->kd_n[k] =
         t->kd_head[k] = t->kd_min_pos[k] = 0;
@@ -995,6 +997,7 @@ void key_classes(yr_amd_tables* t) {
     } else {
       t->kd_m[k] = o.m;
       t->kd_v[k] = o.v;
+      t->kx_next = 1;   // (a guard's bytes may run past the lane: keep the next lane's two)
       info |= ((uint32_t)(uint8_t)(int8_t)o.rs << 8) | ((uint32_t)o.span << 16) |
               ((uint32_t)o.tmax << 20) | ((uint32_t)(uint8_t)(int8_t)o.end << 24);
     }
