@@ -245,6 +245,39 @@ int yr_amd_replay(
     void* user);
 
 /*
+ * ---- Device trace of the walk (tracing) ----
+ *
+ * The analogue of the reference walk's YR_DEBUG_VERBOSITY == 2 trace
+ * (libyara/scanner.c:83-96), computed on the GPU: one row per block position
+ * i in [0, size] whose walk state (after bytes [0, i)) is not the root,
+ * ascending, with the state's slot and match_table[state].  The state is
+ * walked with the reference's own transition rule over the untouched
+ * transition table (scanner.c:123-141), independently of the scan kernel's
+ * filter path, so the rows with match != 0 are exactly the candidate stream
+ * of yr_amd_scan_device over the same block (the reference prints the rows
+ * i < size; the row i == size is its final check, scanner.c:145-160).
+ * d_data: DEVICE pointer to the block.  Writes min(total, cap) rows into the
+ * host array out (may be NULL when cap == 0); *count = total.  With
+ * YR_DEBUG_VERBOSITY >= 2 in the environment every row is also printed to
+ * stderr in the reference's format.  Meant for small blocks (debugging).
+ */
+typedef struct
+{
+  uint64_t position;
+  uint32_t state;
+  uint32_t match;  /* match_table[state]: 1-based match-list head, 0 = none */
+} yr_amd_trace_rec;
+
+int yr_amd_trace_walk(
+    yr_amd_scanner* scanner,
+    const uint8_t* d_data,
+    size_t size,
+    uint64_t data_base,
+    yr_amd_trace_rec* out,
+    uint64_t cap,
+    uint64_t* count);
+
+/*
  * ---- On-device literal pre-verification ----
  *
  * The string records of the rules (YR_STRING, libyara/include/yara/types.h),

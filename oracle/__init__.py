@@ -46,6 +46,9 @@ def lib():
                                          _u64p, _u32p, ctypes.c_int64]
         L.oracle_candidates.restype = ctypes.c_int64
         L.oracle_candidates.argtypes = [_u32p, _u32p, _u8p, ctypes.c_uint64, _u64p, ctypes.c_int64]
+        L.oracle_trace.restype = ctypes.c_int64
+        L.oracle_trace.argtypes = [_u32p, _u32p, _u8p, ctypes.c_uint64, _u64p, _u32p, _u32p,
+                                   ctypes.c_int64]
         L.oracle_count_slice.restype = ctypes.c_int64
         L.oracle_count_slice.argtypes = [_u32p, _u32p, _u8p, ctypes.c_uint64, ctypes.c_uint64,
                                          ctypes.c_uint32]
@@ -157,6 +160,26 @@ def candidates(tab, data: np.ndarray) -> np.ndarray:
                                   _p(out, _u64p), cap)
         if cnt <= cap:
             return out[:cnt]
+        cap = int(cnt)
+
+
+def trace(tab, data: np.ndarray):
+    """The walk's debug trace (scanner.c:83-96): (positions, states, matches) of
+    every position i in [0, len(data)] whose state is not the root."""
+    T, M = _c(tab.T, np.uint32), _c(tab.M, np.uint32)
+    d = _c(data, np.uint8)
+    if d.size == 0:
+        d = np.zeros(1, np.uint8)
+    L = lib()
+    cap = 1 << 16
+    while True:
+        pos = np.empty(cap, np.uint64)
+        st = np.empty(cap, np.uint32)
+        mt = np.empty(cap, np.uint32)
+        cnt = L.oracle_trace(_p(T, _u32p), _p(M, _u32p), _p(d, _u8p), data.size, _p(pos, _u64p),
+                             _p(st, _u32p), _p(mt, _u32p), cap)
+        if cnt <= cap:
+            return pos[:cnt], st[:cnt], mt[:cnt]
         cap = int(cnt)
 
 

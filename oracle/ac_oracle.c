@@ -123,6 +123,43 @@ int64_t oracle_candidates(
 }
 
 /*
+ * The walk's debug trace (scanner.c:83-96 at YR_DEBUG_VERBOSITY 2, plus the
+ * final state at i == n, scanner.c:145): every position i in [0, n] whose
+ * state is not the root, with the state and M[state].  The sequential walk
+ * from the block start, as the reference runs it.
+ */
+int64_t oracle_trace(
+    const uint32_t* T,
+    const uint32_t* M,
+    const uint8_t* data,
+    uint64_t n,
+    uint64_t* pos,
+    uint32_t* states,
+    uint32_t* matches,
+    int64_t cap)
+{
+  int64_t count = 0;
+  uint32_t state = 0;
+  uint64_t i = 0;
+  for (;;)
+  {
+    if (state != 0)
+    {
+      if (count < cap)
+      {
+        pos[count] = i;
+        states[count] = state;
+        matches[count] = M[state];
+      }
+      count++;
+    }
+    if (i >= n) break;
+    state = ac_step(T, state, data[i++]);
+  }
+  return count;
+}
+
+/*
  * Candidate count over positions (lo, hi] of a block of n bytes, starting the
  * walk at root on byte max(0, lo - warm).  With warm >= the trie depth (4 for
  * libyara, limits.h:68) the state stream equals the full walk's.  Used by the

@@ -287,6 +287,23 @@ class Scanner:
                                                         ctypes.byref(allp)))
         return p.value or 0, cnt.value, bool(allp.value)
 
+    def trace_walk(self, d_ptr: int, size: int, data_base: int = 0, cap=None):
+        """Device trace of the walk over a device-resident block (yr_amd_trace_walk,
+        the analogue of scanner.c:83-96): structured array of (position, state,
+        match) for every position in [0, size] whose state is not the root."""
+        cnt = ctypes.c_uint64()
+        if cap is None:
+            _lib.check("yr_amd_trace_walk",
+                       _lib.lib().yr_amd_trace_walk(self._h, ctypes.c_void_p(d_ptr), size, data_base,
+                                                    None, 0, ctypes.byref(cnt)))
+            cap = cnt.value
+        out = np.zeros(cap, dtype=_lib.TRACE_REC_DTYPE)
+        _lib.check("yr_amd_trace_walk",
+                   _lib.lib().yr_amd_trace_walk(self._h, ctypes.c_void_p(d_ptr), size, data_base,
+                                                ctypes.c_void_p(out.ctypes.data if cap else 0), cap,
+                                                ctypes.byref(cnt)))
+        return out[:min(cap, cnt.value)], cnt.value
+
     def set_timing(self, enable: bool = True):
         _lib.check("yr_amd_scanner_set_timing", _lib.lib().yr_amd_scanner_set_timing(self._h, int(enable)))
 

@@ -62,6 +62,7 @@ class VerifyRec(ctypes.Structure):
 
 
 VERIFY_REC_DTYPE = [("offset", "<u8"), ("pool_index", "<u4"), ("candidate", "<u4")]
+TRACE_REC_DTYPE = [("position", "<u8"), ("state", "<u4"), ("match", "<u4")]   # yr_amd_trace_rec
 
 # name -> (restype, argtypes); every function include/yara_amd.h declares
 PROTOTYPES = {
@@ -81,6 +82,8 @@ PROTOTYPES = {
                                          ctypes.POINTER(_int)]),
     "yr_amd_replay": (_int, [_vp, _u8p, ctypes.c_size_t, _u64p, ctypes.c_uint64, _int, VERIFY_FN,
                              _vp]),
+    "yr_amd_trace_walk": (_int, [_vp, _vp, ctypes.c_size_t, ctypes.c_uint64, _vp, ctypes.c_uint64,
+                                 ctypes.POINTER(ctypes.c_uint64)]),
     "yr_amd_fill_xorshift64": (_int, [_vp, ctypes.c_uint64, ctypes.c_uint64, ctypes.c_uint64, _vp]),
     "yr_amd_scanner_set_timing": (_int, [_vp, _int]),
     "yr_amd_scanner_kernel_ms": (_int, [_vp, ctypes.POINTER(ctypes.c_float)]),

@@ -29,6 +29,12 @@ hipError_t launch_compact(const ScanParams& p, uint64_t* seg_offset, uint64_t* s
 hipError_t launch_xorshift(uint8_t* buf, uint64_t n, const uint64_t* states, uint32_t n_chunks,
                            uint32_t chunk, hipStream_t s);
 hipError_t configure_scan_kernel();
+hipError_t launch_trace_count(const uint32_t* T, const uint8_t* data, uint64_t n_pos,
+                              uint32_t* block_count, uint32_t n_blocks, hipStream_t s);
+hipError_t launch_trace_write(const uint32_t* T, const uint32_t* M, const uint8_t* data,
+                              uint64_t n_pos, const uint64_t* block_offset,
+                              yr_amd_trace_rec* out, uint64_t cap, uint32_t n_blocks,
+                              hipStream_t s);
 }  // namespace yamd
 
 namespace yamd {
@@ -128,6 +134,10 @@ struct yr_amd_scanner {
   uint64_t* d_summary = nullptr;
 
   std::vector<uint64_t> h_positions;
+
+  // yr_amd_trace_walk (debugging): the verbatim transition and match tables
+  uint32_t* d_trace_T = nullptr;
+  uint32_t* d_trace_M = nullptr;
 
   // state of the last yr_amd_scan_window / yr_amd_scan_device
   ScanParams last{};
@@ -396,7 +406,7 @@ int yr_amd_scanner_destroy(yr_amd_scanner* s) {
                   (void*)s->d_summary,
                   (void*)s->d_vcount, (void*)s->d_vkeep, (void*)s->d_vblock, (void*)s->d_vrec,
                   (void*)s->d_vchunk, (void*)s->d_seg_base,
-                  (void*)s->d_seg_next})
+                  (void*)s->d_seg_next, (void*)s->d_trace_T, (void*)s->d_trace_M})
     if (p) (void)hipFree(p);
   if (s->h_summary) (void)hipHostFree(s->h_summary);
   if (s->ev_begin) (void)hipEventDestroy(s->ev_begin);
@@ -1235,6 +1245,68 @@ int yr_amd_scan_block_verified(yr_amd_scanner* s, const uint8_t* data, size_t si
   if (records) *records = s->h_vrec.data();
   if (count) *count = n;
   return YR_AMD_SUCCESS;
+}
+
+int yr_amd_trace_walk(yr_amd_scanner* s, const uint8_t* d_data, size_t size, uint64_t data_base,
+                      yr_amd_trace_rec* out, uint64_t cap, uint64_t* count) {
+  if (s == nullptr || count == nullptr || (d_data == nullptr && size > 0) ||
+      (out == nullptr && cap > 0))
+    return YR_AMD_INVALID_ARGUMENT;
+  const FlatTables& f = s->tables->flat;
+  const uint64_t n_pos = (uint64_t)size + 1;   // positions 0 .. size
+  const uint64_t n_blocks64 = (n_pos + 255) / 256;
+  if (n_blocks64 > 0x7FFFFFFFu) return YR_AMD_INVALID_ARGUMENT;
+  const uint32_t n_blocks = (uint32_t)n_blocks64;
+  HIP_TRY(hipSetDevice(s->tables->device));
+  if (s->d_trace_T == nullptr) {
+    HIP_TRY(hipMalloc(&s->d_trace_T, f.T.size() * sizeof(uint32_t)));
+    HIP_TRY(hipMalloc(&s->d_trace_M, f.M.size() * sizeof(uint32_t)));
+    HIP_TRY(hipMemcpy(s->d_trace_T, f.T.data(), f.T.size() * sizeof(uint32_t), hipMemcpyHostToDevice));
+    HIP_TRY(hipMemcpy(s->d_trace_M, f.M.data(), f.M.size() * sizeof(uint32_t), hipMemcpyHostToDevice));
+  }
+  // per-block counts -> offsets on the host (a debugging path: blocks are small)
+  uint32_t* d_cnt = nullptr;
+  uint64_t* d_off = nullptr;
+  yr_amd_trace_rec* d_out = nullptr;
+  int r = YR_AMD_SUCCESS;
+  std::vector<uint32_t> cnt(n_blocks);
+  std::vector<uint64_t> off(n_blocks);
+  uint64_t total = 0;
+  if (hipMalloc(&d_cnt, n_blocks * sizeof(uint32_t)) != hipSuccess ||
+      launch_trace_count(s->d_trace_T, d_data, n_pos, d_cnt, n_blocks, s->stream) != hipSuccess ||
+      hipMemcpyAsync(cnt.data(), d_cnt, n_blocks * sizeof(uint32_t), hipMemcpyDeviceToHost,
+                     s->stream) != hipSuccess ||
+      hipStreamSynchronize(s->stream) != hipSuccess) {
+    r = YR_AMD_INTERNAL_FATAL_ERROR;
+  } else {
+    for (uint32_t b = 0; b < n_blocks; ++b) {
+      off[b] = total;
+      total += cnt[b];
+    }
+    const uint64_t rows = std::min<uint64_t>(total, cap);
+    if (rows > 0 &&
+        (hipMalloc(&d_off, n_blocks * sizeof(uint64_t)) != hipSuccess ||
+         hipMalloc(&d_out, rows * sizeof(yr_amd_trace_rec)) != hipSuccess ||
+         hipMemcpyAsync(d_off, off.data(), n_blocks * sizeof(uint64_t), hipMemcpyHostToDevice,
+                        s->stream) != hipSuccess ||
+         launch_trace_write(s->d_trace_T, s->d_trace_M, d_data, n_pos, d_off, d_out, rows, n_blocks,
+                            s->stream) != hipSuccess ||
+         hipMemcpyAsync(out, d_out, rows * sizeof(yr_amd_trace_rec), hipMemcpyDeviceToHost,
+                        s->stream) != hipSuccess ||
+         hipStreamSynchronize(s->stream) != hipSuccess))
+      r = YR_AMD_INTERNAL_FATAL_ERROR;
+    if (!r && debug_level() >= 2)
+      for (uint64_t k = 0; k < rows; ++k)
+        fprintf(stderr,
+                "- match_table[state=%u]=%u i=%llu block_data=%p block->base=0x%llx // "
+                "yr_amd_trace_walk()\n",
+                out[k].state, out[k].match, (unsigned long long)out[k].position,
+                (const void*)d_data, (unsigned long long)data_base);
+  }
+  for (void* p : {(void*)d_cnt, (void*)d_off, (void*)d_out})
+    if (p) (void)hipFree(p);
+  if (!r) *count = total;
+  return r;
 }
 
 int yr_amd_replay(const yr_amd_tables* t, const uint8_t* data, size_t size,
