@@ -367,7 +367,33 @@ __device__ __forceinline__ uint32_t byte_keys_any(const uint32_t (&S)[6], const 
 }
 
 // Per-position form (drains): bit j <=> lane byte j equals a 1-byte key.
+// Exact zero-byte flags (bit 7 of each byte of z_d) OR-ed over the keys, then
+// each dword's four flags gathered by one v_dot4_u32_u8 against the place
+// values 2^r (two dwords per chain: bytes of 0x80 times 1..128 stay below 2^16).
+#ifndef YAMD_BK_DOT
+#define YAMD_BK_DOT 1
+#endif
 __device__ __forceinline__ uint32_t byte_keys_mask(const uint32_t (&S)[6], const ScanParams& p) {
+#if YAMD_BK_DOT
+  uint32_t z[4] = {0u, 0u, 0u, 0u};
+  for (uint32_t k = 0; k < p.n_byte_keys; ++k) {
+    const uint32_t v = ((p.byte_keys >> (8 * k)) & 0xFFu) * 0x01010101u;
+#pragma unroll
+    for (int d = 0; d < 4; ++d) {
+      const uint32_t t = S[1 + d] ^ v;
+      // z |= ~(((t & 0x7F7F7F7F) + 0x7F7F7F7F) | t): bit 7 of a byte set iff it is 0
+      asm("v_bitop3_b32 %0, %1, %2, %0 bitop3:0xab"
+          : "+v"(z[d]) : "v"((t & 0x7F7F7F7Fu) + 0x7F7F7F7Fu), "v"(t));
+    }
+  }
+  const uint32_t lo = __builtin_amdgcn_udot4(z[1] & 0x80808080u, 0x80402010u,
+                                             __builtin_amdgcn_udot4(z[0] & 0x80808080u, 0x08040201u, 0u, false),
+                                             false);
+  const uint32_t hi = __builtin_amdgcn_udot4(z[3] & 0x80808080u, 0x80402010u,
+                                             __builtin_amdgcn_udot4(z[2] & 0x80808080u, 0x08040201u, 0u, false),
+                                             false);
+  return (lo >> 7) | (hi << 1);   // (x 128: bytes 0..7 in bits 7..14, 8..15 in 15..22)
+#else
   uint32_t m = 0;
   for (uint32_t k = 0; k < p.n_byte_keys; ++k) {
     const uint32_t v = ((p.byte_keys >> (8 * k)) & 0xFFu) * 0x01010101u;
@@ -379,7 +405,9 @@ __device__ __forceinline__ uint32_t byte_keys_mask(const uint32_t (&S)[6], const
     }
   }
   return m;
+#endif
 }
+
 
 // Kernel variants whose drains defer their first-level loads (WaveQueue).
 #ifndef YAMD_DEFER_FL
@@ -460,8 +488,11 @@ __device__ __forceinline__ void drain(const ScanParams& p, WaveQueue& q, uint32_
     const u32x2 e45 = lds_load<u32x2>(ent + 16);
     const uint32_t S[6] = {e45.x, e01.x, e01.y, e23.x, e23.y, 0u};
     off0 = (e45.y & 0xFFFFu) * kBytesPerLane;
-    if constexpr (kEven<MODE>) m = even_mask<MODE == kModeEvenHash>(S);
-    else m = dense_mask(stage1<0, false>(S, lane));
+    if constexpr (kEven<MODE>) {
+      m = even_mask<MODE == kModeEvenHash>(S);
+    } else {
+      m = dense_mask(stage1<0, false>(S, lane));
+    }
     if constexpr (kByteKeys<MODE>) {
       kmask = byte_keys_mask(S, p);
       m |= kmask;
