@@ -187,15 +187,36 @@ constexpr int kModeByteKeys = 20;
 // the five bytes kept beside certain candidates near a lane's end (tables with
 // guard-decided 1-byte keys: ScanParams::kx_next)
 constexpr int kModeByteKeysNext = 23;
-template <int MODE>
-constexpr bool kByteKeys = MODE == kModeByteKeys || MODE == kModeByteKeysNext;
 // Kernel variant: the product kernel for the even-position filter
-// (internal.h kFilterEven: rule sets whose keys are all 4 bytes long).
+// (internal.h kFilterEven: tables.cpp picks it for sets of 4-byte keys, and
+// for other shapes when its issue model says so).
 constexpr int kModeEven = 21;
 // ... with the hashed block index (internal.h kFilterEvenHash).
 constexpr int kModeEvenHash = 22;
+// The byte-key kernels (20, 23) with the even-position filter, plain / hashed.
+constexpr int kModeByteKeysEven = 26;
+constexpr int kModeByteKeysEvenHash = 27;
+constexpr int kModeByteKeysNextEven = 28;
+constexpr int kModeByteKeysNextEvenHash = 29;
 template <int MODE>
-constexpr bool kEven = MODE == kModeEven || MODE == kModeEvenHash;
+constexpr bool kByteKeys = MODE == kModeByteKeys || MODE == kModeByteKeysNext ||
+                           (MODE >= kModeByteKeysEven && MODE <= kModeByteKeysNextEvenHash);
+// ring entries carry the next lane's first two bytes (ScanParams::kx_next)
+template <int MODE>
+constexpr bool kNextBytes =
+    MODE == kModeByteKeysNext || MODE == kModeByteKeysNextEven || MODE == kModeByteKeysNextEvenHash;
+template <int MODE>
+constexpr bool kEven = MODE == kModeEven || MODE == kModeEvenHash ||
+                       (MODE >= kModeByteKeysEven && MODE <= kModeByteKeysNextEvenHash);
+template <int MODE>
+constexpr bool kEvenHash =
+    MODE == kModeEvenHash || MODE == kModeByteKeysEvenHash || MODE == kModeByteKeysNextEvenHash;
+// the stage-1 filter test a kernel variant runs (stage1's MODE argument)
+template <int MODE>
+constexpr int kStage1Mode = !(kByteKeys<MODE> || MODE == 24 || MODE == 25) ? MODE
+                            : kEvenHash<MODE>                              ? kModeEvenHash
+                            : kEven<MODE>                                  ? kModeEven
+                                                                           : 0;
 // Profiling ablations of the byte-key kernel (diagnostic builds): 24 = the 1-byte
 // keys detected but not appended (the ring holds the filter hits only), 25 =
 // not even detected.  Both on a 1-byte-key rule set; output wrong by construction.
@@ -489,7 +510,7 @@ __device__ __forceinline__ void drain(const ScanParams& p, WaveQueue& q, uint32_
     const uint32_t S[6] = {e45.x, e01.x, e01.y, e23.x, e23.y, 0u};
     off0 = (e45.y & 0xFFFFu) * kBytesPerLane;
     if constexpr (kEven<MODE>) {
-      m = even_mask<MODE == kModeEvenHash>(S);
+      m = even_mask<kEvenHash<MODE>>(S);
     } else {
       m = dense_mask(stage1<0, false>(S, lane));
     }
@@ -569,7 +590,7 @@ __device__ __forceinline__ void drain(const ScanParams& p, WaveQueue& q, uint32_
         // the entry of a tile's last lane: e <= 14 there)
         const uint32_t li = lds_load<uint32_t>(ent + 20);
         const uint32_t e =
-            min(j + p.kx_end, MODE == kModeByteKeysNext && (li & (kWave - 1)) != kWave - 1 ? 16u : 14u);
+            min(j + p.kx_end, kNextBytes<MODE> && (li & (kWave - 1)) != kWave - 1 ? 16u : 14u);
         uint32_t b5;
         if (e <= 14u) {
           x = window4(ent, e);
@@ -807,7 +828,7 @@ __device__ __forceinline__ void ring_append(const ScanParams& p, WaveQueue& q, S
         lds_store2(ent, S[1], S[2]);
         lds_store2(ent + 8, S[3], S[4]);
         // (byte-key kernel: the next lane's first two bytes in the top half)
-        lds_store2(ent + 16, S[0], (tile_off >> 4) + lane | (MODE == kModeByteKeysNext ? S[5] << 16 : 0u));
+        lds_store2(ent + 16, S[0], (tile_off >> 4) + lane | (kNextBytes<MODE> ? S[5] << 16 : 0u));
       }
     }
     q.count += n;
@@ -869,8 +890,8 @@ __device__ __forceinline__ void tile_step(const ScanParams& p, WaveQueue& q, Seg
   tile_context(st, cur, S);
   // the next lane's first dword (wave_shl:1; lane 63: 0), for the five bytes
   // kept beside a certain candidate near the lane's end (drain)
-  if constexpr (MODE == kModeByteKeysNext) S[5] = __builtin_amdgcn_mov_dpp(cur.x, 0x130, 0xF, 0xF, true);
-  uint32_t any = stage1<(kByteKeys<MODE> || kByteKeyAblation<MODE>) ? 0 : MODE, true>(S, lane);
+  if constexpr (kNextBytes<MODE>) S[5] = __builtin_amdgcn_mov_dpp(cur.x, 0x130, 0xF, 0xF, true);
+  uint32_t any = stage1<kStage1Mode<MODE>, true>(S, lane);
   if constexpr (kByteKeys<MODE>) any |= byte_keys_any(S, p);
   if constexpr (MODE == 24) asm volatile("" ::"v"(byte_keys_any(S, p)));
   if constexpr (kDeferFl<MODE>)
@@ -1175,13 +1196,19 @@ hipError_t launch_scan(const ScanParams& p, int grid, hipStream_t s, int mode) {
     case 25: hipLaunchKernelGGL(scan_segments_kernel<25>, dim3(grid), dim3(kWGThreads), lds, s, p); break;
 #endif
     default:
-      if (p.n_byte_keys != 0 && p.kx_next != 0)
-        hipLaunchKernelGGL(scan_segments_kernel<kModeByteKeysNext>, dim3(grid), dim3(kWGThreads),
-                           lds, s, p);
-      else if (p.n_byte_keys != 0)
-        hipLaunchKernelGGL(scan_segments_kernel<kModeByteKeys>, dim3(grid), dim3(kWGThreads), lds,
-                           s, p);
-      else if (p.filter_mode == kFilterEven)
+      if (p.n_byte_keys != 0) {
+        const int m = (p.kx_next != 0 ? 2 : 0) + (p.filter_mode == kFilterEven       ? 1
+                                                  : p.filter_mode == kFilterEvenHash ? 3
+                                                                                     : 0) * 4;
+        switch (m) {
+          case 0: hipLaunchKernelGGL(scan_segments_kernel<kModeByteKeys>, dim3(grid), dim3(kWGThreads), lds, s, p); break;
+          case 2: hipLaunchKernelGGL(scan_segments_kernel<kModeByteKeysNext>, dim3(grid), dim3(kWGThreads), lds, s, p); break;
+          case 4: hipLaunchKernelGGL(scan_segments_kernel<kModeByteKeysEven>, dim3(grid), dim3(kWGThreads), lds, s, p); break;
+          case 6: hipLaunchKernelGGL(scan_segments_kernel<kModeByteKeysNextEven>, dim3(grid), dim3(kWGThreads), lds, s, p); break;
+          case 12: hipLaunchKernelGGL(scan_segments_kernel<kModeByteKeysEvenHash>, dim3(grid), dim3(kWGThreads), lds, s, p); break;
+          default: hipLaunchKernelGGL(scan_segments_kernel<kModeByteKeysNextEvenHash>, dim3(grid), dim3(kWGThreads), lds, s, p); break;
+        }
+      } else if (p.filter_mode == kFilterEven)
         hipLaunchKernelGGL(scan_segments_kernel<kModeEven>, dim3(grid), dim3(kWGThreads), lds, s, p);
       else if (p.filter_mode == kFilterEvenHash)
         hipLaunchKernelGGL(scan_segments_kernel<kModeEvenHash>, dim3(grid), dim3(kWGThreads), lds, s,
@@ -1220,6 +1247,10 @@ hipError_t configure_scan_kernel() {
                         (const void*)scan_segments_kernel<kModeByteKeysNext>,
                         (const void*)scan_segments_kernel<kModeEven>,
                         (const void*)scan_segments_kernel<kModeEvenHash>,
+                        (const void*)scan_segments_kernel<kModeByteKeysEven>,
+                        (const void*)scan_segments_kernel<kModeByteKeysEvenHash>,
+                        (const void*)scan_segments_kernel<kModeByteKeysNextEven>,
+                        (const void*)scan_segments_kernel<kModeByteKeysNextEvenHash>,
 #if YAMD_DIAG
                         (const void*)scan_segments_kernel<1>,
                         (const void*)scan_segments_kernel<2>, (const void*)scan_segments_kernel<3>,

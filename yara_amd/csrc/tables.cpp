@@ -22,6 +22,8 @@
 #include <stdlib.h>
 #include <string.h>
 
+#include <algorithm>
+#include <cmath>
 #include <unordered_map>
 #include <utility>
 
@@ -277,34 +279,10 @@ int flatten_tables(const uint32_t* T, const uint32_t* M, uint32_t n_slots,
     for (const Key& k : out.keys)
       if (k.len == 1) out.byte_keys |= (k.bytes & 0xFFu) << (8 * out.n_byte_keys++);
   }
+  // The pair filter: every key window in both roles, every position tested
+  // (1-byte keys tested byte by byte are not in it).
   out.filter.assign(kFilterWords, 0u);
-  // 4-byte keys only: the even-position filter (internal.h kFilterEven).  A key
-  // ending at an even position has its suffix window there; one ending at an
-  // odd position has its prefix window ending at the even position before it.
-  // (YAMD_PAIR_FILTER: the pair filter regardless -- A/B measurements.)
-  if (out.len_mask == (1u << 4) && diag_env("YAMD_PAIR_FILTER") == nullptr) {
-    // both block forms; the one whose blocks pass fewer random windows
-    // (sum over blocks of |lo bits| x |hi bits|) unless the plain form is
-    // within 25 % (its test is one instruction shorter).  YAMD_EVEN_FILTER =
-    // plain / hash forces one (A/B measurements).
-    std::vector<uint32_t> f[2];
-    uint64_t pass[2] = {0, 0};
-    for (int h = 0; h < 2; ++h) {
-      f[h].assign(kFilterWords, 0u);
-      for (const Key& k : out.keys) {
-        filter_put(f[h], filter_probe_even(k.bytes >> 8, h));        // suffix
-        filter_put(f[h], filter_probe_even(k.bytes & 0xFFFFFFu, h));  // prefix
-      }
-      for (uint32_t b = 0; b < kFilterWords / 2; ++b)
-        pass[h] += (uint64_t)__builtin_popcount(f[h][2 * b]) * __builtin_popcount(f[h][2 * b + 1]);
-    }
-    const char* e = diag_env("YAMD_EVEN_FILTER");
-    const bool hashed = e ? strcmp(e, "hash") == 0 : 4 * pass[1] < 3 * pass[0];
-    out.filter_mode = hashed ? kFilterEvenHash : kFilterEven;
-    out.filter = std::move(f[hashed ? 1 : 0]);
-  }
   for (const Key& k : out.keys) {
-    if (out.filter_mode != kFilterPair) break;
     if (k.len == 1 && out.n_byte_keys != 0) continue;
     switch (k.len) {
       case 4: filter_set(out.filter, k.bytes >> 8); break;
@@ -315,6 +293,98 @@ int flatten_tables(const uint32_t* T, const uint32_t* M, uint32_t n_slots,
       case 1:
         for (uint32_t xy = 0; xy < 65536; ++xy) filter_set(out.filter, xy | (k.bytes << 16));
         break;
+    }
+  }
+  // The even-position filter (internal.h kFilterEven): the left role alone,
+  // tested at the even positions k only, a pass standing for k and k + 1.  So
+  // every key must have a window ending at k whichever of k, k + 1 it ends at:
+  // a 4-byte key its suffix (ending at k) and its prefix (ending at k + 1); a
+  // 3-byte key (p,q,r) itself and (*,p,q) -- the 256 windows with any first
+  // byte, one block's low word and 8 bits of its high word in the plain form;
+  // a 2-byte key (p,q) (*,p,q) and (*,*,p) -- the 64 plain blocks with last
+  // byte p, all bits.  Not with 1-byte keys in the filter (they would pass
+  // every window).  Both block forms are built; random windows pass a filter
+  // with probability sum over blocks of |lo bits| x |hi bits| / 2^24.
+  // (YAMD_PAIR_FILTER: the pair filter regardless -- A/B measurements.)
+  const bool byte_keys_all = out.keys_by_len[1] == out.n_byte_keys;
+  if (byte_keys_all && diag_env("YAMD_PAIR_FILTER") == nullptr) {
+    auto pass_sum = [](const std::vector<uint32_t>& f) {
+      uint64_t sum = 0;
+      for (uint32_t b = 0; b < kFilterWords / 2; ++b)
+        sum += (uint64_t)__builtin_popcount(f[2 * b]) * __builtin_popcount(f[2 * b + 1]);
+      return sum;
+    };
+    std::vector<uint32_t> f[2];
+    uint64_t pass[2] = {0, 0};
+    for (int h = 0; h < 2; ++h) {
+      f[h].assign(kFilterWords, 0u);
+      for (const Key& k : out.keys) {
+        switch (k.len) {
+          case 4:
+            filter_put(f[h], filter_probe_even(k.bytes >> 8, h));        // suffix
+            filter_put(f[h], filter_probe_even(k.bytes & 0xFFFFFFu, h));  // prefix
+            break;
+          case 3:
+            filter_put(f[h], filter_probe_even(k.bytes, h));
+            for (uint32_t x = 0; x < 256; ++x) filter_put(f[h], filter_probe_even(x | (k.bytes << 8), h));
+            break;
+          case 2:
+            for (uint32_t x = 0; x < 256; ++x) filter_put(f[h], filter_probe_even(x | (k.bytes << 8), h));
+            for (uint32_t xy = 0; xy < 65536; ++xy)
+              filter_put(f[h], filter_probe_even(xy | (k.bytes << 16), h));
+            break;
+          default: break;   // 1-byte keys: tested byte by byte
+        }
+      }
+      pass[h] = pass_sum(f[h]);
+    }
+    const char* e = diag_env("YAMD_EVEN_FILTER");
+    int pick = -1;   // -1: pair, 0: even plain, 1: even hashed
+    if (e != nullptr) {
+      pick = strcmp(e, "hash") == 0 ? 1 : 0;
+    } else if (out.len_mask == (1u << 4)) {
+      // 4-byte keys only: always even; the hashed form unless the plain one
+      // passes at most 4/3 as many windows (its test is one instruction shorter)
+      pick = 4 * pass[1] < 3 * pass[0] ? 1 : 0;
+    } else {
+      // Other shapes: a per-tile issue model in VALU-equivalents per 1 KiB tile
+      // (~7 us of a 4 GiB scan each; fitted to the kernel times of rx, short,
+      // hex, fuzz1, fuzz4, bytekeys and C under both filters,
+      // profiles/r03_even_shapes_ab.json): stage 1 (pair 91, even 55, hashed
+      // even 63) + 12 per 1-byte key tested + the ring append in tiles with an
+      // entry (12) + per entry of certain 1-byte-key hits 6 and per entry of
+      // filter passes 5 (first level) or 23 (2-byte keys: every hit position
+      // goes to the bucket probes), never below the kernel's floor (pair 100,
+      // even 89: the input stream plus the loop).  A plain even block whose
+      // last byte is a 1-byte key passes only at positions that are certain
+      // candidates anyway, so its passes add no entries.
+      const double K = out.n_byte_keys, d_filt = (out.len_mask & 6u) ? 23.0 : 5.0;
+      auto is_byte_key = [&](uint32_t c) {
+        for (uint32_t i = 0; i < out.n_byte_keys; ++i)
+          if (((out.byte_keys >> (8 * i)) & 0xFFu) == c) return true;
+        return false;
+      };
+      uint64_t pass_plain_new = 0;
+      for (uint32_t b = 0; b < kFilterWords / 2; ++b)
+        if (!is_byte_key((b >> 6) & 0xFFu))
+          pass_plain_new += (uint64_t)__builtin_popcount(f[0][2 * b]) * __builtin_popcount(f[0][2 * b + 1]);
+      auto cost = [&](double stage1, double floor, double p_window, int tests) {
+        const double cert = 1.0 - std::pow(1.0 - K / 256.0, (double)kBytesPerLane);
+        const double filt = 1.0 - std::pow(1.0 - p_window, tests);
+        const double lane = 1.0 - (1.0 - cert) * (1.0 - filt);
+        const double c = stage1 + 12.0 * K + 12.0 * (1.0 - std::pow(1.0 - lane, (double)kWave)) +
+                         kWave * (6.0 * cert + d_filt * filt);
+        return std::max(floor, c);
+      };
+      const double c_pair = cost(91.0, 100.0, pass_sum(out.filter) / 16777216.0, kBytesPerLane);
+      const double c_even[2] = {cost(55.0, 89.0, pass_plain_new / 16777216.0, kBytesPerLane / 2),
+                                cost(63.0, 89.0, pass[1] / 16777216.0, kBytesPerLane / 2)};
+      const int h = c_even[1] < c_even[0] ? 1 : 0;
+      if (c_even[h] < 0.97 * c_pair) pick = h;
+    }
+    if (pick >= 0) {
+      out.filter_mode = pick ? kFilterEvenHash : kFilterEven;
+      out.filter = std::move(f[pick]);
     }
   }
   for (uint32_t w : out.filter) out.filter_set_bits += (uint32_t)__builtin_popcount(w);
