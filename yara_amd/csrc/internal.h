@@ -34,6 +34,7 @@ constexpr int kTile = kWave * kBytesPerLane;        // 1024 B
 constexpr uint32_t kSegment = 1u << 20;   // max segment: 1 MiB (ring entries hold offset/16 in 16 bits)
 constexpr uint32_t kSegmentTarget = kSegment;   // preferred segment size (scanner.cpp)
 constexpr uint32_t kMaxByteKeys = 4;   // 1-byte keys tested in stage 1 (more: filter)
+constexpr uint32_t kMaxPairKeys = 4;   // even filters: 2-byte keys tested as aligned half-words
 constexpr int kWavesPerWG = 16;
 constexpr int kWGThreads = kWave * kWavesPerWG;     // 1024
 
@@ -223,6 +224,8 @@ struct ScanParams {
                             // written by the compaction), and
   uint32_t* live;           // [0] = count, then the other candidates' indices (any order)
   uint32_t filter_mode;     // kFilterPair / kFilterEven / kFilterEvenHash (FlatTables)
+  uint32_t pair_keys[2];    // even filters: FlatTables::pair_keys / n_pair_keys (16-bit
+  uint32_t n_pair_keys;     // test of the 2-byte keys ending at odd positions)
   uint32_t* seg_next;       // null: wave w takes segments w, w + waves, ...; else each wave
                             // takes its first segment by index and the next ones from this
                             // counter (initialised to the launch's wave count)

@@ -387,6 +387,47 @@ __device__ __forceinline__ uint32_t byte_keys_any(const uint32_t (&S)[6], const 
   return acc & 0x80808080u;
 }
 
+// Even-position filters: the 2-byte keys (p, q) ending at an odd position k + 1
+// are the aligned half-words p | q << 8 of the lane (tables.cpp pair_test;
+// their (*, *, p) windows would make every byte p a filter pass).  Same
+// zero test as byte_keys_any, per 16-bit half: nonzero iff some half matches.
+__device__ __forceinline__ uint32_t pair_keys_any(const uint32_t (&S)[6], const ScanParams& p) {
+  uint32_t acc = 0;
+  for (uint32_t k = 0; k < p.n_pair_keys; ++k) {   // wave-uniform, 0..kMaxPairKeys
+    const uint32_t v = ((p.pair_keys[k >> 1] >> (16 * (k & 1u))) & 0xFFFFu) * 0x00010001u;
+#pragma unroll
+    for (int d = 1; d <= 4; ++d) {
+      const uint32_t t = S[d] ^ v;
+      asm("v_bitop3_b32 %0, %1, %2, %0 bitop3:0xba" : "+v"(acc) : "v"(t - 0x00010001u), "v"(t));
+    }
+  }
+  return acc & 0x80008000u;
+}
+
+// Per-position form (drains): bit j (odd) <=> lane bytes j - 1, j are a 2-byte key.
+__device__ __forceinline__ uint32_t pair_keys_mask(const uint32_t (&S)[6], const ScanParams& p) {
+  uint32_t z[4] = {0u, 0u, 0u, 0u};
+  for (uint32_t k = 0; k < p.n_pair_keys; ++k) {
+    const uint32_t v = ((p.pair_keys[k >> 1] >> (16 * (k & 1u))) & 0xFFFFu) * 0x00010001u;
+#pragma unroll
+    for (int d = 0; d < 4; ++d) {
+      const uint32_t t = S[1 + d] ^ v;
+      // bit 15 / 31 set iff that half is 0 (exact: no carry between the halves)
+      asm("v_bitop3_b32 %0, %1, %2, %0 bitop3:0xab"
+          : "+v"(z[d]) : "v"((t & 0x7FFF7FFFu) + 0x7FFF7FFFu), "v"(t));
+    }
+  }
+  // flags in bytes 1 and 3 of each dword: the byte-key gather puts them at bits
+  // 4d + 1 and 4d + 3
+  const uint32_t lo = __builtin_amdgcn_udot4(z[1] & 0x80008000u, 0x80402010u,
+                                             __builtin_amdgcn_udot4(z[0] & 0x80008000u, 0x08040201u, 0u, false),
+                                             false);
+  const uint32_t hi = __builtin_amdgcn_udot4(z[3] & 0x80008000u, 0x80402010u,
+                                             __builtin_amdgcn_udot4(z[2] & 0x80008000u, 0x08040201u, 0u, false),
+                                             false);
+  return (lo >> 7) | (hi << 1);
+}
+
 // Per-position form (drains): bit j <=> lane byte j equals a 1-byte key.
 // Exact zero-byte flags (bit 7 of each byte of z_d) OR-ed over the keys, then
 // each dword's four flags gathered by one v_dot4_u32_u8 against the place
@@ -511,6 +552,7 @@ __device__ __forceinline__ void drain(const ScanParams& p, WaveQueue& q, uint32_
     off0 = (e45.y & 0xFFFFu) * kBytesPerLane;
     if constexpr (kEven<MODE>) {
       m = even_mask<kEvenHash<MODE>>(S);
+      if (p.n_pair_keys != 0) m |= pair_keys_mask(S, p);
     } else {
       m = dense_mask(stage1<0, false>(S, lane));
     }
@@ -892,6 +934,8 @@ __device__ __forceinline__ void tile_step(const ScanParams& p, WaveQueue& q, Seg
   // kept beside a certain candidate near the lane's end (drain)
   if constexpr (kNextBytes<MODE>) S[5] = __builtin_amdgcn_mov_dpp(cur.x, 0x130, 0xF, 0xF, true);
   uint32_t any = stage1<kStage1Mode<MODE>, true>(S, lane);
+  if constexpr (kEven<MODE>)
+    if (p.n_pair_keys != 0) any |= pair_keys_any(S, p);
   if constexpr (kByteKeys<MODE>) any |= byte_keys_any(S, p);
   if constexpr (MODE == 24) asm volatile("" ::"v"(byte_keys_any(S, p)));
   if constexpr (kDeferFl<MODE>)

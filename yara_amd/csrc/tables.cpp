@@ -307,6 +307,8 @@ int flatten_tables(const uint32_t* T, const uint32_t* M, uint32_t n_slots,
   // with probability sum over blocks of |lo bits| x |hi bits| / 2^24.
   // (YAMD_PAIR_FILTER: the pair filter regardless -- A/B measurements.)
   const bool byte_keys_all = out.keys_by_len[1] == out.n_byte_keys;
+  // 2-byte keys ending at odd positions: a half-word test in stage 1 when few
+  const bool pair_test = out.keys_by_len[2] <= kMaxPairKeys;
   if (byte_keys_all && diag_env("YAMD_PAIR_FILTER") == nullptr) {
     auto pass_sum = [](const std::vector<uint32_t>& f) {
       uint64_t sum = 0;
@@ -330,8 +332,9 @@ int flatten_tables(const uint32_t* T, const uint32_t* M, uint32_t n_slots,
             break;
           case 2:
             for (uint32_t x = 0; x < 256; ++x) filter_put(f[h], filter_probe_even(x | (k.bytes << 8), h));
-            for (uint32_t xy = 0; xy < 65536; ++xy)
-              filter_put(f[h], filter_probe_even(xy | (k.bytes << 16), h));
+            if (!pair_test)
+              for (uint32_t xy = 0; xy < 65536; ++xy)
+                filter_put(f[h], filter_probe_even(xy | (k.bytes << 16), h));
             break;
           default: break;   // 1-byte keys: tested byte by byte
         }
@@ -376,15 +379,23 @@ int flatten_tables(const uint32_t* T, const uint32_t* M, uint32_t n_slots,
                          kWave * (6.0 * cert + d_filt * filt);
         return std::max(floor, c);
       };
+      // (+12 per 2-byte key tested as half-words: 3 per dword, like a 1-byte key)
+      const double s_pair = pair_test ? 12.0 * out.keys_by_len[2] : 0.0;
       const double c_pair = cost(91.0, 100.0, pass_sum(out.filter) / 16777216.0, kBytesPerLane);
-      const double c_even[2] = {cost(55.0, 89.0, pass_plain_new / 16777216.0, kBytesPerLane / 2),
-                                cost(63.0, 89.0, pass[1] / 16777216.0, kBytesPerLane / 2)};
+      const double c_even[2] = {cost(55.0 + s_pair, 89.0, pass_plain_new / 16777216.0, kBytesPerLane / 2),
+                                cost(63.0 + s_pair, 89.0, pass[1] / 16777216.0, kBytesPerLane / 2)};
       const int h = c_even[1] < c_even[0] ? 1 : 0;
       if (c_even[h] < 0.97 * c_pair) pick = h;
     }
     if (pick >= 0) {
       out.filter_mode = pick ? kFilterEvenHash : kFilterEven;
       out.filter = std::move(f[pick]);
+      if (pair_test)
+        for (const Key& k : out.keys)
+          if (k.len == 2) {
+            out.pair_keys[out.n_pair_keys / 2] |= (k.bytes & 0xFFFFu) << (16 * (out.n_pair_keys % 2));
+            ++out.n_pair_keys;
+          }
     }
   }
   for (uint32_t w : out.filter) out.filter_set_bits += (uint32_t)__builtin_popcount(w);

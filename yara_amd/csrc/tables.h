@@ -41,6 +41,11 @@ struct FlatTables {
   // being inserted into the window filter (each would fill it with 65,536
   // windows): up to kMaxByteKeys key bytes, packed low byte first
   uint32_t byte_keys = 0, n_byte_keys = 0;
+  // even-position filters: up to kMaxPairKeys 2-byte keys (p | q << 8, two per
+  // word) tested in stage 1 as the aligned half-words of the lane, i.e. where
+  // they end at an odd position, instead of as the filter's (*, *, p) windows
+  // (which would pass every byte p)
+  uint32_t pair_keys[2] = {0, 0}, n_pair_keys = 0;
   // bit b set: some trie node of depth >= 2 ends with byte b (so a position
   // whose last byte is the 1-byte key b may have a deeper state than b's node)
   uint32_t deep_last[8] = {0, 0, 0, 0, 0, 0, 0, 0};
