@@ -179,6 +179,15 @@ struct WaveQueue {
   uint32_t wa, oa, ia, da;
   uint32_t wb, ob, ib, db;
 };
+
+// A key count read where it is tested: an opaque copy, so the compiler does not
+// hoist the loop-exit tests out of the tile loop as lane masks (it spilled
+// them to VGPR lanes: two v_readlane per key and tile)
+__device__ __forceinline__ uint32_t uniform_count(uint32_t n) {
+  asm volatile("" : "+s"(n));
+  return n;
+}
+
 constexpr uint32_t kNoHit = 0xFFFFFFFFu;
 // Kernel variant: the product kernel for rule sets whose 1-byte keys are tested
 // byte by byte in stage 1 (byte_keys_any below) instead of in the filter.
@@ -375,8 +384,10 @@ __device__ __forceinline__ uint32_t even_mask(const uint32_t (&S)[6]) {
 // Does some byte of the lane's 16 equal a 1-byte key?  (nonzero = yes)
 __device__ __forceinline__ uint32_t byte_keys_any(const uint32_t (&S)[6], const ScanParams& p) {
   uint32_t acc = 0;
-  for (uint32_t k = 0; k < p.n_byte_keys; ++k) {   // wave-uniform, 1..kMaxByteKeys
-    const uint32_t v = ((p.byte_keys >> (8 * k)) & 0xFFu) * 0x01010101u;
+#pragma unroll
+  for (uint32_t k = 0; k < kMaxByteKeys; ++k) {   // 1..kMaxByteKeys keys (wave-uniform)
+    if (k != 0 && k >= uniform_count(p.n_byte_keys)) break;
+    const uint32_t v = ((p.byte_keys >> (8 * k)) & 0xFFu) * 0x01010101u;   // (k: a constant)
 #pragma unroll
     for (int d = 1; d <= 4; ++d) {
       const uint32_t t = S[d] ^ v;
@@ -393,7 +404,9 @@ __device__ __forceinline__ uint32_t byte_keys_any(const uint32_t (&S)[6], const 
 // zero test as byte_keys_any, per 16-bit half: nonzero iff some half matches.
 __device__ __forceinline__ uint32_t pair_keys_any(const uint32_t (&S)[6], const ScanParams& p) {
   uint32_t acc = 0;
-  for (uint32_t k = 0; k < p.n_pair_keys; ++k) {   // wave-uniform, 0..kMaxPairKeys
+#pragma unroll
+  for (uint32_t k = 0; k < kMaxPairKeys; ++k) {   // 1..kMaxPairKeys keys (wave-uniform)
+    if (k != 0 && k >= uniform_count(p.n_pair_keys)) break;
     const uint32_t v = ((p.pair_keys[k >> 1] >> (16 * (k & 1u))) & 0xFFFFu) * 0x00010001u;
 #pragma unroll
     for (int d = 1; d <= 4; ++d) {
@@ -407,7 +420,9 @@ __device__ __forceinline__ uint32_t pair_keys_any(const uint32_t (&S)[6], const 
 // Per-position form (drains): bit j (odd) <=> lane bytes j - 1, j are a 2-byte key.
 __device__ __forceinline__ uint32_t pair_keys_mask(const uint32_t (&S)[6], const ScanParams& p) {
   uint32_t z[4] = {0u, 0u, 0u, 0u};
-  for (uint32_t k = 0; k < p.n_pair_keys; ++k) {
+#pragma unroll
+  for (uint32_t k = 0; k < kMaxPairKeys; ++k) {
+    if (k != 0 && k >= uniform_count(p.n_pair_keys)) break;
     const uint32_t v = ((p.pair_keys[k >> 1] >> (16 * (k & 1u))) & 0xFFFFu) * 0x00010001u;
 #pragma unroll
     for (int d = 0; d < 4; ++d) {
@@ -438,8 +453,10 @@ __device__ __forceinline__ uint32_t pair_keys_mask(const uint32_t (&S)[6], const
 __device__ __forceinline__ uint32_t byte_keys_mask(const uint32_t (&S)[6], const ScanParams& p) {
 #if YAMD_BK_DOT
   uint32_t z[4] = {0u, 0u, 0u, 0u};
-  for (uint32_t k = 0; k < p.n_byte_keys; ++k) {
-    const uint32_t v = ((p.byte_keys >> (8 * k)) & 0xFFu) * 0x01010101u;
+#pragma unroll
+  for (uint32_t k = 0; k < kMaxByteKeys; ++k) {
+    if (k != 0 && k >= uniform_count(p.n_byte_keys)) break;
+    const uint32_t v = ((p.byte_keys >> (8 * k)) & 0xFFu) * 0x01010101u;   // (k: a constant)
 #pragma unroll
     for (int d = 0; d < 4; ++d) {
       const uint32_t t = S[1 + d] ^ v;
