@@ -513,6 +513,35 @@ constexpr bool kDeferFl =
     YAMD_DEFER_FL &&
     (MODE == 0 || MODE == 12 || kByteKeys<MODE> || kEven<MODE> || kByteKeyAblation<MODE>);
 
+// The output entry of a certain candidate (its last byte a 1-byte key) at lane
+// byte j of ring entry ent: it needs no window for the exact check, so the scan
+// keeps five bytes next to it for key_class instead, lane bytes e - 3 .. e + 1,
+// the key at place j + 3 - e of them: e = min(j + kx_end, 16), where bytes 16
+// and 17 are the next lane's first two (ring entry bytes 22, 23; not in the
+// entry of a tile's last lane: e <= 14 there).  y: in, the segment offset;
+// out, with the key place, the fifth byte and the deep flag.
+template <int MODE>
+__device__ __forceinline__ void certain_entry(const ScanParams& p, uint32_t ent, uint32_t j,
+                                              uint32_t& x, uint32_t& y) {
+  const uint32_t li = lds_load<uint32_t>(ent + 20);
+  const uint32_t e =
+      min(j + p.kx_end, kNextBytes<MODE> && (li & (kWave - 1)) != kWave - 1 ? 16u : 14u);
+  uint32_t b5;
+  if (e <= 14u) {
+    x = window4(ent, e);
+    b5 = lds_load<uint8_t>(ent + e + 1);
+  } else {   // lane bytes 12..17
+    const uint64_t w6 = lds_load<uint32_t>(ent + 12) | (uint64_t)(li >> 16) << 32;
+    x = (uint32_t)(w6 >> (8 * (e - 15u)));
+    b5 = (uint32_t)(w6 >> (8 * (e - 11u))) & 0xFFu;
+  }
+  y |= b5 << kOutByteShift | (j + 5 - e) << kOutKeyShift;
+  if (p.kx_deep != 0u) {   // (the byte before the key, bytes -4..-1 at 16..19)
+    const uint32_t b = lds_load<uint8_t>(ent + (j != 0u ? j - 1u : 19u));
+    if (excluded(b, p.kd_x0[0], p.kd_x1[0])) y |= kOutDeep;
+  }
+}
+
 // Consume a deferred drain's first-level words: the lanes' hits that pass go,
 // in order, to the pending list.
 template <int MODE>
@@ -642,28 +671,7 @@ __device__ __forceinline__ void drain(const ScanParams& p, WaveQueue& q, uint32_
       maybe &= maybe - 1;
       uint32_t y = off0 + j, x;
       if (kByteKeys<MODE> && ((kmask >> j) & 1u)) {
-        // a certain candidate needs no window for the exact check: keep five
-        // bytes next to it for key_class, lane bytes e - 3 .. e + 1, the key at
-        // place j + 3 - e of them: e = min(j + kx_end, 16), where bytes 16
-        // and 17 are the next lane's first two (ring entry bytes 22, 23; not in
-        // the entry of a tile's last lane: e <= 14 there)
-        const uint32_t li = lds_load<uint32_t>(ent + 20);
-        const uint32_t e =
-            min(j + p.kx_end, kNextBytes<MODE> && (li & (kWave - 1)) != kWave - 1 ? 16u : 14u);
-        uint32_t b5;
-        if (e <= 14u) {
-          x = window4(ent, e);
-          b5 = lds_load<uint8_t>(ent + e + 1);
-        } else {   // lane bytes 12..17
-          const uint64_t w6 = lds_load<uint32_t>(ent + 12) | (uint64_t)(li >> 16) << 32;
-          x = (uint32_t)(w6 >> (8 * (e - 15u)));
-          b5 = (uint32_t)(w6 >> (8 * (e - 11u))) & 0xFFu;
-        }
-        y |= b5 << kOutByteShift | (j + 5 - e) << kOutKeyShift;
-        if (p.kx_deep != 0u) {   // (the byte before the key, bytes -4..-1 at 16..19)
-          const uint32_t b = lds_load<uint8_t>(ent + (j != 0u ? j - 1u : 19u));
-          if (excluded(b, p.kd_x0[0], p.kd_x1[0])) y |= kOutDeep;
-        }
+        certain_entry<MODE>(p, ent, j, x, y);
       } else {
         x = window4(ent, j);
       }
