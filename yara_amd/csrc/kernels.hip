@@ -488,6 +488,9 @@ __device__ __forceinline__ uint32_t byte_keys_mask(const uint32_t (&S)[6], const
 }
 
 
+#ifndef YAMD_PRIO
+#define YAMD_PRIO 0
+#endif
 // Kernel variants whose drains defer their first-level loads (WaveQueue).
 #ifndef YAMD_DEFER_FL
 #define YAMD_DEFER_FL 1
@@ -877,8 +880,15 @@ __device__ __forceinline__ void ring_append(const ScanParams& p, WaveQueue& q, S
   const uint64_t lanes = __ballot(any != 0);
   if (lanes != 0) {
     const uint32_t n = (uint32_t)__popcll(lanes);
-    if (q.count + n > kQueueCap)
+    if (q.count + n > kQueueCap) {
+#if YAMD_PRIO
+      __builtin_amdgcn_s_setprio(0);   // (experiment: streaming waves first)
+#endif
       drain<MODE, true>(p, q, lane, st.seg_start, st.seg_len, st.out, st.found);
+#if YAMD_PRIO
+      __builtin_amdgcn_s_setprio(1);
+#endif
+    }
     if (any != 0) {
       // slot = count (scalar, folded into the base) + the appending lanes below
       const uint32_t below = __builtin_amdgcn_mbcnt_hi(
@@ -964,7 +974,15 @@ __device__ __forceinline__ void tile_step(const ScanParams& p, WaveQueue& q, Seg
   if constexpr (kByteKeys<MODE>) any |= byte_keys_any(S, p);
   if constexpr (MODE == 24) asm volatile("" ::"v"(byte_keys_any(S, p)));
   if constexpr (kDeferFl<MODE>)
-    if (q.defer) drain_complete<MODE>(p, q, lane, st.seg_start, st.out, st.found);
+    if (q.defer) {
+#if YAMD_PRIO >= 2
+      __builtin_amdgcn_s_setprio(0);
+#endif
+      drain_complete<MODE>(p, q, lane, st.seg_start, st.out, st.found);
+#if YAMD_PRIO >= 2
+      __builtin_amdgcn_s_setprio(1);
+#endif
+    }
   ring_append<MODE, TAIL>(p, q, st, S, any, tile_off, lane);
   issue_first_level<MODE>(p, q);
 }
@@ -1050,9 +1068,18 @@ __global__ __launch_bounds__(kWGThreads, 1) void scan_segments_kernel(ScanParams
   extern __shared__ __attribute__((aligned(16))) uint32_t lds[];
   uint32_t* filt = lds;
   {
+    // 128 KiB: 8 x 16 B per thread, all 8 loads in flight before the stores
+    // (a loop over blockDim.x waited for each load in turn: 8 L2 round trips
+    // before the first tile)
     const uint4* src = reinterpret_cast<const uint4*>(p.filter);
     uint4* dst = reinterpret_cast<uint4*>(filt);
-    for (uint32_t i = threadIdx.x; i < kFilterWords / 4; i += blockDim.x) dst[i] = src[i];
+    constexpr uint32_t kPer = kFilterWords / 4 / kWGThreads;
+    static_assert(kPer * kWGThreads * 4 == kFilterWords, "filter copy: whole uint4s per thread");
+    uint4 v[kPer];
+#pragma unroll
+    for (uint32_t k = 0; k < kPer; ++k) v[k] = src[threadIdx.x + k * kWGThreads];
+#pragma unroll
+    for (uint32_t k = 0; k < kPer; ++k) dst[threadIdx.x + k * kWGThreads] = v[k];
   }
   __syncthreads();
   const uint32_t lane = lane_id();
@@ -1065,6 +1092,9 @@ __global__ __launch_bounds__(kWGThreads, 1) void scan_segments_kernel(ScanParams
     WaveQueue q;   // (per segment: its per-lane state then stays in registers)
     q.ring = kFilterBytes + wid * (kQueueCap * kQueueEntryWords * 4);
     q.pend = kFilterBytes + kQueueBytes + wid * (kWave * 8);
+#if YAMD_PRIO
+    __builtin_amdgcn_s_setprio(1);
+#endif
     scan_segment<MODE>(p, q, seg, lane);
     if (p.seg_next == nullptr) {
       seg += total_waves;
