@@ -488,8 +488,14 @@ __device__ __forceinline__ uint32_t byte_keys_mask(const uint32_t (&S)[6], const
 }
 
 
+// Wave priorities: the streaming waves (stage 1, the appends) run at
+// s_setprio 1, a wave inside a drain or a deferred first-level completion at 0,
+// so the arbiter issues the waves that keep the input stream going first while
+// a drain's long VALU burst fills the gaps (C -1.3 to -2.5 %, rx -2 %, B/E
+// within noise: profiles/r03_copy_prio_ab.json, r03_prio_ab.json).  1 = drains
+// only, 0 = off (A/B builds).
 #ifndef YAMD_PRIO
-#define YAMD_PRIO 0
+#define YAMD_PRIO 2
 #endif
 // Kernel variants whose drains defer their first-level loads (WaveQueue).
 #ifndef YAMD_DEFER_FL
@@ -882,7 +888,7 @@ __device__ __forceinline__ void ring_append(const ScanParams& p, WaveQueue& q, S
     const uint32_t n = (uint32_t)__popcll(lanes);
     if (q.count + n > kQueueCap) {
 #if YAMD_PRIO
-      __builtin_amdgcn_s_setprio(0);   // (experiment: streaming waves first)
+      __builtin_amdgcn_s_setprio(0);   // (streaming waves first)
 #endif
       drain<MODE, true>(p, q, lane, st.seg_start, st.seg_len, st.out, st.found);
 #if YAMD_PRIO
