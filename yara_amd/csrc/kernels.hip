@@ -492,8 +492,8 @@ __device__ __forceinline__ uint32_t byte_keys_mask(const uint32_t (&S)[6], const
 // s_setprio 1, a wave inside a drain or a deferred first-level completion at 0,
 // so the arbiter issues the waves that keep the input stream going first while
 // a drain's long VALU burst fills the gaps (C -1.3 to -2.5 %, rx -2 %, B/E
-// within noise: profiles/r03_copy_prio_ab.json, r03_prio_ab.json).  1 = drains
-// only, 0 = off (A/B builds).
+// within noise: profiles/r03_copy_prio_ab.json, r03_prio_ab.json,
+// r03_prio3_ab.json).  1 = drains only, 0 = off (A/B builds).
 #ifndef YAMD_PRIO
 #define YAMD_PRIO 2
 #endif

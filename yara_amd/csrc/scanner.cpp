@@ -426,8 +426,16 @@ int yr_amd_scanner_set_timing(yr_amd_scanner* s, int enable) {
   if (s == nullptr) return YR_AMD_INVALID_ARGUMENT;
   if (enable && s->ev_begin == nullptr) {
     HIP_TRY(hipSetDevice(s->tables->device));
-    HIP_TRY(hipEventCreate(&s->ev_begin));
-    HIP_TRY(hipEventCreate(&s->ev_end));
+    // the kernel's begin/end markers only time it: no system-scope fence (a
+    // cache writeback + invalidate at each record, ~5 us of stream gap per
+    // marker, profiles/r03_step_gaps.json); ev_compact also completes the scan
+    // for the host (last_done) and keeps it
+#ifndef YAMD_EV_NOFENCE
+#define YAMD_EV_NOFENCE 1
+#endif
+    const unsigned marker = YAMD_EV_NOFENCE ? hipEventDisableSystemFence : hipEventDefault;
+    HIP_TRY(hipEventCreateWithFlags(&s->ev_begin, marker));
+    HIP_TRY(hipEventCreateWithFlags(&s->ev_end, marker));
     HIP_TRY(hipEventCreate(&s->ev_compact));
   }
   s->timing = enable != 0;
