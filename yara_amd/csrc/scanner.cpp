@@ -197,6 +197,12 @@ static int debug_level() {
   return level;
 }
 
+// Scan-kernel timing markers without a system-scope fence (yr_amd_scanner_set_timing;
+// 0 = default events, for A/B builds)
+#ifndef YAMD_EV_NOFENCE
+#define YAMD_EV_NOFENCE 1
+#endif
+
 #define HIP_TRY(expr)                                   \
   do {                                                  \
     if ((expr) != hipSuccess) return YR_AMD_INTERNAL_FATAL_ERROR; \
@@ -430,9 +436,6 @@ int yr_amd_scanner_set_timing(yr_amd_scanner* s, int enable) {
     // cache writeback + invalidate at each record, ~5 us of stream gap per
     // marker, profiles/r03_step_gaps.json); ev_compact also completes the scan
     // for the host (last_done) and keeps it
-#ifndef YAMD_EV_NOFENCE
-#define YAMD_EV_NOFENCE 1
-#endif
     const unsigned marker = YAMD_EV_NOFENCE ? hipEventDisableSystemFence : hipEventDefault;
     HIP_TRY(hipEventCreateWithFlags(&s->ev_begin, marker));
     HIP_TRY(hipEventCreateWithFlags(&s->ev_end, marker));
