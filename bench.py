@@ -206,15 +206,20 @@ def main():
     def launch(k):
         scanners[k % depth].scan_window(buf.data_ptr(), lo, hi, total, begin, end)
 
+    gather_s = [0.0]   # wall time of this rank's gathers (N > 1), timed steps only
+
     def finish(k, timed_kernel=False):
         sc = scanners[k % depth]
         ptr, cnt, _ = sc.device_result()            # ascending block positions in HBM
         kms = sc.kernel_ms() if timed_kernel else None
         if world == 1:
             return (ptr, cnt), kms
+        t_g = time.perf_counter()
         pos = torch.empty(max(cnt, 1), dtype=torch.int64, device=dev)
         memcpy(pos.data_ptr(), ptr, cnt * 8, 3)
         pos = ydist.gather_positions(pos[:cnt])     # RCCL: counts + padded gather
+        if timed_kernel:
+            gather_s[0] += time.perf_counter() - t_g
         return pos, kms
 
     def run(steps, timed_kernel=False):
@@ -326,7 +331,33 @@ def main():
     elapsed = time.perf_counter() - t0
     for sc in scanners:
         sc.set_timing(False)
+    per_rank = None
     if world > 1:
+        # attribution of an N > 1 step (max over ranks below): every rank's
+        # own scan-kernel average (HIP events), its wall time and the wall time
+        # it spent in the candidate gathers, so a slow rank and a slow gather
+        # are told apart
+        mine = torch.tensor([sum(kernel_ms) / len(kernel_ms), min(kernel_ms), max(kernel_ms),
+                             elapsed, gather_s[0]], dtype=torch.float64,
+                            device=dev if args.backend == "nccl" else "cpu")
+        rows = [torch.empty_like(mine) for _ in range(world)]
+        dist.all_gather(rows, mine)
+        rows = [r.cpu().tolist() for r in rows]
+
+        def mma(v, nd=4):
+            return {"min": round(min(v), nd), "max": round(max(v), nd),
+                    "avg": round(sum(v) / len(v), nd), "by_rank": [round(x, nd) for x in v]}
+        per_rank = {
+            "per_rank_kernel_ms": mma([r[0] for r in rows]),
+            "per_rank_kernel_ms_extremes": {"min": round(min(r[1] for r in rows), 4),
+                                            "max": round(max(r[2] for r in rows), 4)},
+            "per_rank_step_ms": mma([r[3] / args.steps * 1e3 for r in rows]),
+            "per_rank_gather_ms_per_step": mma([r[4] / args.steps * 1e3 for r in rows]),
+            "what": "per rank over the timed steps: scan-kernel HIP-event average (and the "
+                    "extreme single launches), the rank's wall time per step, and its wall time "
+                    "per step inside the candidate gather (D2D copy + %s counts all-gather + "
+                    "padded gather); scans of later steps are queued behind, so gather time "
+                    "overlaps the GPU" % ("RCCL" if args.backend == "nccl" else args.backend)}
         t = torch.tensor([elapsed], dtype=torch.float64,
                          device=dev if args.backend == "nccl" else "cpu")
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
@@ -420,6 +451,8 @@ def main():
             "check": check,
             "other_rule_sets": other,
         }
+        if per_rank is not None:
+            line["multi"] = per_rank
         print(json.dumps(line), flush=True)
     if world > 1:
         dist.destroy_process_group()

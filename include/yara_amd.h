@@ -475,6 +475,42 @@ int yr_amd_pipeline_next(
 int yr_amd_pipeline_drain(yr_amd_pipeline* pipeline);
 
 /*
+ * The copy that moves a caller's block into pipeline / multi-device staging
+ * memory: copy n bytes from src to dst, return 0, or nonzero if the source
+ * could not be read.  It may run on the caller's thread and on the library's
+ * helper threads, several at once on disjoint pieces.  A libyara caller passes
+ * one that runs memcpy inside YR_TRYCATCH (exception.h:150-185) on the thread
+ * that calls it, so a block that faults while being copied (a file mapping
+ * truncated underneath) fails the submission with YR_AMD_COULD_NOT_MAP_FILE
+ * -- scanner.c:493-496's mapping of the walk's fault -- instead of raising
+ * SIGBUS on a thread with no handler.  Default (NULL): memcpy, and every page
+ * of a block must be readable.
+ */
+typedef int (*yr_amd_copy_fn)(void* user, void* dst, const void* src, size_t n);
+int yr_amd_pipeline_set_copy(yr_amd_pipeline* pipeline, yr_amd_copy_fn fn, void* user);
+
+/*
+ * A pipeline whose blocks are split across n devices:
+ * tables[k] as for yr_amd_multi_create.  Each block is copied once into a
+ * pinned buffer (yr_amd_pipeline_submit_dma: in parallel; _submit: in the
+ * caller's thread), every device DMAs its window of it (its byte range plus
+ * the verify halos, yr_amd_multi_shard's bounds) and scans and pre-verifies it;
+ * yr_amd_pipeline_next returns the devices' records concatenated in order --
+ * exactly the single-device record stream of the block.  Blocks overlap as in
+ * the single-device pipeline (block k+1's copy and DMA while block k is
+ * scanned or replayed).  n = 1 is yr_amd_pipeline_create.  A block whose
+ * device ranges could exceed YR_AMD_VERIFY_MAX_CANDIDATES candidates fails
+ * in yr_amd_pipeline_next with YR_AMD_INVALID_ARGUMENT (callers route such
+ * blocks to the host replay first, as integration/yr_gpu_scanner.c does).
+ */
+int yr_amd_pipeline_create_multi(yr_amd_tables* const* tables, uint32_t n, uint32_t depth,
+                                 yr_amd_pipeline** pipeline);
+
+/* Blocks smaller than `bytes` are not split: each goes whole to one device,
+ * round-robin (default 0: every block is split). */
+int yr_amd_pipeline_set_split_min(yr_amd_pipeline* pipeline, uint64_t bytes);
+
+/*
  * ---- Multi-device block scans ----
  *
  * One process, n devices (n <= YR_AMD_MAX_DEVICES; a device may repeat: n
@@ -509,7 +545,12 @@ int yr_amd_multi_shard(const yr_amd_multi* multi, uint64_t size, uint32_t k, uin
  * records owned by the multi scanner (valid until its next call).  A device
  * whose range could exceed YR_AMD_VERIFY_MAX_CANDIDATES candidates (range + 1
  * > the limit) makes it return YR_AMD_INVALID_ARGUMENT before any work: use
- * the single-device replay (yr_amd_scan_block + yr_amd_replay) then. */
+ * the single-device replay (yr_amd_scan_block + yr_amd_replay) then.  The
+ * block is staged through two pinned 256 MiB buffers (copied in parallel
+ * through the copy function of yr_amd_multi_set_copy, DMA'd to every device
+ * whose window overlaps them); a failed copy returns
+ * YR_AMD_COULD_NOT_MAP_FILE. */
+int yr_amd_multi_set_copy(yr_amd_multi* multi, yr_amd_copy_fn fn, void* user);
 int yr_amd_multi_scan_block_verified(
     yr_amd_multi* multi,
     const uint8_t* data,

@@ -400,7 +400,11 @@ int main(int argc, char** argv)
   g_mode = mode;
   const uint8_t* d_arg = scan_whole ? NULL : scan_data;
   int rs = run(rules, NULL, d_arg, n, bsize, overlap, &a, &ts);
+  double tm0[3], tm1[3], tmin[3] = {0, 0, 0};
+  yr_gpu_scanner_timing(gs, tm0);
   int rg = run(rules, gs, d_arg, n, bsize, overlap, &b, &tg);
+  yr_gpu_scanner_timing(gs, tm1);
+  for (int k = 0; k < 3; k++) tmin[k] = tm1[k] - tm0[k];
   /* E2E_REPEAT=N: N more timed runs of each side (steady state: warm caches,
    * allocated staging); the reported times are the minimum */
   int reps = getenv("E2E_REPEAT") ? atoi(getenv("E2E_REPEAT")) : 0;
@@ -415,8 +419,14 @@ int main(int argc, char** argv)
     x.n = x.cap = 0;
     x.r = NULL;
     x.dumped = 0;
+    yr_gpu_scanner_timing(gs, tm0);
     run(rules, gs, d_arg, n, bsize, overlap, &x, &t);
-    if (t < tg) tg = t;
+    yr_gpu_scanner_timing(gs, tm1);
+    if (t < tg)
+    {
+      tg = t;
+      for (int q = 0; q < 3; q++) tmin[q] = tm1[q] - tm0[q];
+    }
     free(x.r);
     free(x.rule_msg);
   }
@@ -472,11 +482,12 @@ int main(int argc, char** argv)
          "\"matches_stock\": %zu, \"matches_gpu\": %zu, \"rules_matching\": %d, "
          "\"same_matches\": %s, \"same_rule_reports\": %s, \"finished\": [%d, %d], "
          "\"stock_s\": %.4f, \"gpu_s\": %.4f, \"too_many\": [%d, %d], \"threads\": %d, "
-         "\"threads_ok\": %s, \"devices\": %d, \"multi_blocks\": %llu}\n",
+         "\"threads_ok\": %s, \"devices\": %d, \"multi_blocks\": %llu, "
+         "\"gpu_copy_s\": %.4f, \"gpu_wait_s\": %.4f, \"gpu_replay_s\": %.4f}\n",
          g_mode, n, bsize, rs, rg, a.n, b.n, n_match_rules, same_matches ? "true" : "false",
          same_rules ? "true" : "false", a.finished, b.finished, ts, tg, a.too_many, b.too_many,
          threads, threads_ok ? "true" : "false", n_devs,
-         (unsigned long long) yr_gpu_scanner_multi_blocks(gs));
+         (unsigned long long) yr_gpu_scanner_multi_blocks(gs), tmin[0], tmin[1], tmin[2]);
   yr_gpu_scanner_destroy(gs);
   yr_gpu_rules_destroy(gr);
   yr_rules_destroy(rules);

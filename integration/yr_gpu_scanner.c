@@ -43,6 +43,8 @@
 #include <yara/scan.h>
 #include <yara/stopwatch.h>
 
+#include <time.h>
+
 #include "exception.h" /* libyara/exception.h: YR_TRYCATCH (exception.h:150-185) */
 
 struct YR_GPU_RULES
@@ -64,9 +66,11 @@ struct YR_GPU_SCANNER
   uint32_t depth;
   uint32_t inflight;
   int direct;            /* single in-memory block (scan_mem): no staging copy */
-  yr_amd_multi* multi;   /* n_devices > 1: large blocks split across the devices */
+  yr_amd_multi* multi;   /* n_devices > 1: a large direct block split across the devices */
   uint64_t multi_min;    /* smallest block that is split */
   uint64_t multi_blocks; /* blocks scanned across the devices (statistics) */
+  int trycatch;          /* the scan's !SCAN_FLAGS_NO_TRYCATCH, for _guarded_copy */
+  double t_copy, t_gpu, t_replay; /* yr_gpu_scanner_timing */
 #ifdef YR_HAVE_BLOCK_SCANNER
   YR_BLOCK_SCANNER block_scanner; /* yr_gpu_scanner_attach */
 #endif
@@ -292,23 +296,54 @@ void yr_gpu_rules_destroy(YR_GPU_RULES* g)
   free(g);
 }
 
+/* The copy that moves a block into the library's pinned staging
+ * (yr_amd_copy_fn): memcpy inside YR_TRYCATCH on whichever thread runs it --
+ * the caller's or one of the library's helpers -- so a block that faults while
+ * it is copied (a file mapping truncated underneath) fails the copy, and the
+ * scan returns ERROR_COULD_NOT_MAP_FILE exactly as scanner.c:493-496 maps a
+ * fault of the walk, instead of SIGBUS on a helper thread. */
+static int _guarded_copy(void* user, void* dst, const void* src, size_t n)
+{
+  YR_GPU_SCANNER* gs = (YR_GPU_SCANNER*) user;
+  int result = 0;
+  YR_TRYCATCH(gs->trycatch, { memcpy(dst, src, n); }, { result = 1; });
+  return result;
+}
+
 int yr_gpu_scanner_create(YR_GPU_RULES* g, YR_GPU_SCANNER** out)
 {
   *out = NULL;
   YR_GPU_SCANNER* s = (YR_GPU_SCANNER*) calloc(1, sizeof(YR_GPU_SCANNER));
   if (s == NULL) return ERROR_INSUFFICIENT_MEMORY;
+  s->multi_min = YR_GPU_MULTI_MIN_BLOCK;
+  s->trycatch = 1;
   int r = yr_amd_scanner_create(g->tables, NULL, &s->scanner);
   if (r == ERROR_SUCCESS)
   {
+    /* several devices: one pipeline over all of them -- blocks of at least
+     * multi_min split across the devices, smaller ones whole to one device
+     * (round-robin), all in one ordered stream, so a large block never waits
+     * for the blocks in flight to drain */
     s->depth = 2;
-    r = yr_amd_pipeline_create(g->tables, s->depth, &s->pipe);
-    if (r != ERROR_SUCCESS) yr_amd_scanner_destroy(s->scanner);
+    r = g->n_devices > 1
+            ? yr_amd_pipeline_create_multi(g->dev_tables, g->n_devices, s->depth, &s->pipe)
+            : yr_amd_pipeline_create(g->tables, s->depth, &s->pipe);
+    if (r == ERROR_SUCCESS) r = yr_amd_pipeline_set_copy(s->pipe, _guarded_copy, s);
+    if (r == ERROR_SUCCESS && g->n_devices > 1)
+      r = yr_amd_pipeline_set_split_min(s->pipe, s->multi_min);
+    if (r != ERROR_SUCCESS)
+    {
+      yr_amd_pipeline_destroy(s->pipe);
+      yr_amd_scanner_destroy(s->scanner);
+    }
   }
   if (r == ERROR_SUCCESS && g->n_devices > 1)
   {
     r = yr_amd_multi_create(g->dev_tables, g->n_devices, &s->multi);
+    if (r == ERROR_SUCCESS) r = yr_amd_multi_set_copy(s->multi, _guarded_copy, s);
     if (r != ERROR_SUCCESS)
     {
+      yr_amd_multi_destroy(s->multi);
       yr_amd_pipeline_destroy(s->pipe);
       yr_amd_scanner_destroy(s->scanner);
     }
@@ -318,7 +353,6 @@ int yr_gpu_scanner_create(YR_GPU_RULES* g, YR_GPU_SCANNER** out)
     free(s);
     return r;
   }
-  s->multi_min = YR_GPU_MULTI_MIN_BLOCK;
   s->gpu_rules = g;
   s->preverify = 1;
   *out = s;
@@ -333,11 +367,26 @@ void yr_gpu_scanner_set_preverify(YR_GPU_SCANNER* s, int enable)
 void yr_gpu_scanner_set_multi_min_block(YR_GPU_SCANNER* s, uint64_t bytes)
 {
   s->multi_min = bytes;
+  if (s->multi != NULL) yr_amd_pipeline_set_split_min(s->pipe, bytes);
 }
 
 uint64_t yr_gpu_scanner_multi_blocks(const YR_GPU_SCANNER* s)
 {
   return s->multi_blocks;
+}
+
+static double _now(void)
+{
+  struct timespec t;
+  clock_gettime(CLOCK_MONOTONIC, &t);
+  return t.tv_sec + 1e-9 * t.tv_nsec;
+}
+
+void yr_gpu_scanner_timing(const YR_GPU_SCANNER* s, double t[3])
+{
+  t[0] = s->t_copy;
+  t[1] = s->t_gpu;
+  t[2] = s->t_replay;
 }
 
 void yr_gpu_scanner_destroy(YR_GPU_SCANNER* s)
@@ -500,13 +549,18 @@ static int _replay_next(YR_SCANNER* scanner, YR_GPU_SCANNER* gs)
   const uint8_t* data = NULL;
   size_t size = 0;
   uint64_t base = 0;
+  double t0 = _now();
   int result = yr_amd_pipeline_next(gs->pipe, &recs, &n, &data, &size, &base);
+  double t1 = _now();
+  gs->t_gpu += t1 - t0;
   gs->inflight--;
   if (result != ERROR_SUCCESS) return result;
   /* the walk of this block starts here: its position-0 timeout check */
   uint64_t next_check = 0;
   FAIL_ON_ERROR(_timeout_upto(scanner, &next_check, 0, size));
-  return _replay_records(scanner, recs, n, data, size, base, next_check);
+  result = _replay_records(scanner, recs, n, data, size, base, next_check);
+  gs->t_replay += _now() - t1;
+  return result;
 }
 
 /* One block into the pipeline; replays the oldest when `depth` are in flight. */
@@ -518,21 +572,18 @@ static int _pipeline_block(
 {
   int result = ERROR_SUCCESS;
   /* The block is copied into the pipeline's pinned buffer by several threads
-   * at once (yr_amd_pipeline_submit_dma), and a fault in a helper thread
-   * cannot be unwound through this thread's trycatch.  So every page is
-   * touched first, inside the trycatch: a block that faults (a truncated
-   * mapping) yields ERROR_COULD_NOT_MAP_FILE as scanner.c:493-496 does. */
+   * at once (yr_amd_pipeline_submit_dma), each chunk through _guarded_copy:
+   * a fault on any of them (a truncated mapping) fails the submission with
+   * ERROR_COULD_NOT_MAP_FILE as scanner.c:493-496 does.  The outer trycatch
+   * only keeps libyara's signal handler installed while the helpers copy (a
+   * helper's own trycatch restores the handler it found when it ends). */
+  gs->trycatch = !(scanner->flags & SCAN_FLAGS_NO_TRYCATCH);
+  double t0 = _now();
   YR_TRYCATCH(
-      !(scanner->flags & SCAN_FLAGS_NO_TRYCATCH),
-      {
-        volatile uint8_t sink = 0;
-        for (size_t o = 0; o < block->size; o += 4096) sink ^= data[o];
-        if (block->size > 0) sink ^= data[block->size - 1];
-        (void) sink;
-      },
+      gs->trycatch,
+      { result = yr_amd_pipeline_submit_dma(gs->pipe, data, block->size, block->base); },
       { result = ERROR_COULD_NOT_MAP_FILE; });
-  if (result != ERROR_SUCCESS) return result;
-  result = yr_amd_pipeline_submit_dma(gs->pipe, data, block->size, block->base);
+  gs->t_copy += _now() - t0;
   if (result != ERROR_SUCCESS) return result;
   gs->inflight++;
   if (gs->inflight == gs->depth) return _replay_next(scanner, gs);
@@ -553,37 +604,51 @@ static int _direct_block(
   int result = ERROR_SUCCESS;
   uint64_t next_check = 0;
   FAIL_ON_ERROR(_timeout_upto(scanner, &next_check, 0, block->size));
-  /* The H2D below reads the caller's buffer inside the HIP runtime, where a
-   * fault cannot be unwound.  Touch every page of it first, inside the
-   * trycatch, so a buffer that faults (a truncated file mapping, an unmapped
-   * range) yields ERROR_COULD_NOT_MAP_FILE as scanner.c:493-496 does; ~3 ms
-   * per GiB of resident memory. */
-  YR_TRYCATCH(
-      !(scanner->flags & SCAN_FLAGS_NO_TRYCATCH),
-      {
-        volatile uint8_t sink = 0;
-        for (size_t o = 0; o < block->size; o += 4096) sink ^= data[o];
-        if (block->size > 0) sink ^= data[block->size - 1];
-        (void) sink;
-      },
-      { result = ERROR_COULD_NOT_MAP_FILE; });
-  if (result != ERROR_SUCCESS) return result;
   const yr_amd_verify_rec* recs = NULL;
   uint64_t n = 0;
+  gs->trycatch = !(scanner->flags & SCAN_FLAGS_NO_TRYCATCH);
+  double t0 = _now();
   if (use_multi)
   {
-    FAIL_ON_ERROR(yr_amd_multi_scan_block_verified(
-        gs->multi, data, block->size, block->base, &recs, &n));
+    /* staged through pinned memory by _guarded_copy (helper threads
+     * included): a fault fails the call with ERROR_COULD_NOT_MAP_FILE; the
+     * outer trycatch keeps libyara's handler installed meanwhile */
+    YR_TRYCATCH(
+        gs->trycatch,
+        {
+          result = yr_amd_multi_scan_block_verified(
+              gs->multi, data, block->size, block->base, &recs, &n);
+        },
+        { result = ERROR_COULD_NOT_MAP_FILE; });
+    if (result != ERROR_SUCCESS) return result;
   }
   else
   {
+    /* The H2D below reads the caller's buffer inside the HIP runtime, where a
+     * fault cannot be unwound.  Touch every page of it first, inside the
+     * trycatch, so a buffer that faults (a truncated file mapping, an unmapped
+     * range) yields ERROR_COULD_NOT_MAP_FILE as scanner.c:493-496 does; ~3 ms
+     * per GiB of resident memory. */
+    YR_TRYCATCH(
+        gs->trycatch,
+        {
+          volatile uint8_t sink = 0;
+          for (size_t o = 0; o < block->size; o += 4096) sink ^= data[o];
+          if (block->size > 0) sink ^= data[block->size - 1];
+          (void) sink;
+        },
+        { result = ERROR_COULD_NOT_MAP_FILE; });
+    if (result != ERROR_SUCCESS) return result;
     FAIL_ON_ERROR(
         yr_amd_scan_block_verified(gs->scanner, data, block->size, block->base, &recs, &n));
   }
+  double t1 = _now();
+  gs->t_gpu += t1 - t0;
   YR_TRYCATCH(
       !(scanner->flags & SCAN_FLAGS_NO_TRYCATCH),
       { result = _replay_records(scanner, recs, n, data, block->size, block->base, next_check); },
       { result = ERROR_COULD_NOT_MAP_FILE; });
+  gs->t_replay += _now() - t1;
   return result;
 }
 
@@ -614,22 +679,17 @@ static int _scan_one_block(
    * rule set, or a dense key): a block that could exceed it is replayed from
    * the GPU scan's stream instead -- after the blocks still in flight, in
    * order.  The same limit as the library's, so no block reaches a refusal. */
-  int use_multi = gs->multi != NULL && gs->preverify && block->size >= gs->multi_min &&
-                  _multi_fits(gs, block->size);
-  int replay_block = !use_multi &&
-                     (!gs->preverify ||
-                      (uint64_t) block->size + 1 > YR_AMD_VERIFY_MAX_CANDIDATES);
-  while ((replay_block || use_multi) && gs->inflight > 0)
-    FAIL_ON_ERROR(_replay_next(scanner, gs));
+  int split = gs->multi != NULL && block->size >= gs->multi_min;
+  int fits = split ? _multi_fits(gs, block->size)
+                   : (uint64_t) block->size + 1 <= YR_AMD_VERIFY_MAX_CANDIDATES;
+  int replay_block = !gs->preverify || !fits;
+  while (replay_block && gs->inflight > 0) FAIL_ON_ERROR(_replay_next(scanner, gs));
   if (replay_block) return _yr_gpu_scan_mem_block(scanner, gs, data, block);
-  /* a large block across the devices, whole (the caller's buffer, probed
-   * inside the trycatch) -- after the blocks still in flight, in order */
-  if (use_multi)
-  {
-    gs->multi_blocks++;
-    return _direct_block(scanner, gs, data, block, 1);
-  }
-  if (gs->direct) return _direct_block(scanner, gs, data, block, 0);
+  if (split) gs->multi_blocks++;
+  /* the one block of scan_mem, in place (a large one across the devices) */
+  if (gs->direct) return _direct_block(scanner, gs, data, block, split);
+  /* the pipeline (across the devices when split), in order behind the
+   * blocks in flight */
   return _pipeline_block(scanner, gs, data, block);
 }
 

@@ -47,6 +47,14 @@ void yr_gpu_scanner_set_multi_min_block(YR_GPU_SCANNER* s, uint64_t bytes);
 /* How many blocks this scanner has split across its devices. */
 uint64_t yr_gpu_scanner_multi_blocks(const YR_GPU_SCANNER* s);
 
+/* Where a GPU scan's wall time goes (seconds, cumulative over the scanner's
+ * scans; measurement support -- tools/e2e_rate.sh): t[0] host copy of blocks
+ * into the pipeline's pinned staging, t[1] waiting for the GPU (H2D, scan,
+ * on-device pre-verification and the records' D2H of blocks not yet done when
+ * their replay is due, and the whole of the direct single-block path), t[2]
+ * the host replay of the records into yr_scan_verify_match (scan.c / re.c). */
+void yr_gpu_scanner_timing(const YR_GPU_SCANNER* s, double t[3]);
+
 /* Drop-in counterparts of yr_scanner_scan_mem_blocks / yr_scanner_scan_mem
  * (scanner.c:417, :633): same arguments, callbacks, flags and error codes. */
 int yr_gpu_scanner_scan_mem_blocks(

@@ -14,6 +14,11 @@
 //                             must return (any error code), never fault
 //   host_check re <code.bin> every offset of a program blob through
 //                             yr_amd_re_code_extent (malformed programs)
+//   host_check copypool <jobs> <seed>
+//                             hostio.h CopyPool: <jobs> back-to-back copies
+//                             of 8-40 MiB (the parallel path), some with a copy
+//                             function that fails one chunk; every job must
+//                             copy all its bytes and report exactly its failure
 #include <stdint.h>
 #include <stdio.h>
 #include <stdlib.h>
@@ -22,6 +27,7 @@
 #include <vector>
 
 #include "../../include/yara_amd.h"
+#include "../../yara_amd/csrc/hostio.h"
 
 static std::vector<uint8_t> slurp(const char* path) {
   std::vector<uint8_t> v;
@@ -168,7 +174,54 @@ static int run_re(const char* path) {
   return 0;
 }
 
+struct FailAt {
+  const uint8_t* src;
+  size_t bad;   // fail the chunk holding this source offset (SIZE_MAX: none)
+};
+static int fail_copy(void* user, void* dst, const void* src, size_t n) {
+  const FailAt* f = (const FailAt*)user;
+  const size_t off = (const uint8_t*)src - f->src;
+  memcpy(dst, src, n);   // (a failing chunk still writes: the caller must not care)
+  return f->bad >= off && f->bad < off + n ? 1 : 0;
+}
+
+static int run_copypool(int jobs, uint64_t seed) {
+  yamd::CopyPool pool(7);
+  const size_t max = 40u << 20;
+  std::vector<uint8_t> src(max), dst(max);
+  uint64_t x = seed * 0x9E3779B97F4A7C15ull + 1;
+  auto rnd = [&] { x ^= x << 13; x ^= x >> 7; x ^= x << 17; return x; };
+  for (size_t i = 0; i < max; i += 8) {
+    const uint64_t v = rnd();
+    memcpy(&src[i], &v, 8);
+  }
+  int failures = 0;
+  for (int j = 0; j < jobs; ++j) {
+    const size_t size = (8u << 20) + rnd() % (max - (8u << 20));
+    const size_t so = rnd() % 64, dofs = rnd() % 64;   // unaligned starts
+    const size_t n = size - 64;
+    memset(dst.data(), 0, max);
+    FailAt f{src.data() + so, (rnd() % 3 == 0) ? rnd() % n : SIZE_MAX};
+    yamd::CopyFn fn;
+    fn.fn = fail_copy;
+    fn.user = &f;
+    const bool ok = pool.copy(dst.data() + dofs, src.data() + so, n, fn);
+    if (ok != (f.bad == SIZE_MAX)) {
+      fprintf(stderr, "job %d: copy returned %d, injected failure at %zu\n", j, ok, f.bad);
+      return 1;
+    }
+    if (memcmp(dst.data() + dofs, src.data() + so, n) != 0) {
+      fprintf(stderr, "job %d: bytes differ\n", j);
+      return 1;
+    }
+    failures += !ok;
+  }
+  printf("%d copy jobs, %d with an injected failure: ok\n", jobs, failures);
+  return 0;
+}
+
 int main(int argc, char** argv) {
+  if (argc >= 4 && !strcmp(argv[1], "copypool")) return run_copypool(atoi(argv[2]), strtoull(argv[3], 0, 10));
   if (argc >= 3 && !strcmp(argv[1], "tables")) return run_tables(argv[2]);
   if (argc >= 5 && !strcmp(argv[1], "yarc")) return run_yarc(argv[2], atoi(argv[3]), strtoull(argv[4], 0, 10));
   if (argc >= 3 && !strcmp(argv[1], "re")) return run_re(argv[2]);

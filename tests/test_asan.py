@@ -62,3 +62,13 @@ def test_regexp_program_validation_under_sanitizers(name, tmp_path):
     code.tofile(str(tmp_path / "code.bin"))
     out = _run("re", tmp_path / "code.bin")
     assert "well-formed" in out
+
+
+def test_copy_pool_under_sanitizers():
+    """The parallel host copy (yara_amd/csrc/hostio.h CopyPool) behind
+    yr_amd_pipeline_submit_dma and the multi-device staging: back-to-back jobs
+    on the multi-threaded path (>= 8 MiB), injected copy failures reported for
+    exactly their job, every byte copied (a helper could take a
+    chunk of the next job)."""
+    out = _run("copypool", 60, 7)
+    assert "60 copy jobs" in out

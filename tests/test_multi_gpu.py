@@ -124,3 +124,94 @@ def test_multi_needs_matching_tables():
         yara_amd.Multi([_tables("C", 1)[0], _tables("lit", 1)[0]])
     with pytest.raises(yara_amd.YaraAmdError):
         yara_amd.Multi([])
+
+
+# ---- the block pipeline across devices (yr_amd_pipeline_create_multi) ----
+
+def _blocks(data, sizes):
+    out, b = [], 0
+    for s in sizes:
+        out.append((b, data[b:b + s]))
+        b += s
+    return out
+
+
+@pytest.mark.parametrize("dma", [True, False])
+@pytest.mark.parametrize("n", [1, 2, 3, 8])
+@pytest.mark.parametrize("rules,kind", [("C", "planted_C"), ("rx", "rx"), ("short", "alpha"),
+                                        ("root", "alpha"), ("lit", "lit")])
+def test_multi_pipeline_records_equal_single_device(rules, kind, n, dma):
+    """Blocks through a pipeline over n logical devices -- those of at least
+    split_min bytes split into device windows, the smaller ones whole to one
+    device (round-robin) -- come back in order with exactly the single-device
+    records of each block (candidate indices rebased onto the block)."""
+    sizes = [9 * MiB + 5, 3 * MiB, 1, 0, 6 * MiB + 17, 2 * MiB - 3, 12 * MiB]
+    if rules == "root":
+        sizes = [s // 8 for s in sizes]
+    data = _data(kind, sum(sizes))
+    single = yara_amd.Scanner(_tables(rules, 1)[0])
+    want = [single.verify_calls(blk, data_base=b) for b, blk in _blocks(data, sizes)]
+    tabs = _tables(rules, n)
+    pipe = yara_amd.Pipeline(tabs if n > 1 else tabs[0], depth=2, split_min=4 * MiB)
+    got, inflight = [], 0
+    for b, blk in _blocks(data, sizes):
+        if inflight == 2:
+            got.append(pipe.next())
+            inflight -= 1
+        pipe.submit(blk, base=b, dma=dma)
+        inflight += 1
+    while inflight:
+        got.append(pipe.next())
+        inflight -= 1
+    pipe.close()
+    assert len(got) == len(want)
+    for (b, blk), w, (recs, bytes_back, base) in zip(_blocks(data, sizes), want, got):
+        assert base == b
+        np.testing.assert_array_equal(bytes_back, blk)
+        for f in ("offset", "pool_index", "candidate"):
+            np.testing.assert_array_equal(recs[f], w[f], err_msg=f)
+    assert sum(len(w) for w in want) > 0
+
+
+@pytest.mark.parametrize("n", [1, 3])
+def test_pipeline_copy_failure_is_could_not_map(n):
+    """The caller's copy function fails one chunk (what the libyara shim's
+    YR_TRYCATCH copy reports for a truncated mapping): the submission fails
+    with YR_AMD_COULD_NOT_MAP_FILE on the parallel path, and the pipeline keeps
+    working for the next block."""
+    data = _data("lit", 24 * MiB)
+    tabs = _tables("lit", n)
+    pipe = yara_amd.Pipeline(tabs if n > 1 else tabs[0], depth=2)
+    bad = int(data.ctypes.data) + 13 * MiB + 5
+
+    def failing(d, s, k):
+        ctypes.memmove(d, s, k)
+        return 1 if s <= bad < s + k else 0
+    pipe.set_copy(failing)
+    with pytest.raises(yara_amd.YaraAmdError) as e:
+        pipe.submit(data, base=0, dma=True)
+    assert e.value.code == yara_amd.COULD_NOT_MAP_FILE
+    pipe.set_copy(lambda d, s, k: (ctypes.memmove(d, s, k), 0)[1])
+    pipe.submit(data, base=0, dma=True)
+    recs = pipe.next()[0]
+    single = yara_amd.Scanner(_tables("lit", 1)[0]).verify_calls(data)
+    np.testing.assert_array_equal(recs, single)
+    pipe.close()
+
+
+def test_multi_copy_failure_is_could_not_map():
+    data = _data("lit", 40 * MiB)
+    m = yara_amd.Multi(_tables("lit", 3))
+    bad = int(data.ctypes.data) + 33 * MiB
+
+    def failing(d, s, k):
+        ctypes.memmove(d, s, k)
+        return 1 if s <= bad < s + k else 0
+    m.set_copy(failing)
+    with pytest.raises(yara_amd.YaraAmdError) as e:
+        m.verify_calls(data)
+    assert e.value.code == yara_amd.COULD_NOT_MAP_FILE
+    m.set_copy(None)
+    np.testing.assert_array_equal(m.verify_calls(data),
+                                  yara_amd.Scanner(_tables("lit", 1)[0]).verify_calls(data))
+    m.close()

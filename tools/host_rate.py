@@ -3,10 +3,15 @@ metric, which times HBM-resident data).  Blocks of a host buffer go through
   (a) yr_amd_scan_block_verified, one block at a time, and
   (b) the block pipeline (yr_amd_pipeline_*) at several depths, with the
       host-memcpy submit and with the DMA submit (yr_amd_pipeline_submit_dma),
+  (c) with --devices: the pipeline across N logical devices
+      (yr_amd_pipeline_create_multi, DMA submit, depth 2; on a one-GPU box the
+      N devices share its link) and the single-call multi-device scan of the
+      whole buffer (yr_amd_multi_scan_block_verified: staged through pinned
+      memory),
 and the records are fetched to the host (the replay into yr_scan_verify_match
 is the caller's and is not timed here).
 
-    python tools/host_rate.py [--gib 2] [--block-mib 256] [--rules C]
+    python tools/host_rate.py [--gib 2] [--block-mib 256] [--rules C] [--devices 1,2,4,8]
 """
 import argparse
 import json
@@ -26,6 +31,8 @@ def main():
     ap.add_argument("--block-mib", type=int, default=256)
     ap.add_argument("--rules", default="C")
     ap.add_argument("--depths", default="1,2,3")
+    ap.add_argument("--devices", default="")
+    ap.add_argument("--skip-single", action="store_true")
     a = ap.parse_args()
     import numpy as np
     import oracle
@@ -51,7 +58,7 @@ def main():
         tot += len(sc.verify_calls(blk, data_base=b))
     res["single_block_GBps"] = round(n / (time.perf_counter() - t0) / 1e9, 2)
     res["records"] = tot
-    for dma in (False, True):
+    for dma in (() if a.skip_single else (False, True)):
         for depth in [int(x) for x in a.depths.split(",")]:
             pipe = yara_amd.Pipeline(tab, depth=depth)
 
@@ -74,6 +81,36 @@ def main():
             res[key] = round(n / (time.perf_counter() - t0) / 1e9, 2)
             assert tot2 == tot
             pipe.close()
+    for nd in [int(x) for x in a.devices.split(",") if x]:
+        tabs = [tab] + [yara_amd.Tables.from_npz(tables_npz(a.rules), device=0, strings=True)
+                        for _ in range(nd - 1)]
+        pipe = yara_amd.Pipeline(tabs if nd > 1 else tab, depth=2)
+
+        def run_multi():
+            inflight, tot2 = 0, 0
+            for b, blk in blocks:
+                if inflight == 2:
+                    tot2 += len(pipe.next(copy_data=False)[0])
+                    inflight -= 1
+                pipe.submit(blk, base=b, dma=True)
+                inflight += 1
+            while inflight:
+                tot2 += len(pipe.next(copy_data=False)[0])
+                inflight -= 1
+            return tot2
+        run_multi()
+        t0 = time.perf_counter()
+        tot2 = run_multi()
+        res["multi_pipeline_dma_n%d_GBps" % nd] = round(n / (time.perf_counter() - t0) / 1e9, 2)
+        assert tot2 == tot, (tot2, tot)
+        pipe.close()
+        m = yara_amd.Multi(tabs)
+        whole = len(m.verify_calls(data))
+        t0 = time.perf_counter()
+        whole = len(m.verify_calls(data))
+        res["multi_whole_n%d_GBps" % nd] = round(n / (time.perf_counter() - t0) / 1e9, 2)
+        res["multi_whole_records"] = whole
+        m.close()
     print(json.dumps(res), flush=True)
 
 

@@ -344,13 +344,40 @@ class Pipeline:
     scanned and pre-verified on the GPU while the caller consumes the oldest.
     Mirrors the block loop of yr_scanner_scan_mem_blocks (scanner.c:417-583)."""
 
-    def __init__(self, tables: Tables, depth: int = 2):
+    def __init__(self, tables, depth: int = 2, split_min: int = 0):
+        """``tables``: one Tables, or a list of them (one per logical device:
+        yr_amd_pipeline_create_multi -- each block split across the devices,
+        blocks below ``split_min`` bytes whole to one device)."""
         h = ctypes.c_void_p()
-        _lib.check("yr_amd_pipeline_create",
-                   _lib.lib().yr_amd_pipeline_create(tables.handle, depth, ctypes.byref(h)))
+        if isinstance(tables, (list, tuple)):
+            self.tables = list(tables)
+            arr = (ctypes.c_void_p * len(self.tables))(*[t.handle.value for t in self.tables])
+            _lib.check("yr_amd_pipeline_create_multi",
+                       _lib.lib().yr_amd_pipeline_create_multi(arr, len(self.tables), depth,
+                                                               ctypes.byref(h)))
+        else:
+            self.tables = tables
+            _lib.check("yr_amd_pipeline_create",
+                       _lib.lib().yr_amd_pipeline_create(tables.handle, depth, ctypes.byref(h)))
         self._h = h
         self.depth = depth
-        self.tables = tables
+        self._copy_fn = None
+        if split_min:
+            _lib.check("yr_amd_pipeline_set_split_min",
+                       _lib.lib().yr_amd_pipeline_set_split_min(self._h, split_min))
+
+    def set_copy(self, fn):
+        """fn(dst_ptr, src_ptr, n) -> 0 / nonzero: the copy into the pinned
+        staging (yr_amd_pipeline_set_copy; None: memcpy).  Test hook for the
+        fault path: a nonzero return fails the submission."""
+        if fn is None:
+            self._copy_fn = None
+            _lib.check("yr_amd_pipeline_set_copy",
+                       _lib.lib().yr_amd_pipeline_set_copy(self._h, _lib.COPY_FN(), None))
+            return
+        self._copy_fn = _lib.COPY_FN(lambda _u, d, s, n: fn(d, s, n))
+        _lib.check("yr_amd_pipeline_set_copy",
+                   _lib.lib().yr_amd_pipeline_set_copy(self._h, self._copy_fn, None))
 
     def submit(self, data: np.ndarray, base: int = 0, dma: bool = False):
         """Submit a block: host memcpy in this thread (yr_amd_pipeline_submit),
@@ -410,6 +437,12 @@ class Multi:
         _lib.check("yr_amd_multi_create",
                    _lib.lib().yr_amd_multi_create(arr, len(self.tables), ctypes.byref(h)))
         self._h = h
+
+    def set_copy(self, fn):
+        """As Pipeline.set_copy, for the staging of yr_amd_multi_scan_block_verified."""
+        self._copy_fn = None if fn is None else _lib.COPY_FN(lambda _u, d, s, n: fn(d, s, n))
+        _lib.check("yr_amd_multi_set_copy",
+                   _lib.lib().yr_amd_multi_set_copy(self._h, self._copy_fn or _lib.COPY_FN(), None))
 
     def shard(self, size: int, k: int):
         """(begin, end, window_begin, window_end) of device k."""

@@ -28,6 +28,9 @@ _vp = ctypes.c_void_p
 _int = ctypes.c_int
 
 VERIFY_FN = ctypes.CFUNCTYPE(ctypes.c_int, ctypes.c_void_p, ctypes.c_uint32, ctypes.c_uint64)
+# yr_amd_copy_fn: (user, dst, src, n) -> 0 / nonzero (source unreadable)
+COPY_FN = ctypes.CFUNCTYPE(ctypes.c_int, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p,
+                           ctypes.c_size_t)
 
 
 class TablesInfo(ctypes.Structure):
@@ -104,6 +107,11 @@ PROTOTYPES = {
                                     ctypes.POINTER(ctypes.c_uint64), ctypes.POINTER(_u8p),
                                     ctypes.POINTER(ctypes.c_size_t), ctypes.POINTER(ctypes.c_uint64)]),
     "yr_amd_pipeline_drain": (_int, [_vp]),
+    "yr_amd_pipeline_create_multi": (_int, [ctypes.POINTER(_vp), ctypes.c_uint32, ctypes.c_uint32,
+                                            ctypes.POINTER(_vp)]),
+    "yr_amd_pipeline_set_copy": (_int, [_vp, COPY_FN, _vp]),
+    "yr_amd_pipeline_set_split_min": (_int, [_vp, ctypes.c_uint64]),
+    "yr_amd_multi_set_copy": (_int, [_vp, COPY_FN, _vp]),
     "yr_amd_scan_block_verified": (_int, [_vp, _u8p, ctypes.c_size_t, ctypes.c_uint64,
                                           ctypes.POINTER(ctypes.POINTER(VerifyRec)),
                                           ctypes.POINTER(ctypes.c_uint64)]),

@@ -117,20 +117,41 @@ __device__ __forceinline__ bool exact_check(uint32_t w4, uint64_t pos, const Sca
 // position; true sends it to exact_check.  Rule sets with 1- or 2-byte keys
 // skip this level (every hit goes to exact_check).
 __device__ __forceinline__ bool first_level_test(uint32_t d, uint32_t w4) {
-  return ((d >> fl_bit3(w4)) | (d >> fl_bit4(w4))) & 1u;
+  return ((d >> fl_bit3(w4)) | (d >> fl_bit4(w4))) & 1u;   // (the masks fold into the shifts)
 }
 __device__ __forceinline__ bool first_level(uint32_t w4, const ScanParams& p) {
   if (p.len_mask & 6u) return true;
   return first_level_test(p.exact[kExactFl + fl_word(w4)], w4);
 }
 
-// The 4 bytes ending at lane byte j (0..15) of a ring entry (bytes 0..15 =
-// the lane's 16 bytes, 16..19 = the 4 bytes before the lane), from two LDS
-// dwords: lane bytes j-3 .. j.
+// Ring entry layout (24 bytes, WaveQueue): the 4 bytes before the lane at
+// kEntCtx, the lane's 16 bytes at kEntData, the lane index word at kEntIdx.
+// Context first (YAMD_RING_CTX_FIRST, the default): the 20 bytes are in stream
+// order, so the 4 bytes ending at any lane byte are one unaligned LDS dword
+// (gfx950 runs LDS in unaligned mode; the compiler emits one ds_read_b32).
+#ifndef YAMD_RING_CTX_FIRST
+#define YAMD_RING_CTX_FIRST 1
+#endif
+constexpr uint32_t kEntCtx = YAMD_RING_CTX_FIRST ? 0u : 16u;
+constexpr uint32_t kEntData = YAMD_RING_CTX_FIRST ? 4u : 0u;
+constexpr uint32_t kEntIdx = 20u;
+typedef uint32_t u32_una __attribute__((aligned(1)));
+
+// Lane byte j of a ring entry (j = -4 .. -1: the context bytes).
+__device__ __forceinline__ uint32_t entry_byte_addr(uint32_t ent, int32_t j) {
+  return YAMD_RING_CTX_FIRST ? ent + (uint32_t)(j + 4) : (j >= 0 ? ent + (uint32_t)j : ent + 20u + j);
+}
+
+// The 4 bytes ending at lane byte j (0..15) of a ring entry: lane bytes
+// j-3 .. j (the context bytes for j < 3).
 __device__ __forceinline__ uint32_t window4(uint32_t ent, uint32_t j) {
+#if YAMD_RING_CTX_FIRST
+  return *reinterpret_cast<const __attribute__((address_space(3))) u32_una*>((uintptr_t)(ent + j + 1));
+#else
   const uint32_t o = j - 3, lo = j >= 3 ? ent + (o & ~3u) : ent + 16;
   const uint32_t hi = j >= 3 ? lo + 4 : ent, sh = j >= 3 ? (o & 3u) : j + 1;
   return __builtin_amdgcn_alignbyte(lds_load<uint32_t>(hi), lds_load<uint32_t>(lo), sh);
+#endif
 }
 
 // Lane byte (0..15) of bit b of a tile hit mask: bit 8n + r <=> byte 4n + r.
@@ -174,7 +195,7 @@ struct WaveQueue {
   uint32_t pend_n;  // wave-uniform
   bool defer;       // wave-uniform: the per-lane hits below await their words
   // per lane, the first (a) and second (b) deferred hit: window, segment
-  // offset (kNoHit = none), byte offset into exact[] that the next tile step
+  // offset (kNoHit = none), byte offset into the first level (exact[kExactFl..]) that the next tile step
   // loads (0 = none), the loaded word
   uint32_t wa, oa, ia, da;
   uint32_t wb, ob, ib, db;
@@ -532,21 +553,21 @@ constexpr bool kDeferFl =
 template <int MODE>
 __device__ __forceinline__ void certain_entry(const ScanParams& p, uint32_t ent, uint32_t j,
                                               uint32_t& x, uint32_t& y) {
-  const uint32_t li = lds_load<uint32_t>(ent + 20);
+  const uint32_t li = lds_load<uint32_t>(ent + kEntIdx);
   const uint32_t e =
       min(j + p.kx_end, kNextBytes<MODE> && (li & (kWave - 1)) != kWave - 1 ? 16u : 14u);
   uint32_t b5;
   if (e <= 14u) {
     x = window4(ent, e);
-    b5 = lds_load<uint8_t>(ent + e + 1);
+    b5 = lds_load<uint8_t>(entry_byte_addr(ent, (int32_t)e + 1));
   } else {   // lane bytes 12..17
-    const uint64_t w6 = lds_load<uint32_t>(ent + 12) | (uint64_t)(li >> 16) << 32;
+    const uint64_t w6 = lds_load<uint32_t>(ent + kEntData + 12) | (uint64_t)(li >> 16) << 32;
     x = (uint32_t)(w6 >> (8 * (e - 15u)));
     b5 = (uint32_t)(w6 >> (8 * (e - 11u))) & 0xFFu;
   }
   y |= b5 << kOutByteShift | (j + 5 - e) << kOutKeyShift;
-  if (p.kx_deep != 0u) {   // (the byte before the key, bytes -4..-1 at 16..19)
-    const uint32_t b = lds_load<uint8_t>(ent + (j != 0u ? j - 1u : 19u));
+  if (p.kx_deep != 0u) {   // (the byte before the key; j = 0: the last context byte)
+    const uint32_t b = lds_load<uint8_t>(entry_byte_addr(ent, (int32_t)j - 1));
     if (excluded(b, p.kd_x0[0], p.kd_x1[0])) y |= kOutDeep;
   }
 }
@@ -560,14 +581,21 @@ __device__ __forceinline__ void drain_complete(const ScanParams& p, WaveQueue& q
   const bool hb = q.ob != kNoHit && first_level_test(q.db, q.wb);
   q.defer = false;
   q.ia = q.ib = 0u;
-  const uint32_t c = (uint32_t)ha + (uint32_t)hb;
-  const uint32_t incl = wave_inclusive_scan(c);
-  const uint32_t total = __builtin_amdgcn_readlane(incl, kWave - 1);
+  // each lane's a-hit precedes its b-hit: lane L's first slot is the number of
+  // a- and b-hits in the lanes below it (two ballots and their mbcnts instead
+  // of a DPP scan)
+  const uint64_t ma = __ballot(ha), mb = __ballot(hb);
+  const uint32_t total = (uint32_t)(__popcll(ma) + __popcll(mb));
   if (total == 0) return;
   // in order to the pending list, bucket-probed (one round trip for 64 hits)
   // each time it fills up
   const uint32_t end = q.pend_n + total;
-  const uint32_t i0 = q.pend_n + incl - c, i1 = i0 + (uint32_t)ha;
+  const uint32_t below = __builtin_amdgcn_mbcnt_hi(
+      (uint32_t)(mb >> 32),
+      __builtin_amdgcn_mbcnt_lo((uint32_t)mb,
+                                __builtin_amdgcn_mbcnt_hi((uint32_t)(ma >> 32),
+                                                          __builtin_amdgcn_mbcnt_lo((uint32_t)ma, q.pend_n))));
+  const uint32_t i0 = below, i1 = i0 + (uint32_t)ha;
   for (uint32_t base = 0;; base += kWave) {
     if (ha && i0 - base < kWave) lds_store2(q.pend + 8 * (i0 - base), q.wa, q.oa);
     if (hb && i1 - base < kWave) lds_store2(q.pend + 8 * (i1 - base), q.wb, q.ob);
@@ -603,7 +631,11 @@ __device__ __forceinline__ void drain(const ScanParams& p, WaveQueue& q, uint32_
     const u32x2 e01 = lds_load<u32x2>(ent);
     const u32x2 e23 = lds_load<u32x2>(ent + 8);
     const u32x2 e45 = lds_load<u32x2>(ent + 16);
+#if YAMD_RING_CTX_FIRST
+    const uint32_t S[6] = {e01.x, e01.y, e23.x, e23.y, e45.x, 0u};
+#else
     const uint32_t S[6] = {e45.x, e01.x, e01.y, e23.x, e23.y, 0u};
+#endif
     off0 = (e45.y & 0xFFFFu) * kBytesPerLane;
     if constexpr (kEven<MODE>) {
       m = even_mask<kEvenHash<MODE>>(S);
@@ -615,7 +647,9 @@ __device__ __forceinline__ void drain(const ScanParams& p, WaveQueue& q, uint32_
       kmask = byte_keys_mask(S, p);
       m |= kmask;
     }
-    if (off0 + kBytesPerLane > seg_len) {   // the segment's partial last tile
+    // the segment's partial last tile (its entries are appended after the main
+    // loop's last drain, so only the final drain can hold them)
+    if (!kAsync && off0 + kBytesPerLane > seg_len) {
       const uint32_t lim = off0 >= seg_len ? 0u : seg_len - off0;
       m &= lim >= 16u ? 0xFFFFu : (1u << lim) - 1u;
     }
@@ -630,13 +664,13 @@ __device__ __forceinline__ void drain(const ScanParams& p, WaveQueue& q, uint32_
         const uint32_t j = (uint32_t)__builtin_ctz(m);
         q.wa = window4(ent, j);
         q.oa = off0 + j;
-        q.ia = (kExactFl + fl_word(q.wa)) * 4u;
+        q.ia = fl_word(q.wa) * 4u;   // (issue_first_level adds kExactFl)
       }
       if (m2 != 0u) {
         const uint32_t j = (uint32_t)__builtin_ctz(m2);
         q.wb = window4(ent, j);
         q.ob = off0 + j;
-        q.ib = (kExactFl + fl_word(q.wb)) * 4u;
+        q.ib = fl_word(q.wb) * 4u;
       }
       q.defer = true;
       return;
@@ -846,6 +880,11 @@ __device__ __forceinline__ uint32_t stage1(const uint32_t (&S)[6], uint32_t lane
     default: asm("v_and_b32_sdwa %0, %1, %2 dst_sel:BYTE_3 dst_unused:UNUSED_PRESERVE src0_sel:DWORD src1_sel:DWORD" \
                  : "+v"(acc[(K) & 3]) : "v"(U), "v"(V)); break;                                  \
   }
+  // (the right windows' d | b << 8 of two pairs from one v_perm, as in the
+  // kAny form above)
+  uint32_t y2[kPairs / 2];
+#pragma unroll
+  for (int m = 0; m < kPairs / 2; ++m) y2[m] = __builtin_amdgcn_perm(S[m + 1], S[m], 0x05070305u);
 #pragma unroll
   for (int j = 0; j < kPairs; ++j) {
     const int k = 2 * j;
@@ -857,7 +896,7 @@ __device__ __forceinline__ uint32_t stage1(const uint32_t (&S)[6], uint32_t lane
       const uint32_t x = xs[j];
       const uint32_t ul = ws[j].x >> (x & 31u), vl = ws[j].y >> ((x >> 5) & 31u);
       YAMD_SDWA_AND(k, ul, vl);
-      const uint32_t y = __builtin_amdgcn_perm(0u, x, 0x0c0c0103u);   // d | b << 8
+      const uint32_t y = (j & 1) ? y2[j >> 1] >> 16 : y2[j >> 1];   // d | b << 8 (low 10 bits)
       const uint32_t ur = ws[j].x >> (y & 31u), vr = ws[j].y >> ((y >> 5) & 31u);
       YAMD_SDWA_AND(k + 1, ur, vr);
     }
@@ -908,10 +947,25 @@ __device__ __forceinline__ void ring_append(const ScanParams& p, WaveQueue& q, S
       if constexpr (MODE == 8) {   // ablation: the append's slot arithmetic, no LDS writes
         asm volatile("" ::"v"(ent), "v"((tile_off >> 4) + lane));
       } else {
+        // (byte-key kernel: the next lane's first two bytes in the top half)
+        const uint32_t idx = (tile_off >> 4) + lane | (kNextBytes<MODE> ? S[5] << 16 : 0u);
+#if YAMD_RING_CTX_FIRST
+        // three ds_write2_b32: context, the 16 bytes as loaded, index
+        typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
+        typedef u32x4 u32x4_a4 __attribute__((aligned(4)));
+        u32x4 d;
+        d.x = S[1];
+        d.y = S[2];
+        d.z = S[3];
+        d.w = S[4];
+        *reinterpret_cast<__attribute__((address_space(3))) u32x4_a4*>((uintptr_t)(ent + kEntData)) = d;
+        *reinterpret_cast<__attribute__((address_space(3))) uint32_t*>((uintptr_t)(ent + kEntCtx)) = S[0];
+        *reinterpret_cast<__attribute__((address_space(3))) uint32_t*>((uintptr_t)(ent + kEntIdx)) = idx;
+#else
         lds_store2(ent, S[1], S[2]);
         lds_store2(ent + 8, S[3], S[4]);
-        // (byte-key kernel: the next lane's first two bytes in the top half)
-        lds_store2(ent + 16, S[0], (tile_off >> 4) + lane | (kNextBytes<MODE> ? S[5] << 16 : 0u));
+        lds_store2(ent + 16, S[0], idx);
+#endif
       }
     }
     q.count += n;
@@ -956,7 +1010,7 @@ __device__ __forceinline__ void issue_first_level(const ScanParams& p, WaveQueue
       // write must wait for a possibly still outstanding load)
       asm volatile("" : "+v"(q.da), "+v"(q.db));
     }
-    const char* ex = reinterpret_cast<const char*>(p.exact);
+    const char* ex = reinterpret_cast<const char*>(p.exact + kExactFl);
     q.da = __hip_atomic_load(reinterpret_cast<const uint32_t*>(ex + q.ia), __ATOMIC_RELAXED,
                              __HIP_MEMORY_SCOPE_WAVEFRONT);
     q.db = __hip_atomic_load(reinterpret_cast<const uint32_t*>(ex + q.ib), __ATOMIC_RELAXED,

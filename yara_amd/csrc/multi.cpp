@@ -1,120 +1,239 @@
 // Multi-device block scans behind the C ABI (include/yara_amd.h
-// yr_amd_multi_*).
+// yr_amd_multi_*), and the per-device lanes they share with the
+// multi-device block pipeline (pipeline.cpp).
 //
 // One process drives n devices: a host block is split into n byte ranges
 // (equal 1 MiB-aligned slices, the last takes the rest -- the same bounds as
 // yara_amd/dist.py shard_bounds), device k receives only its WINDOW of the
 // block (its range plus the tables' verify halos, yr_amd_tables_get_info),
 // scans it with yr_amd_scan_window and pre-verifies its own candidates with
-// yr_amd_verify_device, each device on its own stream driven by its own host
-// thread.  Records are block-global, so their concatenation in device order
-// is exactly the single-device record stream of the whole block
+// yr_amd_verify_device.  Records are block-global, so their concatenation in
+// device order is exactly the single-device record stream of the whole block
 // (yr_amd_scan_block_verified): the libyara side replays it into the
 // unmodified yr_scan_verify_match (scanner.c:105-121) as before.  No data-path
 // exchange between devices; the "gather" is the host concatenation.
+//
+// Moving the block: the caller's bytes go through two pinned staging buffers
+// of kStage bytes -- a parallel copy (CopyPool, through the caller's copy
+// function: fault-reporting for mmapped data) fills one while the devices
+// whose windows overlap the other DMA their part of it -- so the host makes
+// one pass over the block at memory bandwidth and the devices take it at link
+// rate, with bounded pinned memory (a 32 GiB block needs 2 x 256 MiB).  Then
+// every device scans and pre-verifies its window on its own persistent worker
+// thread.
 #include <hip/hip_runtime.h>
 #include <string.h>
 
 #include <algorithm>
+#include <condition_variable>
+#include <mutex>
 #include <new>
 #include <thread>
 #include <vector>
 
 #include "../../include/yara_amd.h"
+#include "hostio.h"
 #include "internal.h"
 
-namespace {
+namespace yamd {
 
-constexpr uint64_t kShardAlign = 1u << 20;   // dist.py shard_bounds
-
-struct Lane {
-  yr_amd_tables* tables = nullptr;
-  int device = 0;
-  hipStream_t stream = nullptr;
-  yr_amd_scanner* scanner = nullptr;
-  uint8_t* d_win = nullptr;
-  size_t d_win_cap = 0;
-  std::vector<yr_amd_verify_rec> recs;
-  uint64_t candidates = 0;
-  int status = YR_AMD_SUCCESS;
-  bool last = false;   // the last device (takes the rest of the block)
-};
-
-}  // namespace
-
-struct yr_amd_multi {
-  std::vector<Lane> lanes;
-  uint64_t halo_before = 0, halo_after = 0;
-  std::vector<yr_amd_verify_rec> out;
-};
-
-namespace {
-
-// [begin, end) of device k in a block of `size` bytes (dist.py shard_bounds).
-void shard_of(uint64_t size, uint32_t n, uint32_t k, uint64_t& begin, uint64_t& end) {
-  const uint64_t per = (size / n) / kShardAlign * kShardAlign;
-  begin = (uint64_t)k * per;
-  end = k == n - 1 ? size : begin + per;
+int lane_open(Lane& L, yr_amd_tables* tables) {
+  L.tables = tables;
+  L.device = yr_amd_tables_device(tables);
+  if (L.device < 0 || hipSetDevice(L.device) != hipSuccess ||
+      hipStreamCreateWithFlags(&L.stream, hipStreamNonBlocking) != hipSuccess) {
+    L.stream = nullptr;
+    return YR_AMD_INTERNAL_FATAL_ERROR;
+  }
+  return yr_amd_scanner_create(tables, L.stream, &L.scanner);
 }
 
-// [lo, hi): the bytes device k holds (dist.py shard_window).
-void window_of(uint64_t size, uint64_t begin, uint64_t end, uint64_t before, uint64_t after,
-               uint64_t& lo, uint64_t& hi) {
-  before = std::max<uint64_t>(before, YR_AMD_MAX_ATOM_LENGTH);
-  lo = (begin - std::min(begin, before)) / 16 * 16;
-  hi = std::min(size, end + after);
+void lane_close(Lane& L) {
+  if (L.stream == nullptr) return;
+  (void)hipSetDevice(L.device);
+  (void)hipStreamSynchronize(L.stream);
+  yr_amd_scanner_destroy(L.scanner);
+  L.scanner = nullptr;
+  if (L.d_win) (void)hipFree(L.d_win);
+  L.d_win = nullptr;
+  L.d_win_cap = 0;
+  (void)hipStreamDestroy(L.stream);
+  L.stream = nullptr;
 }
 
-// One device's share of a block: H2D of its window, scan, pre-verification,
-// D2H of its records.
-void run_lane(Lane& L, const uint8_t* data, uint64_t size, uint64_t data_base, uint64_t begin,
-              uint64_t end, uint64_t lo, uint64_t hi) {
+int lane_reserve(Lane& L) {
+  const uint64_t n = std::max<uint64_t>(L.hi - L.lo, 16);
+  if (L.d_win != nullptr && n <= L.d_win_cap) return YR_AMD_SUCCESS;
+  if (hipSetDevice(L.device) != hipSuccess) return YR_AMD_INTERNAL_FATAL_ERROR;
+  if (L.d_win) (void)hipFree(L.d_win);
+  L.d_win = nullptr;
+  L.d_win_cap = 0;
+  if (hipMalloc((void**)&L.d_win, n) != hipSuccess) {
+    L.d_win = nullptr;
+    return YR_AMD_INSUFFICIENT_MEMORY;
+  }
+  L.d_win_cap = n;
+  return YR_AMD_SUCCESS;
+}
+
+int lane_scan(Lane& L, uint64_t size, uint64_t data_base) {
   L.recs.clear();
   L.candidates = 0;
-  L.status = YR_AMD_SUCCESS;
-  // an empty range owns no position (a block smaller than one slice per
-  // device: the last device takes all of it, position 0 included); only an
-  // empty block is scanned, by the last device, for its position 0
-  if (begin == end && !(size == 0 && L.last)) return;
-  if (hipSetDevice(L.device) != hipSuccess) {
-    L.status = YR_AMD_INTERNAL_FATAL_ERROR;
-    return;
-  }
-  const uint64_t n = hi - lo;
-  if (n > L.d_win_cap || L.d_win == nullptr) {
-    if (L.d_win) (void)hipFree(L.d_win);
-    L.d_win = nullptr;
-    L.d_win_cap = 0;
-    if (hipMalloc((void**)&L.d_win, std::max<uint64_t>(n, 16)) != hipSuccess) {
-      L.d_win = nullptr;
-      L.status = YR_AMD_INSUFFICIENT_MEMORY;
-      return;
-    }
-    L.d_win_cap = std::max<uint64_t>(n, 16);
-  }
-  if (n > 0 && hipMemcpyAsync(L.d_win, data + lo, n, hipMemcpyHostToDevice, L.stream) != hipSuccess) {
-    L.status = YR_AMD_COULD_NOT_MAP_FILE;   // as yr_amd_scan_block
-    return;
-  }
-  int r = yr_amd_scan_window(L.scanner, L.d_win, lo, hi, size, begin, end);
+  if (!L.active) return YR_AMD_SUCCESS;
+  if (hipSetDevice(L.device) != hipSuccess) return YR_AMD_INTERNAL_FATAL_ERROR;
+  int r = yr_amd_scan_window(L.scanner, L.d_win, L.lo, L.hi, size, L.begin, L.end);
   int all = 0;
   if (!r) r = yr_amd_scan_device_result(L.scanner, nullptr, &L.candidates, &all);
   // a root-accepting rule set: every position of (begin, end] is a candidate
-  // (and position 0 on the first device)
-  if (all) L.candidates = (end - begin) + (begin == 0 ? 1u : 0u);
+  // (and position 0 on the lane that starts the block)
+  if (all) L.candidates = (L.end - L.begin) + (L.begin == 0 ? 1u : 0u);
   const yr_amd_verify_rec* d_rec = nullptr;
   uint64_t cnt = 0;
   if (!r) r = yr_amd_verify_device(L.scanner, data_base, &d_rec, &cnt);
-  if (r) {
-    L.status = r;
-    return;
-  }
+  if (r) return r;
   L.recs.resize(cnt);
   if (cnt > 0 &&
       (hipMemcpyAsync(L.recs.data(), d_rec, cnt * sizeof(yr_amd_verify_rec), hipMemcpyDeviceToHost,
                       L.stream) != hipSuccess ||
        hipStreamSynchronize(L.stream) != hipSuccess))
-    L.status = YR_AMD_INTERNAL_FATAL_ERROR;
+    return YR_AMD_INTERNAL_FATAL_ERROR;
+  return YR_AMD_SUCCESS;
+}
+
+void lanes_concat(const std::vector<Lane>& lanes, std::vector<yr_amd_verify_rec>& out) {
+  size_t total = 0;
+  for (const Lane& L : lanes) total += L.recs.size();
+  out.resize(total);
+  size_t o = 0;
+  uint64_t cand_base = 0;
+  for (const Lane& L : lanes) {
+    for (size_t i = 0; i < L.recs.size(); ++i) {
+      out[o + i] = L.recs[i];
+      out[o + i].candidate = (uint32_t)(L.recs[i].candidate + cand_base);
+    }
+    o += L.recs.size();
+    cand_base += L.candidates;
+  }
+}
+
+void lanes_split(std::vector<Lane>& lanes, uint64_t size, uint64_t halo_before, uint64_t halo_after,
+                 int whole) {
+  const uint32_t n = (uint32_t)lanes.size();
+  for (uint32_t k = 0; k < n; ++k) {
+    Lane& L = lanes[k];
+    if (whole >= 0) {
+      L.begin = L.lo = 0;
+      L.end = L.hi = (int)k == whole ? size : 0;
+      L.active = (int)k == whole;
+      continue;
+    }
+    shard_of(size, n, k, L.begin, L.end);
+    if (n == 1) {
+      L.lo = 0;
+      L.hi = size;
+    } else {
+      window_of(size, L.begin, L.end, halo_before, halo_after, L.lo, L.hi);
+    }
+    // an empty range owns no position (a block smaller than one slice per
+    // device: the last device takes all of it, position 0 included); only an
+    // empty block is scanned, by the last device, for its position 0
+    L.active = L.begin != L.end || (size == 0 && k == n - 1);
+  }
+}
+
+}  // namespace yamd
+
+using yamd::CopyFn;
+using yamd::CopyPool;
+using yamd::Lane;
+
+struct yr_amd_multi {
+  std::vector<Lane> lanes;
+  uint64_t halo_before = 0, halo_after = 0;
+  std::vector<yr_amd_verify_rec> out;
+  CopyFn copy;
+  CopyPool* pool = nullptr;
+  // staging: two pinned buffers, and per buffer one event per lane (its DMA
+  // out of that buffer)
+  static constexpr size_t kStage = 256u << 20;
+  uint8_t* stage[2] = {nullptr, nullptr};
+  std::vector<hipEvent_t> staged[2];
+  // persistent lane workers (scan + pre-verification)
+  std::vector<std::thread> workers;
+  std::mutex mu;
+  std::condition_variable cv;
+  uint64_t gen = 0, size = 0, base = 0;
+  uint32_t left = 0;
+  bool stop = false;
+};
+
+namespace {
+
+void lane_worker(yr_amd_multi* m, uint32_t k) {
+  Lane& L = m->lanes[k];
+  uint64_t seen = 0;
+  std::unique_lock<std::mutex> lk(m->mu);
+  for (;;) {
+    m->cv.wait(lk, [&] { return m->stop || m->gen != seen; });
+    if (m->stop) return;
+    seen = m->gen;
+    const uint64_t size = m->size, base = m->base;
+    lk.unlock();
+    if (L.status == YR_AMD_SUCCESS) L.status = yamd::lane_scan(L, size, base);
+    lk.lock();
+    if (--m->left == 0) m->cv.notify_all();
+  }
+}
+
+// The block's bytes into every active lane's window: staged through the two
+// pinned buffers, each kStage piece copied once (in parallel, through the
+// caller's copy function) and DMA'd to every lane whose window overlaps it.
+int stage_block(yr_amd_multi* m, const uint8_t* data, uint64_t size) {
+  uint64_t lo = UINT64_MAX, hi = 0;   // the union of the windows
+  for (const Lane& L : m->lanes)
+    if (L.active && L.hi > L.lo) {
+      lo = std::min(lo, L.lo);
+      hi = std::max(hi, L.hi);
+    }
+  if (lo >= hi) return YR_AMD_SUCCESS;
+  for (int b = 0; b < 2; ++b) {
+    if (m->stage[b] == nullptr) {
+      (void)hipSetDevice(m->lanes[0].device);
+      if (hipHostMalloc((void**)&m->stage[b], yr_amd_multi::kStage, hipHostMallocPortable) !=
+          hipSuccess) {
+        m->stage[b] = nullptr;
+        return YR_AMD_INSUFFICIENT_MEMORY;
+      }
+    }
+  }
+  int rc = YR_AMD_SUCCESS;
+  uint32_t piece = 0;
+  for (uint64_t p0 = lo; p0 < hi && rc == YR_AMD_SUCCESS; p0 += yr_amd_multi::kStage, ++piece) {
+    const uint32_t b = piece & 1u;
+    const uint64_t p1 = std::min(hi, p0 + yr_amd_multi::kStage);
+    // the DMAs that last read this buffer must be done before it is refilled
+    for (size_t k = 0; k < m->lanes.size(); ++k)
+      if (piece >= 2 && hipEventSynchronize(m->staged[b][k]) != hipSuccess)
+        return YR_AMD_INTERNAL_FATAL_ERROR;
+    if (!m->pool->copy(m->stage[b], data + p0, p1 - p0, m->copy)) {
+      rc = YR_AMD_COULD_NOT_MAP_FILE;
+      break;
+    }
+    for (size_t k = 0; k < m->lanes.size(); ++k) {
+      Lane& L = m->lanes[k];
+      const uint64_t a = std::max(p0, L.lo), e = std::min(p1, L.hi);
+      if (hipSetDevice(L.device) != hipSuccess) return YR_AMD_INTERNAL_FATAL_ERROR;
+      if (L.active && a < e &&
+          hipMemcpyAsync(L.d_win + (a - L.lo), m->stage[b] + (a - p0), e - a, hipMemcpyHostToDevice,
+                         L.stream) != hipSuccess)
+        return YR_AMD_INTERNAL_FATAL_ERROR;
+      if (hipEventRecord(m->staged[b][k], L.stream) != hipSuccess) return YR_AMD_INTERNAL_FATAL_ERROR;
+    }
+  }
+  // (the scans are queued behind the DMAs on the same streams)
+  for (int b = 0; b < 2 && rc != YR_AMD_SUCCESS; ++b)
+    for (size_t k = 0; k < m->lanes.size(); ++k) (void)hipEventSynchronize(m->staged[b][k]);
+  return rc;
 }
 
 }  // namespace
@@ -145,18 +264,19 @@ int yr_amd_multi_create(yr_amd_tables* const* tables, uint32_t n, yr_amd_multi**
   m->lanes.resize(n);
   int r = YR_AMD_SUCCESS;
   for (uint32_t k = 0; k < n && r == YR_AMD_SUCCESS; ++k) {
-    Lane& L = m->lanes[k];
-    L.tables = tables[k];
-    L.device = yr_amd_tables_device(tables[k]);
-    L.last = k == n - 1;
-    if (L.device < 0 || hipSetDevice(L.device) != hipSuccess ||
-        hipStreamCreateWithFlags(&L.stream, hipStreamNonBlocking) != hipSuccess) {
-      L.stream = nullptr;
-      r = YR_AMD_INTERNAL_FATAL_ERROR;
-      break;
+    r = yamd::lane_open(m->lanes[k], tables[k]);
+    for (int b = 0; b < 2 && r == YR_AMD_SUCCESS; ++b) {
+      hipEvent_t e = nullptr;
+      if (hipEventCreateWithFlags(&e, hipEventDisableTiming) != hipSuccess) r = YR_AMD_INTERNAL_FATAL_ERROR;
+      else m->staged[b].push_back(e);
     }
-    r = yr_amd_scanner_create(L.tables, L.stream, &L.scanner);
   }
+  if (r == YR_AMD_SUCCESS) {
+    m->pool = new (std::nothrow) CopyPool(yamd::copy_helpers());
+    if (m->pool == nullptr) r = YR_AMD_INSUFFICIENT_MEMORY;
+  }
+  if (r == YR_AMD_SUCCESS)
+    for (uint32_t k = 0; k < n; ++k) m->workers.emplace_back(lane_worker, m, k);
   if (r != YR_AMD_SUCCESS) {
     yr_amd_multi_destroy(m);
     return r;
@@ -167,15 +287,26 @@ int yr_amd_multi_create(yr_amd_tables* const* tables, uint32_t n, yr_amd_multi**
 
 int yr_amd_multi_destroy(yr_amd_multi* m) {
   if (m == nullptr) return YR_AMD_SUCCESS;
-  for (Lane& L : m->lanes) {
-    if (L.stream == nullptr) continue;
-    (void)hipSetDevice(L.device);
-    (void)hipStreamSynchronize(L.stream);
-    yr_amd_scanner_destroy(L.scanner);
-    if (L.d_win) (void)hipFree(L.d_win);
-    (void)hipStreamDestroy(L.stream);
+  {
+    std::lock_guard<std::mutex> lk(m->mu);
+    m->stop = true;
   }
+  m->cv.notify_all();
+  for (std::thread& t : m->workers) t.join();
+  for (Lane& L : m->lanes) yamd::lane_close(L);
+  for (int b = 0; b < 2; ++b) {
+    for (hipEvent_t e : m->staged[b]) (void)hipEventDestroy(e);
+    if (m->stage[b]) (void)hipHostFree(m->stage[b]);
+  }
+  delete m->pool;
   delete m;
+  return YR_AMD_SUCCESS;
+}
+
+int yr_amd_multi_set_copy(yr_amd_multi* m, yr_amd_copy_fn fn, void* user) {
+  if (m == nullptr) return YR_AMD_INVALID_ARGUMENT;
+  m->copy.fn = fn;
+  m->copy.user = user;
   return YR_AMD_SUCCESS;
 }
 
@@ -183,8 +314,8 @@ int yr_amd_multi_shard(const yr_amd_multi* m, uint64_t size, uint32_t k, uint64_
                        uint64_t* end, uint64_t* window_begin, uint64_t* window_end) {
   if (m == nullptr || k >= m->lanes.size()) return YR_AMD_INVALID_ARGUMENT;
   uint64_t b, e, lo, hi;
-  shard_of(size, (uint32_t)m->lanes.size(), k, b, e);
-  window_of(size, b, e, m->halo_before, m->halo_after, lo, hi);
+  yamd::shard_of(size, (uint32_t)m->lanes.size(), k, b, e);
+  yamd::window_of(size, b, e, m->halo_before, m->halo_after, lo, hi);
   if (begin) *begin = b;
   if (end) *end = e;
   if (window_begin) *window_begin = lo;
@@ -197,46 +328,39 @@ int yr_amd_multi_scan_block_verified(yr_amd_multi* m, const uint8_t* data, size_
                                      uint64_t* count) {
   if (m == nullptr || (data == nullptr && size > 0)) return YR_AMD_INVALID_ARGUMENT;
   const uint32_t n = (uint32_t)m->lanes.size();
-  std::vector<uint64_t> b(n), e(n), lo(n), hi(n);
+  // every device's window, as yr_amd_multi_shard reports it (n = 1 too)
   for (uint32_t k = 0; k < n; ++k) {
-    shard_of(size, n, k, b[k], e[k]);
-    window_of(size, b[k], e[k], m->halo_before, m->halo_after, lo[k], hi[k]);
+    Lane& L = m->lanes[k];
+    yamd::shard_of(size, n, k, L.begin, L.end);
+    yamd::window_of(size, L.begin, L.end, m->halo_before, m->halo_after, L.lo, L.hi);
+    L.active = L.begin != L.end || (size == 0 && k == n - 1);
     // a device's candidates: positions (b, e], plus 0 on the first
-    if ((e[k] - b[k]) + (b[k] == 0 ? 1u : 0u) > YR_AMD_VERIFY_MAX_CANDIDATES)
+    if ((L.end - L.begin) + (L.begin == 0 ? 1u : 0u) > YR_AMD_VERIFY_MAX_CANDIDATES)
       return YR_AMD_INVALID_ARGUMENT;
   }
-  if (n == 1) {
-    run_lane(m->lanes[0], data, size, data_base, b[0], e[0], lo[0], hi[0]);
-  } else {
-    // one host thread per device: the H2D copies of the windows (pageable
-    // memory, staged by the runtime) and the scans proceed in parallel
-    std::vector<std::thread> th;
-    th.reserve(n);
-    for (uint32_t k = 0; k < n; ++k)
-      th.emplace_back(run_lane, std::ref(m->lanes[k]), data, (uint64_t)size, data_base, b[k], e[k],
-                      lo[k], hi[k]);
-    for (std::thread& t : th) t.join();
-  }
-  size_t total = 0;
-  for (const Lane& L : m->lanes) {
-    if (L.status != YR_AMD_SUCCESS) return L.status;
-    total += L.recs.size();
-  }
-  // in device order = the whole block's order; each device's candidate index
-  // rebased onto the whole block's stream (mod 2^32, as a single scan's)
-  m->out.resize(total);
-  size_t o = 0;
-  uint64_t cand_base = 0;
-  for (const Lane& L : m->lanes) {
-    for (size_t i = 0; i < L.recs.size(); ++i) {
-      m->out[o + i] = L.recs[i];
-      m->out[o + i].candidate = (uint32_t)(L.recs[i].candidate + cand_base);
+  for (Lane& L : m->lanes) {
+    L.status = YR_AMD_SUCCESS;
+    if (L.active) {
+      const int r = yamd::lane_reserve(L);
+      if (r) return r;
     }
-    o += L.recs.size();
-    cand_base += L.candidates;
   }
+  int rc = stage_block(m, data, size);
+  if (rc) return rc;
+  {
+    std::unique_lock<std::mutex> lk(m->mu);
+    m->size = size;
+    m->base = data_base;
+    m->left = n;
+    ++m->gen;
+    m->cv.notify_all();
+    m->cv.wait(lk, [&] { return m->left == 0; });
+  }
+  for (const Lane& L : m->lanes)
+    if (L.status != YR_AMD_SUCCESS) return L.status;
+  yamd::lanes_concat(m->lanes, m->out);
   if (records) *records = m->out.data();
-  if (count) *count = total;
+  if (count) *count = m->out.size();
   return YR_AMD_SUCCESS;
 }
 

@@ -1145,9 +1145,12 @@ int yr_amd_verify_device(yr_amd_scanner* s, uint64_t data_base, const yr_amd_ver
   } else {
     v.positions = s->d_positions;
     v.count = s->last_count;
-    // (profiling needs every call past the early returns: no skipping)
-    v.dead = t->profile ? nullptr : L.dead;
-    v.live = t->profile ? nullptr : L.live;
+    // (profiling needs every call past the early returns: no skipping; the
+    // live list counts in 32 bits, so a stream of 2^32 candidates -- all of
+    // them possibly undecided -- is decided without the classes too)
+    const bool classes = !t->profile && s->last_count <= 0xFFFFFFFFull;
+    v.dead = classes ? L.dead : nullptr;
+    v.live = classes ? L.live : nullptr;
     for (int k = 0; k < 4; ++k) {
       v.kd_n[k] = L.kd_n[k];
       v.kd_head[k] = L.kd_head[k];
@@ -1277,10 +1280,19 @@ int yr_amd_trace_walk(yr_amd_scanner* s, const uint8_t* d_data, size_t size, uin
   const uint32_t n_blocks = (uint32_t)n_blocks64;
   HIP_TRY(hipSetDevice(s->tables->device));
   if (s->d_trace_T == nullptr) {
-    HIP_TRY(hipMalloc(&s->d_trace_T, f.T.size() * sizeof(uint32_t)));
-    HIP_TRY(hipMalloc(&s->d_trace_M, f.M.size() * sizeof(uint32_t)));
-    HIP_TRY(hipMemcpy(s->d_trace_T, f.T.data(), f.T.size() * sizeof(uint32_t), hipMemcpyHostToDevice));
-    HIP_TRY(hipMemcpy(s->d_trace_M, f.M.data(), f.M.size() * sizeof(uint32_t), hipMemcpyHostToDevice));
+    // both tables into locals first: the cache is set only once complete, so
+    // a failed allocation or upload leaves it empty for the next call
+    uint32_t *dT = nullptr, *dM = nullptr;
+    const size_t nT = f.T.size() * sizeof(uint32_t), nM = f.M.size() * sizeof(uint32_t);
+    if (hipMalloc(&dT, nT) != hipSuccess || hipMalloc(&dM, nM) != hipSuccess ||
+        hipMemcpy(dT, f.T.data(), nT, hipMemcpyHostToDevice) != hipSuccess ||
+        hipMemcpy(dM, f.M.data(), nM, hipMemcpyHostToDevice) != hipSuccess) {
+      if (dT) (void)hipFree(dT);
+      if (dM) (void)hipFree(dM);
+      return YR_AMD_INTERNAL_FATAL_ERROR;
+    }
+    s->d_trace_T = dT;
+    s->d_trace_M = dM;
   }
   // per-block counts -> offsets on the host (a debugging path: blocks are small)
   uint32_t* d_cnt = nullptr;
