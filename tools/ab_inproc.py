@@ -1,0 +1,122 @@
+"""A/B of scan-kernel builds INSIDE ONE PROCESS (measurement tool).
+
+Every variant library (yara_amd/_variants/<name>.so; "base" = the product
+build yara_amd/libyara_amd.so) is loaded side by side with its own ctypes
+handle, tables and scanner on the same device-resident input; the variants
+then take turns, `--reps` timed scans each per round, in an order that
+alternates every round, for `--rounds` rounds.  Same process, same clock
+state, interleaved at sub-second granularity: the box-to-box and
+process-to-process drift of separate runs (2-4 %) cancels, so 1 % effects
+resolve.  Reports per variant the median / min kernel time (HIP events around
+the scan kernel) and the median per-round ratio to the first variant.
+
+    python tools/ab_inproc.py --rules C base,r3 [--rounds 20] [--reps 5]
+"""
+import argparse
+import ctypes
+import json
+import os
+import statistics
+import sys
+
+import numpy as np
+
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+_vp = ctypes.c_void_p
+
+
+def load(name):
+    path = (os.path.join(REPO, "yara_amd", "libyara_amd.so") if name == "base"
+            else os.path.join(REPO, "yara_amd", "_variants", name + ".so"))
+    L = ctypes.CDLL(path, mode=getattr(os, "RTLD_LOCAL", 0) | os.RTLD_NOW)
+    for fn, args in (("yr_amd_tables_create", [_vp, _vp, ctypes.c_uint32, _vp, _vp, ctypes.c_uint32,
+                                                ctypes.c_int, ctypes.POINTER(_vp)]),
+                     ("yr_amd_scanner_create", [_vp, _vp, ctypes.POINTER(_vp)]),
+                     ("yr_amd_scan_device", [_vp, _vp, ctypes.c_uint64, ctypes.c_uint64, ctypes.c_uint64]),
+                     ("yr_amd_scan_device_result", [_vp, ctypes.POINTER(_vp), ctypes.POINTER(ctypes.c_uint64),
+                                                    ctypes.POINTER(ctypes.c_int)]),
+                     ("yr_amd_scanner_set_timing", [_vp, ctypes.c_int]),
+                     ("yr_amd_scanner_kernel_ms", [_vp, ctypes.POINTER(ctypes.c_float)]),
+                     ("yr_amd_scanner_scan_ms", [_vp, ctypes.POINTER(ctypes.c_float)]),
+                     ("yr_amd_fill_xorshift64", [_vp, ctypes.c_uint64, ctypes.c_uint64, ctypes.c_uint64, _vp])):
+        getattr(L, fn).argtypes = args
+        getattr(L, fn).restype = ctypes.c_int
+    return L
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("variants")
+    ap.add_argument("--rules", default="C")
+    ap.add_argument("--gib", type=float, default=4.0)
+    ap.add_argument("--rounds", type=int, default=20)
+    ap.add_argument("--reps", type=int, default=5)
+    ap.add_argument("--warm-s", type=float, default=1.0)
+    a = ap.parse_args()
+    import time
+    import torch
+    names = a.variants.split(",")
+    n = int(a.gib * (1 << 30))
+    buf = torch.empty(n + 16, dtype=torch.uint8, device="cuda")
+    libs = [load(v) for v in names]
+    assert libs[0].yr_amd_fill_xorshift64(_vp(buf.data_ptr()), n, 1, 0, None) == 0
+    torch.cuda.synchronize()
+    z = np.load(os.path.join(REPO, "tests", "golden", "tables", a.rules + ".npz"))
+    T = np.ascontiguousarray(z["T"], np.uint32)
+    M = np.ascontiguousarray(z["M"], np.uint32)
+    nx = np.ascontiguousarray(z["pool_next"], np.uint32)
+    bt = np.ascontiguousarray(z["pool_backtrack"], np.uint16)
+    scanners = []
+    for L in libs:
+        t, s = _vp(), _vp()
+        assert L.yr_amd_tables_create(T.ctypes.data, M.ctypes.data, T.size, nx.ctypes.data,
+                                      bt.ctypes.data, nx.size, 0, ctypes.byref(t)) == 0
+        assert L.yr_amd_scanner_create(t, None, ctypes.byref(s)) == 0
+        L.yr_amd_scanner_set_timing(s, 1)
+        scanners.append((L, t, s))
+
+    def scan(i):
+        L, _, s = scanners[i]
+        cnt = ctypes.c_uint64()
+        assert L.yr_amd_scan_device(s, _vp(buf.data_ptr()), n, 0, n) == 0
+        assert L.yr_amd_scan_device_result(s, None, ctypes.byref(cnt), None) == 0
+        km, sm = ctypes.c_float(), ctypes.c_float()
+        L.yr_amd_scanner_kernel_ms(s, ctypes.byref(km))
+        L.yr_amd_scanner_scan_ms(s, ctypes.byref(sm))
+        return km.value, sm.value, cnt.value
+
+    t0 = time.perf_counter()
+    k = 0
+    while time.perf_counter() - t0 < a.warm_s:   # clock ramp (bench.py)
+        scan(k % len(names))
+        k += 1
+    kern = {v: [] for v in names}
+    scanms = {v: [] for v in names}
+    counts = {}
+    ratios = {v: [] for v in names}
+    for r in range(a.rounds):
+        order = list(range(len(names))) if r % 2 == 0 else list(reversed(range(len(names))))
+        med = {}
+        for i in order:
+            ks = []
+            for _ in range(a.reps):
+                km, sm, c = scan(i)
+                ks.append(km)
+                scanms[names[i]].append(sm)
+                counts[names[i]] = c
+            kern[names[i]] += ks
+            med[names[i]] = statistics.median(ks)
+        for v in names:
+            ratios[v].append(med[v] / med[names[0]])
+    out = {"rules": a.rules, "bytes": n, "rounds": a.rounds, "reps": a.reps, "variants": {}}
+    for v in names:
+        out["variants"][v] = {"kernel_median_ms": round(statistics.median(kern[v]), 4),
+                              "kernel_min_ms": round(min(kern[v]), 4),
+                              "scan_median_ms": round(statistics.median(scanms[v]), 4),
+                              "ratio_to_first_median": round(statistics.median(ratios[v]), 4),
+                              "candidates": counts[v]}
+    print(json.dumps(out, indent=1))
+
+
+if __name__ == "__main__":
+    main()

@@ -228,22 +228,31 @@ constexpr int kModeByteKeysEven = 26;
 constexpr int kModeByteKeysEvenHash = 27;
 constexpr int kModeByteKeysNextEven = 28;
 constexpr int kModeByteKeysNextEvenHash = 29;
+// Profiling ablations of a product variant V (diagnostic builds): MODE =
+// 100 * A + V, A = 1 stage 1 only (the filter and the byte/pair key tests, no
+// ring), 2 ring appends whose drains drop the entries, 3 the 1-byte keys
+// detected but not appended (the ring holds the filter hits only), 4 the
+// 1-byte keys not detected.  Output wrong by construction.
 template <int MODE>
-constexpr bool kByteKeys = MODE == kModeByteKeys || MODE == kModeByteKeysNext ||
-                           (MODE >= kModeByteKeysEven && MODE <= kModeByteKeysNextEvenHash);
+constexpr int kBase = MODE >= 100 ? MODE % 100 : MODE;
+template <int MODE>
+constexpr int kAbl = MODE >= 100 ? MODE / 100 : 0;
+template <int MODE>
+constexpr bool kByteKeys = kBase<MODE> == kModeByteKeys || kBase<MODE> == kModeByteKeysNext ||
+                           (kBase<MODE> >= kModeByteKeysEven && kBase<MODE> <= kModeByteKeysNextEvenHash);
 // ring entries carry the next lane's first two bytes (ScanParams::kx_next)
 template <int MODE>
-constexpr bool kNextBytes =
-    MODE == kModeByteKeysNext || MODE == kModeByteKeysNextEven || MODE == kModeByteKeysNextEvenHash;
+constexpr bool kNextBytes = kBase<MODE> == kModeByteKeysNext || kBase<MODE> == kModeByteKeysNextEven ||
+                            kBase<MODE> == kModeByteKeysNextEvenHash;
 template <int MODE>
-constexpr bool kEven = MODE == kModeEven || MODE == kModeEvenHash ||
-                       (MODE >= kModeByteKeysEven && MODE <= kModeByteKeysNextEvenHash);
+constexpr bool kEven = kBase<MODE> == kModeEven || kBase<MODE> == kModeEvenHash ||
+                       (kBase<MODE> >= kModeByteKeysEven && kBase<MODE> <= kModeByteKeysNextEvenHash);
 template <int MODE>
-constexpr bool kEvenHash =
-    MODE == kModeEvenHash || MODE == kModeByteKeysEvenHash || MODE == kModeByteKeysNextEvenHash;
+constexpr bool kEvenHash = kBase<MODE> == kModeEvenHash || kBase<MODE> == kModeByteKeysEvenHash ||
+                           kBase<MODE> == kModeByteKeysNextEvenHash;
 // the stage-1 filter test a kernel variant runs (stage1's MODE argument)
 template <int MODE>
-constexpr int kStage1Mode = !(kByteKeys<MODE> || MODE == 24 || MODE == 25) ? MODE
+constexpr int kStage1Mode = !(kByteKeys<MODE> || MODE == 24 || MODE == 25) ? kBase<MODE>
                             : kEvenHash<MODE>                              ? kModeEvenHash
                             : kEven<MODE>                                  ? kModeEven
                                                                            : 0;
@@ -540,7 +549,7 @@ template <int MODE>
 constexpr bool kHoldFl = YAMD_HOLD_FL && !kEven<MODE>;
 template <int MODE>
 constexpr bool kDeferFl =
-    YAMD_DEFER_FL &&
+    YAMD_DEFER_FL && kAbl<MODE> != 1 &&
     (MODE == 0 || MODE == 12 || kByteKeys<MODE> || kEven<MODE> || kByteKeyAblation<MODE>);
 
 // The output entry of a certain candidate (its last byte a 1-byte key) at lane
@@ -620,7 +629,7 @@ __device__ __forceinline__ void drain(const ScanParams& p, WaveQueue& q, uint32_
     if (q.defer) drain_complete<MODE>(p, q, lane, seg_start, out, found);
   const uint32_t n = q.count;   // <= kQueueCap = kWave
   q.count = 0;
-  if constexpr (MODE == 7 || MODE == 8) return;   // ablations: appends only, entries dropped
+  if constexpr (MODE == 7 || MODE == 8 || kAbl<MODE> == 2) return;   // ablations: entries dropped
   __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
   uint32_t maybe = 0, off0 = 0, m = 0;   // m: bit j = lane byte j passes the filter
   uint32_t kmask = 0;                    // bit j = lane byte j is a 1-byte key (certain)
@@ -1031,7 +1040,10 @@ __device__ __forceinline__ void tile_step(const ScanParams& p, WaveQueue& q, Seg
   uint32_t any = stage1<kStage1Mode<MODE>, true>(S, lane);
   if constexpr (kEven<MODE>)
     if (p.n_pair_keys != 0) any |= pair_keys_any(S, p);
-  if constexpr (kByteKeys<MODE>) any |= byte_keys_any(S, p);
+  if constexpr (kByteKeys<MODE>) {
+    if constexpr (kAbl<MODE> == 3) asm volatile("" ::"v"(byte_keys_any(S, p)));   // ablation
+    else if constexpr (kAbl<MODE> != 4) any |= byte_keys_any(S, p);
+  }
   if constexpr (MODE == 24) asm volatile("" ::"v"(byte_keys_any(S, p)));
   if constexpr (kDeferFl<MODE>)
     if (q.defer) {
@@ -1043,7 +1055,11 @@ __device__ __forceinline__ void tile_step(const ScanParams& p, WaveQueue& q, Seg
       __builtin_amdgcn_s_setprio(1);
 #endif
     }
-  ring_append<MODE, TAIL>(p, q, st, S, any, tile_off, lane);
+  if constexpr (kAbl<MODE> == 1) {   // ablation: stage 1 only
+    asm volatile("" ::"v"(any));
+  } else {
+    ring_append<MODE, TAIL>(p, q, st, S, any, tile_off, lane);
+  }
   issue_first_level<MODE>(p, q);
 }
 
@@ -1353,6 +1369,21 @@ hipError_t launch_scan(const ScanParams& p, int grid, hipStream_t s, int mode) {
     case 12: hipLaunchKernelGGL(scan_segments_kernel<12>, dim3(grid), dim3(kWGThreads), lds, s, p); break;
     case 24: hipLaunchKernelGGL(scan_segments_kernel<24>, dim3(grid), dim3(kWGThreads), lds, s, p); break;
     case 25: hipLaunchKernelGGL(scan_segments_kernel<25>, dim3(grid), dim3(kWGThreads), lds, s, p); break;
+    case 101: case 102: case 103: case 104: {
+      // the ablations of the byte-key variant the product would run (even
+      // filters plain only; others: the pair filter)
+      if (p.n_byte_keys == 0) return hipErrorInvalidValue;
+      const int base = p.filter_mode == kFilterEven ? (p.kx_next ? kModeByteKeysNextEven : kModeByteKeysEven)
+                                                    : (p.kx_next ? kModeByteKeysNext : kModeByteKeys);
+#define YAMD_ABL(A, V)                                                                             \
+  if (mode == 100 + A && base == V)                                                                \
+    hipLaunchKernelGGL(scan_segments_kernel<100 * A + V>, dim3(grid), dim3(kWGThreads), lds, s, p);
+#define YAMD_ABL4(A) YAMD_ABL(A, kModeByteKeys) YAMD_ABL(A, kModeByteKeysNext) YAMD_ABL(A, kModeByteKeysEven) YAMD_ABL(A, kModeByteKeysNextEven)
+      YAMD_ABL4(1) YAMD_ABL4(2) YAMD_ABL4(3) YAMD_ABL4(4)
+#undef YAMD_ABL4
+#undef YAMD_ABL
+      break;
+    }
 #endif
     default:
       if (p.n_byte_keys != 0) {
@@ -1419,6 +1450,12 @@ hipError_t configure_scan_kernel() {
                         (const void*)scan_segments_kernel<10>, (const void*)scan_segments_kernel<11>,
                         (const void*)scan_segments_kernel<12>,
                         (const void*)scan_segments_kernel<24>, (const void*)scan_segments_kernel<25>,
+#define YAMD_ABL_K(A) (const void*)scan_segments_kernel<100 * A + kModeByteKeys>,                  \
+                      (const void*)scan_segments_kernel<100 * A + kModeByteKeysNext>,              \
+                      (const void*)scan_segments_kernel<100 * A + kModeByteKeysEven>,              \
+                      (const void*)scan_segments_kernel<100 * A + kModeByteKeysNextEven>,
+                        YAMD_ABL_K(1) YAMD_ABL_K(2) YAMD_ABL_K(3) YAMD_ABL_K(4)
+#undef YAMD_ABL_K
 #endif
                        }) {
     hipError_t r = hipFuncSetAttribute(k, hipFuncAttributeMaxDynamicSharedMemorySize, lds);

@@ -472,7 +472,7 @@ int yr_amd__diag_key_classes(const yr_amd_tables* t, uint32_t* out) {
 }
 
 int yr_amd__diag_kernel_mode(yr_amd_scanner* s, int mode) {
-  if (s == nullptr || mode < 0 || (mode > 12 && mode != 24 && mode != 25))
+  if (s == nullptr || mode < 0 || (mode > 12 && mode != 24 && mode != 25 && (mode < 101 || mode > 104)))
     return YR_AMD_INVALID_ARGUMENT;
   s->diag_mode = mode;
   return YR_AMD_SUCCESS;
@@ -1245,12 +1245,13 @@ int yr_amd_scan_block_verified(yr_amd_scanner* s, const uint8_t* data, size_t si
   if (s == nullptr || (data == nullptr && size > 0)) return YR_AMD_INVALID_ARGUMENT;
   if (!s->tables->has_strings) return YR_AMD_INVALID_ARGUMENT;
   HIP_TRY(hipSetDevice(s->tables->device));
-  if (size > 0) {
-    int r = grow(s->d_block, s->d_block_cap, size);
-    if (r) return r;
-    if (hipMemcpyAsync(s->d_block, data, size, hipMemcpyHostToDevice, s->stream) != hipSuccess)
-      return YR_AMD_COULD_NOT_MAP_FILE;
-  }
+  // (a device buffer even for an empty block: a root-accepting rule set
+  // pre-verifies its position 0, which needs a data pointer)
+  int rg = grow(s->d_block, s->d_block_cap, std::max<size_t>(size, 16));
+  if (rg) return rg;
+  if (size > 0 &&
+      hipMemcpyAsync(s->d_block, data, size, hipMemcpyHostToDevice, s->stream) != hipSuccess)
+    return YR_AMD_COULD_NOT_MAP_FILE;
   int r = yr_amd_scan_device(s, s->d_block, size, 0, size);
   if (!r) r = yr_amd_scan_device_result(s, nullptr, nullptr, nullptr);
   const yr_amd_verify_rec* d_rec = nullptr;
