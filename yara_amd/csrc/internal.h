@@ -143,8 +143,18 @@ __host__ __device__ inline uint32_t fl_mulhi24(uint32_t a, uint32_t b) {
 __host__ __device__ inline uint32_t fl_word(uint32_t w4) {
   return fl_mul24(w4 >> 8, 0x9E3779u) >> (32 - YAMD_FL_LOG2);
 }
+#ifndef YAMD_FL_MULHI
+#define YAMD_FL_MULHI 1
+#endif
+#if YAMD_FL_MULHI
 __host__ __device__ inline uint32_t fl_bit3(uint32_t w4) { return fl_mulhi24(w4 >> 8, 0xEBCA77u) & 31u; }
 __host__ __device__ inline uint32_t fl_bit4(uint32_t w4) { return fl_mulhi24(w4, 0xB2AE35u) & 31u; }
+#else   // (round 3: 3-byte keys in bits 0..15, 4-byte keys in 16..31)
+__host__ __device__ inline uint32_t fl_bit3(uint32_t w4) { return fl_mul24(w4 >> 8, 0xEBCA77u) >> 28; }
+__host__ __device__ inline uint32_t fl_bit4(uint32_t w4) {
+  return 16u + (fl_mul24((w4 >> 8) ^ (w4 << 16), 0xB2AE35u) >> 28);
+}
+#endif
 
 __host__ __device__ inline uint32_t bucket_hash1(uint32_t key) {
   uint32_t h = key * 0x9E3779B1u;

@@ -545,6 +545,24 @@ __device__ __forceinline__ uint32_t byte_keys_mask(const uint32_t (&S)[6], const
 #ifndef YAMD_CARRY_DPP2
 #define YAMD_CARRY_DPP2 1
 #endif
+// Byte-key kernels: a drain whose hits are all certain candidates, with
+// nothing pending, writes them straight to the segment's output (drain()).
+// Off: short 3.6 % faster without it, rx equal (profiles/r04_ab_inproc_h2.json).
+#ifndef YAMD_BK_DIRECT
+#define YAMD_BK_DIRECT 0
+#endif
+// A/B switches of this round's drain changes (profiles/r04_*): the main loop's
+// drains skip the partial-tile mask, the drain re-test shares one v_perm
+// between two pairs, drain_complete orders its hits by two ballots.
+#ifndef YAMD_ASYNC_NO_TAIL
+#define YAMD_ASYNC_NO_TAIL 1
+#endif
+#ifndef YAMD_DRAIN_Y2
+#define YAMD_DRAIN_Y2 1
+#endif
+#ifndef YAMD_DC_BALLOT
+#define YAMD_DC_BALLOT 1
+#endif
 template <int MODE>
 constexpr bool kHoldFl = YAMD_HOLD_FL && !kEven<MODE>;
 template <int MODE>
@@ -581,6 +599,31 @@ __device__ __forceinline__ void certain_entry(const ScanParams& p, uint32_t ent,
   }
 }
 
+// Byte-key kernels: a drain's hits go to the pending list RAW (the ring entry,
+// the lane byte, a certain flag: one LDS store per hit in the per-lane loop,
+// whose trip count is the wave's largest per-lane hit count -- ~4 for ~1 hit
+// per lane on the dense sets), and the window / certain-candidate bytes are
+// then computed for the entries [from, pend_n) one lane each, while the ring
+// entries are still valid.
+#ifndef YAMD_BK_RESOLVE
+#define YAMD_BK_RESOLVE 1
+#endif
+template <int MODE>
+constexpr bool kBkResolve = YAMD_BK_RESOLVE && kByteKeys<MODE>;
+template <int MODE>
+__device__ __forceinline__ void resolve_pending(const ScanParams& p, WaveQueue& q, uint32_t lane,
+                                                uint32_t from) {
+  __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+  if (lane >= from && lane < q.pend_n) {
+    const u32x2 e = lds_load<u32x2>(q.pend + 8 * lane);
+    const uint32_t ent = e.x & 0xFFFFFFu, j = e.x >> 24;
+    uint32_t x, y = e.y & 0x7FFFFFFFu;
+    if (e.y >> 31) certain_entry<MODE>(p, ent, j, x, y);
+    else x = window4(ent, j);
+    lds_store2(q.pend + 8 * lane, x, y);
+  }
+}
+
 // Consume a deferred drain's first-level words: the lanes' hits that pass go,
 // in order, to the pending list.
 template <int MODE>
@@ -593,6 +636,7 @@ __device__ __forceinline__ void drain_complete(const ScanParams& p, WaveQueue& q
   // each lane's a-hit precedes its b-hit: lane L's first slot is the number of
   // a- and b-hits in the lanes below it (two ballots and their mbcnts instead
   // of a DPP scan)
+#if YAMD_DC_BALLOT
   const uint64_t ma = __ballot(ha), mb = __ballot(hb);
   const uint32_t total = (uint32_t)(__popcll(ma) + __popcll(mb));
   if (total == 0) return;
@@ -605,6 +649,14 @@ __device__ __forceinline__ void drain_complete(const ScanParams& p, WaveQueue& q
                                 __builtin_amdgcn_mbcnt_hi((uint32_t)(ma >> 32),
                                                           __builtin_amdgcn_mbcnt_lo((uint32_t)ma, q.pend_n))));
   const uint32_t i0 = below, i1 = i0 + (uint32_t)ha;
+#else
+  const uint32_t c = (uint32_t)ha + (uint32_t)hb;
+  const uint32_t incl = wave_inclusive_scan(c);
+  const uint32_t total = __builtin_amdgcn_readlane(incl, kWave - 1);
+  if (total == 0) return;
+  const uint32_t end = q.pend_n + total;
+  const uint32_t i0 = q.pend_n + incl - c, i1 = i0 + (uint32_t)ha;
+#endif
   for (uint32_t base = 0;; base += kWave) {
     if (ha && i0 - base < kWave) lds_store2(q.pend + 8 * (i0 - base), q.wa, q.oa);
     if (hb && i1 - base < kWave) lds_store2(q.pend + 8 * (i1 - base), q.wb, q.ob);
@@ -658,7 +710,7 @@ __device__ __forceinline__ void drain(const ScanParams& p, WaveQueue& q, uint32_
     }
     // the segment's partial last tile (its entries are appended after the main
     // loop's last drain, so only the final drain can hold them)
-    if (!kAsync && off0 + kBytesPerLane > seg_len) {
+    if ((!YAMD_ASYNC_NO_TAIL || !kAsync) && off0 + kBytesPerLane > seg_len) {
       const uint32_t lim = off0 >= seg_len ? 0u : seg_len - off0;
       m &= lim >= 16u ? 0xFFFFu : (1u << lim) - 1u;
     }
@@ -712,17 +764,46 @@ __device__ __forceinline__ void drain(const ScanParams& p, WaveQueue& q, uint32_
   }
   const uint32_t total = __builtin_amdgcn_readlane(incl, kWave - 1);
   if (total == 0) return;
+#if YAMD_BK_DIRECT
+  if constexpr (kByteKeys<MODE> && kAbl<MODE> == 0) {
+    // Only certain candidates (1-byte keys) and nothing pending: they need no
+    // probe, so each lane writes its own straight to the segment's output at
+    // its place in the drain's order -- no pending-list round trip (the
+    // dense sets' drains are nearly all of this kind).
+    if (q.pend_n == 0 && __ballot((maybe & ~kmask) != 0u) == 0) {
+      uint32_t o = found + incl - c;
+      while (maybe != 0u) {
+        const uint32_t j = (uint32_t)__builtin_ctz(maybe);
+        maybe &= maybe - 1;
+        uint32_t y = off0 + j, x;
+        certain_entry<MODE>(p, ent, j, x, y);
+        if (o < p.seg_cap) {
+          out[o] = y;
+          if (p.seg_x != nullptr) p.seg_x[(out - p.seg_out) + o] = x;
+        }
+        ++o;
+      }
+      found += total;
+      return;
+    }
+  }
+#endif
   // in order to the pending list, bucket-probed (one round trip for 64 hits)
   // each time it fills up -- dense true hits (1-byte keys) can yield up to 16
   // per lane; probing them in place would cost one round trip per hit
   const uint32_t end = q.pend_n + total;
   uint32_t idx = q.pend_n + incl - c;
+  uint32_t from = q.pend_n;   // (kBkResolve: the first pending entry still raw)
   for (uint32_t base = 0;; base += kWave) {
     while (maybe != 0u && idx < base + kWave) {
       const uint32_t j = (uint32_t)__builtin_ctz(maybe);
       maybe &= maybe - 1;
       uint32_t y = off0 + j, x;
-      if (kByteKeys<MODE> && ((kmask >> j) & 1u)) {
+      if constexpr (kBkResolve<MODE>) {
+        // raw: the ring entry, the lane byte and "certain"; resolved below
+        x = ent | j << 24;
+        y |= ((kmask >> j) & 1u) << 31;
+      } else if (kByteKeys<MODE> && ((kmask >> j) & 1u)) {
         certain_entry<MODE>(p, ent, j, x, y);
       } else {
         x = window4(ent, j);
@@ -732,9 +813,12 @@ __device__ __forceinline__ void drain(const ScanParams& p, WaveQueue& q, uint32_
     }
     if (end <= base + kWave) {
       q.pend_n = end - base;
+      if constexpr (kBkResolve<MODE>) resolve_pending<MODE>(p, q, lane, from);
       return;
     }
     q.pend_n = kWave;
+    if constexpr (kBkResolve<MODE>) resolve_pending<MODE>(p, q, lane, from);
+    from = 0;
     flush_pending<MODE>(p, q, lane, seg_start, out, found);
   }
 }
@@ -897,6 +981,7 @@ __device__ __forceinline__ uint32_t stage1(const uint32_t (&S)[6], uint32_t lane
 #pragma unroll
   for (int j = 0; j < kPairs; ++j) {
     const int k = 2 * j;
+    (void)y2;
     if constexpr (MODE == 3) {
       acc[k & 3] ^= xs[j];
     } else if constexpr (MODE == 6) {
@@ -905,7 +990,11 @@ __device__ __forceinline__ uint32_t stage1(const uint32_t (&S)[6], uint32_t lane
       const uint32_t x = xs[j];
       const uint32_t ul = ws[j].x >> (x & 31u), vl = ws[j].y >> ((x >> 5) & 31u);
       YAMD_SDWA_AND(k, ul, vl);
+#if YAMD_DRAIN_Y2
       const uint32_t y = (j & 1) ? y2[j >> 1] >> 16 : y2[j >> 1];   // d | b << 8 (low 10 bits)
+#else
+      const uint32_t y = __builtin_amdgcn_perm(0u, x, 0x0c0c0103u);   // d | b << 8
+#endif
       const uint32_t ur = ws[j].x >> (y & 31u), vr = ws[j].y >> ((y >> 5) & 31u);
       YAMD_SDWA_AND(k + 1, ur, vr);
     }
