@@ -183,6 +183,7 @@ def main():
     shard = int(args.gib_per_gpu * GiB)
     total = shard * world                           # one logical block, sharded
     begin, end = ydist.shard_bounds(total, world, rank)
+    begins_all = [ydist.shard_bounds(total, world, r)[0] for r in range(world)]
     # the rank's window of the block: its shard plus the tables' verify halos
     # (yr_amd_tables_info), so on-device pre-verification of its own candidates
     # is exactly the whole block's (dist.py); N = 1: the whole block
@@ -217,7 +218,8 @@ def main():
         t_g = time.perf_counter()
         pos = torch.empty(max(cnt, 1), dtype=torch.int64, device=dev)
         memcpy(pos.data_ptr(), ptr, cnt * 8, 3)
-        pos = ydist.gather_positions(pos[:cnt])     # RCCL: counts + padded gather
+        # RCCL: counts + padded gather of 32-bit offsets from each shard's begin
+        pos = ydist.gather_positions(pos[:cnt], begins=begins_all)
         if timed_kernel:
             gather_s[0] += time.perf_counter() - t_g
         return pos, kms

@@ -39,12 +39,16 @@ def _worker(rank, world, port, n, period, q, no_gather=False):
         b, e = ydist.shard_bounds(n, world, rank, align=period)
         local = torch.from_numpy(_shard_candidates(tab, data, b, e))
         out = ydist.gather_positions(local)
+        # 32-bit offsets from each rank's shard begin (bench.py's N > 1 gather)
+        begins = [ydist.shard_bounds(n, world, r, align=period)[0] for r in range(world)]
+        out32 = ydist.gather_positions(local, begins=begins)
         # two-column rows (the records path: {offset, pool index})
         rows = torch.stack([local, local * 3 + rank], 1)
         out2 = ydist.gather_rows(rows)
         if rank == 0:
             full = oracle.candidates(tab, data).astype(np.int64)
             ok = bool(np.array_equal(out.numpy(), full)) and out.numel() > 0
+            ok &= bool(np.array_equal(out32.numpy(), full))
             ok &= tuple(out2.shape) == (full.size, 2)
             ok &= bool(np.array_equal(out2[:, 0].numpy(), full))
             q.put(ok)

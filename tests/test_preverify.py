@@ -317,3 +317,51 @@ def test_scan_side_guard_after_key(tail):
     off = P.astype(np.uint64) - z["pool_backtrack"][K].astype(np.uint64)
     np.testing.assert_array_equal(r["offset"], off[keep])
     np.testing.assert_array_equal(r["pool_index"], K[keep])
+
+
+@pytest.mark.gpu
+def test_live_list_overflow_path(tmp_path):
+    """The compaction collects a segment's undecided candidates in an LDS
+    buffer and sends what does not fit straight to the global live list
+    (kernels.hip seg_scatter_kernel).  The diagnostic build's buffer holds one,
+    so the dense golden cases overflow it in every segment: its records must
+    equal the product build's, call for call (a subprocess: one library per
+    process)."""
+    import json
+    import os
+    import subprocess
+    import sys
+    import yara_amd
+    from conftest import REPO
+    diag = os.path.join(REPO, "yara_amd", "_diag", "libyara_amd.so")
+    if not os.path.exists(diag):
+        pytest.skip("diagnostic build missing (make -C yara_amd/csrc diag)")
+    cases = ["rx_1M", "fuzz0_256K", "fuzz3_256K", "bytekeys_1M", "short_1M"]
+    want = {}
+    for case in cases:
+        rec = CASES[case]
+        tab = yara_amd.Tables.from_npz(tables_npz(rec["rules"]), device=0, strings=True)
+        r = yara_amd.Scanner(tab).verify_calls(case_data(rec))
+        want[case] = [r["offset"].tolist(), r["pool_index"].tolist()]
+    script = (
+        "import json, sys\n"
+        "sys.path[:0] = [%r, %r, %r]\n"
+        "import yara_amd\n"
+        "from conftest import case_data, golden, tables_npz\n"
+        "cases = golden()['cases']\n"
+        "out = {}\n"
+        "for case in %r:\n"
+        "    rec = cases[case]\n"
+        "    tab = yara_amd.Tables.from_npz(tables_npz(rec['rules']), device=0, strings=True)\n"
+        "    r = yara_amd.Scanner(tab).verify_calls(case_data(rec))\n"
+        "    out[case] = [r['offset'].tolist(), r['pool_index'].tolist()]\n"
+        "json.dump(out, open(%r, 'w'))\n" % (REPO, os.path.join(REPO, "tests"),
+                                             os.path.join(REPO, "tests", "golden"), cases,
+                                             str(tmp_path / "diag.json")))
+    p = subprocess.run([sys.executable, "-c", script], capture_output=True, text=True, timeout=240,
+                       env=dict(os.environ, YARA_AMD_LIB=diag))
+    assert p.returncode == 0, p.stderr[-3000:]
+    got = json.load(open(tmp_path / "diag.json"))
+    for case in cases:
+        assert len(want[case][0]) > 0, case
+        assert got[case] == want[case], case

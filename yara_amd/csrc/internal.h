@@ -126,14 +126,16 @@ constexpr uint32_t kExactZero4 = 1u;   // flag: the 4-byte key 0x00000000 exists
 
 // First level of the exact check (one dword = one cache line per filter hit
 // instead of four 16-byte buckets): the word is chosen by the last 3 bytes of
-// the position's window; a 3-byte key sets one of its 32 bits picked by the
-// same 3 bytes, a 4-byte key one picked by its FIRST 3 bytes (with the word,
-// all 4 bytes count).  A clear bit proves "no 3-/4-byte key ends here"; a set
-// one sends the position to the bucket tables.  w4 = the 4 bytes ending at
-// the position.  The hashes are 24 x 24-bit products, so the device uses the
-// full-rate v_mul_u32_u24 / v_mul_hi_u32_u24 (low / high 32 bits of the 48-bit
-// product) rather than the quarter-rate 32-bit multiplies; a bit index is the
-// product's low 5 bits (the shifter reads only those: no mask).
+// the position's window; a 3-byte key sets one of its bits 0..15 (picked by
+// the same 3 bytes), a 4-byte key one of bits 16..31 (picked by all 4).  A
+// clear bit proves "no 3-/4-byte key ends here"; a set one sends the position
+// to the bucket tables.  w4 = the 4 bytes ending at the position.
+// The hashes are 24 x 24-bit products (low 32 bits), so the device uses the
+// full-rate v_mul_u32_u24 rather than the quarter-rate v_mul_lo_u32; the
+// 4-byte bit folds the window's first byte into the top byte of the other 3.
+// (YAMD_FL_MULHI=1: both bits over all 32 from the high halves of 24-bit
+// products, 6 instead of 12 instructions per deferred hit -- but config C's
+// kernel 3 % slower in one-process A/B, profiles/r04_ab_inproc.json; off.)
 __host__ __device__ inline uint32_t fl_mul24(uint32_t a, uint32_t b) {
   return (a & 0xFFFFFFu) * (b & 0xFFFFFFu);
 }
@@ -144,7 +146,7 @@ __host__ __device__ inline uint32_t fl_word(uint32_t w4) {
   return fl_mul24(w4 >> 8, 0x9E3779u) >> (32 - YAMD_FL_LOG2);
 }
 #ifndef YAMD_FL_MULHI
-#define YAMD_FL_MULHI 1
+#define YAMD_FL_MULHI 0
 #endif
 #if YAMD_FL_MULHI
 __host__ __device__ inline uint32_t fl_bit3(uint32_t w4) { return fl_mulhi24(w4 >> 8, 0xEBCA77u) & 31u; }

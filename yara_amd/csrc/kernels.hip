@@ -284,22 +284,26 @@ static_assert(kQueueCap == kWave, "a drain takes the whole ring, one entry per l
 // the key (or the scan's test of it, deep) and the guard are decided only if
 // every byte they test lies in w and the scanned range.  Pre-verification then never
 // reads the input for the candidate.
-__device__ __forceinline__ uint32_t key_class(const ScanParams& p, uint64_t w, int32_t kp,
-                                              bool deep, uint64_t pos) {
+// A 1-byte key's class parameters (ScanParams::kd_*), one 32-byte record per
+// key in LDS: the compaction finds a candidate's key by a zero-byte test on
+// the packed key bytes and reads its record (two ds_read_b128) instead of
+// selecting every field over the keys.
+struct KeyClassRec {
+  uint32_t info, m, v, x0, x1, min_pos, pad0, pad1;
+};
+__device__ __forceinline__ uint32_t key_class(const ScanParams& p, const KeyClassRec* kc, uint64_t w,
+                                              int32_t kp, bool deep, uint64_t pos) {
   if (kp < 0 && p.n_byte_keys != 1) return 0;
   const uint32_t key = kp < 0 ? (p.byte_keys & 0xFFu) : (uint32_t)(w >> (8 * kp)) & 0xFFu;
-  uint32_t info = 0, m = 0, v = 0, x0 = 0, x1 = 0, kidx = 0, min_pos = 0;
-#pragma unroll
-  for (uint32_t k = 0; k < kMaxByteKeys; ++k) {
-    const bool is = k < p.n_byte_keys && key == ((p.byte_keys >> (8 * k)) & 0xFFu);
-    info = is ? p.kd_info[k] : info;
-    m = is ? p.kd_m[k] : m;
-    v = is ? p.kd_v[k] : v;
-    x0 = is ? p.kd_x0[k] : x0;
-    x1 = is ? p.kd_x1[k] : x1;
-    min_pos = is ? p.kd_min_pos[k] : min_pos;
-    kidx = is ? k : kidx;
-  }
+  // the key's index: the lowest zero byte of byte_keys ^ key x 4 among the
+  // first n_byte_keys bytes (the lowest flag of the zero-byte test is exact)
+  const uint32_t t = p.byte_keys ^ (key * 0x01010101u);
+  const uint32_t nmask = p.n_byte_keys >= 4 ? 0x80808080u : 0x80808080u & ((1u << (8 * p.n_byte_keys)) - 1u);
+  const uint32_t z = (t - 0x01010101u) & ~t & nmask;
+  if (z == 0) return 0;
+  const uint32_t kidx = (uint32_t)__builtin_ctz(z) >> 3;
+  const KeyClassRec r = kc[kidx];
+  const uint32_t info = r.info, m = r.m, v = r.v, x0 = r.x0, x1 = r.x1, min_pos = r.min_pos;
   if (!(info & 1u)) return 0;
   if (info & 2u) {   // the byte before the key among the exclusions: a deeper state
     if (kp >= 1) {
@@ -599,14 +603,15 @@ __device__ __forceinline__ void certain_entry(const ScanParams& p, uint32_t ent,
   }
 }
 
-// Byte-key kernels: a drain's hits go to the pending list RAW (the ring entry,
-// the lane byte, a certain flag: one LDS store per hit in the per-lane loop,
-// whose trip count is the wave's largest per-lane hit count -- ~4 for ~1 hit
-// per lane on the dense sets), and the window / certain-candidate bytes are
-// then computed for the entries [from, pend_n) one lane each, while the ring
-// entries are still valid.
+// Byte-key kernels, YAMD_BK_RESOLVE=1: a drain's hits go to the pending list
+// RAW (the ring entry, the lane byte, a certain flag: one LDS store per hit in
+// the per-lane loop, whose trip count is the wave's largest per-lane hit
+// count), and the window / certain-candidate bytes are then computed for the
+// entries [from, pend_n) one lane each, while the ring entries are still
+// valid.  Measured 5 % SLOWER on rx, short and fuzz0 (one-process A/B,
+// profiles/r04_ab_inproc.json): off.
 #ifndef YAMD_BK_RESOLVE
-#define YAMD_BK_RESOLVE 1
+#define YAMD_BK_RESOLVE 0
 #endif
 template <int MODE>
 constexpr bool kBkResolve = YAMD_BK_RESOLVE && kByteKeys<MODE>;
@@ -1333,69 +1338,94 @@ __global__ __launch_bounds__(1024) void seg_offsets_kernel(const uint32_t* seg_c
 
 constexpr uint32_t kScatterWaves = 8;   // waves per segment in the scatter
 
+// per-segment LDS buffer of live candidates (the diagnostic build holds one,
+// so that the GPU suite exercises the overflow path, tests/test_preverify.py)
+constexpr uint32_t kLiveBuf = YAMD_DIAG ? 1 : 2048;
+
 __global__ __launch_bounds__(kScatterWaves * kWave) void seg_scatter_kernel(
     ScanParams p, const uint64_t* seg_offset, uint64_t* positions) {
   // one block per segment (segments hold up to ~10^4 candidates), its waves
   // interleaved 64 candidates apart
-  __shared__ uint32_t wlive[kScatterWaves + 1];
+  __shared__ KeyClassRec kc[kMaxByteKeys];
+  __shared__ uint32_t lbuf[kLiveBuf];
+  __shared__ uint32_t lcount, lglobal;
+  const bool classes = p.dead != nullptr;   // (uniform)
+  if (threadIdx.x < kMaxByteKeys) {
+    const uint32_t k = threadIdx.x;
+    kc[k] = KeyClassRec{p.kd_info[k], p.kd_m[k], p.kd_v[k], p.kd_x0[k], p.kd_x1[k], p.kd_min_pos[k], 0u, 0u};
+  }
+  if (threadIdx.x == 0) lcount = 0;
+  __syncthreads();
   const uint32_t seg = blockIdx.x;
   const uint32_t c = min(p.seg_count[seg], p.seg_cap);
   const uint64_t base = p.byte_begin + (uint64_t)seg * p.seg_bytes + 1;  // position = byte + 1
   const size_t at0 = p.seg_base ? p.seg_base[seg] : (size_t)seg * p.seg_cap;
   const uint32_t* src = p.seg_out + at0;
+  const uint32_t* sx = classes ? p.seg_x + at0 : nullptr;
   const uint64_t first = seg_offset[seg];
   uint64_t* dst = positions + first;
   const uint32_t lane = threadIdx.x % kWave, w = threadIdx.x / kWave;
   constexpr uint32_t kStride = kScatterWaves * kWave;
-  uint32_t n_live = 0;
-  // (latency-bound: a few hundred candidates per wave; the loads of an
-  // iteration issue together and unrolled iterations overlap)
-#pragma unroll 4
-  for (uint32_t i0 = w * kWave; i0 < c; i0 += kStride) {   // (wave-uniform trips: the ballot)
-    const uint32_t i = i0 + lane;
-    const uint32_t e = i < c ? src[i] : 0u;
-    const uint64_t pos = base + (e & kOutOffsetMask);
-    if (i < c) dst[i] = pos;
-    if (p.dead == nullptr) continue;
-    // the certain candidates' classes from the bytes the scan kept beside them
-    const uint32_t x = i < c ? p.seg_x[at0 + i] : 0u;
-    uint32_t cls = i < c ? 0u : kClassDead;
-    if (i < c && (e & kCertainMask) != 0u)
-      cls = key_class(p, x | (uint64_t)(e >> kOutByteShift & 0xFFu) << 32,
-                      (int32_t)(e >> kOutKeyShift & 7u) - 2, (e & kOutDeep) != 0u, pos);
-    if (i < c) p.dead[first + i] = (uint8_t)cls;
-    n_live += (uint32_t)__popcll(__ballot(cls == 0u));
-  }
-  if (p.dead == nullptr) return;
-  // the undecided candidates onto the live list: one atomic per segment (one
-  // per 64 candidates, serialised on the counter, took 1.2 ms for 34 M
-  // candidates), then each lane reads its own class bytes back
-  if (lane == 0) wlive[w] = n_live;
-  __syncthreads();
-  if (threadIdx.x == 0) {
-    uint32_t run = 0;
-    for (uint32_t k = 0; k < kScatterWaves; ++k) {
-      const uint32_t n = wlive[k];
-      wlive[k] = run;
-      run += n;
+  // Latency-bound (a few hundred candidates per wave): every iteration's
+  // entry and kept bytes are loaded one iteration ahead.
+  uint32_t e = 0, x = 0;
+  {
+    const uint32_t i = w * kWave + lane;
+    if (i < c) {
+      e = src[i];
+      if (classes) x = sx[i];
     }
-    wlive[kScatterWaves] = run ? atomicAdd(p.live, run) + 1 : 0u;
   }
-  __syncthreads();
-  if (n_live == 0) return;
-  uint32_t at = wlive[kScatterWaves] + wlive[w];
-  const uint8_t* cl = p.dead + first;
-#pragma unroll 4
-  for (uint32_t i0 = w * kWave; i0 < c; i0 += kStride) {
+  for (uint32_t i0 = w * kWave; i0 < c; i0 += kStride) {   // (wave-uniform trips: the ballots)
     const uint32_t i = i0 + lane;
-    const bool live = i < c && cl[i] == 0u;
+    const bool valid = i < c;
+    const uint32_t ec = e, xc = x;
+    e = x = 0u;
+    if (i + kStride < c) {
+      e = src[i + kStride];
+      if (classes) x = sx[i + kStride];
+    }
+    const uint64_t pos = base + (ec & kOutOffsetMask);
+    if (valid) dst[i] = pos;
+    if (!classes) continue;
+    // the certain candidates' classes from the bytes the scan kept beside them
+    uint32_t cls = 0u;
+    if (valid && (ec & kCertainMask) != 0u)
+      cls = key_class(p, kc, xc | (uint64_t)(ec >> kOutByteShift & 0xFFu) << 32,
+                      (int32_t)(ec >> kOutKeyShift & 7u) - 2, (ec & kOutDeep) != 0u, pos);
+    if (valid) p.dead[first + i] = (uint8_t)cls;
+    // the undecided ones onto the live list (any order): the segment's LDS
+    // buffer, copied out with ONE global atomic per segment (one per wave and
+    // iteration, serialised on the counter, took 1.2 ms for 34 M candidates);
+    // what does not fit goes straight to the global list
+    const bool live = valid && cls == 0u;
     const uint64_t lm = __ballot(live);
-    if (live)
-      p.live[at + __builtin_amdgcn_mbcnt_hi((uint32_t)(lm >> 32),
-                                            __builtin_amdgcn_mbcnt_lo((uint32_t)lm, 0u))] =
-          (uint32_t)(first + i);
-    at += (uint32_t)__popcll(lm);
+    if (lm != 0) {
+      uint32_t b = 0;
+      if (lane == 0) b = atomicAdd(&lcount, (uint32_t)__popcll(lm));
+      b = __builtin_amdgcn_readfirstlane(b);
+      const uint32_t slot =
+          b + __builtin_amdgcn_mbcnt_hi((uint32_t)(lm >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)lm, 0u));
+      if (live && slot < kLiveBuf) lbuf[slot] = (uint32_t)(first + i);
+      const uint64_t om = __ballot(live && slot >= kLiveBuf);
+      if (om != 0) {
+        uint32_t g = 0;
+        if (lane == 0) g = atomicAdd(p.live, (uint32_t)__popcll(om));
+        g = __builtin_amdgcn_readfirstlane(g);
+        if (live && slot >= kLiveBuf)
+          p.live[1 + g + __builtin_amdgcn_mbcnt_hi((uint32_t)(om >> 32),
+                                                   __builtin_amdgcn_mbcnt_lo((uint32_t)om, 0u))] =
+              (uint32_t)(first + i);
+      }
+    }
   }
+  if (!classes) return;
+  __syncthreads();
+  const uint32_t n = min(lcount, kLiveBuf);
+  if (n == 0) return;
+  if (threadIdx.x == 0) lglobal = atomicAdd(p.live, n) + 1u;
+  __syncthreads();
+  for (uint32_t t = threadIdx.x; t < n; t += kStride) p.live[lglobal + t] = lbuf[t];
 }
 
 // ---------------------------------------------------------------------------

@@ -65,13 +65,13 @@ def _gather_backend(group):
     return "gather" if dist.get_backend(group) in ("nccl", "gloo") else "all_gather"
 
 
-def gather_rows(local: torch.Tensor, group=None, dst: int = 0):
+def gather_rows(local: torch.Tensor, group=None, dst: int = 0, split: bool = False):
     """Gather every rank's int64 rows [m_r, w] to `dst`: all_gather of the
     counts, one padded gather (payloads are KB-MB, far below what the xGMI
     links move per microsecond).  Returns the rank-ordered concatenation on
-    `dst`, None elsewhere."""
-    if local.dim() != 2 or local.dtype != torch.int64:
-        raise ValueError("rows must be a 2-d int64 tensor")
+    `dst` (with ``split``: the list of every rank's rows), None elsewhere."""
+    if local.dim() != 2 or local.dtype not in (torch.int64, torch.int32):
+        raise ValueError("rows must be a 2-d int64 or int32 tensor")
     world = dist.get_world_size(group)
     rank = dist.get_rank(group)
     if dist.get_backend(group) == "gloo":
@@ -85,24 +85,48 @@ def gather_rows(local: torch.Tensor, group=None, dst: int = 0):
     if local.shape[0] == width:
         padded = local.contiguous()
     else:
-        padded = torch.full((width, w), -1, dtype=torch.int64, device=local.device)
+        padded = torch.full((width, w), -1, dtype=local.dtype, device=local.device)
         padded[:local.shape[0]] = local
     if _gather_backend(group) == "gather":
         bufs = [torch.empty_like(padded) for _ in range(world)] if rank == dst else None
         dist.gather(padded, bufs, dst=dst, group=group)
     else:
-        flat = torch.empty((world * width, w), dtype=torch.int64, device=local.device)
+        flat = torch.empty((world * width, w), dtype=local.dtype, device=local.device)
         dist.all_gather_into_tensor(flat, padded, group=group)
         bufs = list(flat.view(world, width, w))
     if rank != dst:
         return None
+    if split:
+        return [b[:c] for b, c in zip(bufs, counts)]
     return torch.cat([b[:c] for b, c in zip(bufs, counts)])
 
 
-def gather_positions(local: torch.Tensor, group=None, dst: int = 0):
-    """Gather every rank's ascending int64 candidate positions to `dst`."""
-    out = gather_rows(local.reshape(-1, 1).to(torch.int64), group, dst)
-    return None if out is None else out.reshape(-1)
+def gather_positions(local: torch.Tensor, group=None, dst: int = 0, begins=None):
+    """Gather every rank's ascending int64 candidate positions to `dst`.
+
+    With ``begins`` (every rank's shard begin, its positions in (begin,
+    begin + 2^32]: shards of at most 4 GiB) each rank sends p - begin - 1 as a
+    32-bit word -- half the bytes over the links -- and `dst` restores them;
+    its own positions it keeps as they are (rank 0's shard holds position 0,
+    which has no such offset)."""
+    if begins is None:
+        out = gather_rows(local.reshape(-1, 1).to(torch.int64), group, dst)
+        return None if out is None else out.reshape(-1)
+    world = dist.get_world_size(group)
+    rank = dist.get_rank(group)
+    if len(begins) != world:
+        raise ValueError("one shard begin per rank")
+    off = (local.to(torch.int64) - (begins[rank] + 1)).to(torch.int32)   # (wraps past 2^31)
+    rows = gather_rows(off.reshape(-1, 1), group, dst, split=True)
+    if rows is None:
+        return None
+    parts = []
+    for r, part in enumerate(rows):
+        if r == rank:
+            parts.append(local.to(torch.int64).to(part.device))
+        else:
+            parts.append((part.reshape(-1).to(torch.int64) & 0xFFFFFFFF) + (begins[r] + 1))
+    return torch.cat(parts)
 
 
 def records_to_rows(d_records: int, count: int, device) -> torch.Tensor:
