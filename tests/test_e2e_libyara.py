@@ -224,6 +224,26 @@ def test_scan_mem_of_truncated_mapping(tmp_path, preverify):
 
 
 @needs_check
+@pytest.mark.parametrize("block,devices", [(12 << 20, None), (12 << 20, "0,0,0"), (0, "0,0")],
+                         ids=["pipeline", "pipeline-3-devices", "scan_mem-2-devices"])
+def test_truncated_mapping_through_pinned_staging(tmp_path, block, devices):
+    """The same truncated mapping through the paths that copy the block into
+    pinned staging with helper threads (yr_amd_pipeline_submit_dma, the
+    multi-device pipeline, the staged multi-device scan_mem): every chunk is
+    copied by the shim's _guarded_copy inside YR_TRYCATCH, so the pages past
+    the truncation fault on a helper thread and the scan returns
+    ERROR_COULD_NOT_MAP_FILE like the stock walk -- no SIGBUS, no hang
+    (ADVICE r03).  12 MiB blocks: the parallel copy path (>= 8 MiB); the file
+    is cut in the middle of the second block."""
+    lit = _rules_file(tmp_path, "lit")
+    spec = _data_file(tmp_path, planted.lit_buffer(oracle.xorshift, 32 << 20, 13), "d.bin")
+    extra = {} if devices is None else {"E2E_DEVICES": devices, "E2E_MULTI_MIN": str(1 << 20)}
+    rc, res = _run(lit, spec, block=block, mode="truncmap", **extra)
+    assert res["rc_stock"] == 4 and res["rc_gpu"] == 4, res   # ERROR_COULD_NOT_MAP_FILE
+    assert res["finished"] == [0, 0], res
+
+
+@needs_check
 @pytest.mark.parametrize("rules,block", [("C", 0), ("lit", 65536)])
 def test_threads_share_one_gpu_rules(tmp_path, rules, block):
     """N threads, each with its own YR_SCANNER and YR_GPU_SCANNER, scanning
