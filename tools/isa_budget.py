@@ -17,7 +17,7 @@ import os
 import re
 
 REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
-ASM = os.path.join(REPO, "yara_amd", "_build", "kernels-hip-amdgcn-amd-amdhsa-gfx950.s")
+ASM = os.environ.get("YAMD_ASM") or os.path.join(REPO, "yara_amd", "_build", "kernels-hip-amdgcn-amd-amdhsa-gfx950.s")
 HALF = ("v_alignbyte_b32", "v_perm_b32", "v_bitop3_b32", "v_mad_u32_u24", "v_lshl_add_u32",
         "v_add3_u32", "v_mbcnt_lo_u32_b32", "v_mbcnt_hi_u32_b32", "v_readlane_b32",
         "v_readfirstlane_b32", "v_writelane_b32", "v_lshl_add_u64", "v_bfe_u32", "v_lshl_or_b32",

@@ -1014,6 +1014,32 @@ __device__ __forceinline__ uint32_t stage1(const uint32_t (&S)[6], uint32_t lane
          ((acc[2] & 0x01010101u) << 2) | ((acc[3] & 0x01010101u) << 3);
 }
 
+// One ring entry: the 16-byte unit's bytes S[1..4] (as loaded: no register
+// moves), the 4 bytes before them S[0], and the unit's index in the segment
+// (offset / 16; byte-key kernels: the next unit's first two bytes in the top
+// half).
+template <int MODE>
+__device__ __forceinline__ void write_entry(uint32_t ent, const uint32_t (&S)[6], uint32_t unit) {
+  const uint32_t idx = unit | (kNextBytes<MODE> ? S[5] << 16 : 0u);
+#if YAMD_RING_CTX_FIRST
+  // three ds_write2_b32: context, the 16 bytes as loaded, index
+  typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
+  typedef u32x4 u32x4_a4 __attribute__((aligned(4)));
+  u32x4 d;
+  d.x = S[1];
+  d.y = S[2];
+  d.z = S[3];
+  d.w = S[4];
+  *reinterpret_cast<__attribute__((address_space(3))) u32x4_a4*>((uintptr_t)(ent + kEntData)) = d;
+  *reinterpret_cast<__attribute__((address_space(3))) uint32_t*>((uintptr_t)(ent + kEntCtx)) = S[0];
+  *reinterpret_cast<__attribute__((address_space(3))) uint32_t*>((uintptr_t)(ent + kEntIdx)) = idx;
+#else
+  lds_store2(ent, S[1], S[2]);
+  lds_store2(ent + 8, S[3], S[4]);
+  lds_store2(ent + 16, S[0], idx);
+#endif
+}
+
 // The ordered append of a tile's hits to the wave ring.  TAIL: the segment's
 // last, partial tile (positions past seg_len are masked off).
 template <int MODE, bool TAIL>
@@ -1050,25 +1076,7 @@ __device__ __forceinline__ void ring_append(const ScanParams& p, WaveQueue& q, S
       if constexpr (MODE == 8) {   // ablation: the append's slot arithmetic, no LDS writes
         asm volatile("" ::"v"(ent), "v"((tile_off >> 4) + lane));
       } else {
-        // (byte-key kernel: the next lane's first two bytes in the top half)
-        const uint32_t idx = (tile_off >> 4) + lane | (kNextBytes<MODE> ? S[5] << 16 : 0u);
-#if YAMD_RING_CTX_FIRST
-        // three ds_write2_b32: context, the 16 bytes as loaded, index
-        typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
-        typedef u32x4 u32x4_a4 __attribute__((aligned(4)));
-        u32x4 d;
-        d.x = S[1];
-        d.y = S[2];
-        d.z = S[3];
-        d.w = S[4];
-        *reinterpret_cast<__attribute__((address_space(3))) u32x4_a4*>((uintptr_t)(ent + kEntData)) = d;
-        *reinterpret_cast<__attribute__((address_space(3))) uint32_t*>((uintptr_t)(ent + kEntCtx)) = S[0];
-        *reinterpret_cast<__attribute__((address_space(3))) uint32_t*>((uintptr_t)(ent + kEntIdx)) = idx;
-#else
-        lds_store2(ent, S[1], S[2]);
-        lds_store2(ent + 8, S[3], S[4]);
-        lds_store2(ent + 16, S[0], idx);
-#endif
+        write_entry<MODE>(ent, S, (tile_off >> 4) + lane);
       }
     }
     q.count += n;
@@ -1157,6 +1165,119 @@ __device__ __forceinline__ void tile_step(const ScanParams& p, WaveQueue& q, Seg
   issue_first_level<MODE>(p, q);
 }
 
+// Wide steps (YAMD_WIDE=1): 32 bytes per lane, a 2 KiB wave tile read as two
+// 16-byte halves per lane (lane L: bytes 32L .. 32L + 31), so the step's fixed
+// costs -- the lane-context DPP moves, the append's ballot-to-slot arithmetic,
+// the loop control, the deferred-drain test, the two first-level loads -- are
+// paid once per 2 KiB.  Ring entries stay 16-byte units (unit = offset / 16)
+// in position order: lane L's half 0, its half 1, lane L + 1's half 0, ...
+#ifndef YAMD_WIDE
+#define YAMD_WIDE 0
+#endif
+template <int MODE>
+constexpr bool kWide = YAMD_WIDE && (MODE == 0 || (MODE >= 20 && MODE <= 29));
+static_assert(!YAMD_WIDE || YAMD_CARRY_DPP2, "wide steps take the lane-0 context by the second DPP move");
+
+template <int MODE>
+__device__ __forceinline__ uint32_t unit_any(const ScanParams& p, const uint32_t (&S)[6], uint32_t lane) {
+  uint32_t any = stage1<kStage1Mode<MODE>, true>(S, lane);
+  if constexpr (kEven<MODE>)
+    if (p.n_pair_keys != 0) any |= pair_keys_any(S, p);
+  if constexpr (kByteKeys<MODE>) any |= byte_keys_any(S, p);
+  return any;
+}
+
+// A lane's hit halves at ring slot count + below (half 1 after half 0).
+template <int MODE>
+__device__ __forceinline__ void wide_entries(const WaveQueue& q, uint32_t below, uint32_t any0,
+                                             uint32_t any1, const uint32_t (&S0)[6],
+                                             const uint32_t (&S1)[6], uint32_t unit) {
+  const uint32_t base = q.ring + q.count * (kQueueEntryWords * 4);   // scalar
+  uint32_t ent;
+  asm("v_mad_u32_u24 %0, %1, 24, %2" : "=v"(ent) : "v"(below), "s"(base));
+  if (any0 != 0u) write_entry<MODE>(ent, S0, unit);
+  if (any1 != 0u) write_entry<MODE>(any0 != 0u ? ent + kQueueEntryWords * 4 : ent, S1, unit + 1u);
+}
+
+template <int MODE>
+__device__ __forceinline__ void wide_step(const ScanParams& p, WaveQueue& q, SegState& st,
+                                          const uint4& a, const uint4& b, uint32_t tile_off,
+                                          uint32_t lane) {
+  uint32_t S0[6], S1[6];
+  // half 0's context: the previous lane's last dword (lane 0: the previous
+  // tile's, kept in st.carry); half 1's: the lane's own a.w
+  const uint32_t rot = __builtin_amdgcn_mov_dpp(b.w, 0x13C, 0xF, 0xF, true);   // wave_ror:1
+  S0[0] = __builtin_amdgcn_update_dpp(st.carry, b.w, 0x138, 0xF, 0xF, false);  // wave_shr:1
+  st.carry = rot;
+  S0[1] = a.x;
+  S0[2] = a.y;
+  S0[3] = a.z;
+  S0[4] = a.w;
+  S0[5] = kNextBytes<MODE> ? b.x : 0u;
+  S1[0] = a.w;
+  S1[1] = b.x;
+  S1[2] = b.y;
+  S1[3] = b.z;
+  S1[4] = b.w;
+  // (the next lane's first dword, wave_shl:1; lane 63: 0)
+  S1[5] = kNextBytes<MODE> ? __builtin_amdgcn_mov_dpp(a.x, 0x130, 0xF, 0xF, true) : 0u;
+  const uint32_t any0 = unit_any<MODE>(p, S0, lane), any1 = unit_any<MODE>(p, S1, lane);
+  if constexpr (kDeferFl<MODE>)
+    if (q.defer) {
+#if YAMD_PRIO >= 2
+      __builtin_amdgcn_s_setprio(0);
+#endif
+      drain_complete<MODE>(p, q, lane, st.seg_start, st.out, st.found);
+#if YAMD_PRIO >= 2
+      __builtin_amdgcn_s_setprio(1);
+#endif
+    }
+  // per lane 0, 1 or 2 hit halves: lanes with one count once (m0 | m1),
+  // lanes with both once more (m0 & m1, rare)
+  const uint64_t m0 = __ballot(any0 != 0u), m1 = __ballot(any1 != 0u);
+  const uint64_t m01 = m0 | m1, mb = m0 & m1;
+  const uint32_t n = (uint32_t)(__popcll(m01) + __popcll(mb));
+  if (n != 0) {
+    uint32_t below = __builtin_amdgcn_mbcnt_hi((uint32_t)(m01 >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m01, 0u));
+    if (mb != 0u)
+      below = __builtin_amdgcn_mbcnt_hi((uint32_t)(mb >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)mb, below));
+    const uint32_t unit = (tile_off >> 4) + 2 * lane;
+    bool wr = (any0 | any1) != 0u;
+    uint32_t take = n;
+    if (n > kQueueCap) {
+      // more hit halves than the ring holds (> 64 of 128): lanes 0-31 first,
+      // then 32-63, so that the ring order stays the position order
+      const uint32_t n_lo = (uint32_t)(__popcll(m01 & 0xFFFFFFFFull) + __popcll(mb & 0xFFFFFFFFull));
+      if (q.count + n_lo > kQueueCap) {
+        __builtin_amdgcn_s_setprio(0);
+        drain<MODE, true>(p, q, lane, st.seg_start, st.seg_len, st.out, st.found);
+        __builtin_amdgcn_s_setprio(1);
+      }
+      if (wr && lane < kWave / 2) wide_entries<MODE>(q, below, any0, any1, S0, S1, unit);
+      q.count += n_lo;
+      take = n - n_lo;
+      below -= n_lo;
+      wr = wr && lane >= kWave / 2;
+      // (that drain may have deferred its first-level loads: issue them, so
+      // that the drain below -- there always is one -- completes it)
+      if constexpr (kDeferFl<MODE>)
+        if (q.defer) issue_first_level<MODE>(p, q);
+    }
+    if (q.count + take > kQueueCap) {
+#if YAMD_PRIO
+      __builtin_amdgcn_s_setprio(0);
+#endif
+      drain<MODE, true>(p, q, lane, st.seg_start, st.seg_len, st.out, st.found);
+#if YAMD_PRIO
+      __builtin_amdgcn_s_setprio(1);
+#endif
+    }
+    if (wr) wide_entries<MODE>(q, below, any0, any1, S0, S1, unit);
+    q.count += take;
+  }
+  issue_first_level<MODE>(p, q);
+}
+
 // Stream one segment [seg_start, seg_start + seg_len) of the block: full tiles
 // in the main loop (unmasked; the next tile's loads in flight, two tile
 // registers used alternately so no copy waits for a load), then the partial
@@ -1203,7 +1324,32 @@ __device__ __forceinline__ void scan_segment(const ScanParams& p, WaveQueue& q, 
   q.oa = q.ob = kNoHit;
 
   const uint32_t n_full = st.seg_len / kTile;            // tiles needing no mask / bounds
-  if (n_full > 0) {
+  if constexpr (kWide<MODE>) {
+    const uint32_t n_wide = n_full / 2;                  // 2 KiB wide tiles
+    if (n_wide > 0) {
+      constexpr uint32_t kWideTile = 2 * kTile;
+      const uint32_t last = (n_wide - 1) * kWideTile;
+      const __amdgpu_buffer_rsrc_t rsrc = segment_rsrc(base);
+      const uint32_t lane32 = lane * (2 * kBytesPerLane);
+      uint4 a0 = load_tile_full(rsrc, 0, lane32), a1 = load_tile_full(rsrc, kBytesPerLane, lane32), b0, b1;
+      asm volatile("" : "+v"(a0.x), "+v"(a0.y), "+v"(a0.z), "+v"(a0.w), "+v"(a1.x), "+v"(a1.y), "+v"(a1.z),
+                   "+v"(a1.w));
+      uint32_t i = 0;
+      for (; i + 2 <= n_wide; i += 2) {
+        b0 = load_tile_full(rsrc, (i + 1) * kWideTile, lane32);
+        b1 = load_tile_full(rsrc, (i + 1) * kWideTile + kBytesPerLane, lane32);
+        wide_step<MODE>(p, q, st, a0, a1, i * kWideTile, lane);
+        const uint32_t nx = min((i + 2) * kWideTile, last);
+        a0 = load_tile_full(rsrc, nx, lane32);
+        a1 = load_tile_full(rsrc, nx + kBytesPerLane, lane32);
+        wide_step<MODE>(p, q, st, b0, b1, (i + 1) * kWideTile, lane);
+      }
+      if (i < n_wide) wide_step<MODE>(p, q, st, a0, a1, i * kWideTile, lane);
+    }
+    if (n_full % 2 != 0)   // an odd last full tile: one ordinary step
+      tile_step<MODE, false>(p, q, st, load_tile(base, (n_full - 1) * kTile, lane, avail),
+                             (n_full - 1) * kTile, lane);
+  } else if (n_full > 0) {
     const uint32_t last = (n_full - 1) * kTile;
     const __amdgpu_buffer_rsrc_t rsrc = segment_rsrc(base);
     const uint32_t lane16 = lane * kBytesPerLane;
