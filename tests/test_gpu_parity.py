@@ -402,6 +402,41 @@ def test_verify_refuses_more_than_2_32_candidates():
     assert len(sc.verify_calls(small)) > 0
 
 
+@pytest.mark.slow
+def test_verify_exactly_2_32_candidates_with_key_classes():
+    """The largest stream yr_amd_verify_device accepts: exactly 2^32 candidates
+    (a zero-filled 4 GiB block, 1-byte key 00) under a rule set whose 1-byte
+    keys have candidate classes.  The compaction's live-list counter is 32-bit,
+    so the scanner decides no classes for a stream past 0xFFFFFFFF candidates
+    (scanner.cpp) -- a wrapped counter would have dropped every candidate.  On
+    zero bytes the record count is affine in the block size past the first few
+    bytes (edge effects at both ends are fixed), so two small blocks predict
+    the 4 GiB one exactly."""
+    torch = _torch()
+    n = 1 << 32
+    if torch.cuda.mem_get_info()[0] < 170 << 30:
+        pytest.skip("needs ~170 GiB of free HBM (positions, classes and records of 2^32 candidates)")
+    sc = yara_amd.Scanner(yara_amd.Tables.from_npz(tables_npz("bytekeys"), device=0, strings=True))
+    counts = {}
+    for m in (1 << 20, 1 << 21):
+        z = torch.zeros(m + 16, dtype=torch.uint8, device="cuda")
+        sc.scan_device(z.data_ptr(), m)
+        _, cnt, allp = sc.device_result()
+        assert cnt == m
+        counts[m] = sc.verify_device(0)[1]
+        del z
+    slope = (counts[1 << 21] - counts[1 << 20]) // (1 << 20)
+    assert slope * (1 << 20) == counts[1 << 21] - counts[1 << 20] and slope > 0
+    expect = counts[1 << 20] + slope * (n - (1 << 20))
+    d = torch.zeros(n + 16, dtype=torch.uint8, device="cuda")
+    sc.scan_device(d.data_ptr(), n)
+    _, cnt, allp = sc.device_result()
+    assert not allp and cnt == n
+    assert sc.verify_device(0)[1] == expect
+    del d
+    torch.cuda.empty_cache()
+
+
 def test_block_larger_than_4gib():
     """A single 8 GiB block (past 32-bit byte offsets: 8,192 segments, positions
     above 2^32): its candidates up to 4 GiB equal the golden C_4G stream (the

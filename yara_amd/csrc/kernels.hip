@@ -267,6 +267,19 @@ constexpr bool kByteKeyAblation = MODE == 24 || MODE == 25;
 constexpr uint32_t kCertainMask = 7u << kOutKeyShift;
 static_assert(kSegment <= kOutOffsetMask + 1u, "segment offsets must leave the top bits free");
 
+// Byte-key drains without divergent branches (YAMD_BK_FLAT=1): a hit's
+// window / certain-candidate bytes are computed by selects from one unaligned
+// LDS read (the entry of a kernel that keeps the next lane's two bytes holds
+// them right after the lane's 16, its unit index in the top half:
+// kIdxHigh), instead of per-hit branches on "certain" and on "the bytes reach
+// past the lane".
+#ifndef YAMD_BK_FLAT
+#define YAMD_BK_FLAT 0
+#endif
+template <int MODE>
+constexpr bool kIdxHigh = YAMD_BK_FLAT && kNextBytes<MODE>;
+static_assert(!YAMD_BK_FLAT || YAMD_RING_CTX_FIRST, "flat byte-key drains read the context-first entry");
+
 // b one of the (up to 8, repeated to fill) bytes of x0, x1: zero-byte test
 __device__ __forceinline__ bool excluded(uint32_t b, uint32_t x0, uint32_t x1) {
   const uint32_t pv = b * 0x01010101u, a = pv ^ x0, c = pv ^ x1;
@@ -585,6 +598,17 @@ template <int MODE>
 __device__ __forceinline__ void certain_entry(const ScanParams& p, uint32_t ent, uint32_t j,
                                               uint32_t& x, uint32_t& y) {
   const uint32_t li = lds_load<uint32_t>(ent + kEntIdx);
+  if constexpr (kIdxHigh<MODE>) {   // lane bytes 16, 17 follow byte 15 in the entry
+    const uint32_t e = min(j + p.kx_end, ((li >> 16) & (kWave - 1)) != kWave - 1 ? 16u : 14u);
+    x = window4(ent, e);
+    y |= (uint32_t)lds_load<uint8_t>(entry_byte_addr(ent, (int32_t)e + 1)) << kOutByteShift |
+         (j + 5 - e) << kOutKeyShift;
+    if (p.kx_deep != 0u) {
+      const uint32_t b = lds_load<uint8_t>(entry_byte_addr(ent, (int32_t)j - 1));
+      if (excluded(b, p.kd_x0[0], p.kd_x1[0])) y |= kOutDeep;
+    }
+    return;
+  }
   const uint32_t e =
       min(j + p.kx_end, kNextBytes<MODE> && (li & (kWave - 1)) != kWave - 1 ? 16u : 14u);
   uint32_t b5;
@@ -690,6 +714,7 @@ __device__ __forceinline__ void drain(const ScanParams& p, WaveQueue& q, uint32_
   __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
   uint32_t maybe = 0, off0 = 0, m = 0;   // m: bit j = lane byte j passes the filter
   uint32_t kmask = 0;                    // bit j = lane byte j is a 1-byte key (certain)
+  uint32_t ridx = 0;                     // (byte-key kernels: the entry's index word)
   const uint32_t ent = q.ring + lane * (kQueueEntryWords * 4);
   if (lane < n) {
     // the entry's 16 positions again, now with a per-position result: the
@@ -702,7 +727,8 @@ __device__ __forceinline__ void drain(const ScanParams& p, WaveQueue& q, uint32_
 #else
     const uint32_t S[6] = {e45.x, e01.x, e01.y, e23.x, e23.y, 0u};
 #endif
-    off0 = (e45.y & 0xFFFFu) * kBytesPerLane;
+    off0 = (kIdxHigh<MODE> ? e45.y >> 16 : e45.y & 0xFFFFu) * kBytesPerLane;
+    if constexpr (kByteKeys<MODE>) ridx = e45.y;
     if constexpr (kEven<MODE>) {
       m = even_mask<kEvenHash<MODE>>(S);
       if (p.n_pair_keys != 0) m |= pair_keys_mask(S, p);
@@ -799,6 +825,11 @@ __device__ __forceinline__ void drain(const ScanParams& p, WaveQueue& q, uint32_
   const uint32_t end = q.pend_n + total;
   uint32_t idx = q.pend_n + incl - c;
   uint32_t from = q.pend_n;   // (kBkResolve: the first pending entry still raw)
+  // the last lane byte a certain candidate may keep: 16 (the next lane's two
+  // bytes are in the entry) unless the entry is a tile's last lane
+  const uint32_t elim = kIdxHigh<MODE> && ((ridx >> 16) & (kWave - 1)) != kWave - 1 ? 16u : 14u;
+  (void)elim;
+  (void)ridx;
   for (uint32_t base = 0;; base += kWave) {
     while (maybe != 0u && idx < base + kWave) {
       const uint32_t j = (uint32_t)__builtin_ctz(maybe);
@@ -808,6 +839,19 @@ __device__ __forceinline__ void drain(const ScanParams& p, WaveQueue& q, uint32_
         // raw: the ring entry, the lane byte and "certain"; resolved below
         x = ent | j << 24;
         y |= ((kmask >> j) & 1u) << 31;
+      } else if constexpr (kByteKeys<MODE> && YAMD_BK_FLAT) {
+        // certain (a 1-byte key ends at j): the five bytes e - 3 .. e + 1 kept
+        // for key_class, e = min(j + kx_end, last kept byte); otherwise the
+        // window ending at j.  Selects, no divergent branch.
+        const bool cert = ((kmask >> j) & 1u) != 0u;
+        const uint32_t e = cert ? min(j + p.kx_end, elim) : j;
+        x = window4(ent, e);
+        const uint32_t b5 = lds_load<uint8_t>(entry_byte_addr(ent, (int32_t)e + 1));
+        uint32_t c = b5 << kOutByteShift | (j + 5 - e) << kOutKeyShift;
+        if (p.kx_deep != 0u)   // (uniform) the byte before the key
+          if (excluded(lds_load<uint8_t>(entry_byte_addr(ent, (int32_t)j - 1)), p.kd_x0[0], p.kd_x1[0]))
+            c |= kOutDeep;
+        y |= cert ? c : 0u;
       } else if (kByteKeys<MODE> && ((kmask >> j) & 1u)) {
         certain_entry<MODE>(p, ent, j, x, y);
       } else {
@@ -1020,7 +1064,10 @@ __device__ __forceinline__ uint32_t stage1(const uint32_t (&S)[6], uint32_t lane
 // half).
 template <int MODE>
 __device__ __forceinline__ void write_entry(uint32_t ent, const uint32_t (&S)[6], uint32_t unit) {
-  const uint32_t idx = unit | (kNextBytes<MODE> ? S[5] << 16 : 0u);
+  // (kIdxHigh: the next lane's two bytes first, so that they follow the
+  // lane's 16 in the entry)
+  const uint32_t idx = kIdxHigh<MODE> ? __builtin_amdgcn_perm(unit, S[5], 0x05040100u)
+                                      : unit | (kNextBytes<MODE> ? S[5] << 16 : 0u);
 #if YAMD_RING_CTX_FIRST
   // three ds_write2_b32: context, the 16 bytes as loaded, index
   typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
