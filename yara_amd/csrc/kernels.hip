@@ -304,9 +304,17 @@ static_assert(kQueueCap == kWave, "a drain takes the whole ring, one entry per l
 struct KeyClassRec {
   uint32_t info, m, v, x0, x1, min_pos, pad0, pad1;
 };
+// last = the last valid byte of w (4: the five kept bytes; 7: eight bytes the
+// compaction read from the input, the key at byte 2).  *more (if given) is
+// set when the class is undecided only because a byte it needs lies outside
+// w, and eight bytes with the key at byte 2 would hold them.
 __device__ __forceinline__ uint32_t key_class(const ScanParams& p, const KeyClassRec* kc, uint64_t w,
-                                              int32_t kp, bool deep, uint64_t pos) {
-  if (kp < 0 && p.n_byte_keys != 1) return 0;
+                                              int32_t kp, bool deep, uint64_t pos, int32_t last = 4,
+                                              bool* more = nullptr) {
+  if (kp < 0 && p.n_byte_keys != 1) {
+    if (more) *more = true;
+    return 0;
+  }
   const uint32_t key = kp < 0 ? (p.byte_keys & 0xFFu) : (uint32_t)(w >> (8 * kp)) & 0xFFu;
   // the key's index: the lowest zero byte of byte_keys ^ key x 4 among the
   // first n_byte_keys bytes (the lowest flag of the zero-byte test is exact)
@@ -322,16 +330,21 @@ __device__ __forceinline__ uint32_t key_class(const ScanParams& p, const KeyClas
     if (kp >= 1) {
       if (excluded((uint32_t)(w >> (8 * kp - 8)) & 0xFFu, x0, x1)) return 0;
     } else if (!p.kx_deep || deep) {
+      if (more && !p.kx_deep) *more = true;   // (the byte before the key is not in w)
       return 0;
     }
   }
   if (info & 4u) return pos >= min_pos ? (kClassKept | kidx << 2) : 0u;
   // shift jj tests w bytes s0 + jj + t for the t <= tmax with mask byte t set
-  const int32_t s0 = kp + (int32_t)(int8_t)(info >> 8);
+  const int32_t g = (int32_t)(int8_t)(info >> 8), s0 = kp + g;
   const uint32_t span = (info >> 16) & 15u, tmax = (info >> 20) & 3u;
   // (the scan read nothing past byte_end: a range of a larger block has zeros there)
   const int64_t end = (int64_t)pos + (int8_t)(info >> 24);
-  if (s0 < 0 || s0 + (int32_t)(span + tmax) > 4 || end > (int64_t)p.byte_end) return 0;
+  if (end > (int64_t)p.byte_end) return 0;
+  if (s0 < 0 || s0 + (int32_t)(span + tmax) > last) {
+    if (more && 2 + g >= 0 && 2 + g + (int32_t)(span + tmax) <= 7) *more = true;
+    return 0;
+  }
   bool hit = false;
   for (uint32_t jj = 0; jj <= span; ++jj) hit |= ((uint32_t)(w >> (8 * ((uint32_t)s0 + jj))) & m) == v;
   return hit ? 0u : kClassDead;
@@ -1531,6 +1544,12 @@ __global__ __launch_bounds__(1024) void seg_offsets_kernel(const uint32_t* seg_c
 
 constexpr uint32_t kScatterWaves = 8;   // waves per segment in the scatter
 
+// The compaction reads the input bytes a certain candidate's class needs when
+// the scan's five kept bytes do not hold them (YAMD_CLASS_FETCH, key_class).
+#ifndef YAMD_CLASS_FETCH
+#define YAMD_CLASS_FETCH 0
+#endif
+
 // per-segment LDS buffer of live candidates (the diagnostic build holds one,
 // so that the GPU suite exercises the overflow path, tests/test_preverify.py)
 constexpr uint32_t kLiveBuf = YAMD_DIAG ? 1 : 2048;
@@ -1583,9 +1602,29 @@ __global__ __launch_bounds__(kScatterWaves * kWave) void seg_scatter_kernel(
     if (!classes) continue;
     // the certain candidates' classes from the bytes the scan kept beside them
     uint32_t cls = 0u;
-    if (valid && (ec & kCertainMask) != 0u)
+    if (valid && (ec & kCertainMask) != 0u) {
+      bool more = false;
       cls = key_class(p, kc, xc | (uint64_t)(ec >> kOutByteShift & 0xFFu) << 32,
-                      (int32_t)(ec >> kOutKeyShift & 7u) - 2, (ec & kOutDeep) != 0u, pos);
+                      (int32_t)(ec >> kOutKeyShift & 7u) - 2, (ec & kOutDeep) != 0u, pos, 4,
+                      YAMD_CLASS_FETCH ? &more : nullptr);
+      // Undecided only because the guard's bytes (or the byte before the key)
+      // lie outside the five the scan kept -- the key near its lane's end:
+      // read eight bytes around the key from the input (three aligned dwords
+      // inside [byte_begin - 4, byte_end), the bytes the scan itself may read)
+      // and decide again, rather than leave the candidate to the live list.
+      if (more) {
+        const uint64_t kb = pos - 1;   // the key's byte
+        const uint64_t a4 = (kb - 2) & ~3ull;
+        if (kb >= 2 && a4 + 4 >= p.byte_begin && a4 + 12 <= p.byte_end) {
+          const uint32_t* d = reinterpret_cast<const uint32_t*>(p.data + a4);
+          const uint32_t d0 = d[0], d1 = d[1], d2 = d[2];
+          const uint32_t sh = (uint32_t)(kb - 2 - a4);
+          const uint64_t w8 = __builtin_amdgcn_alignbyte(d1, d0, sh) |
+                              (uint64_t)__builtin_amdgcn_alignbyte(d2, d1, sh) << 32;
+          cls = key_class(p, kc, w8, 2, false, pos, 7);
+        }
+      }
+    }
     if (valid) p.dead[first + i] = (uint8_t)cls;
     // the undecided ones onto the live list (any order): the segment's LDS
     // buffer, copied out with ONE global atomic per segment (one per wave and
