@@ -645,10 +645,12 @@ __device__ __forceinline__ void certain_entry(const ScanParams& p, uint32_t ent,
 // the per-lane loop, whose trip count is the wave's largest per-lane hit
 // count), and the window / certain-candidate bytes are then computed for the
 // entries [from, pend_n) one lane each, while the ring entries are still
-// valid.  Measured 5 % SLOWER on rx, short and fuzz0 (one-process A/B,
-// profiles/r04_ab_inproc.json): off.
+// valid.  One-process A/B in both variant orders (profiles/r04_ab_inproc.json,
+// gpurun h7, h8): rx -1.5 %, short -2.5 to -3.3 %, fuzz0 / fuzz3 within 1 %.
+// (A first single-order call had it 5 % slower: a per-process placement
+// offset, DESIGN.md section 5 "Measurement method".)
 #ifndef YAMD_BK_RESOLVE
-#define YAMD_BK_RESOLVE 0
+#define YAMD_BK_RESOLVE 1
 #endif
 template <int MODE>
 constexpr bool kBkResolve = YAMD_BK_RESOLVE && kByteKeys<MODE>;
@@ -1545,9 +1547,11 @@ __global__ __launch_bounds__(1024) void seg_offsets_kernel(const uint32_t* seg_c
 constexpr uint32_t kScatterWaves = 8;   // waves per segment in the scatter
 
 // The compaction reads the input bytes a certain candidate's class needs when
-// the scan's five kept bytes do not hold them (YAMD_CLASS_FETCH, key_class).
+// the scan's five kept bytes do not hold them (YAMD_CLASS_FETCH, key_class):
+// fuzz0's pre-verification 0.63 -> 0.32 ms for 0.08 ms more compaction, rx
+// +0.02 ms, short / fuzz3 unchanged (profiles/r04_ab_inproc.json, gpurun h8).
 #ifndef YAMD_CLASS_FETCH
-#define YAMD_CLASS_FETCH 0
+#define YAMD_CLASS_FETCH 1
 #endif
 
 // per-segment LDS buffer of live candidates (the diagnostic build holds one,

@@ -107,6 +107,8 @@ struct VerifyParams {
   VerifyRec* out;             // records (pass 1)
   uint64_t out_cap;           // records that fit in out; pass 1 drops the rest (the
                               // host re-runs it when the total turns out larger)
+  uint64_t first;             // pass 0: the launch's first candidate (launch_verify
+                              // slices the stream: a dispatch holds < 2^32 work-items)
 };
 
 hipError_t launch_verify(const VerifyParams& p, int pass, hipStream_t s);

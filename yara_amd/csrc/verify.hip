@@ -994,7 +994,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(5))) void v
   const uint32_t codebuf = (uint32_t)(uintptr_t)(code + threadIdx.x * kCodeBytes);
   const uint64_t groups = (p.count + kGroup - 1) / kGroup;
   if (!PASS) {
-    const uint64_t c = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    const uint64_t c = p.first + (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
     uint32_t n = 0;
     if (c < p.count) verify_one<0>(p, c, lds, codebuf, 0, 0, 0, n);
     const uint32_t sum = wave_sum(n);
@@ -1142,7 +1142,19 @@ static uint32_t resident_blocks(const void* kernel) {
 hipError_t launch_verify(const VerifyParams& p, int pass, hipStream_t s) {
   if (p.count == 0) return hipSuccess;
   if (pass == 0) {
-    hipLaunchKernelGGL(verify_kernel<0>, dim3((uint32_t)((p.count + 255) / 256)), dim3(256), 0, s, p);
+    // one thread per candidate, in slices of 2^31: an AQL dispatch's grid size
+    // is a 32-bit count of work-items, so 2^32 candidates (the largest stream
+    // yr_amd_verify_device accepts) do not fit one launch.  (Slices are whole
+    // groups: kGroup divides 2^31.)
+    constexpr uint64_t kSlice = 1ull << 31;
+    static_assert(kSlice % kGroup == 0, "slices of whole groups");
+    VerifyParams q = p;
+    for (q.first = 0; q.first < p.count; q.first += kSlice) {
+      const uint64_t n = std::min<uint64_t>(p.count - q.first, kSlice);
+      hipLaunchKernelGGL(verify_kernel<0>, dim3((uint32_t)((n + 255) / 256)), dim3(256), 0, s, q);
+      const hipError_t e = hipGetLastError();
+      if (e != hipSuccess) return e;
+    }
   } else {
     const uint64_t waves = verify_groups(p.count);
     const uint32_t blocks = (uint32_t)std::min<uint64_t>(
