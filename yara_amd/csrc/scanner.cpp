@@ -96,9 +96,6 @@ struct yr_amd_tables {
   uint32_t kd_m[4] = {0, 0, 0, 0}, kd_v[4] = {0, 0, 0, 0}, kd_info[4] = {0, 0, 0, 0};
   uint32_t kd_x0[4] = {0, 0, 0, 0}, kd_x1[4] = {0, 0, 0, 0};
   uint32_t kd_n[4] = {0, 0, 0, 0}, kd_head[4] = {0, 0, 0, 0}, kd_min_pos[4] = {0, 0, 0, 0};
-  // the kept keys' lists, [4][kKeptMax][2] = pool index, backtrack (VerifyParams::kd_list)
-  uint32_t h_kd_list[4 * kKeptMax * 2] = {};
-  uint32_t* d_kd_list = nullptr;
   bool kd_any = false;
   uint32_t kx_end = 2, kx_deep = 0, kx_next = 0;   // ScanParams::kx_end / kx_deep / kx_next
   uint32_t* d_nodes = nullptr;        // accepting nodes by string (FlatTables::nodes)
@@ -333,8 +330,7 @@ int yr_amd_tables_create(const uint32_t* transition_table, const uint32_t* match
 int yr_amd_tables_destroy(yr_amd_tables* t) {
   if (t == nullptr) return YR_AMD_SUCCESS;
   for (void* p : {(void*)t->d_filter, (void*)t->d_exact, (void*)t->d_nodes, (void*)t->d_pool,
-                  (void*)t->d_str_bytes, (void*)t->d_lowercase, (void*)t->d_re_code,
-                  (void*)t->d_kd_list})
+                  (void*)t->d_str_bytes, (void*)t->d_lowercase, (void*)t->d_re_code})
     if (p) (void)hipFree(p);
   delete t;
   return YR_AMD_SUCCESS;
@@ -935,7 +931,6 @@ void key_classes(yr_amd_tables* t) {
   for (int k = 0; k < 4; ++k)
     t->kd_m[k] = t->kd_v[k] = t->kd_info[k] = t->kd_x0[k] = t->kd_x1[k] = t->kd_n[k] =
         t->kd_head[k] = t->kd_min_pos[k] = 0;
-  std::fill(std::begin(t->h_kd_list), std::end(t->h_kd_list), 0u);
   if (f.root_accepting || t->h_pool.empty() || diag_env("YAMD_NO_KEY_CLASSES") != nullptr) return;
   // Per key the class it can have, then the five bytes the scan keeps beside
   // its certain candidates (kernels.hip key_class): lane bytes key - kp ..
@@ -1027,11 +1022,6 @@ void key_classes(yr_amd_tables* t) {
       t->kd_n[k] = o.n;
       t->kd_head[k] = o.head;
       t->kd_min_pos[k] = o.min_pos;
-      uint32_t q = o.head;
-      for (uint32_t e = 0; e < o.n && q != 0; ++e, q = t->h_pool[q - 1].next) {
-        t->h_kd_list[(k * kKeptMax + e) * 2] = q - 1;
-        t->h_kd_list[(k * kKeptMax + e) * 2 + 1] = t->h_pool[q - 1].backtrack;
-      }
     } else {
       t->kd_m[k] = o.m;
       t->kd_v[k] = o.v;
@@ -1043,16 +1033,6 @@ void key_classes(yr_amd_tables* t) {
     t->kd_x0[k] = o.xs0;
     t->kd_x1[k] = o.xs1;
     t->kd_any = true;
-  }
-  // the kept lists for the write pass (without them -- an allocation or copy
-  // failure -- it walks the pool as for any other candidate)
-  if (t->d_kd_list == nullptr &&
-      hipMalloc((void**)&t->d_kd_list, sizeof(t->h_kd_list)) != hipSuccess)
-    t->d_kd_list = nullptr;
-  if (t->d_kd_list != nullptr &&
-      hipMemcpy(t->d_kd_list, t->h_kd_list, sizeof(t->h_kd_list), hipMemcpyHostToDevice) != hipSuccess) {
-    (void)hipFree(t->d_kd_list);
-    t->d_kd_list = nullptr;
   }
 }
 }  // namespace
@@ -1171,7 +1151,6 @@ int yr_amd_verify_device(yr_amd_scanner* s, uint64_t data_base, const yr_amd_ver
     const bool classes = !t->profile && s->last_count <= 0xFFFFFFFFull;
     v.dead = classes ? L.dead : nullptr;
     v.live = classes ? L.live : nullptr;
-    v.kd_list = classes ? t->d_kd_list : nullptr;
     for (int k = 0; k < 4; ++k) {
       v.kd_n[k] = L.kd_n[k];
       v.kd_head[k] = L.kd_head[k];

@@ -82,8 +82,6 @@ struct VerifyParams {
                               // list can have an effect (ScanParams::dead), and
   const uint32_t* live;       // [0] = count, then the other candidates' indices
   uint32_t kd_n[4], kd_head[4];   // the "kept" keys' list lengths and heads (ScanParams)
-  const uint32_t* kd_list;    // [4][kKeptMax][2]: a kept key's list, in pool order: pool
-                              // index, backtrack (null: walk the pool)
   uint64_t count;             // candidates (size + 1 when all)
   int all;                    // every position of a range is a candidate:
   uint64_t all_first;         //   i = all_first + c
@@ -125,7 +123,6 @@ struct KeptLists {
 hipError_t launch_block_offsets(uint64_t* block_off, uint64_t* chunk_off, uint64_t count,
                                 uint64_t* total, const uint8_t* cls, const KeptLists& kept,
                                 hipStream_t s);
-constexpr uint32_t kKeptMax = 32;         // entries per kept key's list (at most 30)
 constexpr uint64_t kGroup = 64;           // candidates per group (one wave)
 constexpr uint64_t kChunkGroups = 1024;   // groups per chunk of the offsets scan
 uint64_t verify_groups(uint64_t count);

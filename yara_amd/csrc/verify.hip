@@ -943,16 +943,14 @@ __device__ __forceinline__ uint32_t wave_sum(uint32_t v) {
   for (int d = 32; d >= 1; d >>= 1) v += __shfl_xor(v, d, 64);
   return v;
 }
-// Exclusive prefix sum over the 64 lanes with DPP moves (no LDS traffic):
-// Hillis-Steele inside each 16-lane row, then row_bcast:15 / row_bcast:31.
 __device__ __forceinline__ uint32_t wave_exclusive(uint32_t v) {
+  const uint32_t lane = threadIdx.x & 63u;
   uint32_t inc = v;
-  inc += __builtin_amdgcn_update_dpp(0u, inc, 0x111, 0xF, 0xF, true);   // row_shr:1
-  inc += __builtin_amdgcn_update_dpp(0u, inc, 0x112, 0xF, 0xF, true);   // row_shr:2
-  inc += __builtin_amdgcn_update_dpp(0u, inc, 0x114, 0xF, 0xF, true);   // row_shr:4
-  inc += __builtin_amdgcn_update_dpp(0u, inc, 0x118, 0xF, 0xF, true);   // row_shr:8
-  inc += __builtin_amdgcn_update_dpp(0u, inc, 0x142, 0xA, 0xF, false);  // row_bcast:15
-  inc += __builtin_amdgcn_update_dpp(0u, inc, 0x143, 0xC, 0xF, false);  // row_bcast:31
+#pragma unroll
+  for (int d = 1; d < 64; d <<= 1) {
+    const uint32_t u = __shfl_up(inc, d, 64);
+    if (lane >= (uint32_t)d) inc += u;
+  }
   return inc - v;
 }
 __device__ __forceinline__ uint32_t wave_in_block() {
@@ -964,19 +962,14 @@ __device__ __forceinline__ void verify_group(const VerifyParams& p, uint64_t g, 
                                              uint32_t lds, uint32_t codebuf) {
   const uint64_t c = g * kGroup + (threadIdx.x & 63u);
   // the scan's class (kernels.hip key_class): dead -- nothing; kept -- every
-  // call of the key's list; else pass 0's decisions.  (The class byte and the
-  // position are loaded together: a kept candidate's records need nothing
-  // else but its key's list, a few cached words.)
-  const bool in = c < p.count;
-  const uint32_t cls = in && p.dead != nullptr ? p.dead[c] : 0u;
-  const uint64_t i = in && p.kd_list != nullptr && !p.all ? p.positions[c] : 0u;
+  // call of the key's list; else pass 0's decisions
+  const uint32_t cls = c < p.count && p.dead != nullptr ? p.dead[c] : 0u;
   uint32_t keep = 0, n = 0, head = 0;
-  const uint32_t key = (cls >> 2) & 3u;
   if (cls & kClassKept) {
-    n = p.kd_n[key];
+    n = p.kd_n[(cls >> 2) & 3u];
     keep = (1u << n) - 1u;
-    head = p.kd_head[key];
-  } else if (in && !(cls & kClassDead)) {
+    head = p.kd_head[(cls >> 2) & 3u];
+  } else if (c < p.count && !(cls & kClassDead)) {
     keep = p.keep[c];
     if (keep != 0) {
       n = p.counts[c];
@@ -984,19 +977,7 @@ __device__ __forceinline__ void verify_group(const VerifyParams& p, uint64_t g, 
     }
   }
   const uint32_t pre = wave_exclusive(n);
-  if ((cls & kClassKept) && p.kd_list != nullptr) {
-    // the key's list without walking the pool (scanner.cpp key_classes)
-    const uint32_t* L = p.kd_list + 2 * kKeptMax * key;
-    for (uint32_t t = 0; t < n; ++t) {
-      VerifyRec r;
-      r.offset = i - L[2 * t + 1];
-      r.pool_index = L[2 * t];
-      r.candidate = (uint32_t)c;
-      if (o + pre + t < p.out_cap) p.out[o + pre + t] = r;
-    }
-  } else if (keep != 0) {
-    verify_one<1>(p, c, lds, codebuf, keep, head, o + pre, n);
-  }
+  if (keep != 0) verify_one<1>(p, c, lds, codebuf, keep, head, o + pre, n);
 }
 
 // PASS 0: one candidate per lane; each wave's record count goes to its group.
