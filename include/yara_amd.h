@@ -133,10 +133,6 @@ typedef struct
    * windows ending at even positions only, each key's prefix and suffix),
    * 2 = the same with a hashed block index. */
   uint32_t filter_mode;
-  /* 1: tables with 1-byte keys whose filter / 2-byte-key passes are rare next
-   * to the 1-byte-key candidates; the scan's drains re-test those only when
-   * such a pass was queued (a kernel choice, no effect on the results). */
-  uint32_t rare_filter_passes;
 } yr_amd_tables_info;
 
 int yr_amd_tables_get_info(const yr_amd_tables* tables, yr_amd_tables_info* info);

@@ -73,7 +73,7 @@ def main():
                         "frac": round(n / (k * 1e-3) / 1e9 / HBM_PEAK_GBS, 4),
                         "candidates": int(cnt)})
         rec.update({"root_accepting": bool(info["root_accepting"]),
-               "keys_by_length": info["keys_by_length"], "rare_filter_passes": info.get("rare_filter_passes"),
+               "keys_by_length": info["keys_by_length"],
                "filter_fill": round(info["filter_set_bits"] / float(1 << info["filter_bits"]), 4)})
         if not a.no_verify:
             sc.scan_device(buf.data_ptr(), n)

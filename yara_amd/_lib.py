@@ -49,7 +49,6 @@ class TablesInfo(ctypes.Structure):
         ("verify_halo_before", ctypes.c_uint64),
         ("verify_halo_after", ctypes.c_uint64),
         ("filter_mode", ctypes.c_uint32),
-        ("rare_filter_passes", ctypes.c_uint32),
     ]
 
 

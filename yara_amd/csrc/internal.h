@@ -240,9 +240,6 @@ struct ScanParams {
   uint32_t filter_mode;     // kFilterPair / kFilterEven / kFilterEvenHash (FlatTables)
   uint32_t pair_keys[2];    // even filters: FlatTables::pair_keys / n_pair_keys (16-bit
   uint32_t n_pair_keys;     // test of the 2-byte keys ending at odd positions)
-  uint32_t fp_skip;         // byte-key kernels: a drain re-tests the filter and the 2-byte
-                            // keys only if an entry appended since the last drain passed
-                            // them in stage 1 (FlatTables::fp_skip: rare filter passes)
   uint32_t* seg_next;       // null: wave w takes segments w, w + waves, ...; else each wave
                             // takes its first segment by index and the next ones from this
                             // counter (initialised to the launch's wave count)

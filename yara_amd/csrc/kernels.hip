@@ -194,8 +194,6 @@ struct WaveQueue {
   uint32_t pend;    // LDS address: kWave pairs {w4, segment offset}
   uint32_t pend_n;  // wave-uniform
   bool defer;       // wave-uniform: the per-lane hits below await their words
-  bool fp;          // wave-uniform (ScanParams::fp_skip): an entry in the ring passed
-                    // the filter or a 2-byte key in stage 1
   // per lane, the first (a) and second (b) deferred hit: window, segment
   // offset (kNoHit = none), byte offset into the first level (exact[kExactFl..]) that the next tile step
   // loads (0 = none), the loaded word
@@ -727,9 +725,6 @@ __device__ __forceinline__ void drain(const ScanParams& p, WaveQueue& q, uint32_
     if (q.defer) drain_complete<MODE>(p, q, lane, seg_start, out, found);
   const uint32_t n = q.count;   // <= kQueueCap = kWave
   q.count = 0;
-  // (fp_skip: no entry passed the filter or a 2-byte key -- only 1-byte keys to find)
-  const bool full = !kByteKeys<MODE> || !p.fp_skip || q.fp;
-  q.fp = false;
   if constexpr (MODE == 7 || MODE == 8 || kAbl<MODE> == 2) return;   // ablations: entries dropped
   __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
   uint32_t maybe = 0, off0 = 0, m = 0;   // m: bit j = lane byte j passes the filter
@@ -750,12 +745,10 @@ __device__ __forceinline__ void drain(const ScanParams& p, WaveQueue& q, uint32_
     off0 = (kIdxHigh<MODE> ? e45.y >> 16 : e45.y & 0xFFFFu) * kBytesPerLane;
     if constexpr (kByteKeys<MODE>) ridx = e45.y;
     if constexpr (kEven<MODE>) {
-      if (full) {
-        m = even_mask<kEvenHash<MODE>>(S);
-        if (p.n_pair_keys != 0) m |= pair_keys_mask(S, p);
-      }
+      m = even_mask<kEvenHash<MODE>>(S);
+      if (p.n_pair_keys != 0) m |= pair_keys_mask(S, p);
     } else {
-      if (full) m = dense_mask(stage1<0, false>(S, lane));
+      m = dense_mask(stage1<0, false>(S, lane));
     }
     if constexpr (kByteKeys<MODE>) {
       kmask = byte_keys_mask(S, p);
@@ -1114,7 +1107,7 @@ __device__ __forceinline__ void write_entry(uint32_t ent, const uint32_t (&S)[6]
 template <int MODE, bool TAIL>
 __device__ __forceinline__ void ring_append(const ScanParams& p, WaveQueue& q, SegState& st,
                                             const uint32_t (&S)[6], uint32_t any,
-                                            uint32_t tile_off, uint32_t lane, bool tile_fp = true) {
+                                            uint32_t tile_off, uint32_t lane) {
   if constexpr (MODE >= 2 && MODE <= 6) return;
   const uint32_t lane_off = tile_off + lane * kBytesPerLane;
   if constexpr (TAIL) {
@@ -1132,7 +1125,6 @@ __device__ __forceinline__ void ring_append(const ScanParams& p, WaveQueue& q, S
       __builtin_amdgcn_s_setprio(1);
 #endif
     }
-    if constexpr (kByteKeys<MODE>) q.fp = q.fp || tile_fp;
     if (any != 0) {
       // slot = count (scalar, folded into the base) + the appending lanes below
       const uint32_t below = __builtin_amdgcn_mbcnt_hi(
@@ -1212,9 +1204,7 @@ __device__ __forceinline__ void tile_step(const ScanParams& p, WaveQueue& q, Seg
   uint32_t any = stage1<kStage1Mode<MODE>, true>(S, lane);
   if constexpr (kEven<MODE>)
     if (p.n_pair_keys != 0) any |= pair_keys_any(S, p);
-  bool tile_fp = true;   // (some lane passed the filter or a 2-byte key)
   if constexpr (kByteKeys<MODE>) {
-    if (p.fp_skip) tile_fp = __ballot(any != 0u) != 0u;
     if constexpr (kAbl<MODE> == 3) asm volatile("" ::"v"(byte_keys_any(S, p)));   // ablation
     else if constexpr (kAbl<MODE> != 4) any |= byte_keys_any(S, p);
   }
@@ -1232,7 +1222,7 @@ __device__ __forceinline__ void tile_step(const ScanParams& p, WaveQueue& q, Seg
   if constexpr (kAbl<MODE> == 1) {   // ablation: stage 1 only
     asm volatile("" ::"v"(any));
   } else {
-    ring_append<MODE, TAIL>(p, q, st, S, any, tile_off, lane, tile_fp);
+    ring_append<MODE, TAIL>(p, q, st, S, any, tile_off, lane);
   }
   issue_first_level<MODE>(p, q);
 }
@@ -1327,7 +1317,6 @@ __device__ __forceinline__ void wide_step(const ScanParams& p, WaveQueue& q, Seg
       }
       if (wr && lane < kWave / 2) wide_entries<MODE>(q, below, any0, any1, S0, S1, unit);
       q.count += n_lo;
-      q.fp = true;
       take = n - n_lo;
       below -= n_lo;
       wr = wr && lane >= kWave / 2;
@@ -1347,7 +1336,6 @@ __device__ __forceinline__ void wide_step(const ScanParams& p, WaveQueue& q, Seg
     }
     if (wr) wide_entries<MODE>(q, below, any0, any1, S0, S1, unit);
     q.count += take;
-    q.fp = true;   // (no separate filter-pass ballot here: drains re-test everything)
   }
   issue_first_level<MODE>(p, q);
 }
@@ -1392,7 +1380,6 @@ __device__ __forceinline__ void scan_segment(const ScanParams& p, WaveQueue& q, 
   q.count = 0;
   q.pend_n = 0;
   q.defer = false;
-  q.fp = false;
   q.ia = q.ib = 0u;
   q.da = q.db = 0u;
   q.wa = q.wb = 0u;

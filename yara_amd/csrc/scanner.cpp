@@ -360,7 +360,6 @@ int yr_amd_tables_get_info(const yr_amd_tables* t, yr_amd_tables_info* info) {
   info->filter_bits = kFilterLog2Bits;
   info->filter_set_bits = f.filter_set_bits;
   info->filter_mode = f.filter_mode;
-  info->rare_filter_passes = f.fp_skip;
   info->exact_slots = 4 * (f.t3_mask + 1 + f.t4_mask + 1);
   uint32_t mb = 0;
   for (uint16_t b : f.pool_backtrack) mb = std::max<uint32_t>(mb, b);
@@ -572,7 +571,6 @@ int yr_amd_scan_window(yr_amd_scanner* s, const uint8_t* d_window, uint64_t wind
   p.pair_keys[0] = t->flat.pair_keys[0];
   p.pair_keys[1] = t->flat.pair_keys[1];
   p.n_pair_keys = t->flat.n_pair_keys;
-  p.fp_skip = t->flat.fp_skip;
   p.kx_end = t->kx_end;
   p.kx_deep = t->kx_deep;
   p.kx_next = t->kx_next;

@@ -389,21 +389,6 @@ int flatten_tables(const uint32_t* T, const uint32_t* M, uint32_t n_slots,
     }
     if (pick >= 0) {
       out.filter_mode = pick ? kFilterEvenHash : kFilterEven;
-      // Rare filter / 2-byte-key passes against the certain candidates: the
-      // drains skip that part of their re-test unless an entry appended since
-      // the last drain passed it (kernels.hip fp_skip; ~60-90 VALU per drain
-      // saved, one ballot per tile spent).  On when the expected passing
-      // entries per drain of 64 are below 0.3.
-      if (out.n_byte_keys != 0 && diag_env("YAMD_NO_FP_SKIP") == nullptr) {
-        const double K = out.n_byte_keys;
-        const double cert = 1.0 - std::pow(1.0 - K / 256.0, (double)kBytesPerLane);
-        const double pw = (double)pass[pick] / 16777216.0;
-        const double pp = pair_test ? (kBytesPerLane / 2) * out.keys_by_len[2] / 65536.0 : 0.0;
-        const double fp = 1.0 - std::pow(1.0 - pw, kBytesPerLane / 2) * (1.0 - pp);
-        const double entry = 1.0 - (1.0 - cert) * (1.0 - fp);
-        out.fp_skip = kWave * fp / entry < 0.3 ? 1u : 0u;
-        if (diag_env("YAMD_FP_SKIP") != nullptr) out.fp_skip = 1u;
-      }
       out.filter = std::move(f[pick]);
       if (pair_test)
         for (const Key& k : out.keys)

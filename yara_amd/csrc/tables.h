@@ -46,10 +46,6 @@ struct FlatTables {
   // they end at an odd position, instead of as the filter's (*, *, p) windows
   // (which would pass every byte p)
   uint32_t pair_keys[2] = {0, 0}, n_pair_keys = 0;
-  // byte-key tables whose filter / 2-byte-key passes are rare next to the
-  // certain candidates: drains skip that re-test unless a stage-1 pass was
-  // appended since the last one (ScanParams::fp_skip)
-  uint32_t fp_skip = 0;
   // bit b set: some trie node of depth >= 2 ends with byte b (so a position
   // whose last byte is the 1-byte key b may have a deeper state than b's node)
   uint32_t deep_last[8] = {0, 0, 0, 0, 0, 0, 0, 0};
