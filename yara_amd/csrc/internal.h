@@ -32,10 +32,7 @@ constexpr int kWave = 64;
 constexpr int kBytesPerLane = 16;
 constexpr int kTile = kWave * kBytesPerLane;        // 1024 B
 constexpr uint32_t kSegment = 1u << 20;   // max segment: 1 MiB (ring entries hold offset/16 in 16 bits)
-#ifndef YAMD_SEG_TARGET_KIB
-#define YAMD_SEG_TARGET_KIB 1024
-#endif
-constexpr uint32_t kSegmentTarget = YAMD_SEG_TARGET_KIB * 1024u;   // preferred segment size (scanner.cpp)
+constexpr uint32_t kSegmentTarget = kSegment;   // preferred segment size (scanner.cpp)
 constexpr uint32_t kMaxByteKeys = 4;   // 1-byte keys tested in stage 1 (more: filter)
 constexpr uint32_t kMaxPairKeys = 4;   // even filters: 2-byte keys tested as aligned half-words
 constexpr int kWavesPerWG = 16;

@@ -1544,7 +1544,7 @@ __global__ __launch_bounds__(1024) void seg_offsets_kernel(const uint32_t* seg_c
   }
 }
 
-constexpr uint32_t kScatterWaves = 8;   // waves per (1 MiB) segment in the scatter, at most
+constexpr uint32_t kScatterWaves = 8;   // waves per segment in the scatter
 
 // The compaction reads the input bytes a certain candidate's class needs when
 // the scan's five kept bytes do not hold them (YAMD_CLASS_FETCH, key_class):
@@ -1558,11 +1558,10 @@ constexpr uint32_t kScatterWaves = 8;   // waves per (1 MiB) segment in the scat
 // so that the GPU suite exercises the overflow path, tests/test_preverify.py)
 constexpr uint32_t kLiveBuf = YAMD_DIAG ? 1 : 2048;
 
-template <uint32_t W>
-__global__ __launch_bounds__(W * kWave) void seg_scatter_kernel(
+__global__ __launch_bounds__(kScatterWaves * kWave) void seg_scatter_kernel(
     ScanParams p, const uint64_t* seg_offset, uint64_t* positions) {
-  // one block of W waves per segment (segments hold up to ~10^4 candidates),
-  // its waves interleaved 64 candidates apart
+  // one block per segment (segments hold up to ~10^4 candidates), its waves
+  // interleaved 64 candidates apart
   __shared__ KeyClassRec kc[kMaxByteKeys];
   __shared__ uint32_t lbuf[kLiveBuf];
   __shared__ uint32_t lcount, lglobal;
@@ -1582,7 +1581,7 @@ __global__ __launch_bounds__(W * kWave) void seg_scatter_kernel(
   const uint64_t first = seg_offset[seg];
   uint64_t* dst = positions + first;
   const uint32_t lane = threadIdx.x % kWave, w = threadIdx.x / kWave;
-  constexpr uint32_t kStride = W * kWave;
+  constexpr uint32_t kStride = kScatterWaves * kWave;
   // Latency-bound (a few hundred candidates per wave): every iteration's
   // entry and kept bytes are loaded one iteration ahead.
   uint32_t e = 0, x = 0;
@@ -1772,18 +1771,8 @@ hipError_t launch_compact(const ScanParams& p, uint64_t* seg_offset, uint64_t* s
     hipLaunchKernelGGL(seg_offsets_kernel, dim3(1), dim3(1024), 0, s, p.seg_count, p.n_segments,
                        p.seg_cap, seg_offset, summary);
   } else {
-    // one wave per 128 KiB of segment, at most kScatterWaves: the same waves in
-    // flight for any segment size (a 4 GiB block: 32,768 waves)
-    const uint32_t per = p.seg_bytes / (128u << 10);
-    const uint64_t* so = seg_offset;
-    if (per >= 8)
-      hipLaunchKernelGGL(seg_scatter_kernel<8>, dim3(p.n_segments), dim3(8 * kWave), 0, s, p, so, positions);
-    else if (per >= 4)
-      hipLaunchKernelGGL(seg_scatter_kernel<4>, dim3(p.n_segments), dim3(4 * kWave), 0, s, p, so, positions);
-    else if (per >= 2)
-      hipLaunchKernelGGL(seg_scatter_kernel<2>, dim3(p.n_segments), dim3(2 * kWave), 0, s, p, so, positions);
-    else
-      hipLaunchKernelGGL(seg_scatter_kernel<1>, dim3(p.n_segments), dim3(kWave), 0, s, p, so, positions);
+    hipLaunchKernelGGL(seg_scatter_kernel, dim3(p.n_segments), dim3(kScatterWaves * kWave), 0, s, p,
+                       (const uint64_t*)seg_offset, positions);
   }
   return hipGetLastError();
 }
