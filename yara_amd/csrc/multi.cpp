@@ -212,27 +212,32 @@ int stage_block(yr_amd_multi* m, const uint8_t* data, uint64_t size) {
     const uint32_t b = piece & 1u;
     const uint64_t p1 = std::min(hi, p0 + yr_amd_multi::kStage);
     // the DMAs that last read this buffer must be done before it is refilled
-    for (size_t k = 0; k < m->lanes.size(); ++k)
-      if (piece >= 2 && hipEventSynchronize(m->staged[b][k]) != hipSuccess)
-        return YR_AMD_INTERNAL_FATAL_ERROR;
+    for (size_t k = 0; k < m->lanes.size() && rc == YR_AMD_SUCCESS; ++k)
+      if (piece >= 2 && hipEventSynchronize(m->staged[b][k]) != hipSuccess) rc = YR_AMD_INTERNAL_FATAL_ERROR;
+    if (rc != YR_AMD_SUCCESS) break;
     if (!m->pool->copy(m->stage[b], data + p0, p1 - p0, m->copy)) {
       rc = YR_AMD_COULD_NOT_MAP_FILE;
       break;
     }
-    for (size_t k = 0; k < m->lanes.size(); ++k) {
+    for (size_t k = 0; k < m->lanes.size() && rc == YR_AMD_SUCCESS; ++k) {
       Lane& L = m->lanes[k];
       const uint64_t a = std::max(p0, L.lo), e = std::min(p1, L.hi);
-      if (hipSetDevice(L.device) != hipSuccess) return YR_AMD_INTERNAL_FATAL_ERROR;
-      if (L.active && a < e &&
-          hipMemcpyAsync(L.d_win + (a - L.lo), m->stage[b] + (a - p0), e - a, hipMemcpyHostToDevice,
-                         L.stream) != hipSuccess)
-        return YR_AMD_INTERNAL_FATAL_ERROR;
-      if (hipEventRecord(m->staged[b][k], L.stream) != hipSuccess) return YR_AMD_INTERNAL_FATAL_ERROR;
+      if (hipSetDevice(L.device) != hipSuccess ||
+          (L.active && a < e &&
+           hipMemcpyAsync(L.d_win + (a - L.lo), m->stage[b] + (a - p0), e - a, hipMemcpyHostToDevice,
+                          L.stream) != hipSuccess) ||
+          hipEventRecord(m->staged[b][k], L.stream) != hipSuccess)
+        rc = YR_AMD_INTERNAL_FATAL_ERROR;
     }
   }
-  // (the scans are queued behind the DMAs on the same streams)
-  for (int b = 0; b < 2 && rc != YR_AMD_SUCCESS; ++b)
-    for (size_t k = 0; k < m->lanes.size(); ++k) (void)hipEventSynchronize(m->staged[b][k]);
+  // (the scans are queued behind the DMAs on the same streams.)  On failure no
+  // DMA may still read a staging buffer when the call returns: the next call
+  // refills both without waiting
+  if (rc != YR_AMD_SUCCESS)
+    for (size_t k = 0; k < m->lanes.size(); ++k) {
+      (void)hipSetDevice(m->lanes[k].device);
+      (void)hipStreamSynchronize(m->lanes[k].stream);
+    }
   return rc;
 }
 

@@ -102,7 +102,11 @@ int run_lane_dma(Slot& s, Lane& L) {
   if (L.hi > L.lo && hipMemcpyAsync(L.d_win, s.h_pinned + L.lo, L.hi - L.lo, hipMemcpyHostToDevice,
                                     L.stream) != hipSuccess)
     return YR_AMD_INTERNAL_FATAL_ERROR;
-  return yamd::lane_scan(L, s.size, s.base);
+  r = yamd::lane_scan(L, s.size, s.base);
+  // (a failed scan may have left the DMA queued: the slot's pinned copy is
+  // refilled by a later submission, so nothing may still read it)
+  if (r != YR_AMD_SUCCESS) (void)hipStreamSynchronize(L.stream);
+  return r;
 }
 
 void lane_main(yr_amd_pipeline* p, uint32_t idx, uint32_t k) {
