@@ -1544,7 +1544,10 @@ __global__ __launch_bounds__(1024) void seg_offsets_kernel(const uint32_t* seg_c
   }
 }
 
-constexpr uint32_t kScatterWaves = 8;   // waves per segment in the scatter
+constexpr uint32_t kScatterWaves = 8;   // waves per segment in the scatter (dense segments)
+#ifndef YAMD_SCATTER_ADAPT
+#define YAMD_SCATTER_ADAPT 1
+#endif
 
 // The compaction reads the input bytes a certain candidate's class needs when
 // the scan's five kept bytes do not hold them (YAMD_CLASS_FETCH, key_class):
@@ -1558,10 +1561,11 @@ constexpr uint32_t kScatterWaves = 8;   // waves per segment in the scatter
 // so that the GPU suite exercises the overflow path, tests/test_preverify.py)
 constexpr uint32_t kLiveBuf = YAMD_DIAG ? 1 : 2048;
 
-__global__ __launch_bounds__(kScatterWaves * kWave) void seg_scatter_kernel(
+template <uint32_t W>
+__global__ __launch_bounds__(W * kWave) void seg_scatter_kernel(
     ScanParams p, const uint64_t* seg_offset, uint64_t* positions) {
-  // one block per segment (segments hold up to ~10^4 candidates), its waves
-  // interleaved 64 candidates apart
+  // one block of W waves per segment (segments hold up to ~10^4 candidates),
+  // its waves interleaved 64 candidates apart
   __shared__ KeyClassRec kc[kMaxByteKeys];
   __shared__ uint32_t lbuf[kLiveBuf];
   __shared__ uint32_t lcount, lglobal;
@@ -1581,7 +1585,7 @@ __global__ __launch_bounds__(kScatterWaves * kWave) void seg_scatter_kernel(
   const uint64_t first = seg_offset[seg];
   uint64_t* dst = positions + first;
   const uint32_t lane = threadIdx.x % kWave, w = threadIdx.x / kWave;
-  constexpr uint32_t kStride = kScatterWaves * kWave;
+  constexpr uint32_t kStride = W * kWave;
   // Latency-bound (a few hundred candidates per wave): every iteration's
   // entry and kept bytes are loaded one iteration ahead.
   uint32_t e = 0, x = 0;
@@ -1771,8 +1775,15 @@ hipError_t launch_compact(const ScanParams& p, uint64_t* seg_offset, uint64_t* s
     hipLaunchKernelGGL(seg_offsets_kernel, dim3(1), dim3(1024), 0, s, p.seg_count, p.n_segments,
                        p.seg_cap, seg_offset, summary);
   } else {
-    hipLaunchKernelGGL(seg_scatter_kernel, dim3(p.n_segments), dim3(kScatterWaves * kWave), 0, s, p,
-                       (const uint64_t*)seg_offset, positions);
+    // sparse segments (the default capacity, no rerun at exact offsets: at
+    // most one candidate per 256 bytes) take two waves each, dense ones
+    // kScatterWaves (a 4 GiB block: 8,192 instead of 32,768 waves)
+    if (YAMD_SCATTER_ADAPT && p.seg_base == nullptr && p.seg_cap <= p.seg_bytes / 256)
+      hipLaunchKernelGGL(seg_scatter_kernel<2>, dim3(p.n_segments), dim3(2 * kWave), 0, s, p,
+                         (const uint64_t*)seg_offset, positions);
+    else
+      hipLaunchKernelGGL(seg_scatter_kernel<kScatterWaves>, dim3(p.n_segments), dim3(kScatterWaves * kWave),
+                         0, s, p, (const uint64_t*)seg_offset, positions);
   }
   return hipGetLastError();
 }
