@@ -28,6 +28,8 @@
 // buffer loads), tile t+1 in flight while tile t is filtered.  Roofline: HBM
 // read bandwidth (1 algorithmic byte per input byte); in practice the kernel
 // is VALU-issue bound.
+#include <hip/hip_ext.h>
+
 #include "internal.h"
 
 namespace yamd {
@@ -1710,24 +1712,35 @@ __global__ __launch_bounds__(256) void xorshift_fill_kernel(uint8_t* buf, uint64
 // Launch wrappers (host side, called from scanner.cpp).
 namespace yamd {
 
-hipError_t launch_scan(const ScanParams& p, int grid, hipStream_t s, int mode) {
+// t0 / t1 (timing): events stamped with the kernel's own start and end
+// (hipExtLaunchKernel), so the measured duration is the kernel's -- not the
+// gaps of separate markers around it on the stream.
+#define YAMD_LAUNCH_SCAN(K)                                                                      \
+  do {                                                                                           \
+    if (t0 != nullptr || t1 != nullptr)                                                          \
+      hipExtLaunchKernelGGL(K, dim3(grid), dim3(kWGThreads), (uint32_t)lds, s, t0, t1, 0u, p);   \
+    else                                                                                         \
+      hipLaunchKernelGGL(K, dim3(grid), dim3(kWGThreads), lds, s, p);                            \
+  } while (0)
+hipError_t launch_scan(const ScanParams& p, int grid, hipStream_t s, int mode, hipEvent_t t0,
+                       hipEvent_t t1) {
   const size_t lds = kScanLdsBytes;
   switch (YAMD_DIAG ? mode : 0) {
 #if YAMD_DIAG   // profiling ablations (tools/ablate.py): diagnostic builds only
-    case 1: hipLaunchKernelGGL(scan_segments_kernel<1>, dim3(grid), dim3(kWGThreads), lds, s, p); break;
-    case 2: hipLaunchKernelGGL(scan_segments_kernel<2>, dim3(grid), dim3(kWGThreads), lds, s, p); break;
-    case 3: hipLaunchKernelGGL(scan_segments_kernel<3>, dim3(grid), dim3(kWGThreads), lds, s, p); break;
-    case 4: hipLaunchKernelGGL(scan_segments_kernel<4>, dim3(grid), dim3(kWGThreads), lds, s, p); break;
-    case 5: hipLaunchKernelGGL(scan_segments_kernel<5>, dim3(grid), dim3(kWGThreads), lds, s, p); break;
-    case 6: hipLaunchKernelGGL(scan_segments_kernel<6>, dim3(grid), dim3(kWGThreads), lds, s, p); break;
-    case 7: hipLaunchKernelGGL(scan_segments_kernel<7>, dim3(grid), dim3(kWGThreads), lds, s, p); break;
-    case 8: hipLaunchKernelGGL(scan_segments_kernel<8>, dim3(grid), dim3(kWGThreads), lds, s, p); break;
-    case 9: hipLaunchKernelGGL(scan_segments_kernel<9>, dim3(grid), dim3(kWGThreads), lds, s, p); break;
-    case 10: hipLaunchKernelGGL(scan_segments_kernel<10>, dim3(grid), dim3(kWGThreads), lds, s, p); break;
-    case 11: hipLaunchKernelGGL(scan_segments_kernel<11>, dim3(grid), dim3(kWGThreads), lds, s, p); break;
-    case 12: hipLaunchKernelGGL(scan_segments_kernel<12>, dim3(grid), dim3(kWGThreads), lds, s, p); break;
-    case 24: hipLaunchKernelGGL(scan_segments_kernel<24>, dim3(grid), dim3(kWGThreads), lds, s, p); break;
-    case 25: hipLaunchKernelGGL(scan_segments_kernel<25>, dim3(grid), dim3(kWGThreads), lds, s, p); break;
+    case 1: YAMD_LAUNCH_SCAN(scan_segments_kernel<1>); break;
+    case 2: YAMD_LAUNCH_SCAN(scan_segments_kernel<2>); break;
+    case 3: YAMD_LAUNCH_SCAN(scan_segments_kernel<3>); break;
+    case 4: YAMD_LAUNCH_SCAN(scan_segments_kernel<4>); break;
+    case 5: YAMD_LAUNCH_SCAN(scan_segments_kernel<5>); break;
+    case 6: YAMD_LAUNCH_SCAN(scan_segments_kernel<6>); break;
+    case 7: YAMD_LAUNCH_SCAN(scan_segments_kernel<7>); break;
+    case 8: YAMD_LAUNCH_SCAN(scan_segments_kernel<8>); break;
+    case 9: YAMD_LAUNCH_SCAN(scan_segments_kernel<9>); break;
+    case 10: YAMD_LAUNCH_SCAN(scan_segments_kernel<10>); break;
+    case 11: YAMD_LAUNCH_SCAN(scan_segments_kernel<11>); break;
+    case 12: YAMD_LAUNCH_SCAN(scan_segments_kernel<12>); break;
+    case 24: YAMD_LAUNCH_SCAN(scan_segments_kernel<24>); break;
+    case 25: YAMD_LAUNCH_SCAN(scan_segments_kernel<25>); break;
     case 101: case 102: case 103: case 104: {
       // the ablations of the byte-key variant the product would run (even
       // filters plain only; others: the pair filter)
@@ -1736,7 +1749,7 @@ hipError_t launch_scan(const ScanParams& p, int grid, hipStream_t s, int mode) {
                                                     : (p.kx_next ? kModeByteKeysNext : kModeByteKeys);
 #define YAMD_ABL(A, V)                                                                             \
   if (mode == 100 + A && base == V)                                                                \
-    hipLaunchKernelGGL(scan_segments_kernel<100 * A + V>, dim3(grid), dim3(kWGThreads), lds, s, p);
+    YAMD_LAUNCH_SCAN(scan_segments_kernel<100 * A + V>);
 #define YAMD_ABL4(A) YAMD_ABL(A, kModeByteKeys) YAMD_ABL(A, kModeByteKeysNext) YAMD_ABL(A, kModeByteKeysEven) YAMD_ABL(A, kModeByteKeysNextEven)
       YAMD_ABL4(1) YAMD_ABL4(2) YAMD_ABL4(3) YAMD_ABL4(4)
 #undef YAMD_ABL4
@@ -1750,24 +1763,24 @@ hipError_t launch_scan(const ScanParams& p, int grid, hipStream_t s, int mode) {
                                                   : p.filter_mode == kFilterEvenHash ? 3
                                                                                      : 0) * 4;
         switch (m) {
-          case 0: hipLaunchKernelGGL(scan_segments_kernel<kModeByteKeys>, dim3(grid), dim3(kWGThreads), lds, s, p); break;
-          case 2: hipLaunchKernelGGL(scan_segments_kernel<kModeByteKeysNext>, dim3(grid), dim3(kWGThreads), lds, s, p); break;
-          case 4: hipLaunchKernelGGL(scan_segments_kernel<kModeByteKeysEven>, dim3(grid), dim3(kWGThreads), lds, s, p); break;
-          case 6: hipLaunchKernelGGL(scan_segments_kernel<kModeByteKeysNextEven>, dim3(grid), dim3(kWGThreads), lds, s, p); break;
-          case 12: hipLaunchKernelGGL(scan_segments_kernel<kModeByteKeysEvenHash>, dim3(grid), dim3(kWGThreads), lds, s, p); break;
-          default: hipLaunchKernelGGL(scan_segments_kernel<kModeByteKeysNextEvenHash>, dim3(grid), dim3(kWGThreads), lds, s, p); break;
+          case 0: YAMD_LAUNCH_SCAN(scan_segments_kernel<kModeByteKeys>); break;
+          case 2: YAMD_LAUNCH_SCAN(scan_segments_kernel<kModeByteKeysNext>); break;
+          case 4: YAMD_LAUNCH_SCAN(scan_segments_kernel<kModeByteKeysEven>); break;
+          case 6: YAMD_LAUNCH_SCAN(scan_segments_kernel<kModeByteKeysNextEven>); break;
+          case 12: YAMD_LAUNCH_SCAN(scan_segments_kernel<kModeByteKeysEvenHash>); break;
+          default: YAMD_LAUNCH_SCAN(scan_segments_kernel<kModeByteKeysNextEvenHash>); break;
         }
       } else if (p.filter_mode == kFilterEven)
-        hipLaunchKernelGGL(scan_segments_kernel<kModeEven>, dim3(grid), dim3(kWGThreads), lds, s, p);
+        YAMD_LAUNCH_SCAN(scan_segments_kernel<kModeEven>);
       else if (p.filter_mode == kFilterEvenHash)
-        hipLaunchKernelGGL(scan_segments_kernel<kModeEvenHash>, dim3(grid), dim3(kWGThreads), lds, s,
-                           p);
+        YAMD_LAUNCH_SCAN(scan_segments_kernel<kModeEvenHash>);
       else
-        hipLaunchKernelGGL(scan_segments_kernel<0>, dim3(grid), dim3(kWGThreads), lds, s, p);
+        YAMD_LAUNCH_SCAN(scan_segments_kernel<0>);
       break;
   }
   return hipGetLastError();
 }
+#undef YAMD_LAUNCH_SCAN
 
 hipError_t launch_compact(const ScanParams& p, uint64_t* seg_offset, uint64_t* summary,
                           uint64_t* positions, bool scatter, hipStream_t s) {

@@ -23,7 +23,8 @@
 #include "verify.h"
 
 namespace yamd {
-hipError_t launch_scan(const ScanParams& p, int grid, hipStream_t s, int mode);
+hipError_t launch_scan(const ScanParams& p, int grid, hipStream_t s, int mode, hipEvent_t t0 = nullptr,
+                       hipEvent_t t1 = nullptr);
 hipError_t launch_compact(const ScanParams& p, uint64_t* seg_offset, uint64_t* summary,
                           uint64_t* positions, bool scatter, hipStream_t s);
 hipError_t launch_xorshift(uint8_t* buf, uint64_t n, const uint64_t* states, uint32_t n_chunks,
@@ -254,6 +255,9 @@ uint32_t choose_seg_bytes(uint64_t nbytes, int num_cus, uint32_t target) {
   return (uint32_t)std::min<uint64_t>(std::max<uint64_t>(per, 4 * kTile), kSegment);
 }
 
+#ifndef YAMD_EXT_EVENTS
+#define YAMD_EXT_EVENTS 1
+#endif
 int run_scan(yr_amd_scanner* s) {
   // scan, per-segment offsets and the scatter are queued back to back: the
   // output is sized for the clipped worst case (every segment at capacity),
@@ -268,11 +272,18 @@ int run_scan(yr_amd_scanner* s) {
   s->last.dead = s->tables->kd_any ? s->d_dead : nullptr;
   s->last.live = s->tables->kd_any ? s->d_live : nullptr;
   s->last.seg_x = s->tables->kd_any ? s->d_seg_x : nullptr;
-  if (s->timing) HIP_TRY(hipEventRecord(s->ev_begin, s->stream));
-  HIP_TRY(launch_scan(p, s->last_grid, s->stream, s->diag_mode));
-  if (s->timing) {
-    HIP_TRY(hipEventRecord(s->ev_end, s->stream));
+  // (timing: the kernel's own start / end stamps, YAMD_EXT_EVENTS; else two
+  // markers around the launch, which also count its dispatch)
+  if (s->timing && YAMD_EXT_EVENTS) {
+    HIP_TRY(launch_scan(p, s->last_grid, s->stream, s->diag_mode, s->ev_begin, s->ev_end));
     s->ev_valid = true;
+  } else {
+    if (s->timing) HIP_TRY(hipEventRecord(s->ev_begin, s->stream));
+    HIP_TRY(launch_scan(p, s->last_grid, s->stream, s->diag_mode));
+    if (s->timing) {
+      HIP_TRY(hipEventRecord(s->ev_end, s->stream));
+      s->ev_valid = true;
+    }
   }
   HIP_TRY(launch_compact(p, s->d_seg_offset, s->d_hsum, nullptr, false, s->stream));
   if (p.live != nullptr) HIP_TRY(hipMemsetAsync(p.live, 0, sizeof(uint32_t), s->stream));
