@@ -134,21 +134,23 @@ __device__ __forceinline__ bool first_level(uint32_t w4, const ScanParams& p) {
 #ifndef YAMD_RING_CTX_FIRST
 #define YAMD_RING_CTX_FIRST 1
 #endif
-constexpr uint32_t kEntCtx = YAMD_RING_CTX_FIRST ? 0u : 16u;
-constexpr uint32_t kEntData = YAMD_RING_CTX_FIRST ? 4u : 0u;
-constexpr uint32_t kEntIdx = 20u;
+// (YAMD_RING_CTX_FIRST=2: the index word first, then the context and the 16
+// bytes, 8-byte aligned: an append writes two qwords and a qword pair)
+constexpr uint32_t kEntCtx = YAMD_RING_CTX_FIRST == 2 ? 4u : YAMD_RING_CTX_FIRST ? 0u : 16u;
+constexpr uint32_t kEntData = YAMD_RING_CTX_FIRST == 2 ? 8u : YAMD_RING_CTX_FIRST ? 4u : 0u;
+constexpr uint32_t kEntIdx = YAMD_RING_CTX_FIRST == 2 ? 0u : 20u;
 typedef uint32_t u32_una __attribute__((aligned(1)));
 
 // Lane byte j of a ring entry (j = -4 .. -1: the context bytes).
 __device__ __forceinline__ uint32_t entry_byte_addr(uint32_t ent, int32_t j) {
-  return YAMD_RING_CTX_FIRST ? ent + (uint32_t)(j + 4) : (j >= 0 ? ent + (uint32_t)j : ent + 20u + j);
+  return YAMD_RING_CTX_FIRST ? ent + kEntData + (uint32_t)j : (j >= 0 ? ent + (uint32_t)j : ent + 20u + j);
 }
 
 // The 4 bytes ending at lane byte j (0..15) of a ring entry: lane bytes
 // j-3 .. j (the context bytes for j < 3).
 __device__ __forceinline__ uint32_t window4(uint32_t ent, uint32_t j) {
 #if YAMD_RING_CTX_FIRST
-  return *reinterpret_cast<const __attribute__((address_space(3))) u32_una*>((uintptr_t)(ent + j + 1));
+  return *reinterpret_cast<const __attribute__((address_space(3))) u32_una*>((uintptr_t)(ent + kEntData + j - 3));
 #else
   const uint32_t o = j - 3, lo = j >= 3 ? ent + (o & ~3u) : ent + 16;
   const uint32_t hi = j >= 3 ? lo + 4 : ent, sh = j >= 3 ? (o & 3u) : j + 1;
@@ -280,7 +282,7 @@ static_assert(kSegment <= kOutOffsetMask + 1u, "segment offsets must leave the t
 #endif
 template <int MODE>
 constexpr bool kIdxHigh = YAMD_BK_FLAT && kNextBytes<MODE>;
-static_assert(!YAMD_BK_FLAT || YAMD_RING_CTX_FIRST, "flat byte-key drains read the context-first entry");
+static_assert(!YAMD_BK_FLAT || YAMD_RING_CTX_FIRST == 1, "flat byte-key drains read the context-first entry");
 
 // b one of the (up to 8, repeated to fill) bytes of x0, x1: zero-byte test
 __device__ __forceinline__ bool excluded(uint32_t b, uint32_t x0, uint32_t x1) {
@@ -739,13 +741,18 @@ __device__ __forceinline__ void drain(const ScanParams& p, WaveQueue& q, uint32_
     const u32x2 e01 = lds_load<u32x2>(ent);
     const u32x2 e23 = lds_load<u32x2>(ent + 8);
     const u32x2 e45 = lds_load<u32x2>(ent + 16);
-#if YAMD_RING_CTX_FIRST
+#if YAMD_RING_CTX_FIRST == 2
+    const uint32_t S[6] = {e01.y, e23.x, e23.y, e45.x, e45.y, 0u};
+    const uint32_t eidx = e01.x;
+#elif YAMD_RING_CTX_FIRST
     const uint32_t S[6] = {e01.x, e01.y, e23.x, e23.y, e45.x, 0u};
+    const uint32_t eidx = e45.y;
 #else
     const uint32_t S[6] = {e45.x, e01.x, e01.y, e23.x, e23.y, 0u};
+    const uint32_t eidx = e45.y;
 #endif
-    off0 = (kIdxHigh<MODE> ? e45.y >> 16 : e45.y & 0xFFFFu) * kBytesPerLane;
-    if constexpr (kByteKeys<MODE>) ridx = e45.y;
+    off0 = (kIdxHigh<MODE> ? eidx >> 16 : eidx & 0xFFFFu) * kBytesPerLane;
+    if constexpr (kByteKeys<MODE>) ridx = eidx;
     if constexpr (kEven<MODE>) {
       m = even_mask<kEvenHash<MODE>>(S);
       if (p.n_pair_keys != 0) m |= pair_keys_mask(S, p);
@@ -1085,7 +1092,18 @@ __device__ __forceinline__ void write_entry(uint32_t ent, const uint32_t (&S)[6]
   // lane's 16 in the entry)
   const uint32_t idx = kIdxHigh<MODE> ? __builtin_amdgcn_perm(unit, S[5], 0x05040100u)
                                       : unit | (kNextBytes<MODE> ? S[5] << 16 : 0u);
-#if YAMD_RING_CTX_FIRST
+#if YAMD_RING_CTX_FIRST == 2
+  // index + context as one qword, the 16 bytes as two (8-byte aligned)
+  typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
+  typedef u32x4 u32x4_a8 __attribute__((aligned(8)));
+  lds_store2(ent, idx, S[0]);
+  u32x4 d;
+  d.x = S[1];
+  d.y = S[2];
+  d.z = S[3];
+  d.w = S[4];
+  *reinterpret_cast<__attribute__((address_space(3))) u32x4_a8*>((uintptr_t)(ent + kEntData)) = d;
+#elif YAMD_RING_CTX_FIRST
   // three ds_write2_b32: context, the 16 bytes as loaded, index
   typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
   typedef u32x4 u32x4_a4 __attribute__((aligned(4)));
