@@ -594,6 +594,13 @@ __device__ __forceinline__ uint32_t byte_keys_mask(const uint32_t (&S)[6], const
 #ifndef YAMD_DRAIN_Y2
 #define YAMD_DRAIN_Y2 1
 #endif
+// Deferring drains without divergent branches (kernels other than the
+// even-filter byte-key ones, which measured 0.5-1.4 % slower with them): the
+// tile loop loses a loop-carried lane mask (six SALU per tile); C -0.6 %,
+// fuzz0 / fuzz3 -3 % (profiles/r04_ab_inproc.json call h22)
+#ifndef YAMD_ASYNC_FLAT
+#define YAMD_ASYNC_FLAT 1
+#endif
 #ifndef YAMD_DC_BALLOT
 #define YAMD_DC_BALLOT 1
 #endif
@@ -603,6 +610,8 @@ template <int MODE>
 constexpr bool kDeferFl =
     YAMD_DEFER_FL && kAbl<MODE> != 1 &&
     (MODE == 0 || MODE == 12 || kByteKeys<MODE> || kEven<MODE> || kByteKeyAblation<MODE>);
+template <int MODE>
+constexpr bool kAsyncFlat = YAMD_ASYNC_FLAT && !(kEven<MODE> && kByteKeys<MODE>);
 
 // The output entry of a certain candidate (its last byte a 1-byte key) at lane
 // byte j of ring entry ent: it needs no window for the exact check, so the scan
@@ -773,20 +782,33 @@ __device__ __forceinline__ void drain(const ScanParams& p, WaveQueue& q, uint32_
   if constexpr (kDeferFl<MODE> && kAsync) {
     const uint32_t m2 = m & (m - 1u);
     if ((p.len_mask & 6u) == 0u && __ballot((m2 & (m2 - 1u)) != 0u) == 0) {
-      q.oa = q.ob = kNoHit;
-      q.wa = q.wb = 0u;
-      q.ia = q.ib = 0u;
-      if (m != 0u) {
-        const uint32_t j = (uint32_t)__builtin_ctz(m);
-        q.wa = window4(ent, j);
-        q.oa = off0 + j;
-        q.ia = fl_word(q.wa) * 4u;   // (issue_first_level adds kExactFl)
-      }
-      if (m2 != 0u) {
-        const uint32_t j = (uint32_t)__builtin_ctz(m2);
-        q.wb = window4(ent, j);
-        q.ob = off0 + j;
-        q.ib = fl_word(q.wb) * 4u;
+      if constexpr (kAsyncFlat<MODE>) {
+        // without branches (no lane mask for the compiler to carry through the
+        // tile loop): a lane without a hit reads its entry's byte 16 window, a
+        // harmless in-entry read, and keeps kNoHit / index 0
+        const uint32_t ja = (uint32_t)__builtin_ctz(m | 0x10000u), jb = (uint32_t)__builtin_ctz(m2 | 0x10000u);
+        q.wa = window4(ent, ja);
+        q.wb = window4(ent, jb);
+        q.oa = m != 0u ? off0 + ja : kNoHit;
+        q.ob = m2 != 0u ? off0 + jb : kNoHit;
+        q.ia = m != 0u ? fl_word(q.wa) * 4u : 0u;   // (issue_first_level adds kExactFl)
+        q.ib = m2 != 0u ? fl_word(q.wb) * 4u : 0u;
+      } else {
+        q.oa = q.ob = kNoHit;
+        q.wa = q.wb = 0u;
+        q.ia = q.ib = 0u;
+        if (m != 0u) {
+          const uint32_t j = (uint32_t)__builtin_ctz(m);
+          q.wa = window4(ent, j);
+          q.oa = off0 + j;
+          q.ia = fl_word(q.wa) * 4u;   // (issue_first_level adds kExactFl)
+        }
+        if (m2 != 0u) {
+          const uint32_t j = (uint32_t)__builtin_ctz(m2);
+          q.wb = window4(ent, j);
+          q.ob = off0 + j;
+          q.ib = fl_word(q.wb) * 4u;
+        }
       }
       q.defer = true;
       return;
