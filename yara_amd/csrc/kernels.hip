@@ -606,10 +606,18 @@ __device__ __forceinline__ uint32_t byte_keys_mask(const uint32_t (&S)[6], const
 #endif
 template <int MODE>
 constexpr bool kHoldFl = YAMD_HOLD_FL && !kEven<MODE>;
+// The byte-key kernels run only for tables with 1-byte keys (launch_scan), so
+// their drains never defer (the deferral needs len_mask & 6 == 0): with
+// YAMD_BK_NO_DEFER they carry none of its per-tile machinery (the two
+// first-level loads, the deferred-drain test).
+#ifndef YAMD_BK_NO_DEFER
+#define YAMD_BK_NO_DEFER 1
+#endif
 template <int MODE>
 constexpr bool kDeferFl =
     YAMD_DEFER_FL && kAbl<MODE> != 1 &&
-    (MODE == 0 || MODE == 12 || kByteKeys<MODE> || kEven<MODE> || kByteKeyAblation<MODE>);
+    (MODE == 0 || MODE == 12 || kByteKeys<MODE> || kEven<MODE> || kByteKeyAblation<MODE>) &&
+    !(YAMD_BK_NO_DEFER && (kByteKeys<MODE> || kByteKeyAblation<MODE>));
 template <int MODE>
 constexpr bool kAsyncFlat = YAMD_ASYNC_FLAT && !(kEven<MODE> && kByteKeys<MODE>);
 
