@@ -198,6 +198,8 @@ struct WaveQueue {
   uint32_t pend;    // LDS address: kWave pairs {w4, segment offset}
   uint32_t pend_n;  // wave-uniform
   bool defer;       // wave-uniform: the per-lane hits below await their words
+  uint32_t facc;    // per lane (byte-key kernels, kBkSkipF): OR of the stage-1 filter
+                    // and 2-byte-key tests of the tiles queued since the last drain
   // per lane, the first (a) and second (b) deferred hit: window, segment
   // offset (kNoHit = none), byte offset into the first level (exact[kExactFl..]) that the next tile step
   // loads (0 = none), the loaded word
@@ -618,6 +620,18 @@ constexpr bool kDeferFl =
     YAMD_DEFER_FL && kAbl<MODE> != 1 &&
     (MODE == 0 || MODE == 12 || kByteKeys<MODE> || kEven<MODE> || kByteKeyAblation<MODE>) &&
     !(YAMD_BK_NO_DEFER && (kByteKeys<MODE> || kByteKeyAblation<MODE>));
+// Byte-key drains re-test the filter and the 2-byte keys only when some tile
+// queued since the last drain passed them in stage 1 (a per-lane OR, one
+// v_or per tile, balloted once per drain): rx's drains skip ~90 of their ~140
+// VALU nearly always (its ring holds 1-byte-key hits).
+#ifndef YAMD_BK_SKIPF
+#define YAMD_BK_SKIPF 1
+#endif
+#ifndef YAMD_WIDE   // (wide steps, below)
+#define YAMD_WIDE 0
+#endif
+template <int MODE>
+constexpr bool kBkSkipF = YAMD_BK_SKIPF && !YAMD_WIDE && kByteKeys<MODE> && kAbl<MODE> == 0;
 template <int MODE>
 constexpr bool kAsyncFlat = YAMD_ASYNC_FLAT && !(kEven<MODE> && kByteKeys<MODE>);
 
@@ -746,6 +760,11 @@ __device__ __forceinline__ void drain(const ScanParams& p, WaveQueue& q, uint32_
     if (q.defer) drain_complete<MODE>(p, q, lane, seg_start, out, found);
   const uint32_t n = q.count;   // <= kQueueCap = kWave
   q.count = 0;
+  bool need_f = true;   // (kBkSkipF: some queued tile passed the filter / a 2-byte key)
+  if constexpr (kBkSkipF<MODE>) {
+    need_f = __ballot(q.facc != 0u) != 0;
+    q.facc = 0u;
+  }
   if constexpr (MODE == 7 || MODE == 8 || kAbl<MODE> == 2) return;   // ablations: entries dropped
   __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
   uint32_t maybe = 0, off0 = 0, m = 0;   // m: bit j = lane byte j passes the filter
@@ -770,11 +789,13 @@ __device__ __forceinline__ void drain(const ScanParams& p, WaveQueue& q, uint32_
 #endif
     off0 = (kIdxHigh<MODE> ? eidx >> 16 : eidx & 0xFFFFu) * kBytesPerLane;
     if constexpr (kByteKeys<MODE>) ridx = eidx;
-    if constexpr (kEven<MODE>) {
-      m = even_mask<kEvenHash<MODE>>(S);
-      if (p.n_pair_keys != 0) m |= pair_keys_mask(S, p);
-    } else {
-      m = dense_mask(stage1<0, false>(S, lane));
+    if (need_f) {
+      if constexpr (kEven<MODE>) {
+        m = even_mask<kEvenHash<MODE>>(S);
+        if (p.n_pair_keys != 0) m |= pair_keys_mask(S, p);
+      } else {
+        m = dense_mask(stage1<0, false>(S, lane));
+      }
     }
     if constexpr (kByteKeys<MODE>) {
       kmask = byte_keys_mask(S, p);
@@ -1254,6 +1275,7 @@ __device__ __forceinline__ void tile_step(const ScanParams& p, WaveQueue& q, Seg
   uint32_t any = stage1<kStage1Mode<MODE>, true>(S, lane);
   if constexpr (kEven<MODE>)
     if (p.n_pair_keys != 0) any |= pair_keys_any(S, p);
+  const uint32_t any_f = any;   // (the filter and 2-byte-key part: kBkSkipF)
   if constexpr (kByteKeys<MODE>) {
     if constexpr (kAbl<MODE> == 3) asm volatile("" ::"v"(byte_keys_any(S, p)));   // ablation
     else if constexpr (kAbl<MODE> != 4) any |= byte_keys_any(S, p);
@@ -1274,6 +1296,8 @@ __device__ __forceinline__ void tile_step(const ScanParams& p, WaveQueue& q, Seg
   } else {
     ring_append<MODE, TAIL>(p, q, st, S, any, tile_off, lane);
   }
+  // (after the append: a drain inside it takes only the earlier tiles' entries)
+  if constexpr (kBkSkipF<MODE>) q.facc |= any_f;
   issue_first_level<MODE>(p, q);
 }
 
@@ -1430,6 +1454,7 @@ __device__ __forceinline__ void scan_segment(const ScanParams& p, WaveQueue& q, 
   q.count = 0;
   q.pend_n = 0;
   q.defer = false;
+  q.facc = 0u;
   q.ia = q.ib = 0u;
   q.da = q.db = 0u;
   q.wa = q.wb = 0u;
