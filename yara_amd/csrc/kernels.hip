@@ -352,6 +352,9 @@ __device__ __forceinline__ uint32_t key_class(const ScanParams& p, const KeyClas
     return 0;
   }
   bool hit = false;
+  // (not vectorized: the vectorizer's masked form of this short loop cost the
+  // compaction ~30 spilled SGPRs)
+#pragma clang loop vectorize(disable) interleave(disable)
   for (uint32_t jj = 0; jj <= span; ++jj) hit |= ((uint32_t)(w >> (8 * ((uint32_t)s0 + jj))) & m) == v;
   return hit ? 0u : kClassDead;
 }
@@ -1659,7 +1662,10 @@ __global__ __launch_bounds__(W * kWave) void seg_scatter_kernel(
   const uint32_t* sx = classes ? p.seg_x + at0 : nullptr;
   const uint64_t first = seg_offset[seg];
   uint64_t* dst = positions + first;
-  const uint32_t lane = threadIdx.x % kWave, w = threadIdx.x / kWave;
+  // (w through readfirstlane: the compiler then knows the loop's trips are
+  // wave-uniform -- otherwise it runs the loop under an exec mask and carries
+  // every wave-uniform value of it as a lane mask)
+  const uint32_t lane = threadIdx.x % kWave, w = __builtin_amdgcn_readfirstlane(threadIdx.x / kWave);
   constexpr uint32_t kStride = W * kWave;
   // Latency-bound (a few hundred candidates per wave): every iteration's
   // entry and kept bytes are loaded one iteration ahead.
