@@ -1634,6 +1634,9 @@ constexpr uint32_t kScatterWaves = 8;   // waves per segment in the scatter (den
 #ifndef YAMD_CLASS_FETCH
 #define YAMD_CLASS_FETCH 1
 #endif
+#ifndef YAMD_CLASS_STAGE
+#define YAMD_CLASS_STAGE 1
+#endif
 
 // per-segment LDS buffer of live candidates (the diagnostic build holds one,
 // so that the GPU suite exercises the overflow path, tests/test_preverify.py)
@@ -1647,6 +1650,12 @@ __global__ __launch_bounds__(W * kWave) void seg_scatter_kernel(
   __shared__ KeyClassRec kc[kMaxByteKeys];
   __shared__ uint32_t lbuf[kLiveBuf];
   __shared__ uint32_t lcount, lglobal;
+  // the classes of a chunk of kChunk candidates, staged here and written out as
+  // aligned dwords (one byte store per candidate ran at ~1.4 TB/s:
+  // profiles/r04_ab_inproc.json h31); +4: the chunk's start is placed at its
+  // absolute index mod 4
+  constexpr uint32_t kChunk = YAMD_CLASS_STAGE ? W * kWave * (W == 2 ? 16u : 8u) : 0xFFFFFFFFu;
+  __shared__ __attribute__((aligned(4))) uint8_t cbuf[YAMD_CLASS_STAGE ? kChunk + 4 : 4];
   const bool classes = p.dead != nullptr;   // (uniform)
   if (threadIdx.x < kMaxByteKeys) {
     const uint32_t k = threadIdx.x;
@@ -1677,7 +1686,10 @@ __global__ __launch_bounds__(W * kWave) void seg_scatter_kernel(
       if (classes) x = sx[i];
     }
   }
-  for (uint32_t i0 = w * kWave; i0 < c; i0 += kStride) {   // (wave-uniform trips: the ballots)
+  for (uint32_t chunk = 0; chunk < c; chunk += kChunk) {   // (block-uniform: the barriers)
+  const uint32_t cend = c - chunk > kChunk ? chunk + kChunk : c;
+  const uint32_t sh0 = (uint32_t)(first + chunk) & 3u;   // cbuf[sh0 + k] = class of chunk + k
+  for (uint32_t i0 = chunk + w * kWave; i0 < cend; i0 += kStride) {   // (wave-uniform trips: the ballots)
     const uint32_t i = i0 + lane;
     const bool valid = i < c;
     const uint32_t ec = e, xc = x;
@@ -1714,7 +1726,10 @@ __global__ __launch_bounds__(W * kWave) void seg_scatter_kernel(
         }
       }
     }
-    if (valid) p.dead[first + i] = (uint8_t)cls;
+    if (valid) {
+      if constexpr (YAMD_CLASS_STAGE) cbuf[sh0 + (i - chunk)] = (uint8_t)cls;
+      else p.dead[first + i] = (uint8_t)cls;
+    }
     // the undecided ones onto the live list (any order): the segment's LDS
     // buffer, copied out with ONE global atomic per segment (one per wave and
     // iteration, serialised on the counter, took 1.2 ms for 34 M candidates);
@@ -1739,6 +1754,26 @@ __global__ __launch_bounds__(W * kWave) void seg_scatter_kernel(
               (uint32_t)(first + i);
       }
     }
+  }
+  if constexpr (YAMD_CLASS_STAGE) {
+    if (classes) {
+      // the chunk's classes: absolute bytes [a, a + m) of p.dead -- head and
+      // tail bytes (shared with the neighbouring segments' blocks) byte by
+      // byte, the aligned dwords between them whole
+      __syncthreads();
+      const uint64_t a = first + chunk;
+      const uint32_t m = cend - chunk;
+      const uint32_t head = min((4u - sh0) & 3u, m);
+      const uint32_t nd = (m - head) / 4u, tail = m - head - 4u * nd;
+      uint8_t* out = p.dead + a;
+      for (uint32_t t = threadIdx.x; t < nd; t += kStride)
+        *reinterpret_cast<uint32_t*>(out + head + 4u * t) =
+            *reinterpret_cast<const uint32_t*>(cbuf + sh0 + head + 4u * t);
+      if (threadIdx.x < head) out[threadIdx.x] = cbuf[sh0 + threadIdx.x];
+      if (threadIdx.x < tail) out[head + 4u * nd + threadIdx.x] = cbuf[sh0 + head + 4u * nd + threadIdx.x];
+      __syncthreads();
+    }
+  }
   }
   if (!classes) return;
   __syncthreads();
