@@ -1687,93 +1687,93 @@ __global__ __launch_bounds__(W * kWave) void seg_scatter_kernel(
     }
   }
   for (uint32_t chunk = 0; chunk < c; chunk += kChunk) {   // (block-uniform: the barriers)
-  const uint32_t cend = c - chunk > kChunk ? chunk + kChunk : c;
-  const uint32_t sh0 = (uint32_t)(first + chunk) & 3u;   // cbuf[sh0 + k] = class of chunk + k
-  for (uint32_t i0 = chunk + w * kWave; i0 < cend; i0 += kStride) {   // (wave-uniform trips: the ballots)
-    const uint32_t i = i0 + lane;
-    const bool valid = i < c;
-    const uint32_t ec = e, xc = x;
-    e = x = 0u;
-    if (i + kStride < c) {
-      e = src[i + kStride];
-      if (classes) x = sx[i + kStride];
-    }
-    const uint64_t pos = base + (ec & kOutOffsetMask);
-    if (valid) dst[i] = pos;
-    if (!classes) continue;
-    // the certain candidates' classes from the bytes the scan kept beside them
-    uint32_t cls = 0u;
-    if (valid && (ec & kCertainMask) != 0u) {
-      bool more = false;
-      cls = key_class(p, kc, xc | (uint64_t)(ec >> kOutByteShift & 0xFFu) << 32,
-                      (int32_t)(ec >> kOutKeyShift & 7u) - 2, (ec & kOutDeep) != 0u, pos, 4,
-                      YAMD_CLASS_FETCH ? &more : nullptr);
-      // Undecided only because the guard's bytes (or the byte before the key)
-      // lie outside the five the scan kept -- the key near its lane's end:
-      // read eight bytes around the key from the input (three aligned dwords
-      // inside [byte_begin - 4, byte_end), the bytes the scan itself may read)
-      // and decide again, rather than leave the candidate to the live list.
-      if (more) {
-        const uint64_t kb = pos - 1;   // the key's byte
-        const uint64_t a4 = (kb - 2) & ~3ull;
-        if (kb >= 2 && a4 + 4 >= p.byte_begin && a4 + 12 <= p.byte_end) {
-          const uint32_t* d = reinterpret_cast<const uint32_t*>(p.data + a4);
-          const uint32_t d0 = d[0], d1 = d[1], d2 = d[2];
-          const uint32_t sh = (uint32_t)(kb - 2 - a4);
-          const uint64_t w8 = __builtin_amdgcn_alignbyte(d1, d0, sh) |
-                              (uint64_t)__builtin_amdgcn_alignbyte(d2, d1, sh) << 32;
-          cls = key_class(p, kc, w8, 2, false, pos, 7);
+    const uint32_t cend = c - chunk > kChunk ? chunk + kChunk : c;
+    const uint32_t sh0 = (uint32_t)(first + chunk) & 3u;   // cbuf[sh0 + k] = class of chunk + k
+    for (uint32_t i0 = chunk + w * kWave; i0 < cend; i0 += kStride) {   // (wave-uniform trips: the ballots)
+      const uint32_t i = i0 + lane;
+      const bool valid = i < c;
+      const uint32_t ec = e, xc = x;
+      e = x = 0u;
+      if (i + kStride < c) {
+        e = src[i + kStride];
+        if (classes) x = sx[i + kStride];
+      }
+      const uint64_t pos = base + (ec & kOutOffsetMask);
+      if (valid) dst[i] = pos;
+      if (!classes) continue;
+      // the certain candidates' classes from the bytes the scan kept beside them
+      uint32_t cls = 0u;
+      if (valid && (ec & kCertainMask) != 0u) {
+        bool more = false;
+        cls = key_class(p, kc, xc | (uint64_t)(ec >> kOutByteShift & 0xFFu) << 32,
+                        (int32_t)(ec >> kOutKeyShift & 7u) - 2, (ec & kOutDeep) != 0u, pos, 4,
+                        YAMD_CLASS_FETCH ? &more : nullptr);
+        // Undecided only because the guard's bytes (or the byte before the key)
+        // lie outside the five the scan kept -- the key near its lane's end:
+        // read eight bytes around the key from the input (three aligned dwords
+        // inside [byte_begin - 4, byte_end), the bytes the scan itself may read)
+        // and decide again, rather than leave the candidate to the live list.
+        if (more) {
+          const uint64_t kb = pos - 1;   // the key's byte
+          const uint64_t a4 = (kb - 2) & ~3ull;
+          if (kb >= 2 && a4 + 4 >= p.byte_begin && a4 + 12 <= p.byte_end) {
+            const uint32_t* d = reinterpret_cast<const uint32_t*>(p.data + a4);
+            const uint32_t d0 = d[0], d1 = d[1], d2 = d[2];
+            const uint32_t sh = (uint32_t)(kb - 2 - a4);
+            const uint64_t w8 = __builtin_amdgcn_alignbyte(d1, d0, sh) |
+                                (uint64_t)__builtin_amdgcn_alignbyte(d2, d1, sh) << 32;
+            cls = key_class(p, kc, w8, 2, false, pos, 7);
+          }
+        }
+      }
+      if (valid) {
+        if constexpr (YAMD_CLASS_STAGE) cbuf[sh0 + (i - chunk)] = (uint8_t)cls;
+        else p.dead[first + i] = (uint8_t)cls;
+      }
+      // the undecided ones onto the live list (any order): the segment's LDS
+      // buffer, copied out with ONE global atomic per segment (one per wave and
+      // iteration, serialised on the counter, took 1.2 ms for 34 M candidates);
+      // what does not fit goes straight to the global list
+      const bool live = valid && cls == 0u;
+      const uint64_t lm = __ballot(live);
+      if (lm != 0) {
+        uint32_t b = 0;
+        if (lane == 0) b = atomicAdd(&lcount, (uint32_t)__popcll(lm));
+        b = __builtin_amdgcn_readfirstlane(b);
+        const uint32_t slot =
+            b + __builtin_amdgcn_mbcnt_hi((uint32_t)(lm >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)lm, 0u));
+        if (live && slot < kLiveBuf) lbuf[slot] = (uint32_t)(first + i);
+        const uint64_t om = __ballot(live && slot >= kLiveBuf);
+        if (om != 0) {
+          uint32_t g = 0;
+          if (lane == 0) g = atomicAdd(p.live, (uint32_t)__popcll(om));
+          g = __builtin_amdgcn_readfirstlane(g);
+          if (live && slot >= kLiveBuf)
+            p.live[1 + g + __builtin_amdgcn_mbcnt_hi((uint32_t)(om >> 32),
+                                                     __builtin_amdgcn_mbcnt_lo((uint32_t)om, 0u))] =
+                (uint32_t)(first + i);
         }
       }
     }
-    if (valid) {
-      if constexpr (YAMD_CLASS_STAGE) cbuf[sh0 + (i - chunk)] = (uint8_t)cls;
-      else p.dead[first + i] = (uint8_t)cls;
-    }
-    // the undecided ones onto the live list (any order): the segment's LDS
-    // buffer, copied out with ONE global atomic per segment (one per wave and
-    // iteration, serialised on the counter, took 1.2 ms for 34 M candidates);
-    // what does not fit goes straight to the global list
-    const bool live = valid && cls == 0u;
-    const uint64_t lm = __ballot(live);
-    if (lm != 0) {
-      uint32_t b = 0;
-      if (lane == 0) b = atomicAdd(&lcount, (uint32_t)__popcll(lm));
-      b = __builtin_amdgcn_readfirstlane(b);
-      const uint32_t slot =
-          b + __builtin_amdgcn_mbcnt_hi((uint32_t)(lm >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)lm, 0u));
-      if (live && slot < kLiveBuf) lbuf[slot] = (uint32_t)(first + i);
-      const uint64_t om = __ballot(live && slot >= kLiveBuf);
-      if (om != 0) {
-        uint32_t g = 0;
-        if (lane == 0) g = atomicAdd(p.live, (uint32_t)__popcll(om));
-        g = __builtin_amdgcn_readfirstlane(g);
-        if (live && slot >= kLiveBuf)
-          p.live[1 + g + __builtin_amdgcn_mbcnt_hi((uint32_t)(om >> 32),
-                                                   __builtin_amdgcn_mbcnt_lo((uint32_t)om, 0u))] =
-              (uint32_t)(first + i);
+    if constexpr (YAMD_CLASS_STAGE) {
+      if (classes) {
+        // the chunk's classes: absolute bytes [a, a + m) of p.dead -- head and
+        // tail bytes (shared with the neighbouring segments' blocks) byte by
+        // byte, the aligned dwords between them whole
+        __syncthreads();
+        const uint64_t a = first + chunk;
+        const uint32_t m = cend - chunk;
+        const uint32_t head = min((4u - sh0) & 3u, m);
+        const uint32_t nd = (m - head) / 4u, tail = m - head - 4u * nd;
+        uint8_t* out = p.dead + a;
+        for (uint32_t t = threadIdx.x; t < nd; t += kStride)
+          *reinterpret_cast<uint32_t*>(out + head + 4u * t) =
+              *reinterpret_cast<const uint32_t*>(cbuf + sh0 + head + 4u * t);
+        if (threadIdx.x < head) out[threadIdx.x] = cbuf[sh0 + threadIdx.x];
+        if (threadIdx.x < tail) out[head + 4u * nd + threadIdx.x] = cbuf[sh0 + head + 4u * nd + threadIdx.x];
+        __syncthreads();
       }
     }
-  }
-  if constexpr (YAMD_CLASS_STAGE) {
-    if (classes) {
-      // the chunk's classes: absolute bytes [a, a + m) of p.dead -- head and
-      // tail bytes (shared with the neighbouring segments' blocks) byte by
-      // byte, the aligned dwords between them whole
-      __syncthreads();
-      const uint64_t a = first + chunk;
-      const uint32_t m = cend - chunk;
-      const uint32_t head = min((4u - sh0) & 3u, m);
-      const uint32_t nd = (m - head) / 4u, tail = m - head - 4u * nd;
-      uint8_t* out = p.dead + a;
-      for (uint32_t t = threadIdx.x; t < nd; t += kStride)
-        *reinterpret_cast<uint32_t*>(out + head + 4u * t) =
-            *reinterpret_cast<const uint32_t*>(cbuf + sh0 + head + 4u * t);
-      if (threadIdx.x < head) out[threadIdx.x] = cbuf[sh0 + threadIdx.x];
-      if (threadIdx.x < tail) out[head + 4u * nd + threadIdx.x] = cbuf[sh0 + head + 4u * nd + threadIdx.x];
-      __syncthreads();
-    }
-  }
   }
   if (!classes) return;
   __syncthreads();
