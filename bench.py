@@ -57,6 +57,12 @@ def parse():
     ap.add_argument("--no-other", action="store_true",
                     help="skip the other rule sets' kernel timings (B, E, rx, short, fuzz0, fuzz3)")
     ap.add_argument("--backend", default="nccl", help="nccl (= RCCL) or gloo (rehearsal)")
+    ap.add_argument("--dist", action="store_true",
+                    help="run the N > 1 code path (process group, per-rank attribution, "
+                         "gathers) even at world size 1")
+    ap.add_argument("--cpu-threads", type=int, default=0,
+                    help="threads of the multi-threaded CPU baselines (0: every CPU this "
+                         "process may run on)")
     ap.add_argument("--clock-warmup-s", type=float, default=0.4,
                     help="back-to-back scans before the measured legs, on every rank")
     return ap.parse_args()
@@ -72,23 +78,48 @@ def cpu_model() -> str:
     return "unknown CPU"
 
 
-def cpu_baseline(rules: str, sample_mib: int, seed: int):
+def cpu_info():
+    """What the host offers this process: nproc, the CPUs it may run on, and
+    the cgroup CPU quota if one is set (a GPU box shares its host)."""
+    info = {"model": cpu_model(), "nproc": os.cpu_count() or 0}
+    try:
+        info["affinity"] = len(os.sched_getaffinity(0))
+    except (AttributeError, OSError):
+        info["affinity"] = info["nproc"]
+    try:
+        q = open("/sys/fs/cgroup/cpu.max").read().split()
+        info["cgroup_cpu_max"] = " ".join(q)
+        if q[0] != "max":
+            info["cgroup_cpus"] = round(int(q[0]) / int(q[1]), 2)
+    except (OSError, ValueError, IndexError):
+        pass
+    return info
+
+
+def _stock_rules(rules: str):
+    ref_so = os.path.join(REPO, "oracle", "_ref", "libyara_ref.so")
+    if not os.path.exists(ref_so):
+        return None, None
+    sys.path.insert(0, os.path.join(REPO, "tests", "golden"))
+    import gen_rules
+    return ref_so, gen_rules.gen(rules).encode()
+
+
+def cpu_baseline(rules: str, data, seed: int):
     """Stock reference libyara yr_rules_scan_mem on the host (kind "reference"),
     or the in-repo restatement of scanner.c:45-176 (kind "port") if the
     reference build did not travel.  1 thread, a bounded prefix of the input."""
     sys.path.insert(0, os.path.join(REPO, "tests", "golden"))
     import oracle
-    n = sample_mib << 20
-    data = oracle.xorshift(n, seed)
-    ref_so = os.path.join(REPO, "oracle", "_ref", "libyara_ref.so")
-    if os.path.exists(ref_so):
-        import gen_rules
+    n = data.size
+    ref_so, src = _stock_rules(rules)
+    if ref_so is not None:
         L = ctypes.CDLL(ref_so)
         L.yr_initialize()
         comp = ctypes.c_void_p()
         assert L.yr_compiler_create(ctypes.byref(comp)) == 0
         L.yr_compiler_add_string.argtypes = [ctypes.c_void_p, ctypes.c_char_p, ctypes.c_char_p]
-        assert L.yr_compiler_add_string(comp, gen_rules.gen(rules).encode(), None) == 0
+        assert L.yr_compiler_add_string(comp, src, None) == 0
         rules_h = ctypes.c_void_p()
         L.yr_compiler_get_rules.argtypes = [ctypes.c_void_p, ctypes.POINTER(ctypes.c_void_p)]
         assert L.yr_compiler_get_rules(comp, ctypes.byref(rules_h)) == 0
@@ -111,25 +142,57 @@ def cpu_baseline(rules: str, sample_mib: int, seed: int):
         kind, what = "port", "in-repo restatement of scanner.c:45-176 (oracle/ac_oracle.c)"
     return {"value": round(n / dt / 1e9, 4), "unit": "GB/s", "cores": 1, "kind": kind,
             "sample": "%s, rule set %s, first %d MiB of the xorshift64 seed-%d input, 1 thread, "
-                      "%.1f s, %s (nproc %d)" % (what, rules, sample_mib, seed, dt, cpu_model(),
+                      "%.1f s, %s (nproc %d)" % (what, rules, n >> 20, seed, dt, cpu_model(),
                                                  os.cpu_count() or 0)}
 
 
-def cpu_parallel(rules: str, sample_mib: int, seed: int, threads: int):
+def cpu_stock_threads(rules: str, data, seed: int, threads: int, min_s: float = 3.0):
+    """SURVEY.md §8d's multi-threaded CPU comparator on STOCK libyara:
+    `threads` threads, each with its own YR_SCANNER (yr_scanner_create, as
+    cli/yara.c:1564-1608 gives each scanning thread one) scanning its own
+    contiguous slice of the sample with a 4-byte warm-up, passes repeated for
+    at least `min_s` seconds (oracle/refmt.c, built against oracle/_ref)."""
+    ref_so, src = _stock_rules(rules)
+    mt_so = os.path.join(REPO, "oracle", "_ref", "librefmt.so")
+    if ref_so is None or not os.path.exists(mt_so):
+        return None
+    L = ctypes.CDLL(mt_so)
+    L.refmt_scan.argtypes = [ctypes.c_char_p, ctypes.c_void_p, ctypes.c_size_t, ctypes.c_int,
+                             ctypes.c_double, ctypes.POINTER(ctypes.c_double),
+                             ctypes.POINTER(ctypes.c_uint64), ctypes.POINTER(ctypes.c_double)]
+    gbps, passes, secs = ctypes.c_double(), ctypes.c_uint64(), ctypes.c_double()
+    rc = L.refmt_scan(src, data.ctypes.data, data.size, threads, min_s, ctypes.byref(gbps),
+                      ctypes.byref(passes), ctypes.byref(secs))
+    if rc != 0:
+        return {"error": "refmt_scan returned %d" % rc}
+    info = cpu_info()
+    return {"value": round(gbps.value, 3), "unit": "GB/s", "cores": threads, "kind": "reference",
+            "sample": "stock libyara 4.2.1 (oracle/_ref), %d threads x one YR_SCANNER each over "
+                      "contiguous slices (4-byte warm-up) of the first %d MiB of the xorshift64 "
+                      "seed-%d input, rule set %s, %d pass(es) in %.1f s (oracle/refmt.c)"
+                      % (threads, data.size >> 20, seed, rules, passes.value, secs.value),
+            "host": info}
+
+
+def cpu_parallel(rules: str, data, threads: int, min_s: float = 2.0):
     """the in-repo restatement of scanner.c:45-176, one walker
-    per contiguous slice with a 4-byte warm-up, `threads` threads (reported
-    beside cpu_baseline; not the baseline itself)."""
+    per contiguous slice with a 4-byte warm-up, `threads` threads, repeated for
+    at least `min_s` seconds (reported beside cpu_baseline)."""
     sys.path.insert(0, os.path.join(REPO, "tests", "golden"))
     import oracle
     from conftest import ref_tables   # noqa
-    data = oracle.xorshift(sample_mib << 20, seed)
     tab = ref_tables(rules)
+    passes = 0
     t0 = time.perf_counter()
-    oracle.count_parallel(tab, data, threads)
-    dt = time.perf_counter() - t0
-    return {"value": round(data.size / dt / 1e9, 4), "unit": "GB/s", "cores": threads,
-            "kind": "port", "sample": "oracle/ac_oracle.c slice walkers, rule set %s, first %d MiB"
-            % (rules, sample_mib)}
+    while True:
+        oracle.count_parallel(tab, data, threads)
+        passes += 1
+        dt = time.perf_counter() - t0
+        if dt >= min_s:
+            break
+    return {"value": round(data.size * passes / dt / 1e9, 3), "unit": "GB/s", "cores": threads,
+            "kind": "port", "sample": "oracle/ac_oracle.c slice walkers, rule set %s, first %d MiB, "
+            "%d pass(es) in %.1f s" % (rules, data.size >> 20, passes, dt)}
 
 
 def load_traffic(kernel_bytes):
@@ -167,10 +230,17 @@ def main():
     local = int(os.environ.get("LOCAL_RANK", "0"))
     if world != args.gpus and world > 1:
         raise SystemExit("--gpus %d but WORLD_SIZE=%d" % (args.gpus, world))
+    # the N > 1 code path: a process group, per-rank attribution, the gathers
+    # (--dist: also at world size 1, e.g. RCCL on one GPU)
+    use_dist = world > 1 or args.dist
+    if use_dist and world == 1:
+        for k, v in (("MASTER_ADDR", "127.0.0.1"), ("MASTER_PORT", "29533"), ("RANK", "0"),
+                     ("WORLD_SIZE", "1")):
+            os.environ.setdefault(k, v)
     ndev = torch.cuda.device_count()
     dev = torch.device("cuda", local % ndev)   # % ndev: gloo rehearsals on fewer GPUs
     torch.cuda.set_device(dev)
-    if world > 1:
+    if use_dist:
         if args.backend == "nccl":
             dist.init_process_group("nccl", device_id=dev)
         else:
@@ -213,13 +283,13 @@ def main():
         sc = scanners[k % depth]
         ptr, cnt, _ = sc.device_result()            # ascending block positions in HBM
         kms = sc.kernel_ms() if timed_kernel else None
-        if world == 1:
+        if not use_dist:
             return (ptr, cnt), kms
         t_g = time.perf_counter()
         pos = torch.empty(max(cnt, 1), dtype=torch.int64, device=dev)
         memcpy(pos.data_ptr(), ptr, cnt * 8, 3)
         # RCCL: counts + padded gather of 32-bit offsets from each shard's begin
-        pos = ydist.gather_positions(pos[:cnt], begins=begins_all)
+        pos = ydist.gather_positions(pos[:cnt], begins=begins_all, end=total)
         if timed_kernel:
             gather_s[0] += time.perf_counter() - t_g
         return pos, kms
@@ -251,7 +321,7 @@ def main():
     for k in range(max(0, n_clock - depth + 1), n_clock):
         scanners[k % depth].device_result()
     torch.cuda.synchronize()
-    if world > 1:
+    if use_dist:
         dist.barrier()
     # Order of the legs: the secondary measurements first (the other rule sets'
     # kernel times, the verification-complete step), the headline last.
@@ -291,50 +361,50 @@ def main():
         scanner.scan_window(buf.data_ptr(), lo, hi, total, begin, end)
         scanner.device_result()
         ptr, n_rec = scanner.verify_device(0)
-        if world > 1:
+        if use_dist:
             return ydist.gather_rows(ydist.records_to_rows(ptr, n_rec, dev))
         return n_rec
     for _ in range(max(args.warmup, 3)):
         verified_step()
-    if world > 1:
+    if use_dist:
         dist.barrier()
     torch.cuda.synchronize()
     t0 = time.perf_counter()
     for _ in range(args.steps):
         v_out = verified_step()
     torch.cuda.synchronize()
-    if world > 1:
+    if use_dist:
         dist.barrier()
     v_elapsed = time.perf_counter() - t0
-    if world > 1:
+    if use_dist:
         t = torch.tensor([v_elapsed], dtype=torch.float64,
                          device=dev if args.backend == "nccl" else "cpu")
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         v_elapsed = float(t.item())
     verified = {"ms_per_step": round(v_elapsed / args.steps * 1e3, 4),
                 "value": round(total * args.steps / v_elapsed / 1e9, 3), "unit": "GB/s",
-                "records": int(v_out if world == 1 else (v_out.shape[0] if v_out is not None else -1)),
+                "records": int(v_out if not use_dist else (v_out.shape[0] if v_out is not None else -1)),
                 "what": "scan + compaction + on-device pre-verification (yr_amd_verify_device)"
-                        + ("" if world == 1 else " of each rank's window + %s gather of the "
+                        + ("" if not use_dist else " of each rank's window + %s gather of the "
                            "{offset, pool index} records to rank 0"
                            % ("RCCL" if args.backend == "nccl" else args.backend))}
 
     run(args.warmup)
     for sc in scanners:
         sc.set_timing(True)
-    if world > 1:
+    if use_dist:
         dist.barrier()
     torch.cuda.synchronize()
     t0 = time.perf_counter()
     pos, kernel_ms = run(args.steps, True)
     torch.cuda.synchronize()
-    if world > 1:
+    if use_dist:
         dist.barrier()
     elapsed = time.perf_counter() - t0
     for sc in scanners:
         sc.set_timing(False)
     per_rank = None
-    if world > 1:
+    if use_dist:
         # attribution of an N > 1 step (max over ranks below): every rank's
         # own scan-kernel average (HIP events), its wall time and the wall time
         # it spent in the candidate gathers, so a slow rank and a slow gather
@@ -390,7 +460,7 @@ def main():
 
     check = None
     if rank == 0 and not args.no_check:
-        if world == 1:
+        if not use_dist:
             ptr, cnt = pos
             pos = torch.empty(max(cnt, 1), dtype=torch.int64, device=dev)
             memcpy(pos.data_ptr(), ptr, cnt * 8, 3)
@@ -415,11 +485,20 @@ def main():
 
     if rank == 0:
         traffic, traffic_src = load_traffic(shard)
-        cpu = cpu_par = None
+        cpu = cpu1 = cpu_par = None
         if world == 1 and not args.no_cpu:
-            cpu = cpu_baseline(args.rules, args.cpu_sample_mib, args.seed)
-            cpu_par = cpu_parallel(args.rules, args.cpu_sample_mib, args.seed,
-                                   min(16, os.cpu_count() or 1))
+            import oracle
+            sample = oracle.xorshift(args.cpu_sample_mib << 20, args.seed)
+            threads = args.cpu_threads or cpu_info()["affinity"]
+            # the CPU comparator: stock libyara on every CPU of the host this
+            # process may use (SURVEY.md §8d "nproc threads"); the 1-thread
+            # stock scan and the restatement's slice walkers beside it
+            cpu = cpu_stock_threads(args.rules, sample, args.seed, threads)
+            cpu1 = cpu_baseline(args.rules, sample, args.seed)
+            cpu_par = cpu_parallel(args.rules, sample, threads)
+            if cpu is None:
+                cpu, cpu1 = cpu1, None
+            del sample
         line = {
             "metric": "scanned GB/s per GPU (4 GiB buffer, 10k atoms) + bit-exact match-set vs CPU",
             "value": round(value, 3),
@@ -437,16 +516,18 @@ def main():
                                    "%.0f GiB per GPU%s" % (
                                        args.rules, {"B": 1000, "C": 10000, "E": 2000}.get(args.rules, 0),
                                        args.gib_per_gpu,
-                                       "" if world == 1 else ", one %d GiB buffer sharded "
+                                       "" if not use_dist else ", one %d GiB buffer sharded "
                                        "(shard + verify halos per GPU), RCCL gather of candidate "
                                        "lists" % (args.gib_per_gpu * world)),
-                       "bytes_per_gpu": shard, "parallelism": "shard%d" % world},
+                       "bytes_per_gpu": shard, "parallelism": "shard%d" % world,
+                       **({"dist_backend": args.backend} if use_dist else {})},
             "roofline": {"bound": "hbm", "achieved": round(achieved, 2), "peak": HBM_PEAK_GBS,
                          "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4),
                          "traffic": traffic,
                          "traffic_source": traffic_src,
                          "kernel": "scan_segments_kernel", "kernel_ms_avg": round(k_avg, 4)},
             "cpu_baseline": cpu,
+            "cpu_baseline_1thread": cpu1,
             "cpu_port_parallel": cpu_par,
             "preverify": preverify,
             "verified_step": verified,
@@ -456,7 +537,7 @@ def main():
         if per_rank is not None:
             line["multi"] = per_rank
         print(json.dumps(line), flush=True)
-    if world > 1:
+    if use_dist:
         dist.destroy_process_group()
 
 

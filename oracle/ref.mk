@@ -45,7 +45,8 @@ CLI := args common threading yara
 
 HOOKED_OBJS := $(filter-out $(OBJ)/scanner.o,$(OBJS)) $(OBJ)/scanner_hooked.o $(OBJ)/refhook.o
 
-all: $(OUT)/libyara_ref.so $(OUT)/libyara_ref_hooked.so $(OUT)/yara $(OUT)/yarac $(OUT)/refdump
+all: $(OUT)/libyara_ref.so $(OUT)/libyara_ref_hooked.so $(OUT)/yara $(OUT)/yarac $(OUT)/refdump \
+     $(OUT)/librefmt.so
 
 define OBJ_RULE
 $(OBJ)/$(subst /,_,$(1)).o: $(REF)/libyara/$(1).c | $(OBJ)
@@ -70,6 +71,12 @@ $(OUT)/libyara_ref_hooked.so: $(HOOKED_OBJS)
 $(OUT)/refdump: oracle/refdump.c $(OUT)/libyara_ref_hooked.so
 	$(CC) -O2 -D_GNU_SOURCE -Wall -I$(REF)/libyara/include -I$(REF)/libyara $< -o $@ \
 	  -L$(OUT) -lyara_ref_hooked -Wl,-rpath,'$$ORIGIN' -lpthread -lm
+
+# stock libyara, one scanner per thread over contiguous slices (bench.py's
+# multi-threaded CPU baseline)
+$(OUT)/librefmt.so: oracle/refmt.c $(OUT)/libyara_ref.so
+	$(CC) -O2 -fPIC -shared -D_GNU_SOURCE -Wall -I$(REF)/libyara/include -I$(REF)/libyara $< -o $@ \
+	  -L$(OUT) -lyara_ref -Wl,-rpath,'$$ORIGIN' -lpthread -lm
 
 $(OUT)/libyara_ref.so: $(OBJS)
 	$(CC) -shared -o $@ $(OBJS) -lpthread -lm

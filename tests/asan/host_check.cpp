@@ -14,7 +14,7 @@
 //                             must return (any error code), never fault
 //   host_check re <code.bin> every offset of a program blob through
 //                             yr_amd_re_code_extent (malformed programs)
-//   host_check copypool <jobs> <seed>
+//   host_check copypool <jobs> <seed> [first generation]
 //                             hostio.h CopyPool: <jobs> back-to-back copies
 //                             of 8-40 MiB (the parallel path), some with a copy
 //                             function that fails one chunk; every job must
@@ -185,8 +185,8 @@ static int fail_copy(void* user, void* dst, const void* src, size_t n) {
   return f->bad >= off && f->bad < off + n ? 1 : 0;
 }
 
-static int run_copypool(int jobs, uint64_t seed) {
-  yamd::CopyPool pool(7);
+static int run_copypool(int jobs, uint64_t seed, uint64_t first_gen) {
+  yamd::CopyPool pool(7, first_gen);
   const size_t max = 40u << 20;
   std::vector<uint8_t> src(max), dst(max);
   uint64_t x = seed * 0x9E3779B97F4A7C15ull + 1;
@@ -221,7 +221,8 @@ static int run_copypool(int jobs, uint64_t seed) {
 }
 
 int main(int argc, char** argv) {
-  if (argc >= 4 && !strcmp(argv[1], "copypool")) return run_copypool(atoi(argv[2]), strtoull(argv[3], 0, 10));
+  if (argc >= 4 && !strcmp(argv[1], "copypool"))
+    return run_copypool(atoi(argv[2]), strtoull(argv[3], 0, 10), argc >= 5 ? strtoull(argv[4], 0, 10) : 0);
   if (argc >= 3 && !strcmp(argv[1], "tables")) return run_tables(argv[2]);
   if (argc >= 5 && !strcmp(argv[1], "yarc")) return run_yarc(argv[2], atoi(argv[3]), strtoull(argv[4], 0, 10));
   if (argc >= 3 && !strcmp(argv[1], "re")) return run_re(argv[2]);

@@ -72,3 +72,12 @@ def test_copy_pool_under_sanitizers():
     chunk of the next job)."""
     out = _run("copypool", 60, 7)
     assert "60 copy jobs" in out
+
+
+def test_copy_pool_across_the_generation_wrap():
+    """The ticket holds 24 bits of the job generation (hostio.h kGenShift = 40):
+    jobs started 20 before the wrap point run on through it (a
+    full-width generation no longer matched its own ticket from job 2^24 on and
+    copy() waited forever)."""
+    out = _run("copypool", 40, 11, (1 << 24) - 20)
+    assert "40 copy jobs" in out

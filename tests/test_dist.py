@@ -41,7 +41,7 @@ def _worker(rank, world, port, n, period, q, no_gather=False):
         out = ydist.gather_positions(local)
         # 32-bit offsets from each rank's shard begin (bench.py's N > 1 gather)
         begins = [ydist.shard_bounds(n, world, r, align=period)[0] for r in range(world)]
-        out32 = ydist.gather_positions(local, begins=begins)
+        out32 = ydist.gather_positions(local, begins=begins, end=n)
         # two-column rows (the records path: {offset, pool index})
         rows = torch.stack([local, local * 3 + rank], 1)
         out2 = ydist.gather_rows(rows)
@@ -70,6 +70,56 @@ def test_sharded_scan_gathers_full_stream(world, no_gather):
     for p in ps:
         p.join(timeout=60)
     assert ok
+
+
+def _edge_worker(rank, world, port, q):
+    """Synthetic positions at every shard's edges (rank 0: position 0), gathered
+    as 32-bit offsets to a dst other than rank 0, and a block whose shards
+    exceed 2^32 positions (the int64 fallback) -- ADVICE r04."""
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        ok = True
+        for n in ((3 << 20) + 77, (9 << 30) + 5, (8 << 32) + 3):
+            bounds = [ydist.shard_bounds(n, world, r) for r in range(world)]
+            begins = [b for b, _ in bounds]
+            b, e = bounds[rank]
+            lo = 0 if rank == 0 else b + 1
+            local = torch.tensor(sorted({lo, lo + 1, (lo + e) // 2, e - 1, e}), dtype=torch.int64)
+            for dst in range(world):
+                out = ydist.gather_positions(local, dst=dst, begins=begins, end=n)
+                if rank == dst:
+                    want = []
+                    for r, (rb, re_) in enumerate(bounds):
+                        rl = 0 if r == 0 else rb + 1
+                        want += sorted({rl, rl + 1, (rl + re_) // 2, re_ - 1, re_})
+                    ok &= out.tolist() == want
+                else:
+                    ok &= out is None
+        with_bad = torch.tensor([0 if rank else 1 << 40], dtype=torch.int64)
+        try:
+            ydist.gather_positions(with_bad, begins=[0] * world, end=1 << 20)
+            ok = False
+        except ValueError:
+            pass
+        q.put((rank, bool(ok)))
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("world", [2, 3])
+def test_gather_positions_edges_and_large_shards(world):
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = 29440 + world
+    ps = [ctx.Process(target=_edge_worker, args=(r, world, port, q)) for r in range(world)]
+    for p in ps:
+        p.start()
+    res = dict(q.get(timeout=300) for _ in range(world))
+    for p in ps:
+        p.join(timeout=60)
+    assert all(res.values()), res
 
 
 def test_shard_bounds_cover_block():

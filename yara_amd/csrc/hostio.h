@@ -48,7 +48,9 @@ class CopyPool {
  public:
   static constexpr size_t kChunk = 4u << 20;
 
-  explicit CopyPool(unsigned helpers) {
+  // first_gen: the generation the first job follows (tests start it next to
+  // the ticket's wrap point)
+  explicit CopyPool(unsigned helpers, uint64_t first_gen = 0) : gen_(first_gen) {
     for (unsigned i = 0; i < helpers; ++i) th_.emplace_back([this] { loop(); });
   }
   ~CopyPool() {
@@ -68,7 +70,11 @@ class CopyPool {
     Job j;
     {
       std::lock_guard<std::mutex> lk(mu_);
-      job_ = Job{dst, src, size, fn, ++gen_};
+      // the ticket keeps 64 - kGenShift bits of the generation: the job's
+      // generation is stored and compared in that width, so it wraps with the
+      // ticket (a full-width generation stopped matching its own
+      // ticket after 2^24 jobs and every claim loop returned at once)
+      job_ = Job{dst, src, size, fn, ++gen_ & kGenMask};
       j = job_;
       done_ = 0;
       failed_ = false;
@@ -84,6 +90,7 @@ class CopyPool {
  private:
   // ticket = generation << kGenShift | next chunk index
   static constexpr unsigned kGenShift = 40;
+  static constexpr uint64_t kGenMask = (1ull << (64 - kGenShift)) - 1;
   struct Job {
     uint8_t* dst = nullptr;
     const uint8_t* src = nullptr;
@@ -126,7 +133,7 @@ class CopyPool {
   std::mutex mu_;
   std::condition_variable cv_, done_cv_;
   Job job_;
-  uint64_t gen_ = 0;
+  uint64_t gen_ = 0;   // full width (the helpers' wake-up test); jobs use gen_ & kGenMask
   size_t done_ = 0;
   bool failed_ = false;
   bool stop_ = false;

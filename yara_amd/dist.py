@@ -101,14 +101,16 @@ def gather_rows(local: torch.Tensor, group=None, dst: int = 0, split: bool = Fal
     return torch.cat([b[:c] for b, c in zip(bufs, counts)])
 
 
-def gather_positions(local: torch.Tensor, group=None, dst: int = 0, begins=None):
+def gather_positions(local: torch.Tensor, group=None, dst: int = 0, begins=None, end=None):
     """Gather every rank's ascending int64 candidate positions to `dst`.
 
-    With ``begins`` (every rank's shard begin, its positions in (begin,
-    begin + 2^32]: shards of at most 4 GiB) each rank sends p - begin - 1 as a
-    32-bit word -- half the bytes over the links -- and `dst` restores them;
-    its own positions it keeps as they are (rank 0's shard holds position 0,
-    which has no such offset)."""
+    With ``begins`` (every rank's shard begin) and ``end`` (the block size, the
+    last rank's end) each rank sends its positions as 32-bit offsets from its
+    own base -- half the bytes over the links -- and `dst` restores them.  Rank
+    r's positions lie in (begin_r, end_r] (rank 0: [0, end_0]), so the base is
+    begin_r + 1 (rank 0: 0) and a shard of at most 2^32 positions fits.  If any
+    shard is larger, every rank takes the int64 gather instead (the decision is
+    made from the arguments alone, so all ranks take the same branch)."""
     if begins is None:
         out = gather_rows(local.reshape(-1, 1).to(torch.int64), group, dst)
         return None if out is None else out.reshape(-1)
@@ -116,17 +118,24 @@ def gather_positions(local: torch.Tensor, group=None, dst: int = 0, begins=None)
     rank = dist.get_rank(group)
     if len(begins) != world:
         raise ValueError("one shard begin per rank")
-    off = (local.to(torch.int64) - (begins[rank] + 1)).to(torch.int32)   # (wraps past 2^31)
+    if end is None:
+        raise ValueError("gather_positions(begins=...) needs the block size (end)")
+    ends = list(begins[1:]) + [end]
+    bases = [0] + [b + 1 for b in begins[1:]]
+    # positions of rank r: [bases[r], ends[r]] -- offsets up to ends[r] - bases[r]
+    if any(e - b > 0xFFFFFFFF for b, e in zip(bases, ends)):
+        out = gather_rows(local.reshape(-1, 1).to(torch.int64), group, dst)
+        return None if out is None else out.reshape(-1)
+    loc = local.to(torch.int64)
+    if loc.numel() and (int(loc.min()) < bases[rank] or int(loc.max()) > ends[rank]):
+        raise ValueError("rank %d: positions outside its shard [%d, %d]"
+                         % (rank, bases[rank], ends[rank]))
+    off = (loc - bases[rank]).to(torch.int32)   # (wraps past 2^31; restored below)
     rows = gather_rows(off.reshape(-1, 1), group, dst, split=True)
     if rows is None:
         return None
-    parts = []
-    for r, part in enumerate(rows):
-        if r == rank:
-            parts.append(local.to(torch.int64).to(part.device))
-        else:
-            parts.append((part.reshape(-1).to(torch.int64) & 0xFFFFFFFF) + (begins[r] + 1))
-    return torch.cat(parts)
+    return torch.cat([(part.reshape(-1).to(torch.int64) & 0xFFFFFFFF) + bases[r]
+                      for r, part in enumerate(rows)])
 
 
 def records_to_rows(d_records: int, count: int, device) -> torch.Tensor:
