@@ -13,8 +13,10 @@
  *       RE_OPCODE_MATCH).
  *
  *   refdump scan <rules.yar> <data> <out_prefix> [block_size overlap]
- *       <data> is a file path or "xs:<seed>:<size>" (SURVEY.md App. A
- *       xorshift64 generator).  Runs stock yr_rules_scan_mem (or
+ *       <data> is a file path, "xs:<seed>:<size>" (SURVEY.md App. A
+ *       xorshift64 generator) or "xst:<state>:<size>" (the same generator
+ *       continued from a raw state, e.g. oracle.xorshift_state(seed, offset):
+ *       bytes [offset, offset + size) of the seed's stream).  Runs stock yr_rules_scan_mem (or
  *       yr_rules_scan_mem_blocks with the tests/util.c-style overlapping block
  *       iterator) and records
  *         <out>.verify   every call the hot loop makes to yr_scan_verify_match:
@@ -259,8 +261,29 @@ static void xorshift_fill(uint8_t* buf, size_t n, uint64_t seed)
   }
 }
 
+static void xorshift_continue(uint8_t* buf, size_t n, uint64_t x)
+{
+  for (size_t i = 0; i < n; i++)
+  {
+    x ^= x << 13;
+    x ^= x >> 7;
+    x ^= x << 17;
+    buf[i] = (uint8_t) (x >> 24);
+  }
+}
+
 static uint8_t* load_data(const char* spec, size_t* size)
 {
+  if (strncmp(spec, "xst:", 4) == 0)
+  {
+    unsigned long long state, n;
+    if (sscanf(spec + 4, "%llu:%llu", &state, &n) != 2) die("bad xst spec", 0);
+    uint8_t* b = malloc(n ? n : 1);
+    if (!b) die("oom", 0);
+    xorshift_continue(b, n, state);
+    *size = n;
+    return b;
+  }
   if (strncmp(spec, "xs:", 3) == 0)
   {
     unsigned long long seed, n;

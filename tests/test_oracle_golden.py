@@ -74,3 +74,45 @@ def test_reference_table_stats_match_survey():
     assert (t["C"]["slots"], t["C"]["pool"]) == (60136, 11530)
     assert (t["E"]["slots"], t["E"]["pool"]) == (58337, 17000)
     assert t["root"]["root_list"] == 1 and t["C"]["root_list"] == 0
+
+
+def test_config_d_shards_pinned_to_stock():
+    """Config D's per-shard goldens (tests/golden/config_d.json) were computed
+    by the stock reference libyara (refdump over each shard's window) and by
+    the oracle restatement, asserted equal (make_config_d.py); shard 0 is the
+    stock golden C_4G."""
+    import json
+    import os
+    from conftest import GOLDEN
+    with open(os.path.join(GOLDEN, "config_d.json")) as f:
+        d = json.load(f)
+    assert d["provenance"] == "stock" and len(d["shards"]) == 8
+    c4 = golden()["cases"]["C_4G"]
+    assert (d["shards"][0]["count"], d["shards"][0]["sha"]) == (c4["candidate_count"],
+                                                               c4["candidate_sha"])
+
+
+def test_oracle_equals_stock_deep_in_config_d(tmp_path):
+    """A live cross-check where the reference build exists (the build
+    container): stock libyara (refdump, "xst:" jump-ahead input) and the oracle
+    give the same candidates over 32 MiB starting 28 GiB into config D's
+    block (shard 7)."""
+    import os
+    import subprocess
+    import gen_rules
+    from conftest import REPO
+    refdump = os.path.join(REPO, "oracle", "_ref", "refdump")
+    if not os.path.exists(refdump):
+        pytest.skip("oracle/_ref/refdump not built (no reference tree)")
+    lo, n = (28 << 30) - 64, (32 << 20) + 64
+    (tmp_path / "C.yar").write_text(gen_rules.gen("C"))
+    subprocess.run([refdump, "scan", str(tmp_path / "C.yar"),
+                    "xst:%d:%d" % (oracle.xorshift_state(1, lo), n), str(tmp_path / "s")],
+                   check=True, stdout=subprocess.DEVNULL)
+    rec = np.fromfile(str(tmp_path / "s.verify"), dtype=[("b", "<u8"), ("p", "<u8"), ("k", "<u4")])
+    stock = np.unique(rec["p"])
+    stock = stock[stock > 64]
+    cand = oracle.candidates(ref_tables("C"), oracle.xorshift_at(n, 1, lo)).astype(np.uint64)
+    cand = cand[cand > 64]
+    assert stock.size > 1000
+    np.testing.assert_array_equal(stock, cand)

@@ -117,10 +117,8 @@ __host__ __device__ inline FilterProbe filter_probe_right(uint32_t w3) {
 constexpr uint32_t kExactBm1 = 0;
 constexpr uint32_t kExactBm2 = 8;
 constexpr uint32_t kExactFl = 8 + 2048;
-#ifndef YAMD_FL_LOG2
-#define YAMD_FL_LOG2 15
-#endif
-constexpr uint32_t kExactFlWords = 1u << YAMD_FL_LOG2;
+constexpr uint32_t kExactFlLog2 = 15;
+constexpr uint32_t kExactFlWords = 1u << kExactFlLog2;
 constexpr uint32_t kExactHeadWords = kExactFl + kExactFlWords;
 constexpr uint32_t kExactZero4 = 1u;   // flag: the 4-byte key 0x00000000 exists
 
@@ -133,30 +131,20 @@ constexpr uint32_t kExactZero4 = 1u;   // flag: the 4-byte key 0x00000000 exists
 // The hashes are 24 x 24-bit products (low 32 bits), so the device uses the
 // full-rate v_mul_u32_u24 rather than the quarter-rate v_mul_lo_u32; the
 // 4-byte bit folds the window's first byte into the top byte of the other 3.
-// (YAMD_FL_MULHI=1: both bits over all 32 from the high halves of 24-bit
-// products, 6 instead of 12 instructions per deferred hit -- but config C's
-// kernel 3 % slower in one-process A/B, profiles/r04_ab_inproc.json; off.)
+// (Both bits over all 32 from the high halves of 24-bit products -- 6 instead
+// of 12 instructions per deferred hit -- measured config C's kernel 3 % slower
+// in one-process A/B, profiles/r04_ab_inproc.json.)
 __host__ __device__ inline uint32_t fl_mul24(uint32_t a, uint32_t b) {
   return (a & 0xFFFFFFu) * (b & 0xFFFFFFu);
 }
-__host__ __device__ inline uint32_t fl_mulhi24(uint32_t a, uint32_t b) {
-  return (uint32_t)(((uint64_t)(a & 0xFFFFFFu) * (uint64_t)(b & 0xFFFFFFu)) >> 32);
-}
 __host__ __device__ inline uint32_t fl_word(uint32_t w4) {
-  return fl_mul24(w4 >> 8, 0x9E3779u) >> (32 - YAMD_FL_LOG2);
+  return fl_mul24(w4 >> 8, 0x9E3779u) >> (32 - kExactFlLog2);
 }
-#ifndef YAMD_FL_MULHI
-#define YAMD_FL_MULHI 0
-#endif
-#if YAMD_FL_MULHI
-__host__ __device__ inline uint32_t fl_bit3(uint32_t w4) { return fl_mulhi24(w4 >> 8, 0xEBCA77u) & 31u; }
-__host__ __device__ inline uint32_t fl_bit4(uint32_t w4) { return fl_mulhi24(w4, 0xB2AE35u) & 31u; }
-#else   // (round 3: 3-byte keys in bits 0..15, 4-byte keys in 16..31)
+// 3-byte keys in bits 0..15, 4-byte keys in 16..31
 __host__ __device__ inline uint32_t fl_bit3(uint32_t w4) { return fl_mul24(w4 >> 8, 0xEBCA77u) >> 28; }
 __host__ __device__ inline uint32_t fl_bit4(uint32_t w4) {
   return 16u + (fl_mul24((w4 >> 8) ^ (w4 << 16), 0xB2AE35u) >> 28);
 }
-#endif
 
 __host__ __device__ inline uint32_t bucket_hash1(uint32_t key) {
   uint32_t h = key * 0x9E3779B1u;

@@ -128,34 +128,23 @@ __device__ __forceinline__ bool first_level(uint32_t w4, const ScanParams& p) {
 
 // Ring entry layout (24 bytes, WaveQueue): the 4 bytes before the lane at
 // kEntCtx, the lane's 16 bytes at kEntData, the lane index word at kEntIdx.
-// Context first (YAMD_RING_CTX_FIRST, the default): the 20 bytes are in stream
-// order, so the 4 bytes ending at any lane byte are one unaligned LDS dword
-// (gfx950 runs LDS in unaligned mode; the compiler emits one ds_read_b32).
-#ifndef YAMD_RING_CTX_FIRST
-#define YAMD_RING_CTX_FIRST 1
-#endif
-// (YAMD_RING_CTX_FIRST=2: the index word first, then the context and the 16
-// bytes, 8-byte aligned: an append writes two qwords and a qword pair)
-constexpr uint32_t kEntCtx = YAMD_RING_CTX_FIRST == 2 ? 4u : YAMD_RING_CTX_FIRST ? 0u : 16u;
-constexpr uint32_t kEntData = YAMD_RING_CTX_FIRST == 2 ? 8u : YAMD_RING_CTX_FIRST ? 4u : 0u;
-constexpr uint32_t kEntIdx = YAMD_RING_CTX_FIRST == 2 ? 0u : 20u;
+// Context first: the 20 bytes are in stream order, so the 4 bytes ending at
+// any lane byte are one unaligned LDS dword (gfx950 runs LDS in unaligned
+// mode; the compiler emits one ds_read_b32).
+constexpr uint32_t kEntCtx = 0u;
+constexpr uint32_t kEntData = 4u;
+constexpr uint32_t kEntIdx = 20u;
 typedef uint32_t u32_una __attribute__((aligned(1)));
 
 // Lane byte j of a ring entry (j = -4 .. -1: the context bytes).
 __device__ __forceinline__ uint32_t entry_byte_addr(uint32_t ent, int32_t j) {
-  return YAMD_RING_CTX_FIRST ? ent + kEntData + (uint32_t)j : (j >= 0 ? ent + (uint32_t)j : ent + 20u + j);
+  return ent + kEntData + (uint32_t)j;
 }
 
 // The 4 bytes ending at lane byte j (0..15) of a ring entry: lane bytes
 // j-3 .. j (the context bytes for j < 3).
 __device__ __forceinline__ uint32_t window4(uint32_t ent, uint32_t j) {
-#if YAMD_RING_CTX_FIRST
   return *reinterpret_cast<const __attribute__((address_space(3))) u32_una*>((uintptr_t)(ent + kEntData + j - 3));
-#else
-  const uint32_t o = j - 3, lo = j >= 3 ? ent + (o & ~3u) : ent + 16;
-  const uint32_t hi = j >= 3 ? lo + 4 : ent, sh = j >= 3 ? (o & 3u) : j + 1;
-  return __builtin_amdgcn_alignbyte(lds_load<uint32_t>(hi), lds_load<uint32_t>(lo), sh);
-#endif
 }
 
 // Lane byte (0..15) of bit b of a tile hit mask: bit 8n + r <=> byte 4n + r.
@@ -272,19 +261,6 @@ constexpr bool kByteKeyAblation = MODE == 24 || MODE == 25;
 // a pending entry becomes the output entry: certain iff its key place is set
 constexpr uint32_t kCertainMask = 7u << kOutKeyShift;
 static_assert(kSegment <= kOutOffsetMask + 1u, "segment offsets must leave the top bits free");
-
-// Byte-key drains without divergent branches (YAMD_BK_FLAT=1): a hit's
-// window / certain-candidate bytes are computed by selects from one unaligned
-// LDS read (the entry of a kernel that keeps the next lane's two bytes holds
-// them right after the lane's 16, its unit index in the top half:
-// kIdxHigh), instead of per-hit branches on "certain" and on "the bytes reach
-// past the lane".
-#ifndef YAMD_BK_FLAT
-#define YAMD_BK_FLAT 0
-#endif
-template <int MODE>
-constexpr bool kIdxHigh = YAMD_BK_FLAT && kNextBytes<MODE>;
-static_assert(!YAMD_BK_FLAT || YAMD_RING_CTX_FIRST == 1, "flat byte-key drains read the context-first entry");
 
 // b one of the (up to 8, repeated to fill) bytes of x0, x1: zero-byte test
 __device__ __forceinline__ bool excluded(uint32_t b, uint32_t x0, uint32_t x1) {
@@ -516,11 +492,7 @@ __device__ __forceinline__ uint32_t pair_keys_mask(const uint32_t (&S)[6], const
 // Exact zero-byte flags (bit 7 of each byte of z_d) OR-ed over the keys, then
 // each dword's four flags gathered by one v_dot4_u32_u8 against the place
 // values 2^r (two dwords per chain: bytes of 0x80 times 1..128 stay below 2^16).
-#ifndef YAMD_BK_DOT
-#define YAMD_BK_DOT 1
-#endif
 __device__ __forceinline__ uint32_t byte_keys_mask(const uint32_t (&S)[6], const ScanParams& p) {
-#if YAMD_BK_DOT
   uint32_t z[4] = {0u, 0u, 0u, 0u};
 #pragma unroll
   for (uint32_t k = 0; k < kMaxByteKeys; ++k) {
@@ -541,19 +513,6 @@ __device__ __forceinline__ uint32_t byte_keys_mask(const uint32_t (&S)[6], const
                                              __builtin_amdgcn_udot4(z[2] & 0x80808080u, 0x08040201u, 0u, false),
                                              false);
   return (lo >> 7) | (hi << 1);   // (x 128: bytes 0..7 in bits 7..14, 8..15 in 15..22)
-#else
-  uint32_t m = 0;
-  for (uint32_t k = 0; k < p.n_byte_keys; ++k) {
-    const uint32_t v = ((p.byte_keys >> (8 * k)) & 0xFFu) * 0x01010101u;
-#pragma unroll
-    for (int d = 0; d < 4; ++d) {
-      const uint32_t t = S[1 + d] ^ v;
-      const uint32_t z = ~(((t & 0x7F7F7F7Fu) + 0x7F7F7F7Fu) | t) & 0x80808080u;   // exact
-      m |= (((z >> 7) & 1u) | ((z >> 14) & 2u) | ((z >> 21) & 4u) | ((z >> 28) & 8u)) << (4 * d);
-    }
-  }
-  return m;
-#endif
 }
 
 
@@ -562,87 +521,38 @@ __device__ __forceinline__ uint32_t byte_keys_mask(const uint32_t (&S)[6], const
 // so the arbiter issues the waves that keep the input stream going first while
 // a drain's long VALU burst fills the gaps (C -1.3 to -2.5 %, rx -2 %, B/E
 // within noise: profiles/r03_copy_prio_ab.json, r03_prio_ab.json,
-// r03_prio3_ab.json).  1 = drains only, 0 = off (A/B builds).
-#ifndef YAMD_PRIO
-#define YAMD_PRIO 2
-#endif
-// Kernel variants whose drains defer their first-level loads (WaveQueue).
-#ifndef YAMD_DEFER_FL
-#define YAMD_DEFER_FL 1
-#endif
+// r03_prio3_ab.json).
+//
+// Branch-weight hints on the tile step's rare paths (the deferred-drain
+// completion, an append that fills the ring, a tile without hits): the common
+// path falls through with no taken branch (C -1.2 %).
+#define YAMD_EXPECT(c, v) __builtin_expect((c), (v))
 // The product and byte-key kernels hold the deferred words' registers until
 // the next loads are issued (issue_first_level): C 0.850 -> 0.835-0.843 ms,
 // the 1-byte-key sets 1.5-2 % faster; the even-position kernels not (B 2.7 %
 // slower, E equal), profiles/r02_hold_fl_ab.json.
-#ifndef YAMD_HOLD_FL
-#define YAMD_HOLD_FL 1
-#endif
-// The lane-0 window context by a second DPP move (tile_context): frees the
-// lane-0 SGPR mask, which the byte-key kernel spilled (two v_readlane per
-// tile): rx 1.20 -> 1.175 ms, short/fuzz 1-2 % faster, C and B/E equal
-// (profiles/r02_carry_dpp2_ab.json).
-#ifndef YAMD_CARRY_DPP2
-#define YAMD_CARRY_DPP2 1
-#endif
-// Byte-key kernels: a drain whose hits are all certain candidates, with
-// nothing pending, writes them straight to the segment's output (drain()).
-// Off: short 3.6 % faster without it, rx equal (profiles/r04_ab_inproc_h2.json).
-#ifndef YAMD_BK_DIRECT
-#define YAMD_BK_DIRECT 0
-#endif
-// A/B switches of this round's drain changes (profiles/r04_*): the main loop's
-// drains skip the partial-tile mask, the drain re-test shares one v_perm
-// between two pairs, drain_complete orders its hits by two ballots.
-#ifndef YAMD_ASYNC_NO_TAIL
-#define YAMD_ASYNC_NO_TAIL 1
-#endif
-#ifndef YAMD_DRAIN_Y2
-#define YAMD_DRAIN_Y2 1
-#endif
-// Deferring drains without divergent branches (kernels other than the
-// even-filter byte-key ones, which measured 0.5-1.4 % slower with them): the
-// tile loop loses a loop-carried lane mask (six SALU per tile); C -0.6 %,
-// fuzz0 / fuzz3 -3 % (profiles/r04_ab_inproc.json call h22)
-#ifndef YAMD_ASYNC_FLAT
-#define YAMD_ASYNC_FLAT 1
-#endif
-// Branch-weight hints on the tile step's append (YAMD_BRANCH_HINTS: the block
-// layout then lets the common path fall through)
-#ifndef YAMD_BRANCH_HINTS
-#define YAMD_BRANCH_HINTS 1
-#endif
-#define YAMD_EXPECT(c, v) (YAMD_BRANCH_HINTS ? __builtin_expect((c), (v)) : (c))
-#ifndef YAMD_DC_BALLOT
-#define YAMD_DC_BALLOT 1
-#endif
 template <int MODE>
-constexpr bool kHoldFl = YAMD_HOLD_FL && !kEven<MODE>;
-// The byte-key kernels run only for tables with 1-byte keys (launch_scan), so
-// their drains never defer (the deferral needs len_mask & 6 == 0): with
-// YAMD_BK_NO_DEFER they carry none of its per-tile machinery (the two
-// first-level loads, the deferred-drain test).
-#ifndef YAMD_BK_NO_DEFER
-#define YAMD_BK_NO_DEFER 1
-#endif
+constexpr bool kHoldFl = !kEven<MODE>;
+// Kernel variants whose drains defer their first-level loads (WaveQueue).  The
+// byte-key kernels run only for tables with 1-byte keys (launch_scan), so
+// their drains never defer (the deferral needs len_mask & 6 == 0): they carry
+// none of its per-tile machinery (the two first-level loads, the
+// deferred-drain test): rx -4.7 %, short -4.6 % (profiles/r04_ab_inproc.json h23).
 template <int MODE>
-constexpr bool kDeferFl =
-    YAMD_DEFER_FL && kAbl<MODE> != 1 &&
-    (MODE == 0 || MODE == 12 || kByteKeys<MODE> || kEven<MODE> || kByteKeyAblation<MODE>) &&
-    !(YAMD_BK_NO_DEFER && (kByteKeys<MODE> || kByteKeyAblation<MODE>));
+constexpr bool kDeferFl = kAbl<MODE> != 1 && (MODE == 0 || MODE == 12 || kEven<MODE>) &&
+                          !(kByteKeys<MODE> || kByteKeyAblation<MODE>);
 // Byte-key drains re-test the filter and the 2-byte keys only when some tile
 // queued since the last drain passed them in stage 1 (a per-lane OR, one
 // v_or per tile, balloted once per drain): rx's drains skip ~90 of their ~140
 // VALU nearly always (its ring holds 1-byte-key hits).
-#ifndef YAMD_BK_SKIPF
-#define YAMD_BK_SKIPF 1
-#endif
-#ifndef YAMD_WIDE   // (wide steps, below)
-#define YAMD_WIDE 0
-#endif
 template <int MODE>
-constexpr bool kBkSkipF = YAMD_BK_SKIPF && !YAMD_WIDE && kByteKeys<MODE> && kAbl<MODE> == 0;
+constexpr bool kBkSkipF = kByteKeys<MODE> && kAbl<MODE> == 0;
+// Deferring drains without divergent branches (kernels other than the
+// even-filter byte-key ones, which measured 0.5-1.4 % slower with them): the
+// tile loop loses a loop-carried lane mask (six SALU per tile); C -0.6 %,
+// fuzz0 / fuzz3 -3 % (profiles/r04_ab_inproc.json call h22)
 template <int MODE>
-constexpr bool kAsyncFlat = YAMD_ASYNC_FLAT && !(kEven<MODE> && kByteKeys<MODE>);
+constexpr bool kAsyncFlat = !(kEven<MODE> && kByteKeys<MODE>);
 
 // The output entry of a certain candidate (its last byte a 1-byte key) at lane
 // byte j of ring entry ent: it needs no window for the exact check, so the scan
@@ -655,17 +565,6 @@ template <int MODE>
 __device__ __forceinline__ void certain_entry(const ScanParams& p, uint32_t ent, uint32_t j,
                                               uint32_t& x, uint32_t& y) {
   const uint32_t li = lds_load<uint32_t>(ent + kEntIdx);
-  if constexpr (kIdxHigh<MODE>) {   // lane bytes 16, 17 follow byte 15 in the entry
-    const uint32_t e = min(j + p.kx_end, ((li >> 16) & (kWave - 1)) != kWave - 1 ? 16u : 14u);
-    x = window4(ent, e);
-    y |= (uint32_t)lds_load<uint8_t>(entry_byte_addr(ent, (int32_t)e + 1)) << kOutByteShift |
-         (j + 5 - e) << kOutKeyShift;
-    if (p.kx_deep != 0u) {
-      const uint32_t b = lds_load<uint8_t>(entry_byte_addr(ent, (int32_t)j - 1));
-      if (excluded(b, p.kd_x0[0], p.kd_x1[0])) y |= kOutDeep;
-    }
-    return;
-  }
   const uint32_t e =
       min(j + p.kx_end, kNextBytes<MODE> && (li & (kWave - 1)) != kWave - 1 ? 16u : 14u);
   uint32_t b5;
@@ -684,7 +583,7 @@ __device__ __forceinline__ void certain_entry(const ScanParams& p, uint32_t ent,
   }
 }
 
-// Byte-key kernels, YAMD_BK_RESOLVE=1: a drain's hits go to the pending list
+// Byte-key kernels: a drain's hits go to the pending list
 // RAW (the ring entry, the lane byte, a certain flag: one LDS store per hit in
 // the per-lane loop, whose trip count is the wave's largest per-lane hit
 // count), and the window / certain-candidate bytes are then computed for the
@@ -693,11 +592,8 @@ __device__ __forceinline__ void certain_entry(const ScanParams& p, uint32_t ent,
 // gpurun h7, h8): rx -1.5 %, short -2.5 to -3.3 %, fuzz0 / fuzz3 within 1 %.
 // (A first single-order call had it 5 % slower: a per-process placement
 // offset, DESIGN.md section 5 "Measurement method".)
-#ifndef YAMD_BK_RESOLVE
-#define YAMD_BK_RESOLVE 1
-#endif
 template <int MODE>
-constexpr bool kBkResolve = YAMD_BK_RESOLVE && kByteKeys<MODE>;
+constexpr bool kBkResolve = kByteKeys<MODE>;
 template <int MODE>
 __device__ __forceinline__ void resolve_pending(const ScanParams& p, WaveQueue& q, uint32_t lane,
                                                 uint32_t from) {
@@ -724,7 +620,6 @@ __device__ __forceinline__ void drain_complete(const ScanParams& p, WaveQueue& q
   // each lane's a-hit precedes its b-hit: lane L's first slot is the number of
   // a- and b-hits in the lanes below it (two ballots and their mbcnts instead
   // of a DPP scan)
-#if YAMD_DC_BALLOT
   const uint64_t ma = __ballot(ha), mb = __ballot(hb);
   const uint32_t total = (uint32_t)(__popcll(ma) + __popcll(mb));
   if (total == 0) return;
@@ -737,14 +632,6 @@ __device__ __forceinline__ void drain_complete(const ScanParams& p, WaveQueue& q
                                 __builtin_amdgcn_mbcnt_hi((uint32_t)(ma >> 32),
                                                           __builtin_amdgcn_mbcnt_lo((uint32_t)ma, q.pend_n))));
   const uint32_t i0 = below, i1 = i0 + (uint32_t)ha;
-#else
-  const uint32_t c = (uint32_t)ha + (uint32_t)hb;
-  const uint32_t incl = wave_inclusive_scan(c);
-  const uint32_t total = __builtin_amdgcn_readlane(incl, kWave - 1);
-  if (total == 0) return;
-  const uint32_t end = q.pend_n + total;
-  const uint32_t i0 = q.pend_n + incl - c, i1 = i0 + (uint32_t)ha;
-#endif
   for (uint32_t base = 0;; base += kWave) {
     if (ha && i0 - base < kWave) lds_store2(q.pend + 8 * (i0 - base), q.wa, q.oa);
     if (hb && i1 - base < kWave) lds_store2(q.pend + 8 * (i1 - base), q.wb, q.ob);
@@ -778,7 +665,6 @@ __device__ __forceinline__ void drain(const ScanParams& p, WaveQueue& q, uint32_
   __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
   uint32_t maybe = 0, off0 = 0, m = 0;   // m: bit j = lane byte j passes the filter
   uint32_t kmask = 0;                    // bit j = lane byte j is a 1-byte key (certain)
-  uint32_t ridx = 0;                     // (byte-key kernels: the entry's index word)
   const uint32_t ent = q.ring + lane * (kQueueEntryWords * 4);
   if (lane < n) {
     // the entry's 16 positions again, now with a per-position result: the
@@ -786,18 +672,9 @@ __device__ __forceinline__ void drain(const ScanParams& p, WaveQueue& q, uint32_
     const u32x2 e01 = lds_load<u32x2>(ent);
     const u32x2 e23 = lds_load<u32x2>(ent + 8);
     const u32x2 e45 = lds_load<u32x2>(ent + 16);
-#if YAMD_RING_CTX_FIRST == 2
-    const uint32_t S[6] = {e01.y, e23.x, e23.y, e45.x, e45.y, 0u};
-    const uint32_t eidx = e01.x;
-#elif YAMD_RING_CTX_FIRST
     const uint32_t S[6] = {e01.x, e01.y, e23.x, e23.y, e45.x, 0u};
     const uint32_t eidx = e45.y;
-#else
-    const uint32_t S[6] = {e45.x, e01.x, e01.y, e23.x, e23.y, 0u};
-    const uint32_t eidx = e45.y;
-#endif
-    off0 = (kIdxHigh<MODE> ? eidx >> 16 : eidx & 0xFFFFu) * kBytesPerLane;
-    if constexpr (kByteKeys<MODE>) ridx = eidx;
+    off0 = (eidx & 0xFFFFu) * kBytesPerLane;
     if (need_f) {
       if constexpr (kEven<MODE>) {
         m = even_mask<kEvenHash<MODE>>(S);
@@ -812,7 +689,7 @@ __device__ __forceinline__ void drain(const ScanParams& p, WaveQueue& q, uint32_
     }
     // the segment's partial last tile (its entries are appended after the main
     // loop's last drain, so only the final drain can hold them)
-    if ((!YAMD_ASYNC_NO_TAIL || !kAsync) && off0 + kBytesPerLane > seg_len) {
+    if (!kAsync && off0 + kBytesPerLane > seg_len) {
       const uint32_t lim = off0 >= seg_len ? 0u : seg_len - off0;
       m &= lim >= 16u ? 0xFFFFu : (1u << lim) - 1u;
     }
@@ -879,41 +756,12 @@ __device__ __forceinline__ void drain(const ScanParams& p, WaveQueue& q, uint32_
   }
   const uint32_t total = __builtin_amdgcn_readlane(incl, kWave - 1);
   if (total == 0) return;
-#if YAMD_BK_DIRECT
-  if constexpr (kByteKeys<MODE> && kAbl<MODE> == 0) {
-    // Only certain candidates (1-byte keys) and nothing pending: they need no
-    // probe, so each lane writes its own straight to the segment's output at
-    // its place in the drain's order -- no pending-list round trip (the
-    // dense sets' drains are nearly all of this kind).
-    if (q.pend_n == 0 && __ballot((maybe & ~kmask) != 0u) == 0) {
-      uint32_t o = found + incl - c;
-      while (maybe != 0u) {
-        const uint32_t j = (uint32_t)__builtin_ctz(maybe);
-        maybe &= maybe - 1;
-        uint32_t y = off0 + j, x;
-        certain_entry<MODE>(p, ent, j, x, y);
-        if (o < p.seg_cap) {
-          out[o] = y;
-          if (p.seg_x != nullptr) p.seg_x[(out - p.seg_out) + o] = x;
-        }
-        ++o;
-      }
-      found += total;
-      return;
-    }
-  }
-#endif
   // in order to the pending list, bucket-probed (one round trip for 64 hits)
   // each time it fills up -- dense true hits (1-byte keys) can yield up to 16
   // per lane; probing them in place would cost one round trip per hit
   const uint32_t end = q.pend_n + total;
   uint32_t idx = q.pend_n + incl - c;
   uint32_t from = q.pend_n;   // (kBkResolve: the first pending entry still raw)
-  // the last lane byte a certain candidate may keep: 16 (the next lane's two
-  // bytes are in the entry) unless the entry is a tile's last lane
-  const uint32_t elim = kIdxHigh<MODE> && ((ridx >> 16) & (kWave - 1)) != kWave - 1 ? 16u : 14u;
-  (void)elim;
-  (void)ridx;
   for (uint32_t base = 0;; base += kWave) {
     while (maybe != 0u && idx < base + kWave) {
       const uint32_t j = (uint32_t)__builtin_ctz(maybe);
@@ -923,19 +771,6 @@ __device__ __forceinline__ void drain(const ScanParams& p, WaveQueue& q, uint32_
         // raw: the ring entry, the lane byte and "certain"; resolved below
         x = ent | j << 24;
         y |= ((kmask >> j) & 1u) << 31;
-      } else if constexpr (kByteKeys<MODE> && YAMD_BK_FLAT) {
-        // certain (a 1-byte key ends at j): the five bytes e - 3 .. e + 1 kept
-        // for key_class, e = min(j + kx_end, last kept byte); otherwise the
-        // window ending at j.  Selects, no divergent branch.
-        const bool cert = ((kmask >> j) & 1u) != 0u;
-        const uint32_t e = cert ? min(j + p.kx_end, elim) : j;
-        x = window4(ent, e);
-        const uint32_t b5 = lds_load<uint8_t>(entry_byte_addr(ent, (int32_t)e + 1));
-        uint32_t c = b5 << kOutByteShift | (j + 5 - e) << kOutKeyShift;
-        if (p.kx_deep != 0u)   // (uniform) the byte before the key
-          if (excluded(lds_load<uint8_t>(entry_byte_addr(ent, (int32_t)j - 1)), p.kd_x0[0], p.kd_x1[0]))
-            c |= kOutDeep;
-        y |= cert ? c : 0u;
       } else if (kByteKeys<MODE> && ((kmask >> j) & 1u)) {
         certain_entry<MODE>(p, ent, j, x, y);
       } else {
@@ -1004,7 +839,6 @@ struct SegState {
   uint32_t* out;
   uint32_t found;
   uint32_t carry;   // lane 0: the 4 bytes before the current tile (its window head)
-  bool lane0;
 };
 
 // Stage 1 of one 1 KiB tile: the filter over its 1024 byte positions.  Returns
@@ -1123,11 +957,7 @@ __device__ __forceinline__ uint32_t stage1(const uint32_t (&S)[6], uint32_t lane
       const uint32_t x = xs[j];
       const uint32_t ul = ws[j].x >> (x & 31u), vl = ws[j].y >> ((x >> 5) & 31u);
       YAMD_SDWA_AND(k, ul, vl);
-#if YAMD_DRAIN_Y2
       const uint32_t y = (j & 1) ? y2[j >> 1] >> 16 : y2[j >> 1];   // d | b << 8 (low 10 bits)
-#else
-      const uint32_t y = __builtin_amdgcn_perm(0u, x, 0x0c0c0103u);   // d | b << 8
-#endif
       const uint32_t ur = ws[j].x >> (y & 31u), vr = ws[j].y >> ((y >> 5) & 31u);
       YAMD_SDWA_AND(k + 1, ur, vr);
     }
@@ -1148,22 +978,7 @@ __device__ __forceinline__ uint32_t stage1(const uint32_t (&S)[6], uint32_t lane
 // half).
 template <int MODE>
 __device__ __forceinline__ void write_entry(uint32_t ent, const uint32_t (&S)[6], uint32_t unit) {
-  // (kIdxHigh: the next lane's two bytes first, so that they follow the
-  // lane's 16 in the entry)
-  const uint32_t idx = kIdxHigh<MODE> ? __builtin_amdgcn_perm(unit, S[5], 0x05040100u)
-                                      : unit | (kNextBytes<MODE> ? S[5] << 16 : 0u);
-#if YAMD_RING_CTX_FIRST == 2
-  // index + context as one qword, the 16 bytes as two (8-byte aligned)
-  typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
-  typedef u32x4 u32x4_a8 __attribute__((aligned(8)));
-  lds_store2(ent, idx, S[0]);
-  u32x4 d;
-  d.x = S[1];
-  d.y = S[2];
-  d.z = S[3];
-  d.w = S[4];
-  *reinterpret_cast<__attribute__((address_space(3))) u32x4_a8*>((uintptr_t)(ent + kEntData)) = d;
-#elif YAMD_RING_CTX_FIRST
+  const uint32_t idx = unit | (kNextBytes<MODE> ? S[5] << 16 : 0u);
   // three ds_write2_b32: context, the 16 bytes as loaded, index
   typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
   typedef u32x4 u32x4_a4 __attribute__((aligned(4)));
@@ -1175,11 +990,6 @@ __device__ __forceinline__ void write_entry(uint32_t ent, const uint32_t (&S)[6]
   *reinterpret_cast<__attribute__((address_space(3))) u32x4_a4*>((uintptr_t)(ent + kEntData)) = d;
   *reinterpret_cast<__attribute__((address_space(3))) uint32_t*>((uintptr_t)(ent + kEntCtx)) = S[0];
   *reinterpret_cast<__attribute__((address_space(3))) uint32_t*>((uintptr_t)(ent + kEntIdx)) = idx;
-#else
-  lds_store2(ent, S[1], S[2]);
-  lds_store2(ent + 8, S[3], S[4]);
-  lds_store2(ent + 16, S[0], idx);
-#endif
 }
 
 // The ordered append of a tile's hits to the wave ring.  TAIL: the segment's
@@ -1197,13 +1007,9 @@ __device__ __forceinline__ void ring_append(const ScanParams& p, WaveQueue& q, S
   if (YAMD_EXPECT(lanes != 0, 1)) {   // (~98 % of config C's tiles)
     const uint32_t n = (uint32_t)__popcll(lanes);
     if (YAMD_EXPECT(q.count + n > kQueueCap, 0)) {
-#if YAMD_PRIO
       __builtin_amdgcn_s_setprio(0);   // (streaming waves first)
-#endif
       drain<MODE, true>(p, q, lane, st.seg_start, st.seg_len, st.out, st.found);
-#if YAMD_PRIO
       __builtin_amdgcn_s_setprio(1);
-#endif
     }
     if (any != 0) {
       // slot = count (scalar, folded into the base) + the appending lanes below
@@ -1234,13 +1040,10 @@ __device__ __forceinline__ void tile_context(SegState& st, const uint4& cur, uin
   // (One DPP move and one select: 1 % faster than a wave_shr:1 into the
   // carry plus a v_readlane of the next one, profiles/r02_carry_ror_ab.json.)
   const uint32_t rot = __builtin_amdgcn_mov_dpp(cur.w, 0x13C, 0xF, 0xF, true);
-#if YAMD_CARRY_DPP2
   // wave_shr:1 without bound_ctrl leaves lane 0 its old value (the carry):
   // a second DPP move instead of a select on a lane-0 SGPR mask
+  // (profiles/r02_carry_dpp2_ab.json)
   S[0] = __builtin_amdgcn_update_dpp(st.carry, cur.w, 0x138, 0xF, 0xF, false);
-#else
-  S[0] = st.lane0 ? st.carry : rot;
-#endif
   st.carry = rot;
   S[1] = cur.x;
   S[2] = cur.y;
@@ -1292,13 +1095,9 @@ __device__ __forceinline__ void tile_step(const ScanParams& p, WaveQueue& q, Seg
   if constexpr (MODE == 24) asm volatile("" ::"v"(byte_keys_any(S, p)));
   if constexpr (kDeferFl<MODE>)
     if (YAMD_EXPECT(q.defer, 0)) {   // (~1 tile in 16)
-#if YAMD_PRIO >= 2
       __builtin_amdgcn_s_setprio(0);
-#endif
       drain_complete<MODE>(p, q, lane, st.seg_start, st.out, st.found);
-#if YAMD_PRIO >= 2
       __builtin_amdgcn_s_setprio(1);
-#endif
     }
   if constexpr (kAbl<MODE> == 1) {   // ablation: stage 1 only
     asm volatile("" ::"v"(any));
@@ -1307,119 +1106,6 @@ __device__ __forceinline__ void tile_step(const ScanParams& p, WaveQueue& q, Seg
   }
   // (after the append: a drain inside it takes only the earlier tiles' entries)
   if constexpr (kBkSkipF<MODE>) q.facc |= any_f;
-  issue_first_level<MODE>(p, q);
-}
-
-// Wide steps (YAMD_WIDE=1): 32 bytes per lane, a 2 KiB wave tile read as two
-// 16-byte halves per lane (lane L: bytes 32L .. 32L + 31), so the step's fixed
-// costs -- the lane-context DPP moves, the append's ballot-to-slot arithmetic,
-// the loop control, the deferred-drain test, the two first-level loads -- are
-// paid once per 2 KiB.  Ring entries stay 16-byte units (unit = offset / 16)
-// in position order: lane L's half 0, its half 1, lane L + 1's half 0, ...
-#ifndef YAMD_WIDE
-#define YAMD_WIDE 0
-#endif
-template <int MODE>
-constexpr bool kWide = YAMD_WIDE && (MODE == 0 || (MODE >= 20 && MODE <= 29));
-static_assert(!YAMD_WIDE || YAMD_CARRY_DPP2, "wide steps take the lane-0 context by the second DPP move");
-
-template <int MODE>
-__device__ __forceinline__ uint32_t unit_any(const ScanParams& p, const uint32_t (&S)[6], uint32_t lane) {
-  uint32_t any = stage1<kStage1Mode<MODE>, true>(S, lane);
-  if constexpr (kEven<MODE>)
-    if (p.n_pair_keys != 0) any |= pair_keys_any(S, p);
-  if constexpr (kByteKeys<MODE>) any |= byte_keys_any(S, p);
-  return any;
-}
-
-// A lane's hit halves at ring slot count + below (half 1 after half 0).
-template <int MODE>
-__device__ __forceinline__ void wide_entries(const WaveQueue& q, uint32_t below, uint32_t any0,
-                                             uint32_t any1, const uint32_t (&S0)[6],
-                                             const uint32_t (&S1)[6], uint32_t unit) {
-  const uint32_t base = q.ring + q.count * (kQueueEntryWords * 4);   // scalar
-  uint32_t ent;
-  asm("v_mad_u32_u24 %0, %1, 24, %2" : "=v"(ent) : "v"(below), "s"(base));
-  if (any0 != 0u) write_entry<MODE>(ent, S0, unit);
-  if (any1 != 0u) write_entry<MODE>(any0 != 0u ? ent + kQueueEntryWords * 4 : ent, S1, unit + 1u);
-}
-
-template <int MODE>
-__device__ __forceinline__ void wide_step(const ScanParams& p, WaveQueue& q, SegState& st,
-                                          const uint4& a, const uint4& b, uint32_t tile_off,
-                                          uint32_t lane) {
-  uint32_t S0[6], S1[6];
-  // half 0's context: the previous lane's last dword (lane 0: the previous
-  // tile's, kept in st.carry); half 1's: the lane's own a.w
-  const uint32_t rot = __builtin_amdgcn_mov_dpp(b.w, 0x13C, 0xF, 0xF, true);   // wave_ror:1
-  S0[0] = __builtin_amdgcn_update_dpp(st.carry, b.w, 0x138, 0xF, 0xF, false);  // wave_shr:1
-  st.carry = rot;
-  S0[1] = a.x;
-  S0[2] = a.y;
-  S0[3] = a.z;
-  S0[4] = a.w;
-  S0[5] = kNextBytes<MODE> ? b.x : 0u;
-  S1[0] = a.w;
-  S1[1] = b.x;
-  S1[2] = b.y;
-  S1[3] = b.z;
-  S1[4] = b.w;
-  // (the next lane's first dword, wave_shl:1; lane 63: 0)
-  S1[5] = kNextBytes<MODE> ? __builtin_amdgcn_mov_dpp(a.x, 0x130, 0xF, 0xF, true) : 0u;
-  const uint32_t any0 = unit_any<MODE>(p, S0, lane), any1 = unit_any<MODE>(p, S1, lane);
-  if constexpr (kDeferFl<MODE>)
-    if (q.defer) {
-#if YAMD_PRIO >= 2
-      __builtin_amdgcn_s_setprio(0);
-#endif
-      drain_complete<MODE>(p, q, lane, st.seg_start, st.out, st.found);
-#if YAMD_PRIO >= 2
-      __builtin_amdgcn_s_setprio(1);
-#endif
-    }
-  // per lane 0, 1 or 2 hit halves: lanes with one count once (m0 | m1),
-  // lanes with both once more (m0 & m1, rare)
-  const uint64_t m0 = __ballot(any0 != 0u), m1 = __ballot(any1 != 0u);
-  const uint64_t m01 = m0 | m1, mb = m0 & m1;
-  const uint32_t n = (uint32_t)(__popcll(m01) + __popcll(mb));
-  if (n != 0) {
-    uint32_t below = __builtin_amdgcn_mbcnt_hi((uint32_t)(m01 >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m01, 0u));
-    if (mb != 0u)
-      below = __builtin_amdgcn_mbcnt_hi((uint32_t)(mb >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)mb, below));
-    const uint32_t unit = (tile_off >> 4) + 2 * lane;
-    bool wr = (any0 | any1) != 0u;
-    uint32_t take = n;
-    if (n > kQueueCap) {
-      // more hit halves than the ring holds (> 64 of 128): lanes 0-31 first,
-      // then 32-63, so that the ring order stays the position order
-      const uint32_t n_lo = (uint32_t)(__popcll(m01 & 0xFFFFFFFFull) + __popcll(mb & 0xFFFFFFFFull));
-      if (q.count + n_lo > kQueueCap) {
-        __builtin_amdgcn_s_setprio(0);
-        drain<MODE, true>(p, q, lane, st.seg_start, st.seg_len, st.out, st.found);
-        __builtin_amdgcn_s_setprio(1);
-      }
-      if (wr && lane < kWave / 2) wide_entries<MODE>(q, below, any0, any1, S0, S1, unit);
-      q.count += n_lo;
-      take = n - n_lo;
-      below -= n_lo;
-      wr = wr && lane >= kWave / 2;
-      // (that drain may have deferred its first-level loads: issue them, so
-      // that the drain below -- there always is one -- completes it)
-      if constexpr (kDeferFl<MODE>)
-        if (q.defer) issue_first_level<MODE>(p, q);
-    }
-    if (q.count + take > kQueueCap) {
-#if YAMD_PRIO
-      __builtin_amdgcn_s_setprio(0);
-#endif
-      drain<MODE, true>(p, q, lane, st.seg_start, st.seg_len, st.out, st.found);
-#if YAMD_PRIO
-      __builtin_amdgcn_s_setprio(1);
-#endif
-    }
-    if (wr) wide_entries<MODE>(q, below, any0, any1, S0, S1, unit);
-    q.count += take;
-  }
   issue_first_level<MODE>(p, q);
 }
 
@@ -1449,7 +1135,6 @@ __device__ __forceinline__ void scan_segment(const ScanParams& p, WaveQueue& q, 
   st.seg_len = (uint32_t)(seg_end - st.seg_start);
   st.out = p.seg_out + (p.seg_base ? p.seg_base[seg] : (size_t)seg * p.seg_cap);
   st.found = 0;
-  st.lane0 = lane == 0;
   // bytes read: [seg_start - 4, seg_end) only -- never past byte_end, so a
   // shard that holds just its window of the block is never read beyond it
   const uint64_t avail = p.byte_end - st.seg_start;
@@ -1470,32 +1155,7 @@ __device__ __forceinline__ void scan_segment(const ScanParams& p, WaveQueue& q, 
   q.oa = q.ob = kNoHit;
 
   const uint32_t n_full = st.seg_len / kTile;            // tiles needing no mask / bounds
-  if constexpr (kWide<MODE>) {
-    const uint32_t n_wide = n_full / 2;                  // 2 KiB wide tiles
-    if (n_wide > 0) {
-      constexpr uint32_t kWideTile = 2 * kTile;
-      const uint32_t last = (n_wide - 1) * kWideTile;
-      const __amdgpu_buffer_rsrc_t rsrc = segment_rsrc(base);
-      const uint32_t lane32 = lane * (2 * kBytesPerLane);
-      uint4 a0 = load_tile_full(rsrc, 0, lane32), a1 = load_tile_full(rsrc, kBytesPerLane, lane32), b0, b1;
-      asm volatile("" : "+v"(a0.x), "+v"(a0.y), "+v"(a0.z), "+v"(a0.w), "+v"(a1.x), "+v"(a1.y), "+v"(a1.z),
-                   "+v"(a1.w));
-      uint32_t i = 0;
-      for (; i + 2 <= n_wide; i += 2) {
-        b0 = load_tile_full(rsrc, (i + 1) * kWideTile, lane32);
-        b1 = load_tile_full(rsrc, (i + 1) * kWideTile + kBytesPerLane, lane32);
-        wide_step<MODE>(p, q, st, a0, a1, i * kWideTile, lane);
-        const uint32_t nx = min((i + 2) * kWideTile, last);
-        a0 = load_tile_full(rsrc, nx, lane32);
-        a1 = load_tile_full(rsrc, nx + kBytesPerLane, lane32);
-        wide_step<MODE>(p, q, st, b0, b1, (i + 1) * kWideTile, lane);
-      }
-      if (i < n_wide) wide_step<MODE>(p, q, st, a0, a1, i * kWideTile, lane);
-    }
-    if (n_full % 2 != 0)   // an odd last full tile: one ordinary step
-      tile_step<MODE, false>(p, q, st, load_tile(base, (n_full - 1) * kTile, lane, avail),
-                             (n_full - 1) * kTile, lane);
-  } else if (n_full > 0) {
+  if (n_full > 0) {
     const uint32_t last = (n_full - 1) * kTile;
     const __amdgpu_buffer_rsrc_t rsrc = segment_rsrc(base);
     const uint32_t lane16 = lane * kBytesPerLane;
@@ -1554,9 +1214,7 @@ __global__ __launch_bounds__(kWGThreads, 1) void scan_segments_kernel(ScanParams
     WaveQueue q;   // (per segment: its per-lane state then stays in registers)
     q.ring = kFilterBytes + wid * (kQueueCap * kQueueEntryWords * 4);
     q.pend = kFilterBytes + kQueueBytes + wid * (kWave * 8);
-#if YAMD_PRIO
     __builtin_amdgcn_s_setprio(1);
-#endif
     scan_segment<MODE>(p, q, seg, lane);
     if (p.seg_next == nullptr) {
       seg += total_waves;
@@ -1644,20 +1302,11 @@ __global__ __launch_bounds__(1024) void seg_offsets_kernel(const uint32_t* seg_c
 }
 
 constexpr uint32_t kScatterWaves = 8;   // waves per segment in the scatter (dense segments)
-#ifndef YAMD_SCATTER_ADAPT
-#define YAMD_SCATTER_ADAPT 1
-#endif
 
 // The compaction reads the input bytes a certain candidate's class needs when
-// the scan's five kept bytes do not hold them (YAMD_CLASS_FETCH, key_class):
+// the scan's five kept bytes do not hold them (key_class's `more`):
 // fuzz0's pre-verification 0.63 -> 0.32 ms for 0.08 ms more compaction, rx
 // +0.02 ms, short / fuzz3 unchanged (profiles/r04_ab_inproc.json, gpurun h8).
-#ifndef YAMD_CLASS_FETCH
-#define YAMD_CLASS_FETCH 1
-#endif
-#ifndef YAMD_CLASS_STAGE
-#define YAMD_CLASS_STAGE 1
-#endif
 
 // per-segment LDS buffer of live candidates (the diagnostic build holds one,
 // so that the GPU suite exercises the overflow path, tests/test_preverify.py)
@@ -1675,8 +1324,8 @@ __global__ __launch_bounds__(W * kWave) void seg_scatter_kernel(
   // aligned dwords (one byte store per candidate ran at ~1.4 TB/s:
   // profiles/r04_ab_inproc.json h31); +4: the chunk's start is placed at its
   // absolute index mod 4
-  constexpr uint32_t kChunk = YAMD_CLASS_STAGE ? W * kWave * (W == 2 ? 16u : 8u) : 0xFFFFFFFFu;
-  __shared__ __attribute__((aligned(4))) uint8_t cbuf[YAMD_CLASS_STAGE ? kChunk + 4 : 4];
+  constexpr uint32_t kChunk = W * kWave * (W == 2 ? 16u : 8u);
+  __shared__ __attribute__((aligned(4))) uint8_t cbuf[kChunk + 4];
   const bool classes = p.dead != nullptr;   // (uniform)
   if (threadIdx.x < kMaxByteKeys) {
     const uint32_t k = threadIdx.x;
@@ -1728,7 +1377,7 @@ __global__ __launch_bounds__(W * kWave) void seg_scatter_kernel(
         bool more = false;
         cls = key_class(p, kc, xc | (uint64_t)(ec >> kOutByteShift & 0xFFu) << 32,
                         (int32_t)(ec >> kOutKeyShift & 7u) - 2, (ec & kOutDeep) != 0u, pos, 4,
-                        YAMD_CLASS_FETCH ? &more : nullptr);
+                        &more);
         // Undecided only because the guard's bytes (or the byte before the key)
         // lie outside the five the scan kept -- the key near its lane's end:
         // read eight bytes around the key from the input (three aligned dwords
@@ -1748,8 +1397,7 @@ __global__ __launch_bounds__(W * kWave) void seg_scatter_kernel(
         }
       }
       if (valid) {
-        if constexpr (YAMD_CLASS_STAGE) cbuf[sh0 + (i - chunk)] = (uint8_t)cls;
-        else p.dead[first + i] = (uint8_t)cls;
+        cbuf[sh0 + (i - chunk)] = (uint8_t)cls;
       }
       // the undecided ones onto the live list (any order): the segment's LDS
       // buffer, copied out with ONE global atomic per segment (one per wave and
@@ -1776,7 +1424,7 @@ __global__ __launch_bounds__(W * kWave) void seg_scatter_kernel(
         }
       }
     }
-    if constexpr (YAMD_CLASS_STAGE) {
+    {
       if (classes) {
         // the chunk's classes: absolute bytes [a, a + m) of p.dead -- head and
         // tail bytes (shared with the neighbouring segments' blocks) byte by
@@ -1926,7 +1574,7 @@ hipError_t launch_compact(const ScanParams& p, uint64_t* seg_offset, uint64_t* s
     // sparse segments (the default capacity, no rerun at exact offsets: at
     // most one candidate per 256 bytes) take two waves each, dense ones
     // kScatterWaves (a 4 GiB block: 8,192 instead of 32,768 waves)
-    if (YAMD_SCATTER_ADAPT && p.seg_base == nullptr && p.seg_cap <= p.seg_bytes / 256)
+    if (p.seg_base == nullptr && p.seg_cap <= p.seg_bytes / 256)
       hipLaunchKernelGGL(seg_scatter_kernel<2>, dim3(p.n_segments), dim3(2 * kWave), 0, s, p,
                          (const uint64_t*)seg_offset, positions);
     else

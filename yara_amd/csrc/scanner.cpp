@@ -198,11 +198,6 @@ static int debug_level() {
   return level;
 }
 
-// Scan-kernel timing markers without a system-scope fence (yr_amd_scanner_set_timing;
-// 0 = default events, for A/B builds)
-#ifndef YAMD_EV_NOFENCE
-#define YAMD_EV_NOFENCE 1
-#endif
 
 #define HIP_TRY(expr)                                   \
   do {                                                  \
@@ -255,9 +250,6 @@ uint32_t choose_seg_bytes(uint64_t nbytes, int num_cus, uint32_t target) {
   return (uint32_t)std::min<uint64_t>(std::max<uint64_t>(per, 4 * kTile), kSegment);
 }
 
-#ifndef YAMD_EXT_EVENTS
-#define YAMD_EXT_EVENTS 1
-#endif
 int run_scan(yr_amd_scanner* s) {
   // scan, per-segment offsets and the scatter are queued back to back: the
   // output is sized for the clipped worst case (every segment at capacity),
@@ -272,18 +264,13 @@ int run_scan(yr_amd_scanner* s) {
   s->last.dead = s->tables->kd_any ? s->d_dead : nullptr;
   s->last.live = s->tables->kd_any ? s->d_live : nullptr;
   s->last.seg_x = s->tables->kd_any ? s->d_seg_x : nullptr;
-  // (timing: the kernel's own start / end stamps, YAMD_EXT_EVENTS; else two
-  // markers around the launch, which also count its dispatch)
-  if (s->timing && YAMD_EXT_EVENTS) {
+  // (timing: the kernel's own start / end stamps -- not two markers around
+  // the launch, which would also count its dispatch)
+  if (s->timing) {
     HIP_TRY(launch_scan(p, s->last_grid, s->stream, s->diag_mode, s->ev_begin, s->ev_end));
     s->ev_valid = true;
   } else {
-    if (s->timing) HIP_TRY(hipEventRecord(s->ev_begin, s->stream));
     HIP_TRY(launch_scan(p, s->last_grid, s->stream, s->diag_mode));
-    if (s->timing) {
-      HIP_TRY(hipEventRecord(s->ev_end, s->stream));
-      s->ev_valid = true;
-    }
   }
   HIP_TRY(launch_compact(p, s->d_seg_offset, s->d_hsum, nullptr, false, s->stream));
   if (p.live != nullptr) HIP_TRY(hipMemsetAsync(p.live, 0, sizeof(uint32_t), s->stream));
@@ -447,7 +434,8 @@ int yr_amd_scanner_set_timing(yr_amd_scanner* s, int enable) {
     // cache writeback + invalidate at each record, ~5 us of stream gap per
     // marker, profiles/r03_step_gaps.json); ev_compact also completes the scan
     // for the host (last_done) and keeps it
-    const unsigned marker = YAMD_EV_NOFENCE ? hipEventDisableSystemFence : hipEventDefault;
+    // (timing markers without a system-scope fence)
+    const unsigned marker = hipEventDisableSystemFence;
     HIP_TRY(hipEventCreateWithFlags(&s->ev_begin, marker));
     HIP_TRY(hipEventCreateWithFlags(&s->ev_end, marker));
     HIP_TRY(hipEventCreate(&s->ev_compact));

@@ -58,9 +58,6 @@ struct Near {
   uint64_t v;   // the 8 bytes, little endian
 };
 constexpr uint64_t kNoNear = ~0ull;
-#ifndef YAMD_GUARD_REG
-#define YAMD_GUARD_REG 0
-#endif
 
 __device__ __forceinline__ uint32_t node_head(const VerifyParams& p, uint64_t i, Near& near) {
   const uint32_t n = i < 4 ? (uint32_t)i : 4u;
@@ -646,60 +643,10 @@ __device__ int general_re_reachable(const uint8_t* __restrict__ code, uint32_t l
 // in the block or the staged window: true (the interpreter decides).  The
 // guard's 4 + span bytes come from four LDS dwords of the staged window and
 // byte shifts; every j is one AND and one compare.
-#ifndef YAMD_GUARD_DIRECT
-#define YAMD_GUARD_DIRECT 0
-#endif
 __device__ bool guard_ok(const VerifyParams& p, const uint8_t* d, uint64_t offset, bool backwards,
                          uint32_t bs, DevGuard g, uint32_t lds, const Near& near) {
   const uint32_t base = bs & 15u, span = bs >> 4, L = base + span + 4;
   if (backwards ? offset < L : p.size - offset < L) return true;
-#if YAMD_GUARD_REG
-  if (near.a != kNoNear) {
-    // every tested byte (a nonzero mask byte, for every j <= span) inside the
-    // 8 bytes node_head loaded: decide from registers
-    const uint64_t r0 = backwards ? offset - L : offset + base;
-    const uint32_t bmin = (uint32_t)__builtin_ctz(g.m) >> 3, bmax = (31u - (uint32_t)__builtin_clz(g.m)) >> 3;
-    if (r0 + bmin >= near.a && r0 + span + bmax < near.a + 8) {
-      bool hit = false;
-      for (uint32_t q = 0; q <= span; ++q) {
-        const int64_t dq = (int64_t)(r0 + q) - (int64_t)near.a;   // in [-3, 7]
-        const uint32_t x = (uint32_t)(dq >= 0 ? near.v >> (8 * dq) : near.v << (-8 * dq));
-        hit |= (x & g.m) == g.v;
-      }
-      return hit;
-    }
-  }
-#endif
-#if YAMD_GUARD_DIRECT
-  {
-    // The guard's span + 4 <= 12 bytes straight into registers: three aligned
-    // 8-byte loads from the 8-byte boundary below the region (24 bytes, at
-    // most 7 of them before it) -- no 48-byte window staged through LDS.  Dense
-    // candidate streams (1-byte atoms: a call every ~128 bytes) read about
-    // half the bytes this way.
-    const uint64_t r0 = backwards ? offset - L : offset + base;
-    const uint64_t a8 = r0 & ~7ull;
-    if (a8 >= p.win_lo && a8 + 24 <= p.win_hi) {   // region: span + 4 <= 12 bytes from r0
-      const uint2* q = reinterpret_cast<const uint2*>(p.data + a8);
-      const uint2 q0 = q[0], q1 = q[1], q2 = q[2];
-      const uint32_t sh = (uint32_t)(r0 - a8), k = sh >> 2, bsh = sh & 3u;
-      // region dwords from dword k of (q0.x, q0.y, q1.x, q1.y, q2.x, q2.y)
-      const uint32_t B0 = k ? q0.y : q0.x, B1 = k ? q1.x : q0.y, B2 = k ? q1.y : q1.x;
-      const uint32_t B3 = k ? q2.x : q1.y;
-      const uint32_t W[3] = {__builtin_amdgcn_alignbyte(B1, B0, bsh),
-                             __builtin_amdgcn_alignbyte(B2, B1, bsh),
-                             __builtin_amdgcn_alignbyte(B3, B2, bsh)};
-      bool hit = false;
-#pragma unroll
-      for (uint32_t t = 0; t <= 8; ++t) {
-        const uint32_t r = (t & 3) == 0 ? W[t >> 2]
-                                        : __builtin_amdgcn_alignbyte(W[(t >> 2) + 1], W[t >> 2], t & 3);
-        hit |= t <= span && (r & g.m) == g.v;
-      }
-      return hit;
-    }
-  }
-#endif
   const ByteWindow w = stage_window(p, d, backwards, lds);
   if (w.lo == nullptr) return true;
   const int32_t rel0 = (int32_t)(d - w.lo);
