@@ -219,6 +219,28 @@ int yr_amd_scan_device_result(
     int* all_positions);
 
 /*
+ * Verified-only scans (enable = 1): the scans of this scanner serve
+ * yr_amd_verify_device only -- the paths that hand libyara records
+ * (yr_amd_scan_block_verified, the block pipeline and the multi-device calls
+ * set it on their own scanners).  For rule sets with 1-byte keys whose calls
+ * the scan can decide from the bytes next to the key (candidate classes), the
+ * scan kernel itself decides them and leaves the candidates none of whose
+ * calls can have an effect out of the result: yr_amd_scan_device_result then
+ * returns that reduced stream, while the records of yr_amd_verify_device are
+ * unchanged -- the same calls, and the candidate field still indexes the FULL
+ * stream (yr_amd_scan_device_stream_length).  No effect on other rule sets
+ * or with yr_amd_tables_set_profiling.  Default 0.
+ */
+int yr_amd_scanner_set_verified_only(yr_amd_scanner* scanner, int enable);
+
+/*
+ * Length of the full candidate stream of the last completed scan (after
+ * yr_amd_scan_device_result): its count, plus the candidates a verified-only
+ * scan left out.
+ */
+int yr_amd_scan_device_stream_length(yr_amd_scanner* scanner, uint64_t* length);
+
+/*
  * Verification callback: the arguments the reference passes to
  * yr_scan_verify_match(scanner, &rules->ac_match_pool[pool_index], data,
  * size, base, offset) (scanner.c:111-117).  A non-zero return aborts the

@@ -319,49 +319,49 @@ def test_scan_side_guard_after_key(tail):
     np.testing.assert_array_equal(r["pool_index"], K[keep])
 
 
-@pytest.mark.gpu
-def test_live_list_overflow_path(tmp_path):
-    """The compaction collects a segment's undecided candidates in an LDS
-    buffer and sends what does not fit straight to the global live list
-    (kernels.hip seg_scatter_kernel).  The diagnostic build's buffer holds one,
-    so the dense golden cases overflow it in every segment: its records must
-    equal the product build's, call for call (a subprocess: one library per
-    process)."""
-    import json
-    import os
-    import subprocess
-    import sys
+def _device_records(sc, d, n, lo=0, hi=None):
+    import torch
     import yara_amd
-    from conftest import REPO
-    diag = os.path.join(REPO, "yara_amd", "_diag", "libyara_amd.so")
-    if not os.path.exists(diag):
-        pytest.skip("diagnostic build missing (make -C yara_amd/csrc diag)")
-    cases = ["rx_1M", "fuzz0_256K", "fuzz3_256K", "bytekeys_1M", "short_1M"]
-    want = {}
-    for case in cases:
-        rec = CASES[case]
-        tab = yara_amd.Tables.from_npz(tables_npz(rec["rules"]), device=0, strings=True)
-        r = yara_amd.Scanner(tab).verify_calls(case_data(rec))
-        want[case] = [r["offset"].tolist(), r["pool_index"].tolist()]
-    script = (
-        "import json, sys\n"
-        "sys.path[:0] = [%r, %r, %r]\n"
-        "import yara_amd\n"
-        "from conftest import case_data, golden, tables_npz\n"
-        "cases = golden()['cases']\n"
-        "out = {}\n"
-        "for case in %r:\n"
-        "    rec = cases[case]\n"
-        "    tab = yara_amd.Tables.from_npz(tables_npz(rec['rules']), device=0, strings=True)\n"
-        "    r = yara_amd.Scanner(tab).verify_calls(case_data(rec))\n"
-        "    out[case] = [r['offset'].tolist(), r['pool_index'].tolist()]\n"
-        "json.dump(out, open(%r, 'w'))\n" % (REPO, os.path.join(REPO, "tests"),
-                                             os.path.join(REPO, "tests", "golden"), cases,
-                                             str(tmp_path / "diag.json")))
-    p = subprocess.run([sys.executable, "-c", script], capture_output=True, text=True, timeout=240,
-                       env=dict(os.environ, YARA_AMD_LIB=diag))
-    assert p.returncode == 0, p.stderr[-3000:]
-    got = json.load(open(tmp_path / "diag.json"))
-    for case in cases:
-        assert len(want[case][0]) > 0, case
-        assert got[case] == want[case], case
+    from yara_amd._hip import memcpy
+    sc.scan_device(d.data_ptr(), n, lo, n if hi is None else hi)
+    _, cnt, _ = sc.device_result()
+    p, m = sc.verify_device(0x2000)
+    out = np.zeros(m, dtype=yara_amd._lib.VERIFY_REC_DTYPE)
+    if m:
+        h = torch.empty(m * 16, dtype=torch.uint8, device="cuda")
+        memcpy(h.data_ptr(), p, m * 16, 3)
+        out = np.frombuffer(h.cpu().numpy().tobytes(), dtype=yara_amd._lib.VERIFY_REC_DTYPE)
+    return out, cnt, sc.stream_length()
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("rules,case", [
+    ("rx", "rx_1M"), ("fuzz0", "fuzz0_256K"), ("fuzz3", "fuzz3_256K"), ("short", "short_1M"),
+    ("lit", "lit_1M"), ("C", "C_planted16M"),
+    ("rx", "xs64M"), ("fuzz0", "xs64M"), ("fuzz3", "xs64M"), ("short", "xs64M")])
+def test_verified_only_scan_keeps_records_and_candidate_indices(rules, case):
+    """Verified-only scans (yr_amd_scanner_set_verified_only: the scan kernel
+    decides the 1-byte keys' classes from eight bytes around the key and leaves
+    the dead candidates out of its result) yield exactly the records of a full
+    scan -- the same calls, and candidate fields that still index the full
+    candidate stream -- on whole blocks and on byte ranges (the full scan's
+    records are pinned to the reference by the tests above)."""
+    import torch
+    import yara_amd
+    data = oracle.xorshift(64 << 20, 1) if case == "xs64M" else case_data(CASES[case])
+    n = len(data)
+    d = torch.from_numpy(data.copy()).cuda()
+    tab = yara_amd.Tables.from_npz(tables_npz(rules), device=0, strings=True)
+    sc = yara_amd.Scanner(tab)
+    cut = ((n // 3) & ~15)
+    for lo, hi in ((0, n), (0, cut + 5), (cut, n)):
+        full, cnt_full, len_full = _device_records(sc, d, n, lo, hi)
+        sc.set_verified_only(True)
+        got, cnt, length = _device_records(sc, d, n, lo, hi)
+        sc.set_verified_only(False)
+        assert len_full == cnt_full and length == cnt_full, (lo, hi, cnt_full, length)
+        assert cnt <= cnt_full
+        for f in ("offset", "pool_index", "candidate"):
+            np.testing.assert_array_equal(got[f], full[f], err_msg="%s [%d, %d)" % (f, lo, hi))
+        if rules in ("rx", "fuzz0") and case == "xs64M":   # dense candidates, most of them dead
+            assert cnt < cnt_full // 2, (cnt, cnt_full)

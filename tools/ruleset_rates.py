@@ -89,6 +89,42 @@ def main():
                 vs.append((time.perf_counter() - t0) * 1e3)
             rec["verify_ms"] = round(statistics.median(vs), 3)
             rec["records"] = int(nrec)
+            # the verified path as the libyara side runs it (verified-only scans,
+            # yr_amd_scanner_set_verified_only): scan kernel and compaction (HIP
+            # events), then pre-verification; and the whole step's wall time
+            # (scan + result + verify, host waits included)
+            if not info["root_accepting"]:
+                for mode in ("full", "verified_only"):
+                    # (a scanner per mode: each learns its own output capacity)
+                    sc = yara_amd.Scanner(t)
+                    sc.set_verified_only(mode == "verified_only")
+                    for _ in range(5):
+                        sc.scan_device(buf.data_ptr(), n)
+                        sc.device_result()
+                        sc.verify_device(0)
+                    sc.set_timing(True)
+                    ks, ss, ws, vv = [], [], [], []
+                    for _ in range(a.reps):
+                        torch.cuda.synchronize()
+                        t0 = time.perf_counter()
+                        sc.scan_device(buf.data_ptr(), n)
+                        cnt = sc.device_result()[1]
+                        t1 = time.perf_counter()
+                        _, nrec = sc.verify_device(0)
+                        t2 = time.perf_counter()
+                        ks.append(sc.kernel_ms())
+                        ss.append(sc.scan_ms())
+                        vv.append((t2 - t1) * 1e3)
+                        ws.append((t2 - t0) * 1e3)
+                    sc.set_timing(False)
+                    km, sm, vm = statistics.median(ks), statistics.median(ss), statistics.median(vv)
+                    rec[mode] = {"kernel_ms": round(km, 4), "scan_ms": round(sm, 4),
+                                 "verify_ms": round(vm, 4), "scan_plus_verify_ms": round(sm + vm, 4),
+                                 "frac_scan_plus_verify": round(n / ((sm + vm) * 1e-3) / 1e9 / HBM_PEAK_GBS, 4),
+                                 "step_wall_ms": round(statistics.median(ws), 4),
+                                 "candidates": int(cnt), "stream_length": int(sc.stream_length()),
+                                 "records": int(nrec)}
+                sc.set_verified_only(False)
         out[name] = rec
         print(name, rec, file=sys.stderr, flush=True)
         del sc, t

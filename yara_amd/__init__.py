@@ -304,6 +304,19 @@ class Scanner:
                                                 ctypes.byref(cnt)))
         return out[:min(cap, cnt.value)], cnt.value
 
+    def set_verified_only(self, enable: bool = True):
+        """Scans serve verify_device only (yr_amd_scanner_set_verified_only):
+        the result may leave out candidates whose calls the scan proves dead."""
+        _lib.check("yr_amd_scanner_set_verified_only",
+                   _lib.lib().yr_amd_scanner_set_verified_only(self._h, int(enable)))
+
+    def stream_length(self) -> int:
+        """Length of the last scan's full candidate stream."""
+        n = ctypes.c_uint64()
+        _lib.check("yr_amd_scan_device_stream_length",
+                   _lib.lib().yr_amd_scan_device_stream_length(self._h, ctypes.byref(n)))
+        return n.value
+
     def set_timing(self, enable: bool = True):
         _lib.check("yr_amd_scanner_set_timing", _lib.lib().yr_amd_scanner_set_timing(self._h, int(enable)))
 

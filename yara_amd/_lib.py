@@ -89,6 +89,8 @@ PROTOTYPES = {
                                  ctypes.POINTER(ctypes.c_uint64)]),
     "yr_amd_fill_xorshift64": (_int, [_vp, ctypes.c_uint64, ctypes.c_uint64, ctypes.c_uint64, _vp]),
     "yr_amd_scanner_set_timing": (_int, [_vp, _int]),
+    "yr_amd_scanner_set_verified_only": (_int, [_vp, _int]),
+    "yr_amd_scan_device_stream_length": (_int, [_vp, _u64p]),
     "yr_amd_scanner_kernel_ms": (_int, [_vp, ctypes.POINTER(ctypes.c_float)]),
     "yr_amd_scanner_scan_ms": (_int, [_vp, ctypes.POINTER(ctypes.c_float)]),
     "yr_amd_version": (ctypes.c_char_p, []),

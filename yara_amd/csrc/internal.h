@@ -182,6 +182,9 @@ constexpr uint32_t kOutDeep = 0x80000000u;
 constexpr uint32_t kOutOffsetMask = (1u << 20) - 1u;
 constexpr uint32_t kClassDead = 1u;
 constexpr uint32_t kClassKept = 2u;
+constexpr uint32_t kClassFetch = 0xFFu;   // (verified-only scans) undecided from the scan's
+                                          // eight bytes: the compaction reads the input
+constexpr uint32_t kOutPlaceScanClass = 7u;   // key place of an entry carrying its class
 
 struct ScanParams {
   const uint8_t* data;      // block base in HBM (16-byte aligned)
@@ -224,13 +227,32 @@ struct ScanParams {
                             // next lane's first two bytes in each ring entry (kernels.hip)
   uint8_t* dead;            // null, or per output candidate its class (key_class;
                             // written by the compaction), and
-  uint32_t* live;           // [0] = count, then the other candidates' indices (any order)
+  uint32_t* live;           // per segment s, in [seg_offset[s], + live_count[s]): the indices
+                            // of its other candidates (any order)
+  uint32_t* live_count;     // [n_segments]
   uint32_t filter_mode;     // kFilterPair / kFilterEven / kFilterEvenHash (FlatTables)
   uint32_t pair_keys[2];    // even filters: FlatTables::pair_keys / n_pair_keys (16-bit
   uint32_t n_pair_keys;     // test of the 2-byte keys ending at odd positions)
   uint32_t* seg_next;       // null: wave w takes segments w, w + waves, ...; else each wave
                             // takes its first segment by index and the next ones from this
                             // counter (initialised to the launch's wave count)
+  // Verified-only scans (yr_amd_scanner_set_verified_only; byte-key kernels
+  // with candidate classes): the scan decides each certain candidate's class
+  // from eight bytes around its key (kernels.hip resolve_pending) and leaves
+  // the dead ones out of the output.  Output entries of certain candidates
+  // then carry the class code in bits kOutByteShift.. (kClassFetch: let the
+  // compaction read the input) with key place 7, seg_x holds each output
+  // candidate's index in the segment's FULL stream, seg_full[s] the length of
+  // that stream, and the compaction writes the full stream's global index of
+  // every output candidate into cand_index (only if some candidate was left
+  // out: seg_full_offset[n_segments] != the output total).
+  uint32_t drop_dead;
+  const uint32_t* kc;       // [32]: key k's class record (kd_info, kd_m, kd_v, kd_x0, kd_x1,
+                            // kd_min_pos, 0, 0) at [8k, 8k + 8) -- the scan kernel reads it
+                            // into one VGPR and fetches fields by lane permutes
+  uint32_t* seg_full;
+  uint64_t* seg_full_offset;   // [n_segments + 1], written by the offsets kernel
+  uint32_t* cand_index;
 };
 
 }  // namespace yamd

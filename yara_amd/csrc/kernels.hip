@@ -186,6 +186,9 @@ struct WaveQueue {
   uint32_t count;   // wave-uniform: entries in the ring (a drain takes all of them)
   uint32_t pend;    // LDS address: kWave pairs {w4, segment offset}
   uint32_t pend_n;  // wave-uniform
+  uint32_t full;    // wave-uniform (byte-key kernels): candidates of the segment's full
+                    // stream flushed so far (verified-only scans leave the dead out)
+  uint32_t kcv;     // per lane (byte-key kernels): the key class records (scan_key_rec)
   bool defer;       // wave-uniform: the per-lane hits below await their words
   uint32_t facc;    // per lane (byte-key kernels, kBkSkipF): OR of the stage-1 filter
                     // and 2-byte-key tests of the tiles queued since the last drain
@@ -228,10 +231,16 @@ constexpr int kModeByteKeysNextEvenHash = 29;
 // ring), 2 ring appends whose drains drop the entries, 3 the 1-byte keys
 // detected but not appended (the ring holds the filter hits only), 4 the
 // 1-byte keys not detected.  Output wrong by construction.
+// MODE + kDropModes: the same kernel for verified-only scans (ScanParams::
+// drop_dead; byte-key variants only): a separate instance, so that the class
+// decisions add nothing to the others.
+constexpr int kDropModes = 1000;
 template <int MODE>
-constexpr int kBase = MODE >= 100 ? MODE % 100 : MODE;
+constexpr bool kDrop = MODE >= kDropModes;
 template <int MODE>
-constexpr int kAbl = MODE >= 100 ? MODE / 100 : 0;
+constexpr int kBase = MODE % kDropModes >= 100 ? MODE % 100 : MODE % kDropModes;
+template <int MODE>
+constexpr int kAbl = MODE % kDropModes >= 100 ? (MODE % kDropModes) / 100 : 0;
 template <int MODE>
 constexpr bool kByteKeys = kBase<MODE> == kModeByteKeys || kBase<MODE> == kModeByteKeysNext ||
                            (kBase<MODE> >= kModeByteKeysEven && kBase<MODE> <= kModeByteKeysNextEvenHash);
@@ -290,7 +299,10 @@ struct KeyClassRec {
 // compaction read from the input, the key at byte 2).  *more (if given) is
 // set when the class is undecided only because a byte it needs lies outside
 // w, and eight bytes with the key at byte 2 would hold them.
-__device__ __forceinline__ uint32_t key_class(const ScanParams& p, const KeyClassRec* kc, uint64_t w,
+// rec(k): key k's KeyClassRec (the compaction: an LDS table; the scan kernel:
+// selects over its arguments, scan_key_rec).
+template <typename Rec>
+__device__ __forceinline__ uint32_t key_class(const ScanParams& p, Rec rec, uint64_t w,
                                               int32_t kp, bool deep, uint64_t pos, int32_t last = 4,
                                               bool* more = nullptr) {
   if (kp < 0 && p.n_byte_keys != 1) {
@@ -305,7 +317,7 @@ __device__ __forceinline__ uint32_t key_class(const ScanParams& p, const KeyClas
   const uint32_t z = (t - 0x01010101u) & ~t & nmask;
   if (z == 0) return 0;
   const uint32_t kidx = (uint32_t)__builtin_ctz(z) >> 3;
-  const KeyClassRec r = kc[kidx];
+  const KeyClassRec r = rec(kidx);
   const uint32_t info = r.info, m = r.m, v = r.v, x0 = r.x0, x1 = r.x1, min_pos = r.min_pos;
   if (!(info & 1u)) return 0;
   if (info & 2u) {   // the byte before the key among the exclusions: a deeper state
@@ -335,13 +347,25 @@ __device__ __forceinline__ uint32_t key_class(const ScanParams& p, const KeyClas
   return hit ? 0u : kClassDead;
 }
 
+// Key k's class record in the scan kernel (k lane-varying): lane 8k + f of
+// kcv holds field f of key k (ScanParams::kc, loaded once per kernel), fetched
+// by lane permutes -- no memory access, and no SGPRs held for 24 arguments.
+__device__ __forceinline__ KeyClassRec scan_key_rec(uint32_t kcv, uint32_t k) {
+  const int b = (int)(k * 32u);   // ds_bpermute byte address of lane 8k
+  auto f = [&](int i) { return (uint32_t)__builtin_amdgcn_ds_bpermute(b + 4 * i, (int)kcv); };
+  return KeyClassRec{f(0), f(1), f(2), f(3), f(4), f(5), 0u, 0u};
+}
+
 // Bucket-probe every pending hit (one lane each) and append the survivors,
-// in order, to the segment's output.
+// in order, to the segment's output.  Verified-only scans (p.drop_dead):
+// certain candidates of class dead are left out but still counted in the
+// segment's full stream (q.full), and seg_x gets each output candidate's
+// index in that stream.
 template <int MODE>
 __device__ __forceinline__ void flush_pending(const ScanParams& p, WaveQueue& q, uint32_t lane,
                                               uint64_t seg_start, uint32_t* out, uint32_t& found) {
   __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
-  bool keep = false;
+  bool keep = false, dead = false;
   uint32_t off = 0, xv = 0;
   if constexpr (kByteKeys<MODE>) {
     // confirmed entries need no probe; a flush of nothing else makes no
@@ -351,7 +375,9 @@ __device__ __forceinline__ void flush_pending(const ScanParams& p, WaveQueue& q,
     const bool conf = (e.y & kCertainMask) != 0u;
     off = e.y;   // (a certain entry's bits for key_class with it)
     const bool probe = lane < q.pend_n && !conf;
-    keep = lane < q.pend_n && conf;
+    dead = kDrop<MODE> && lane < q.pend_n && conf &&
+           ((e.y >> kOutByteShift) & 0xFFu) == kClassDead;
+    keep = lane < q.pend_n && conf && !dead;
     if (__ballot(probe) != 0 && probe) keep = exact_check(e.x, seg_start + off + 1, p);
     xv = e.x;
   } else if (lane < q.pend_n) {
@@ -360,6 +386,14 @@ __device__ __forceinline__ void flush_pending(const ScanParams& p, WaveQueue& q,
     keep = MODE == 12 ? true : exact_check(e.x, seg_start + off + 1, p);   // 12: ablation
   }
   const uint64_t b = __ballot(keep);
+  uint64_t bf = b;   // the segment's full stream: kept and dead candidates
+  if constexpr (kByteKeys<MODE>) {
+    if constexpr (kDrop<MODE>) {
+      bf = __ballot(keep || dead);
+      xv = q.full + __builtin_amdgcn_mbcnt_hi((uint32_t)(bf >> 32),
+                                              __builtin_amdgcn_mbcnt_lo((uint32_t)bf, 0u));
+    }
+  }
   if (keep) {
     const uint32_t idx = found + __builtin_amdgcn_mbcnt_hi((uint32_t)(b >> 32),
                                                            __builtin_amdgcn_mbcnt_lo((uint32_t)b, 0u));
@@ -369,6 +403,7 @@ __device__ __forceinline__ void flush_pending(const ScanParams& p, WaveQueue& q,
     }
   }
   found += (uint32_t)__popcll(b);
+  if constexpr (kByteKeys<MODE>) q.full += (uint32_t)__popcll(bf);
   q.pend_n = 0;
 }
 
@@ -594,14 +629,70 @@ __device__ __forceinline__ void certain_entry(const ScanParams& p, uint32_t ent,
 // offset, DESIGN.md section 5 "Measurement method".)
 template <int MODE>
 constexpr bool kBkResolve = kByteKeys<MODE>;
+// Verified-only scans: the class of the certain candidate at lane byte j of
+// ring entry ent (key_class over the eight lane bytes j - 2 .. j + 5, the key at
+// byte 2 -- lane bytes 16, 17 are the next lane's first two, kept in the
+// index word's top half by the kernels with kNextBytes), as an output entry:
+// the segment offset, the class code (kClassFetch: undecided only because
+// some byte lies past what the entry holds) and key place 7.
+template <int MODE>
+__device__ __forceinline__ uint32_t scan_class_entry(const ScanParams& p, uint32_t kcv_, uint32_t ent,
+                                                     uint32_t j, uint32_t off, uint64_t seg_start) {
+  const uint32_t li = lds_load<uint32_t>(ent + kEntIdx);
+  // lane bytes j - 2 .. j + 5 = entry bytes j + 2 .. j + 9 (past lane byte 15:
+  // the index word, replaced below)
+  const auto una = [](uint32_t a) {
+    return *reinterpret_cast<const __attribute__((address_space(3))) u32_una*>((uintptr_t)a);
+  };
+  uint64_t w = una(ent + kEntData + j - 2) | (uint64_t)una(ent + kEntData + j + 2) << 32;
+  int32_t have = 18 - (int32_t)j;   // lane bytes j - 2 .. 15
+  if (have < 8) {
+    w &= (1ull << (8 * have)) - 1ull;
+    if (kNextBytes<MODE> && (li & (kWave - 1)) != kWave - 1) {
+      w |= (uint64_t)(li >> 16) << (8 * have);
+      have += 2;
+    }
+  }
+  // the key's record, fetched by lane permutes before any divergent branch (a
+  // permute reading a lane outside EXEC would not see its record): key_class's
+  // own index computation, branch-free
+  const uint32_t key = (uint32_t)(w >> 16) & 0xFFu;
+  const uint32_t t = p.byte_keys ^ (key * 0x01010101u);
+  const uint32_t z = (t - 0x01010101u) & ~t & 0x80808080u;
+  const KeyClassRec r = scan_key_rec(kcv_, (uint32_t)__builtin_ctz(z | 0x80000000u) >> 3);
+  bool more = false;
+  const uint32_t cls = key_class(p, [r](uint32_t) { return r; }, w, 2, false, seg_start + off + 1,
+                                 min(have, 8) - 1, &more);
+  return off | (cls == 0u && more ? kClassFetch : cls) << kOutByteShift |
+         kOutPlaceScanClass << kOutKeyShift;
+}
+
 template <int MODE>
 __device__ __forceinline__ void resolve_pending(const ScanParams& p, WaveQueue& q, uint32_t lane,
-                                                uint32_t from) {
+                                                uint32_t from, uint64_t seg_start) {
   __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
-  if (lane >= from && lane < q.pend_n) {
+  const bool act = lane >= from && lane < q.pend_n;
+  if constexpr (kDrop<MODE>) {
+    // every lane (EXEC is full here: the drains run on wave-uniform paths) --
+    // scan_class_entry's permutes need their source lanes active; an idle
+    // lane computes on pending entry `from`'s (raw) entry and stores nothing
+    const u32x2 e = lds_load<u32x2>(q.pend + 8 * (act ? lane : from));
+    const uint32_t ent = e.x & 0xFFFFFFu, j = e.x >> 24;
+    const uint32_t yc = scan_class_entry<MODE>(p, q.kcv, ent, j, e.y & 0x7FFFFFFFu, seg_start);
+    if (act) {
+      uint32_t x = 0u, y = yc;
+      if (!(e.y >> 31)) {
+        x = window4(ent, j);
+        y = e.y;
+      }
+      lds_store2(q.pend + 8 * lane, x, y);
+    }
+    return;
+  }
+  if (act) {
     const u32x2 e = lds_load<u32x2>(q.pend + 8 * lane);
     const uint32_t ent = e.x & 0xFFFFFFu, j = e.x >> 24;
-    uint32_t x, y = e.y & 0x7FFFFFFFu;
+    uint32_t x = 0u, y = e.y & 0x7FFFFFFFu;
     if (e.y >> 31) certain_entry<MODE>(p, ent, j, x, y);
     else x = window4(ent, j);
     lds_store2(q.pend + 8 * lane, x, y);
@@ -781,11 +872,11 @@ __device__ __forceinline__ void drain(const ScanParams& p, WaveQueue& q, uint32_
     }
     if (end <= base + kWave) {
       q.pend_n = end - base;
-      if constexpr (kBkResolve<MODE>) resolve_pending<MODE>(p, q, lane, from);
+      if constexpr (kBkResolve<MODE>) resolve_pending<MODE>(p, q, lane, from, seg_start);
       return;
     }
     q.pend_n = kWave;
-    if constexpr (kBkResolve<MODE>) resolve_pending<MODE>(p, q, lane, from);
+    if constexpr (kBkResolve<MODE>) resolve_pending<MODE>(p, q, lane, from, seg_start);
     from = 0;
     flush_pending<MODE>(p, q, lane, seg_start, out, found);
   }
@@ -1147,6 +1238,7 @@ __device__ __forceinline__ void scan_segment(const ScanParams& p, WaveQueue& q, 
       st.seg_start >= 4 ? *reinterpret_cast<const uint32_t*>(base - 4) : 0u);
   q.count = 0;
   q.pend_n = 0;
+  q.full = 0;
   q.defer = false;
   q.facc = 0u;
   q.ia = q.ib = 0u;
@@ -1182,7 +1274,10 @@ __device__ __forceinline__ void scan_segment(const ScanParams& p, WaveQueue& q, 
   if constexpr (kDeferFl<MODE>)
     if (q.defer) drain_complete<MODE>(p, q, lane, st.seg_start, st.out, st.found);
   if (q.pend_n != 0) flush_pending<MODE>(p, q, lane, st.seg_start, st.out, st.found);
-  if (lane == 0) p.seg_count[seg] = st.found;
+  if (lane == 0) {
+    p.seg_count[seg] = st.found;
+    if (kDrop<MODE>) p.seg_full[seg] = q.full;
+  }
 }
 
 template <int MODE>
@@ -1210,8 +1305,12 @@ __global__ __launch_bounds__(kWGThreads, 1) void scan_segments_kernel(ScanParams
   const uint32_t wid = __builtin_amdgcn_readfirstlane(threadIdx.x / kWave);
   const uint32_t total_waves = gridDim.x * kWavesPerWG;
   uint32_t seg = blockIdx.x * kWavesPerWG + wid;
+  uint32_t kcv = 0u;
+  if constexpr (kDrop<MODE>)
+    if (lane < 32u) kcv = p.kc[lane];
   while (seg < p.n_segments) {
     WaveQueue q;   // (per segment: its per-lane state then stays in registers)
+    q.kcv = kcv;
     q.ring = kFilterBytes + wid * (kQueueCap * kQueueEntryWords * 4);
     q.pend = kFilterBytes + kQueueBytes + wid * (kWave * 8);
     __builtin_amdgcn_s_setprio(1);
@@ -1285,6 +1384,7 @@ __global__ __launch_bounds__(1024) void seg_offsets_kernel(const uint32_t* seg_c
       // (host-mapped coherent memory: system-scope stores)
       __hip_atomic_store(&summary[0], inc, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
       __hip_atomic_store(&summary[1], (uint64_t)m, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+      seg_offset[n] = inc;   // (the total for device-side readers)
     }
   }
   __syncthreads();
@@ -1308,18 +1408,13 @@ constexpr uint32_t kScatterWaves = 8;   // waves per segment in the scatter (den
 // fuzz0's pre-verification 0.63 -> 0.32 ms for 0.08 ms more compaction, rx
 // +0.02 ms, short / fuzz3 unchanged (profiles/r04_ab_inproc.json, gpurun h8).
 
-// per-segment LDS buffer of live candidates (the diagnostic build holds one,
-// so that the GPU suite exercises the overflow path, tests/test_preverify.py)
-constexpr uint32_t kLiveBuf = YAMD_DIAG ? 1 : 2048;
-
 template <uint32_t W>
 __global__ __launch_bounds__(W * kWave) void seg_scatter_kernel(
     ScanParams p, const uint64_t* seg_offset, uint64_t* positions) {
   // one block of W waves per segment (segments hold up to ~10^4 candidates),
   // its waves interleaved 64 candidates apart
   __shared__ KeyClassRec kc[kMaxByteKeys];
-  __shared__ uint32_t lbuf[kLiveBuf];
-  __shared__ uint32_t lcount, lglobal;
+  __shared__ uint32_t lcount;
   // the classes of a chunk of kChunk candidates, staged here and written out as
   // aligned dwords (one byte store per candidate ran at ~1.4 TB/s:
   // profiles/r04_ab_inproc.json h31); +4: the chunk's start is placed at its
@@ -1341,6 +1436,14 @@ __global__ __launch_bounds__(W * kWave) void seg_scatter_kernel(
   const uint32_t* sx = classes ? p.seg_x + at0 : nullptr;
   const uint64_t first = seg_offset[seg];
   uint64_t* dst = positions + first;
+  // verified-only scans: the full stream's index of every output candidate,
+  // when some candidate was left out (otherwise it is the output index)
+  uint32_t* cidx = nullptr;
+  uint32_t full0 = 0;
+  if (p.drop_dead != 0u && p.seg_full_offset[p.n_segments] != seg_offset[p.n_segments]) {
+    cidx = p.cand_index + first;
+    full0 = (uint32_t)p.seg_full_offset[seg];
+  }
   // (w through readfirstlane: the compiler then knows the loop's trips are
   // wave-uniform -- otherwise it runs the loop under an exec mask and carries
   // every wave-uniform value of it as a lane mask)
@@ -1370,14 +1473,22 @@ __global__ __launch_bounds__(W * kWave) void seg_scatter_kernel(
       }
       const uint64_t pos = base + (ec & kOutOffsetMask);
       if (valid) dst[i] = pos;
+      if (valid && cidx != nullptr) cidx[i] = full0 + xc;   // (mod 2^32, as the records')
       if (!classes) continue;
       // the certain candidates' classes from the bytes the scan kept beside them
+      // (verified-only scans: decided by the scan, kernels.hip scan_class_entry)
       uint32_t cls = 0u;
       if (valid && (ec & kCertainMask) != 0u) {
         bool more = false;
-        cls = key_class(p, kc, xc | (uint64_t)(ec >> kOutByteShift & 0xFFu) << 32,
-                        (int32_t)(ec >> kOutKeyShift & 7u) - 2, (ec & kOutDeep) != 0u, pos, 4,
-                        &more);
+        if ((ec >> kOutKeyShift & 7u) == kOutPlaceScanClass) {
+          cls = ec >> kOutByteShift & 0xFFu;
+          more = cls == kClassFetch;
+          if (more) cls = 0u;
+        } else {
+          cls = key_class(p, [](uint32_t k) { return kc[k]; },
+                          xc | (uint64_t)(ec >> kOutByteShift & 0xFFu) << 32,
+                          (int32_t)(ec >> kOutKeyShift & 7u) - 2, (ec & kOutDeep) != 0u, pos, 4, &more);
+        }
         // Undecided only because the guard's bytes (or the byte before the key)
         // lie outside the five the scan kept -- the key near its lane's end:
         // read eight bytes around the key from the input (three aligned dwords
@@ -1392,17 +1503,17 @@ __global__ __launch_bounds__(W * kWave) void seg_scatter_kernel(
             const uint32_t sh = (uint32_t)(kb - 2 - a4);
             const uint64_t w8 = __builtin_amdgcn_alignbyte(d1, d0, sh) |
                                 (uint64_t)__builtin_amdgcn_alignbyte(d2, d1, sh) << 32;
-            cls = key_class(p, kc, w8, 2, false, pos, 7);
+            cls = key_class(p, [](uint32_t k) { return kc[k]; }, w8, 2, false, pos, 7);
           }
         }
       }
       if (valid) {
         cbuf[sh0 + (i - chunk)] = (uint8_t)cls;
       }
-      // the undecided ones onto the live list (any order): the segment's LDS
-      // buffer, copied out with ONE global atomic per segment (one per wave and
-      // iteration, serialised on the counter, took 1.2 ms for 34 M candidates);
-      // what does not fit goes straight to the global list
+      // the undecided ones onto the segment's live list (any order), in the
+      // segment's own range of p.live -- an LDS counter, no global atomic (one
+      // per segment on one global counter serialised ~4,096 of them: rx's
+      // compaction 51 us for 230 k candidates, gpurun r5h4)
       const bool live = valid && cls == 0u;
       const uint64_t lm = __ballot(live);
       if (lm != 0) {
@@ -1411,17 +1522,7 @@ __global__ __launch_bounds__(W * kWave) void seg_scatter_kernel(
         b = __builtin_amdgcn_readfirstlane(b);
         const uint32_t slot =
             b + __builtin_amdgcn_mbcnt_hi((uint32_t)(lm >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)lm, 0u));
-        if (live && slot < kLiveBuf) lbuf[slot] = (uint32_t)(first + i);
-        const uint64_t om = __ballot(live && slot >= kLiveBuf);
-        if (om != 0) {
-          uint32_t g = 0;
-          if (lane == 0) g = atomicAdd(p.live, (uint32_t)__popcll(om));
-          g = __builtin_amdgcn_readfirstlane(g);
-          if (live && slot >= kLiveBuf)
-            p.live[1 + g + __builtin_amdgcn_mbcnt_hi((uint32_t)(om >> 32),
-                                                     __builtin_amdgcn_mbcnt_lo((uint32_t)om, 0u))] =
-                (uint32_t)(first + i);
-        }
+        if (live) p.live[first + slot] = (uint32_t)(first + i);
       }
     }
     {
@@ -1446,11 +1547,7 @@ __global__ __launch_bounds__(W * kWave) void seg_scatter_kernel(
   }
   if (!classes) return;
   __syncthreads();
-  const uint32_t n = min(lcount, kLiveBuf);
-  if (n == 0) return;
-  if (threadIdx.x == 0) lglobal = atomicAdd(p.live, n) + 1u;
-  __syncthreads();
-  for (uint32_t t = threadIdx.x; t < n; t += kStride) p.live[lglobal + t] = lbuf[t];
+  if (threadIdx.x == 0) p.live_count[seg] = lcount;
 }
 
 // ---------------------------------------------------------------------------
@@ -1545,14 +1642,20 @@ hipError_t launch_scan(const ScanParams& p, int grid, hipStream_t s, int mode, h
         const int m = (p.kx_next != 0 ? 2 : 0) + (p.filter_mode == kFilterEven       ? 1
                                                   : p.filter_mode == kFilterEvenHash ? 3
                                                                                      : 0) * 4;
-        switch (m) {
-          case 0: YAMD_LAUNCH_SCAN(scan_segments_kernel<kModeByteKeys>); break;
-          case 2: YAMD_LAUNCH_SCAN(scan_segments_kernel<kModeByteKeysNext>); break;
-          case 4: YAMD_LAUNCH_SCAN(scan_segments_kernel<kModeByteKeysEven>); break;
-          case 6: YAMD_LAUNCH_SCAN(scan_segments_kernel<kModeByteKeysNextEven>); break;
-          case 12: YAMD_LAUNCH_SCAN(scan_segments_kernel<kModeByteKeysEvenHash>); break;
-          default: YAMD_LAUNCH_SCAN(scan_segments_kernel<kModeByteKeysNextEvenHash>); break;
-        }
+#define YAMD_BK_CASES(D)                                                                          \
+  switch (m) {                                                                                    \
+    case 0: YAMD_LAUNCH_SCAN(scan_segments_kernel<D + kModeByteKeys>); break;                     \
+    case 2: YAMD_LAUNCH_SCAN(scan_segments_kernel<D + kModeByteKeysNext>); break;                 \
+    case 4: YAMD_LAUNCH_SCAN(scan_segments_kernel<D + kModeByteKeysEven>); break;                 \
+    case 6: YAMD_LAUNCH_SCAN(scan_segments_kernel<D + kModeByteKeysNextEven>); break;             \
+    case 12: YAMD_LAUNCH_SCAN(scan_segments_kernel<D + kModeByteKeysEvenHash>); break;            \
+    default: YAMD_LAUNCH_SCAN(scan_segments_kernel<D + kModeByteKeysNextEvenHash>); break;        \
+  }
+        if (p.drop_dead != 0u)
+          YAMD_BK_CASES(kDropModes)
+        else
+          YAMD_BK_CASES(0)
+#undef YAMD_BK_CASES
       } else if (p.filter_mode == kFilterEven)
         YAMD_LAUNCH_SCAN(scan_segments_kernel<kModeEven>);
       else if (p.filter_mode == kFilterEvenHash)
@@ -1570,6 +1673,10 @@ hipError_t launch_compact(const ScanParams& p, uint64_t* seg_offset, uint64_t* s
   if (!scatter) {
     hipLaunchKernelGGL(seg_offsets_kernel, dim3(1), dim3(1024), 0, s, p.seg_count, p.n_segments,
                        p.seg_cap, seg_offset, summary);
+    // verified-only scans: the offsets and total of the segments' full streams
+    if (p.drop_dead != 0u)
+      hipLaunchKernelGGL(seg_offsets_kernel, dim3(1), dim3(1024), 0, s, (const uint32_t*)p.seg_full,
+                         p.n_segments, 0xFFFFFFFFu, p.seg_full_offset, summary + 2);
   } else {
     // sparse segments (the default capacity, no rerun at exact offsets: at
     // most one candidate per 256 bytes) take two waves each, dense ones
@@ -1581,6 +1688,14 @@ hipError_t launch_compact(const ScanParams& p, uint64_t* seg_offset, uint64_t* s
       hipLaunchKernelGGL(seg_scatter_kernel<kScatterWaves>, dim3(p.n_segments), dim3(kScatterWaves * kWave),
                          0, s, p, (const uint64_t*)seg_offset, positions);
   }
+  return hipGetLastError();
+}
+
+// Exclusive offsets of n counts, the total at offsets[n] and in summary[0]
+// (pre-verification's live lists).
+hipError_t launch_counts_offsets(const uint32_t* counts, uint32_t n, uint64_t* offsets, uint64_t* summary,
+                                 hipStream_t s) {
+  hipLaunchKernelGGL(seg_offsets_kernel, dim3(1), dim3(1024), 0, s, counts, n, 0xFFFFFFFFu, offsets, summary);
   return hipGetLastError();
 }
 
@@ -1603,6 +1718,12 @@ hipError_t configure_scan_kernel() {
                         (const void*)scan_segments_kernel<kModeByteKeysEvenHash>,
                         (const void*)scan_segments_kernel<kModeByteKeysNextEven>,
                         (const void*)scan_segments_kernel<kModeByteKeysNextEvenHash>,
+                        (const void*)scan_segments_kernel<kDropModes + kModeByteKeys>,
+                        (const void*)scan_segments_kernel<kDropModes + kModeByteKeysNext>,
+                        (const void*)scan_segments_kernel<kDropModes + kModeByteKeysEven>,
+                        (const void*)scan_segments_kernel<kDropModes + kModeByteKeysEvenHash>,
+                        (const void*)scan_segments_kernel<kDropModes + kModeByteKeysNextEven>,
+                        (const void*)scan_segments_kernel<kDropModes + kModeByteKeysNextEvenHash>,
 #if YAMD_DIAG
                         (const void*)scan_segments_kernel<1>,
                         (const void*)scan_segments_kernel<2>, (const void*)scan_segments_kernel<3>,

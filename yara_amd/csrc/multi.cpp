@@ -45,7 +45,10 @@ int lane_open(Lane& L, yr_amd_tables* tables) {
     L.stream = nullptr;
     return YR_AMD_INTERNAL_FATAL_ERROR;
   }
-  return yr_amd_scanner_create(tables, L.stream, &L.scanner);
+  int r = yr_amd_scanner_create(tables, L.stream, &L.scanner);
+  // a lane's scans serve its records only
+  if (!r) r = yr_amd_scanner_set_verified_only(L.scanner, 1);
+  return r;
 }
 
 void lane_close(Lane& L) {
@@ -83,7 +86,10 @@ int lane_scan(Lane& L, uint64_t size, uint64_t data_base) {
   if (hipSetDevice(L.device) != hipSuccess) return YR_AMD_INTERNAL_FATAL_ERROR;
   int r = yr_amd_scan_window(L.scanner, L.d_win, L.lo, L.hi, size, L.begin, L.end);
   int all = 0;
-  if (!r) r = yr_amd_scan_device_result(L.scanner, nullptr, &L.candidates, &all);
+  if (!r) r = yr_amd_scan_device_result(L.scanner, nullptr, nullptr, &all);
+  // (the full stream's length: a verified-only scan's result may leave
+  // candidates out, the records' candidate indices do not)
+  if (!r) r = yr_amd_scan_device_stream_length(L.scanner, &L.candidates);
   // a root-accepting rule set: every position of (begin, end] is a candidate
   // (and position 0 on the lane that starts the block)
   if (all) L.candidates = (L.end - L.begin) + (L.begin == 0 ? 1u : 0u);

@@ -97,9 +97,14 @@ struct yr_amd_tables {
   uint32_t kd_m[4] = {0, 0, 0, 0}, kd_v[4] = {0, 0, 0, 0}, kd_info[4] = {0, 0, 0, 0};
   uint32_t kd_x0[4] = {0, 0, 0, 0}, kd_x1[4] = {0, 0, 0, 0};
   uint32_t kd_n[4] = {0, 0, 0, 0}, kd_head[4] = {0, 0, 0, 0}, kd_min_pos[4] = {0, 0, 0, 0};
+  uint32_t kd_idx[4][4] = {}, kd_bt[4][4] = {};   // a kept key's first list entries (VerifyParams)
   bool kd_any = false;
+  bool kd_guard = false;              // some key's class is guard-decided (can be dead)
+  bool kd_kept = false;               // some key's class is "kept" (every call a record)
+  uint32_t max_list = 0;              // the longest match list (pool chain)
   uint32_t kx_end = 2, kx_deep = 0, kx_next = 0;   // ScanParams::kx_end / kx_deep / kx_next
   uint32_t* d_nodes = nullptr;        // accepting nodes by string (FlatTables::nodes)
+  uint32_t* d_kc = nullptr;           // [32] the key class records (ScanParams::kc)
   DevPoolRec* d_pool = nullptr;       // per pool entry: link, backtrack, string, programs
   uint8_t* d_str_bytes = nullptr;
   uint8_t* d_lowercase = nullptr;
@@ -124,10 +129,19 @@ struct yr_amd_scanner {
   uint64_t* d_positions = nullptr;
   uint8_t* d_dead = nullptr;            // per candidate: the scan proved its calls dead
   size_t dead_cap = 0;
-  uint32_t* d_live = nullptr;           // [0] count, then the other candidates (ScanParams::live)
+  uint32_t* d_live = nullptr;           // per segment, its undecided candidates (ScanParams::live)
   size_t live_cap = 0;
+  uint32_t* d_live_count = nullptr;     // [seg_alloc] (ScanParams::live_count)
+  uint64_t* d_live_off = nullptr;       // [seg_alloc + 1] (VerifyParams::live_off)
   uint32_t* d_seg_x = nullptr;          // beside the segment outputs (ScanParams::seg_x)
   size_t seg_x_cap = 0;
+  // verified-only scans (yr_amd_scanner_set_verified_only; ScanParams::drop_dead)
+  bool verified_only = false;
+  uint32_t* d_seg_full = nullptr;       // [seg_alloc] each segment's full-stream length
+  uint64_t* d_seg_full_offset = nullptr;   // [seg_alloc + 1]
+  uint32_t* d_cand_index = nullptr;     // per output candidate: its full-stream index
+  size_t cand_index_cap = 0;
+  uint64_t last_full_count = 0;         // the last scan's full-stream length
   size_t positions_cap = 0;             // entries
   uint64_t* h_summary = nullptr;        // pinned, coherent: {total, max per segment}
   uint64_t* d_hsum = nullptr;           // h_summary mapped for the device: the offsets
@@ -224,14 +238,28 @@ int grow(T*& p, size_t& cap, size_t need) {
 int ensure_segments(yr_amd_scanner* s, uint32_t n_segments, uint32_t seg_cap) {
   if (n_segments > s->seg_alloc) {
     size_t c = 0;
-    if (s->d_seg_count) (void)hipFree(s->d_seg_count);
-    if (s->d_seg_offset) (void)hipFree(s->d_seg_offset);
+    for (void* q : {(void*)s->d_seg_count, (void*)s->d_seg_offset, (void*)s->d_seg_full,
+                    (void*)s->d_seg_full_offset, (void*)s->d_live_count, (void*)s->d_live_off})
+      if (q) (void)hipFree(q);
+    s->d_live_count = nullptr;
+    s->d_live_off = nullptr;
     s->d_seg_count = nullptr;
     s->d_seg_offset = nullptr;
+    s->d_seg_full = nullptr;
+    s->d_seg_full_offset = nullptr;
     s->seg_alloc = 0;
     if (grow(s->d_seg_count, c, n_segments)) return YR_AMD_INSUFFICIENT_MEMORY;
+    // (+1: the offsets kernel stores the total behind the offsets)
     c = 0;
-    if (grow(s->d_seg_offset, c, n_segments)) return YR_AMD_INSUFFICIENT_MEMORY;
+    if (grow(s->d_seg_offset, c, (size_t)n_segments + 1)) return YR_AMD_INSUFFICIENT_MEMORY;
+    c = 0;
+    if (grow(s->d_seg_full, c, n_segments)) return YR_AMD_INSUFFICIENT_MEMORY;
+    c = 0;
+    if (grow(s->d_seg_full_offset, c, (size_t)n_segments + 1)) return YR_AMD_INSUFFICIENT_MEMORY;
+    c = 0;
+    if (grow(s->d_live_count, c, n_segments)) return YR_AMD_INSUFFICIENT_MEMORY;
+    c = 0;
+    if (grow(s->d_live_off, c, (size_t)n_segments + 1)) return YR_AMD_INSUFFICIENT_MEMORY;
     s->seg_alloc = n_segments;
   }
   return grow(s->d_seg_out, s->seg_out_cap, (size_t)n_segments * seg_cap);
@@ -258,12 +286,17 @@ int run_scan(yr_amd_scanner* s) {
   const size_t out_cap = p.seg_base ? s->rerun_total : (size_t)p.n_segments * p.seg_cap;
   int r = grow(s->d_positions, s->positions_cap, out_cap);
   if (!r && s->tables->kd_any) r = grow(s->d_dead, s->dead_cap, out_cap);
-  if (!r && s->tables->kd_any) r = grow(s->d_live, s->live_cap, out_cap + 1);
+  if (!r && s->tables->kd_any) r = grow(s->d_live, s->live_cap, out_cap);
   if (!r && s->tables->kd_any) r = grow(s->d_seg_x, s->seg_x_cap, out_cap);
+  if (!r && p.drop_dead) r = grow(s->d_cand_index, s->cand_index_cap, out_cap);
   if (r) return r;
   s->last.dead = s->tables->kd_any ? s->d_dead : nullptr;
   s->last.live = s->tables->kd_any ? s->d_live : nullptr;
+  s->last.live_count = s->tables->kd_any ? s->d_live_count : nullptr;
   s->last.seg_x = s->tables->kd_any ? s->d_seg_x : nullptr;
+  s->last.seg_full = p.drop_dead ? s->d_seg_full : nullptr;
+  s->last.seg_full_offset = p.drop_dead ? s->d_seg_full_offset : nullptr;
+  s->last.cand_index = p.drop_dead ? s->d_cand_index : nullptr;
   // (timing: the kernel's own start / end stamps -- not two markers around
   // the launch, which would also count its dispatch)
   if (s->timing) {
@@ -273,7 +306,6 @@ int run_scan(yr_amd_scanner* s) {
     HIP_TRY(launch_scan(p, s->last_grid, s->stream, s->diag_mode));
   }
   HIP_TRY(launch_compact(p, s->d_seg_offset, s->d_hsum, nullptr, false, s->stream));
-  if (p.live != nullptr) HIP_TRY(hipMemsetAsync(p.live, 0, sizeof(uint32_t), s->stream));
   HIP_TRY(launch_compact(p, s->d_seg_offset, s->d_hsum, s->d_positions, true, s->stream));
   // one event marks the end of the scan's work: the timed one when timing (a
   // second event record at the same point would add a ~5 us gap per scan on
@@ -327,7 +359,7 @@ int yr_amd_tables_create(const uint32_t* transition_table, const uint32_t* match
 
 int yr_amd_tables_destroy(yr_amd_tables* t) {
   if (t == nullptr) return YR_AMD_SUCCESS;
-  for (void* p : {(void*)t->d_filter, (void*)t->d_exact, (void*)t->d_nodes, (void*)t->d_pool,
+  for (void* p : {(void*)t->d_filter, (void*)t->d_exact, (void*)t->d_nodes, (void*)t->d_kc, (void*)t->d_pool,
                   (void*)t->d_str_bytes, (void*)t->d_lowercase, (void*)t->d_re_code})
     if (p) (void)hipFree(p);
   delete t;
@@ -392,7 +424,8 @@ int yr_amd_scanner_create(yr_amd_tables* tables, void* stream, yr_amd_scanner** 
     }
     s->own_stream = true;
   }
-  if (hipHostMalloc((void**)&s->h_summary, 2 * sizeof(uint64_t), hipHostMallocCoherent) !=
+  // {total, max per segment, full-stream total, max} (ScanParams::drop_dead)
+  if (hipHostMalloc((void**)&s->h_summary, 4 * sizeof(uint64_t), hipHostMallocCoherent) !=
           hipSuccess ||
       hipHostGetDevicePointer((void**)&s->d_hsum, s->h_summary, 0) != hipSuccess ||
       hipMalloc((void**)&s->d_summary, 2 * sizeof(uint64_t)) != hipSuccess ||
@@ -410,7 +443,8 @@ int yr_amd_scanner_destroy(yr_amd_scanner* s) {
   for (void* p : {(void*)s->d_block, (void*)s->d_seg_count,
                   (void*)s->d_seg_offset,
                   (void*)s->d_seg_out, (void*)s->d_positions, (void*)s->d_dead, (void*)s->d_live,
-                  (void*)s->d_seg_x,
+                  (void*)s->d_seg_x, (void*)s->d_seg_full, (void*)s->d_seg_full_offset,
+                  (void*)s->d_cand_index, (void*)s->d_live_count, (void*)s->d_live_off,
                   (void*)s->d_summary,
                   (void*)s->d_vcount, (void*)s->d_vkeep, (void*)s->d_vblock, (void*)s->d_vrec,
                   (void*)s->d_vchunk, (void*)s->d_seg_base,
@@ -423,6 +457,18 @@ int yr_amd_scanner_destroy(yr_amd_scanner* s) {
   if (s->ev_done) (void)hipEventDestroy(s->ev_done);
   if (s->own_stream && s->stream) (void)hipStreamDestroy(s->stream);
   delete s;
+  return YR_AMD_SUCCESS;
+}
+
+int yr_amd_scanner_set_verified_only(yr_amd_scanner* s, int enable) {
+  if (s == nullptr) return YR_AMD_INVALID_ARGUMENT;
+  s->verified_only = enable != 0;
+  return YR_AMD_SUCCESS;
+}
+
+int yr_amd_scan_device_stream_length(yr_amd_scanner* s, uint64_t* length) {
+  if (s == nullptr || length == nullptr || s->pending) return YR_AMD_INVALID_ARGUMENT;
+  *length = s->last_full_count;
   return YR_AMD_SUCCESS;
 }
 
@@ -467,6 +513,10 @@ int yr_amd__diag_key_classes(const yr_amd_tables* t, uint32_t* out) {
   out[1] = t->flat.byte_keys;
   out[2] = t->flat.n_byte_keys;
   for (int k = 0; k < 4; ++k) out[3 + k] = t->kd_info[k], out[7 + k] = t->kd_m[k], out[11 + k] = t->kd_v[k];
+  // [15..18] kd_x0, [19..22] kd_x1, [23..26] kd_min_pos, [27] kx_deep, [28] kx_next
+  for (int k = 0; k < 4; ++k) out[15 + k] = t->kd_x0[k], out[19 + k] = t->kd_x1[k], out[23 + k] = t->kd_min_pos[k];
+  out[27] = t->kx_deep;
+  out[28] = t->kx_next;
   return YR_AMD_SUCCESS;
 }
 
@@ -511,6 +561,7 @@ int yr_amd_scan_window(yr_amd_scanner* s, const uint8_t* d_window, uint64_t wind
   const yr_amd_tables* t = s->tables;
   s->pending = true;
   s->last_count = 0;
+  s->last_full_count = 0;
   s->ev_valid = false;
   s->win_lo = window_begin;
   s->win_hi = window_end;
@@ -527,7 +578,12 @@ int yr_amd_scan_window(yr_amd_scanner* s, const uint8_t* d_window, uint64_t wind
   s->last_empty = s->last_all || byte_end == byte_begin;
   s->last.dead = nullptr;
   s->last.live = nullptr;
+  s->last.live_count = nullptr;
   s->last.seg_x = nullptr;
+  s->last.drop_dead = 0;
+  s->last.seg_full = nullptr;
+  s->last.seg_full_offset = nullptr;
+  s->last.cand_index = nullptr;
   if (s->last_empty) return YR_AMD_SUCCESS;
   if (d_window == nullptr) return YR_AMD_INVALID_ARGUMENT;
   HIP_TRY(hipSetDevice(t->device));
@@ -584,6 +640,11 @@ int yr_amd_scan_window(yr_amd_scanner* s, const uint8_t* d_window, uint64_t wind
     p.kd_min_pos[k] = t->kd_min_pos[k];
   }
   p.filter_mode = t->flat.filter_mode;
+  // verified-only: the byte-key kernel decides the certain candidates' classes
+  // and leaves the dead ones out (kd_any: 1-byte keys with classes; never with
+  // profiling, whose count-only records need every call)
+  p.drop_dead = s->verified_only && t->kd_guard && !t->profile && t->flat.n_byte_keys != 0 ? 1u : 0u;
+  p.kc = t->d_kc;
   p.n_segments = n_segments;
   p.seg_bytes = seg_bytes;
   p.seg_cap = seg_cap;
@@ -645,6 +706,7 @@ int yr_amd_scan_device_result(yr_amd_scanner* s, const uint64_t** d_positions, u
     if (s->h_summary[0] != total) return YR_AMD_INTERNAL_FATAL_ERROR;
   }
   s->last_count = total;
+  s->last_full_count = s->last.drop_dead ? s->h_summary[2] : total;
   s->pending = false;
   if (d_positions) *d_positions = s->d_positions;
   if (count) *count = total;
@@ -924,9 +986,34 @@ namespace {
 void key_classes(yr_amd_tables* t) {
   const FlatTables& f = t->flat;
   t->kd_any = false;
+  t->kd_guard = false;
+  t->kd_kept = false;
   t->kx_end = 2;
+  {
+    // the longest match list: the longest chain of pool links (each list is
+    // a chain from its head)
+    // chain, memoised (lists share tails: a state's list ends with its
+    // failure state's, ahocorasick.c:254-300); a bad link counts as overlong
+    const size_t np = t->h_pool.size();
+    std::vector<uint32_t> len(np + 1, 0), path;
+    t->max_list = 0;
+    for (size_t q0 = 1; q0 <= np; ++q0) {
+      path.clear();
+      uint32_t q = (uint32_t)q0, tail = 0;
+      while (q != 0 && len[q] == 0) {
+        if (q > np || path.size() > np) { tail = 1000; break; }
+        path.push_back(q);
+        q = t->h_pool[q - 1].next;
+      }
+      if (tail == 0 && q != 0) tail = len[q];
+      for (size_t e = path.size(); e-- > 0;) len[path[e]] = ++tail;
+      t->max_list = std::max(t->max_list, len[q0]);
+    }
+  }
   t->kx_deep = 0;
   t->kx_next = 0;
+  for (int k = 0; k < 4; ++k)
+    for (int e = 0; e < 4; ++e) t->kd_idx[k][e] = t->kd_bt[k][e] = 0;
   for (int k = 0; k < 4; ++k)
     t->kd_m[k] = t->kd_v[k] = t->kd_info[k] = t->kd_x0[k] = t->kd_x1[k] = t->kd_n[k] =
         t->kd_head[k] = t->kd_min_pos[k] = 0;
@@ -1018,12 +1105,19 @@ void key_classes(yr_amd_tables* t) {
     uint32_t info = 1u | (o.nx ? 2u : 0u);
     if (o.kept) {
       info |= 4u;
+      t->kd_kept = true;
       t->kd_n[k] = o.n;
       t->kd_head[k] = o.head;
       t->kd_min_pos[k] = o.min_pos;
+      uint32_t q = o.head;
+      for (uint32_t e = 0; e < 4 && q != 0; ++e, q = t->h_pool[q - 1].next) {
+        t->kd_idx[k][e] = q - 1;
+        t->kd_bt[k][e] = t->h_pool[q - 1].backtrack;
+      }
     } else {
       t->kd_m[k] = o.m;
       t->kd_v[k] = o.v;
+      t->kd_guard = true;
       t->kx_next = 1;   // (a guard's bytes may run past the lane: keep the next lane's two)
       info |= ((uint32_t)(uint8_t)(int8_t)o.rs << 8) | ((uint32_t)o.span << 16) |
               ((uint32_t)o.tmax << 20) | ((uint32_t)(uint8_t)(int8_t)o.end << 24);
@@ -1032,6 +1126,21 @@ void key_classes(yr_amd_tables* t) {
     t->kd_x0[k] = o.xs0;
     t->kd_x1[k] = o.xs1;
     t->kd_any = true;
+  }
+  // the records the scan kernel reads (ScanParams::kc); without them, no
+  // classes at all (the scan then keeps every candidate: still exact)
+  uint32_t kc[32] = {};
+  for (int k = 0; k < 4; ++k) {
+    const uint32_t r[6] = {t->kd_info[k], t->kd_m[k], t->kd_v[k], t->kd_x0[k], t->kd_x1[k], t->kd_min_pos[k]};
+    for (int f = 0; f < 6; ++f) kc[8 * k + f] = r[f];
+  }
+  if ((t->d_kc == nullptr && hipMalloc((void**)&t->d_kc, sizeof(kc)) != hipSuccess) ||
+      hipMemcpy(t->d_kc, kc, sizeof(kc), hipMemcpyHostToDevice) != hipSuccess) {
+    if (t->d_kc) (void)hipFree(t->d_kc);
+    t->d_kc = nullptr;
+    t->kd_any = false;
+    t->kd_guard = false;
+    t->kd_kept = false;
   }
 }
 }  // namespace
@@ -1150,9 +1259,23 @@ int yr_amd_verify_device(yr_amd_scanner* s, uint64_t data_base, const yr_amd_ver
     const bool classes = !t->profile && s->last_count <= 0xFFFFFFFFull;
     v.dead = classes ? L.dead : nullptr;
     v.live = classes ? L.live : nullptr;
+    v.live_count = L.live_count;
+    v.live_first = s->d_seg_offset;
+    v.live_segs = L.n_segments;
+    v.live_off = s->d_live_off;
+    // records in most groups (every candidate of a "kept" key is one): the
+    // write pass as one wave per group
+    v.direct = classes && t->kd_kept && t->max_list <= 31 ? 1 : 0;
+    // a verified-only scan that left candidates out: the records still index
+    // the full stream
+    v.cand_index = L.drop_dead && s->last_full_count != s->last_count ? L.cand_index : nullptr;
     for (int k = 0; k < 4; ++k) {
       v.kd_n[k] = L.kd_n[k];
       v.kd_head[k] = L.kd_head[k];
+      for (int e = 0; e < 4; ++e) {
+        v.kd_idx[k][e] = t->kd_idx[k][e];
+        v.kd_bt[k][e] = t->kd_bt[k][e];
+      }
     }
   }
   const FlatTables& f = t->flat;
@@ -1173,10 +1296,12 @@ int yr_amd_verify_device(yr_amd_scanner* s, uint64_t data_base, const yr_amd_ver
   // YR_AMD_VERIFY_MAX_CANDIDATES (2^32; possible only on blocks of 4 GiB or
   // more) is refused -- replay it on the host (yr_amd_scan_block +
   // yr_amd_replay) instead, as the libyara shim does for such blocks
-  if (v.count > YR_AMD_VERIFY_MAX_CANDIDATES) return YR_AMD_INVALID_ARGUMENT;
+  if (v.count > YR_AMD_VERIFY_MAX_CANDIDATES ||
+      (!v.all && s->last_full_count > YR_AMD_VERIFY_MAX_CANDIDATES))
+    return YR_AMD_INVALID_ARGUMENT;
   if (v.count > 0) {
     if (v.data == nullptr) return YR_AMD_INVALID_ARGUMENT;
-    int r = grow(s->d_vcount, s->vcount_cap, v.count);
+    int r = grow(s->d_vcount, s->vcount_cap, 2 * v.count);
     if (!r) r = grow(s->d_vkeep, s->vkeep_cap, 2 * v.count);
     if (!r) r = grow(s->d_vblock, s->vblock_cap, verify_groups(v.count) + 1);
     if (!r) r = grow(s->d_vchunk, s->vchunk_cap, verify_chunks(v.count) + 1);
@@ -1187,6 +1312,7 @@ int yr_amd_verify_device(yr_amd_scanner* s, uint64_t data_base, const yr_amd_ver
     if (!r) r = grow(s->d_vrec, s->vrec_cap, std::min<uint64_t>(v.count / 16 + 1, 1u << 20));
     if (r) return r;
     v.counts = s->d_vcount;
+    v.live_dense = s->d_vcount + v.count;   // (d_vcount: 2 x count, below)
     v.keep = s->d_vkeep;
     v.heads = s->d_vkeep + v.count;
     v.block_off = s->d_vblock;
@@ -1200,7 +1326,7 @@ int yr_amd_verify_device(yr_amd_scanner* s, uint64_t data_base, const yr_amd_ver
       // counts added to the groups' (zeroed here)
       HIP_TRY(hipMemsetAsync(v.block_off, 0, (verify_groups(v.count) + 1) * sizeof(uint64_t),
                              s->stream));
-      HIP_TRY(launch_verify_live(v, s->stream));
+      HIP_TRY(launch_verify_live(v, s->d_summary, s->stream));
     } else {
       HIP_TRY(launch_verify(v, 0, s->stream));
     }
@@ -1251,7 +1377,11 @@ int yr_amd_scan_block_verified(yr_amd_scanner* s, const uint8_t* data, size_t si
   if (size > 0 &&
       hipMemcpyAsync(s->d_block, data, size, hipMemcpyHostToDevice, s->stream) != hipSuccess)
     return YR_AMD_COULD_NOT_MAP_FILE;
+  // (a verified-only scan: nothing but the records leaves this call)
+  const bool was = s->verified_only;
+  s->verified_only = true;
   int r = yr_amd_scan_device(s, s->d_block, size, 0, size);
+  s->verified_only = was;
   if (!r) r = yr_amd_scan_device_result(s, nullptr, nullptr, nullptr);
   const yr_amd_verify_rec* d_rec = nullptr;
   uint64_t n = 0;

@@ -80,8 +80,24 @@ struct VerifyParams {
   const uint64_t* positions;  // ascending candidates (unused when all)
   const uint8_t* dead;        // null, or per candidate 1 = the scan proved no call of its
                               // list can have an effect (ScanParams::dead), and
-  const uint32_t* live;       // [0] = count, then the other candidates' indices
+  const uint32_t* live;       // per scan segment s: its other candidates' indices in
+                              // [live_first[s], + live_count[s]) (ScanParams::live)
+  const uint32_t* live_count; // [live_segs]
+  const uint64_t* live_first; // [live_segs] the segments' first candidate
+  uint32_t live_segs;
+  uint64_t* live_off;         // [live_segs + 1] workspace: the lists' offsets in live_dense, total
+  uint32_t* live_dense;       // [count] workspace: the lists concatenated
+  int direct;                 // pass 1 as a grid of one wave per group without LDS
+                              // (verify_write_kernel: records in most groups, the "kept"
+                              // 1-byte keys; lists of at most 31 entries, no profiling)
+                              // instead of persistent waves
+  const uint32_t* cand_index; // null, or per candidate its index in the scan's full stream
+                              // (verified-only scans that left candidates out): the
+                              // records' candidate field
   uint32_t kd_n[4], kd_head[4];   // the "kept" keys' list lengths and heads (ScanParams)
+  // the first kKeptDirect entries of each "kept" key's list: 0-based pool index
+  // and backtrack (pass 1 writes such a candidate's records without the pool)
+  uint32_t kd_idx[4][4], kd_bt[4][4];
   uint64_t count;             // candidates (size + 1 when all)
   int all;                    // every position of a range is a candidate:
   uint64_t all_first;         //   i = all_first + c
@@ -112,11 +128,12 @@ struct VerifyParams {
 };
 
 hipError_t launch_verify(const VerifyParams& p, int pass, hipStream_t s);
-// Pass 0 over the scan's live list (p.live; block_off zeroed): the dead
+// Pass 0 over the scan's live lists (p.live; block_off zeroed): the dead
 // candidates keep nothing and are never read.
-hipError_t launch_verify_live(const VerifyParams& p, hipStream_t s);
+hipError_t launch_verify_live(const VerifyParams& p, uint64_t* summary, hipStream_t s);
 // The "kept" keys' list lengths (the class byte's key index): their records
 // count into the group totals without pass 0.
+constexpr uint32_t kKeptDirect = 4;
 struct KeptLists {
   uint32_t n[4];
 };

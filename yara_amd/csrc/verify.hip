@@ -807,7 +807,7 @@ __device__ bool call_matters(const VerifyParams& p, const DevPoolRec& st, uint64
 // than 31 entries.
 constexpr uint32_t kKeepOverflow = 1u << 31;
 constexpr uint32_t kRecCountOnly = 0x80000000u;   // include/yara_amd.h YR_AMD_REC_COUNT_ONLY
-template <int PASS>
+template <int PASS, bool kLean = false>
 __device__ __forceinline__ void verify_one(const VerifyParams& p, uint64_t c, uint32_t lds,
                                            uint32_t codebuf, uint32_t keep, uint32_t head,
                                            uint64_t o, uint32_t& count) {
@@ -830,7 +830,9 @@ __device__ __forceinline__ void verify_one(const VerifyParams& p, uint64_t c, ui
   }
   // profiling: pass 1 decides again (the keep mask does not tell count-only
   // records from kept ones)
-  const bool decide = !PASS || (keep & kKeepOverflow) || p.profile;
+  // (kLean: a write pass without LDS -- only for tables whose lists fit the
+  // keep mask, without profiling: it never decides)
+  const bool decide = !kLean && (!PASS || (keep & kKeepOverflow) || p.profile);
   uint32_t n = 0, t = 0, mask = 0;
   // scanner.c:105-121: the list of state_i in pool order
   for (uint32_t k = head; k != 0; ++t) {
@@ -858,7 +860,7 @@ __device__ __forceinline__ void verify_one(const VerifyParams& p, uint64_t c, ui
       VerifyRec r;
       r.offset = i - bt;
       r.pool_index = (kk - 1) | (count_only ? kRecCountOnly : 0u);
-      r.candidate = (uint32_t)c;
+      r.candidate = p.cand_index != nullptr ? p.cand_index[c] : (uint32_t)c;
       if (o < p.out_cap) p.out[o] = r;
       ++o;
     } else if (t < 31) {
@@ -924,7 +926,84 @@ __device__ __forceinline__ void verify_group(const VerifyParams& p, uint64_t g, 
     }
   }
   const uint32_t pre = wave_exclusive(n);
-  if (keep != 0) verify_one<1>(p, c, lds, codebuf, keep, head, o + pre, n);
+  if ((cls & kClassKept) && n <= kKeptDirect) {
+    // every call of the key's list, from the key's own list copy: no pool
+    // records, no list walk (the dense "kept" keys' candidates)
+    const uint32_t k = (cls >> 2) & 3u;
+    const uint64_t i = p.positions[c];
+    uint64_t at = o + pre;
+    for (uint32_t t = 0; t < n; ++t, ++at) {
+      VerifyRec r;
+      r.offset = i - p.kd_bt[k][t];
+      r.pool_index = p.kd_idx[k][t];
+      r.candidate = p.cand_index != nullptr ? p.cand_index[c] : (uint32_t)c;
+      if (at < p.out_cap) p.out[at] = r;
+    }
+  } else if (keep != 0) {
+    verify_one<1>(p, c, lds, codebuf, keep, head, o + pre, n);
+  }
+}
+
+// The write pass as a grid covering every group, kWriteGroups groups per wave
+// (p.first: the launch's first group) -- for tables whose groups mostly have
+// records (the "kept" 1-byte keys: every candidate a record), where the
+// persistent waves of verify_kernel<1> take their groups one after another.
+// No LDS (every decision is pass 0's: VerifyParams::direct is set only where
+// lists fit the keep mask and without profiling), and every load the wave's
+// groups need -- offsets, classes, positions, pass 0's keep masks -- issued
+// together: one memory round trip before their records are written
+// (short, 16.8 M records: 234 us with one group per wave and LDS, 157 us
+// without LDS, gpurun r5h6 / r5h7).
+constexpr uint32_t kWriteGroups = 4;   // groups per wave (verify_write_kernel)
+__global__ __launch_bounds__(256) void verify_write_kernel(VerifyParams p) {
+  const uint64_t groups = (p.count + kGroup - 1) / kGroup;
+  const uint64_t g0 = p.first + ((uint64_t)blockIdx.x * (blockDim.x / 64) + wave_in_block()) * kWriteGroups;
+  if (g0 >= groups) return;
+  // kWriteGroups groups per wave, every load of all of them issued first
+  uint64_t o[kWriteGroups + 1], i[kWriteGroups];
+  uint32_t cls[kWriteGroups];
+#pragma unroll
+  for (uint32_t q = 0; q <= kWriteGroups; ++q) o[q] = g0 + q <= groups ? group_offset(p, g0 + q) : 0;
+#pragma unroll
+  for (uint32_t q = 0; q < kWriteGroups; ++q) {
+    const uint64_t c = (g0 + q) * kGroup + (threadIdx.x & 63u);
+    const bool in = c < p.count;
+    cls[q] = in && p.dead != nullptr ? p.dead[c] : 0u;
+    i[q] = in ? p.positions[c] : 0;
+  }
+#pragma unroll
+  for (uint32_t q = 0; q < kWriteGroups; ++q) {
+    const uint64_t g = g0 + q;
+    if (g >= groups || o[q + 1] == o[q]) continue;   // (wave-uniform)
+    const uint64_t c = g * kGroup + (threadIdx.x & 63u);
+    uint32_t keep = 0, n = 0, head = 0;
+    const uint32_t k = (cls[q] >> 2) & 3u;
+    if (cls[q] & kClassKept) {
+      n = p.kd_n[k];
+      keep = (1u << n) - 1u;
+      head = p.kd_head[k];
+    } else if (c < p.count && !(cls[q] & kClassDead)) {
+      keep = p.keep[c];   // (pass 0 wrote it for live candidates only)
+      if (keep != 0) {
+        n = p.counts[c];
+        head = p.heads[c];
+      }
+    }
+    const uint32_t pre = wave_exclusive(n);
+    if ((cls[q] & kClassKept) && n <= kKeptDirect) {
+      uint64_t at = o[q] + pre;
+      const uint32_t cand = p.cand_index != nullptr ? p.cand_index[c] : (uint32_t)c;
+      for (uint32_t t = 0; t < n; ++t, ++at) {
+        VerifyRec r;
+        r.offset = i[q] - p.kd_bt[k][t];
+        r.pool_index = p.kd_idx[k][t];
+        r.candidate = cand;
+        if (at < p.out_cap) p.out[at] = r;
+      }
+    } else if (keep != 0) {
+      verify_one<1, true>(p, c, 0u, 0u, keep, head, o[q] + pre, n);
+    }
+  }
 }
 
 // PASS 0: one candidate per lane; each wave's record count goes to its group.
@@ -940,7 +1019,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(5))) void v
   const uint32_t lds = (uint32_t)(uintptr_t)(win + threadIdx.x * kWinBytes);
   const uint32_t codebuf = (uint32_t)(uintptr_t)(code + threadIdx.x * kCodeBytes);
   const uint64_t groups = (p.count + kGroup - 1) / kGroup;
-  if (!PASS) {
+  if (PASS == 0) {
     const uint64_t c = p.first + (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
     uint32_t n = 0;
     if (c < p.count) verify_one<0>(p, c, lds, codebuf, 0, 0, 0, n);
@@ -948,6 +1027,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(5))) void v
     if ((threadIdx.x & 63u) == 0 && c / kGroup < groups) p.block_off[c / kGroup] = sum;
     return;
   }
+
   // wave w takes groups w, w + waves, ...; it tests 64 of them for records at
   // once (one lane each: a group without records reads nothing more -- most of
   // a dense rule set's, e.g. rx: 539 records from 525,000 groups), then runs
@@ -967,17 +1047,30 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(5))) void v
   }
 }
 
-// Pass 0 over the live list (persistent blocks): each live candidate decided
-// as verify_kernel<0> does, its record count added to its group's.
+// The scan segments' live lists concatenated (live_off: their offsets, from
+// launch_counts_offsets): one wave per segment, persistent over the segments.
+__global__ __launch_bounds__(256) void live_gather_kernel(VerifyParams p) {
+  const uint32_t waves = gridDim.x * (blockDim.x / 64), lane = threadIdx.x & 63u;
+  for (uint32_t seg = blockIdx.x * (blockDim.x / 64) + wave_in_block(); seg < p.live_segs; seg += waves) {
+    const uint32_t n = p.live_count[seg];
+    const uint32_t* src = p.live + p.live_first[seg];
+    uint32_t* dst = p.live_dense + p.live_off[seg];
+    for (uint32_t h = lane; h < n; h += 64) dst[h] = src[h];
+  }
+}
+
+// Pass 0 over the concatenated live lists (persistent blocks): each live
+// candidate decided as verify_kernel<0> does, its record count added to its
+// group's.
 __global__ __launch_bounds__(256) void verify_live_kernel(VerifyParams p) {
   __shared__ __attribute__((aligned(16))) uint8_t win[256 * kWinBytes];
   __shared__ __attribute__((aligned(16))) uint8_t code[256 * kCodeBytes];
   const uint32_t lds = (uint32_t)(uintptr_t)(win + threadIdx.x * kWinBytes);
   const uint32_t codebuf = (uint32_t)(uintptr_t)(code + threadIdx.x * kCodeBytes);
-  const uint32_t n_live = p.live[0];
+  const uint64_t n_live = p.live_off[p.live_segs];
   for (uint64_t h = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; h < n_live;
        h += (uint64_t)gridDim.x * blockDim.x) {
-    const uint32_t c = p.live[1 + h];
+    const uint32_t c = p.live_dense[h];
     uint32_t n = 0;
     verify_one<0>(p, c, lds, codebuf, 0, 0, 0, n);
     if (n != 0) atomicAdd(reinterpret_cast<unsigned long long*>(p.block_off + c / kGroup),
@@ -1102,6 +1195,18 @@ hipError_t launch_verify(const VerifyParams& p, int pass, hipStream_t s) {
       const hipError_t e = hipGetLastError();
       if (e != hipSuccess) return e;
     }
+  } else if (p.direct) {
+    // kWriteGroups groups per wave, in slices of 2^31 work-items per dispatch
+    constexpr uint64_t kSliceGroups = (1ull << 31) / kGroup;
+    const uint64_t groups = verify_groups(p.count);
+    VerifyParams q = p;
+    for (q.first = 0; q.first < groups; q.first += kSliceGroups) {
+      const uint64_t n = std::min<uint64_t>(groups - q.first, kSliceGroups);
+      const uint64_t waves = (n + kWriteGroups - 1) / kWriteGroups;
+      hipLaunchKernelGGL(verify_write_kernel, dim3((uint32_t)((waves + 3) / 4)), dim3(256), 0, s, q);
+      const hipError_t e = hipGetLastError();
+      if (e != hipSuccess) return e;
+    }
   } else {
     const uint64_t waves = verify_groups(p.count);
     const uint32_t blocks = (uint32_t)std::min<uint64_t>(
@@ -1111,8 +1216,13 @@ hipError_t launch_verify(const VerifyParams& p, int pass, hipStream_t s) {
   return hipGetLastError();
 }
 
-hipError_t launch_verify_live(const VerifyParams& p, hipStream_t s) {
-  if (p.count == 0) return hipSuccess;
+hipError_t launch_counts_offsets(const uint32_t* counts, uint32_t n, uint64_t* offsets, uint64_t* summary,
+                                 hipStream_t s);   // (kernels.hip)
+hipError_t launch_verify_live(const VerifyParams& p, uint64_t* summary, hipStream_t s) {
+  if (p.count == 0 || p.live_segs == 0) return hipSuccess;
+  hipError_t e = launch_counts_offsets(p.live_count, p.live_segs, p.live_off, summary, s);
+  if (e != hipSuccess) return e;
+  hipLaunchKernelGGL(live_gather_kernel, dim3((p.live_segs + 3) / 4), dim3(256), 0, s, p);
   const uint32_t blocks = (uint32_t)std::min<uint64_t>(
       (p.count + 255) / 256, resident_blocks((const void*)verify_live_kernel));
   hipLaunchKernelGGL(verify_live_kernel, dim3(blocks), dim3(256), 0, s, p);
