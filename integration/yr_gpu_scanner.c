@@ -767,6 +767,61 @@ static void _clean_matches(YR_SCANNER* scanner)
       sizeof(YR_MATCHES) * scanner->rules->num_strings);
 }
 
+/* Diagnostics (not part of the drop-in API; tools/replay_profile.py): the
+ * replay of one block's records on a scanner set up as for a scan, timed.
+ * mode 0: the shim's replay (_replay_records: the walk's timeout checks, then
+ * yr_scan_verify_match per record); 1: the shim's per-record work without the
+ * libyara call; 2: yr_scan_verify_match alone, one call per record.  With
+ * timeout_ns > 0 the scanner has that timeout (the checks then read the
+ * clock).  The scan state is cleared afterwards, as a scan's end does. */
+int yr_gpu_replay_profile(
+    YR_SCANNER* scanner,
+    const yr_amd_verify_rec* recs,
+    uint64_t n,
+    const uint8_t* data,
+    size_t size,
+    int mode,
+    uint64_t timeout_ns,
+    double* seconds)
+{
+  uint32_t max_match_data;
+  int result = ERROR_SUCCESS;
+  FAIL_ON_ERROR(yr_get_configuration_uint32(YR_CONFIG_MAX_MATCH_DATA, &max_match_data));
+  FAIL_ON_ERROR(yr_notebook_create(
+      1024 * (sizeof(YR_MATCH) + max_match_data), &scanner->matches_notebook));
+  scanner->timeout = timeout_ns;
+  yr_stopwatch_start(&scanner->stopwatch);
+  double t0 = _now();
+  if (mode == 0)
+  {
+    result = _replay_records(scanner, recs, n, data, size, 0, 0);
+  }
+  else if (mode == 1)
+  {
+    verify_ctx c = {scanner, data, size, 0, 0};
+    volatile uintptr_t sink = 0;
+    for (uint64_t k = 0; k < n && result == ERROR_SUCCESS; k++)
+    {
+      YR_AC_MATCH* m = &scanner->rules->ac_match_pool[recs[k].pool_index];
+      result = _timeout_upto(scanner, &c.next_check, recs[k].offset + m->backtrack, size);
+      sink ^= (uintptr_t) m ^ recs[k].offset;
+    }
+  }
+  else
+  {
+    for (uint64_t k = 0; k < n && result == ERROR_SUCCESS; k++)
+      result = yr_scan_verify_match(
+          scanner, &scanner->rules->ac_match_pool[recs[k].pool_index], data, size, 0,
+          (size_t) recs[k].offset);
+  }
+  *seconds = _now() - t0;
+  scanner->timeout = 0;
+  _clean_matches(scanner);
+  yr_notebook_destroy(scanner->matches_notebook);
+  scanner->matches_notebook = NULL;
+  return result;
+}
+
 /* yr_scanner_scan_mem_blocks (scanner.c:417-583) with the GPU block scan. */
 int yr_gpu_scanner_scan_mem_blocks(
     YR_SCANNER* scanner,

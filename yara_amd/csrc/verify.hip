@@ -962,20 +962,23 @@ __global__ __launch_bounds__(256) void verify_write_kernel(VerifyParams p) {
   // kWriteGroups groups per wave, every load of all of them issued first
   uint64_t o[kWriteGroups + 1], i[kWriteGroups];
   uint32_t cls[kWriteGroups];
+  // (indices clamped rather than loads predicated: no branch between the
+  // loads, so they all go out before the first wait -- the predicated form
+  // compiled to one dependent round trip per group offset)
 #pragma unroll
-  for (uint32_t q = 0; q <= kWriteGroups; ++q) o[q] = g0 + q <= groups ? group_offset(p, g0 + q) : 0;
+  for (uint32_t q = 0; q <= kWriteGroups; ++q) o[q] = group_offset(p, min(g0 + q, groups));
 #pragma unroll
   for (uint32_t q = 0; q < kWriteGroups; ++q) {
-    const uint64_t c = (g0 + q) * kGroup + (threadIdx.x & 63u);
-    const bool in = c < p.count;
-    cls[q] = in && p.dead != nullptr ? p.dead[c] : 0u;
-    i[q] = in ? p.positions[c] : 0;
+    const uint64_t c = min((g0 + q) * kGroup + (threadIdx.x & 63u), p.count - 1);
+    cls[q] = p.dead != nullptr ? p.dead[c] : 0u;
+    i[q] = p.positions[c];
   }
 #pragma unroll
   for (uint32_t q = 0; q < kWriteGroups; ++q) {
     const uint64_t g = g0 + q;
     if (g >= groups || o[q + 1] == o[q]) continue;   // (wave-uniform)
     const uint64_t c = g * kGroup + (threadIdx.x & 63u);
+    if (c >= p.count) cls[q] = 0u;   // (past the stream: no records)
     uint32_t keep = 0, n = 0, head = 0;
     const uint32_t k = (cls[q] >> 2) & 3u;
     if (cls[q] & kClassKept) {
