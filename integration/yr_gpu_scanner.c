@@ -28,6 +28,9 @@
  */
 #include "yr_gpu_scanner.h"
 
+#include <pthread.h>
+#include <setjmp.h>
+#include <signal.h>
 #include <stdlib.h>
 #include <string.h>
 #include <yara.h>
@@ -302,11 +305,63 @@ void yr_gpu_rules_destroy(YR_GPU_RULES* g)
  * it is copied (a file mapping truncated underneath) fails the copy, and the
  * scan returns ERROR_COULD_NOT_MAP_FILE exactly as scanner.c:493-496 maps a
  * fault of the walk, instead of SIGBUS on a helper thread. */
+/* YR_TRYCATCH (exception.h:150-185) saves the SIGBUS/SIGSEGV actions it finds
+ * and restores them when it ends.  Several helpers copying at once would
+ * restore each other's handler in any order -- one helper's exit can uninstall
+ * the handler while another still copies.  So the copies share one counted
+ * installation of libyara's exception_handler: the first copy in installs it,
+ * the last one out restores what was there, and the handler is installed only
+ * while some copy runs (not across the GPU work that follows the copies). */
+static pthread_mutex_t _sig_mu = PTHREAD_MUTEX_INITIALIZER;
+static int _sig_users = 0;
+static struct sigaction _sig_old_bus, _sig_old_segv;
+
+static void _sig_enter(void)
+{
+  pthread_mutex_lock(&_sig_mu);
+  if (_sig_users++ == 0)
+  {
+    struct sigaction act;
+    memset(&act, 0, sizeof(act));
+    act.sa_handler = exception_handler;
+    act.sa_flags = 0;
+    sigfillset(&act.sa_mask);
+    sigaction(SIGBUS, &act, &_sig_old_bus);
+    sigaction(SIGSEGV, &act, &_sig_old_segv);
+  }
+  pthread_mutex_unlock(&_sig_mu);
+}
+
+static void _sig_leave(void)
+{
+  pthread_mutex_lock(&_sig_mu);
+  if (--_sig_users == 0)
+  {
+    sigaction(SIGBUS, &_sig_old_bus, NULL);
+    sigaction(SIGSEGV, &_sig_old_segv, NULL);
+  }
+  pthread_mutex_unlock(&_sig_mu);
+}
+
 static int _guarded_copy(void* user, void* dst, const void* src, size_t n)
 {
   YR_GPU_SCANNER* gs = (YR_GPU_SCANNER*) user;
-  int result = 0;
-  YR_TRYCATCH(gs->trycatch, { memcpy(dst, src, n); }, { result = 1; });
+  if (!gs->trycatch)
+  {
+    memcpy(dst, src, n);
+    return 0;
+  }
+  volatile int result = 0;
+  sigjmp_buf jb;
+  _sig_enter();
+  /* exception_handler jumps to the buffer this thread stored (TLS) */
+  yr_thread_storage_set_value(&yr_trycatch_trampoline_tls, &jb);
+  if (sigsetjmp(jb, 1) == 0)
+    memcpy(dst, src, n);
+  else
+    result = 1;
+  yr_thread_storage_set_value(&yr_trycatch_trampoline_tls, NULL);
+  _sig_leave();
   return result;
 }
 
@@ -574,15 +629,10 @@ static int _pipeline_block(
   /* The block is copied into the pipeline's pinned buffer by several threads
    * at once (yr_amd_pipeline_submit_dma), each chunk through _guarded_copy:
    * a fault on any of them (a truncated mapping) fails the submission with
-   * ERROR_COULD_NOT_MAP_FILE as scanner.c:493-496 does.  The outer trycatch
-   * only keeps libyara's signal handler installed while the helpers copy (a
-   * helper's own trycatch restores the handler it found when it ends). */
+   * ERROR_COULD_NOT_MAP_FILE as scanner.c:493-496 does. */
   gs->trycatch = !(scanner->flags & SCAN_FLAGS_NO_TRYCATCH);
   double t0 = _now();
-  YR_TRYCATCH(
-      gs->trycatch,
-      { result = yr_amd_pipeline_submit_dma(gs->pipe, data, block->size, block->base); },
-      { result = ERROR_COULD_NOT_MAP_FILE; });
+  result = yr_amd_pipeline_submit_dma(gs->pipe, data, block->size, block->base);
   gs->t_copy += _now() - t0;
   if (result != ERROR_SUCCESS) return result;
   gs->inflight++;
@@ -611,15 +661,9 @@ static int _direct_block(
   if (use_multi)
   {
     /* staged through pinned memory by _guarded_copy (helper threads
-     * included): a fault fails the call with ERROR_COULD_NOT_MAP_FILE; the
-     * outer trycatch keeps libyara's handler installed meanwhile */
-    YR_TRYCATCH(
-        gs->trycatch,
-        {
-          result = yr_amd_multi_scan_block_verified(
-              gs->multi, data, block->size, block->base, &recs, &n);
-        },
-        { result = ERROR_COULD_NOT_MAP_FILE; });
+     * included): a fault fails the call with ERROR_COULD_NOT_MAP_FILE */
+    result = yr_amd_multi_scan_block_verified(
+        gs->multi, data, block->size, block->base, &recs, &n);
     if (result != ERROR_SUCCESS) return result;
   }
   else

@@ -185,7 +185,13 @@ void lane_worker(yr_amd_multi* m, uint32_t k) {
     seen = m->gen;
     const uint64_t size = m->size, base = m->base;
     lk.unlock();
-    if (L.status == YR_AMD_SUCCESS) L.status = yamd::lane_scan(L, size, base);
+    if (L.status == YR_AMD_SUCCESS) {
+      L.status = yamd::lane_scan(L, size, base);
+      // a failed scan may leave this block's DMA queued on the lane's stream:
+      // stage_block refills the pinned buffers on the next call without
+      // waiting for it (the invariant stage_block's comment states)
+      if (L.status != YR_AMD_SUCCESS) (void)hipStreamSynchronize(L.stream);
+    }
     lk.lock();
     if (--m->left == 0) m->cv.notify_all();
   }

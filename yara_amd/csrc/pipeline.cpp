@@ -62,11 +62,16 @@ struct Slot {
   SlotState state = kIdle;
   bool dma = false;
   uint64_t gen = 0;                   // submissions of this slot (wakes its lanes)
+  std::condition_variable cv;         // the slot's lanes wait here (under the pipeline's mutex)
   uint32_t left = 0;                  // lanes still working on the submission
   int rc = 0;
   const yr_amd_verify_rec* recs = nullptr;
   uint64_t count = 0;
   std::vector<yr_amd_verify_rec> out;  // concatenated lane records
+  // single device, pageable copy: the scanner's own records (valid until the
+  // slot's next submission), no copy
+  const yr_amd_verify_rec* direct = nullptr;
+  uint64_t direct_count = 0;
 };
 
 }  // namespace
@@ -83,7 +88,7 @@ struct yr_amd_pipeline {
   int held = -1;                 // slot returned by the last pipeline_next
   bool stop = false;
   std::mutex mu;
-  std::condition_variable cv;
+  std::condition_variable cv;    // pipeline_next waits here for the oldest slot
   CopyFn copy;
   CopyPool* copier = nullptr;    // submit_dma's parallel host copy (created on first use)
 };
@@ -115,7 +120,7 @@ void lane_main(yr_amd_pipeline* p, uint32_t idx, uint32_t k) {
   uint64_t seen = 0;
   std::unique_lock<std::mutex> lk(p->mu);
   for (;;) {
-    p->cv.wait(lk, [&] { return p->stop || (s.state == kSubmitted && s.gen != seen); });
+    s.cv.wait(lk, [&] { return p->stop || (s.state == kSubmitted && s.gen != seen); });
     if (p->stop) return;
     seen = s.gen;
     lk.unlock();
@@ -127,7 +132,8 @@ void lane_main(yr_amd_pipeline* p, uint32_t idx, uint32_t k) {
       const yr_amd_verify_rec* recs = nullptr;
       uint64_t n = 0;
       rc = yr_amd_scan_block_verified(L.scanner, s.buf, s.size, s.base, &recs, &n);
-      L.recs.assign(recs, recs + (rc == YR_AMD_SUCCESS ? n : 0));
+      s.direct = rc == YR_AMD_SUCCESS ? recs : nullptr;
+      s.direct_count = rc == YR_AMD_SUCCESS ? n : 0;
       L.candidates = 0;
     }
     lk.lock();
@@ -192,7 +198,7 @@ void start_slot(yr_amd_pipeline* p, Slot& s, size_t size, uint64_t base, bool dm
     s.state = kSubmitted;
     ++p->in_flight;
   }
-  p->cv.notify_all();
+  s.cv.notify_all();
 }
 
 int create(yr_amd_tables* const* tables, uint32_t n, uint32_t depth, yr_amd_pipeline** out) {
@@ -248,6 +254,7 @@ int yr_amd_pipeline_destroy(yr_amd_pipeline* p) {
     p->stop = true;
   }
   p->cv.notify_all();
+  for (Slot& s : p->slots) s.cv.notify_all();
   for (Slot& s : p->slots) {
     for (std::thread& t : s.workers) t.join();
     for (Lane& L : s.lanes) yamd::lane_close(L);
@@ -361,7 +368,10 @@ int yr_amd_pipeline_next(yr_amd_pipeline* p, const yr_amd_verify_rec** records, 
   s.count = 0;
   s.recs = nullptr;
   if (s.rc == YR_AMD_SUCCESS) {
-    if (s.lanes.size() == 1) {
+    if (!s.dma) {   // (single device)
+      s.recs = s.direct;
+      s.count = s.direct_count;
+    } else if (s.lanes.size() == 1) {
       s.recs = s.lanes[0].recs.data();
       s.count = s.lanes[0].recs.size();
     } else {
