@@ -906,6 +906,17 @@ __device__ __forceinline__ uint32_t wave_in_block() {
   return __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
 }
 
+// One of four wave-uniform values (kernel arguments, in SGPRs) by a per-lane
+// index: two selects.  Indexing the argument arrays by a lane's key instead
+// made the compiler copy them to scratch or re-load them from the kernel
+// argument segment -- a dependent memory round trip per record.
+__device__ __forceinline__ uint32_t pick4(uint32_t k, uint32_t a0, uint32_t a1, uint32_t a2, uint32_t a3) {
+  const uint32_t lo = (k & 1u) ? a1 : a0, hi = (k & 1u) ? a3 : a2;
+  return (k & 2u) ? hi : lo;
+}
+#define YAMD_PICK4(k, A) pick4((k), A[0], A[1], A[2], A[3])
+#define YAMD_PICK4T(k, A, t) pick4((k), A[0][t], A[1][t], A[2][t], A[3][t])
+
 // Pass 1 of one group with records (o = its first record's index).
 __device__ __forceinline__ void verify_group(const VerifyParams& p, uint64_t g, uint64_t o,
                                              uint32_t lds, uint32_t codebuf) {
@@ -915,9 +926,9 @@ __device__ __forceinline__ void verify_group(const VerifyParams& p, uint64_t g, 
   const uint32_t cls = c < p.count && p.dead != nullptr ? p.dead[c] : 0u;
   uint32_t keep = 0, n = 0, head = 0;
   if (cls & kClassKept) {
-    n = p.kd_n[(cls >> 2) & 3u];
+    n = YAMD_PICK4((cls >> 2) & 3u, p.kd_n);
     keep = (1u << n) - 1u;
-    head = p.kd_head[(cls >> 2) & 3u];
+    head = YAMD_PICK4((cls >> 2) & 3u, p.kd_head);
   } else if (c < p.count && !(cls & kClassDead)) {
     keep = p.keep[c];
     if (keep != 0) {
@@ -931,13 +942,15 @@ __device__ __forceinline__ void verify_group(const VerifyParams& p, uint64_t g, 
     // records, no list walk (the dense "kept" keys' candidates)
     const uint32_t k = (cls >> 2) & 3u;
     const uint64_t i = p.positions[c];
-    uint64_t at = o + pre;
-    for (uint32_t t = 0; t < n; ++t, ++at) {
+    const uint64_t at = o + pre;
+#pragma unroll
+    for (uint32_t t = 0; t < kKeptDirect; ++t) {
+      if (t >= n) break;
       VerifyRec r;
-      r.offset = i - p.kd_bt[k][t];
-      r.pool_index = p.kd_idx[k][t];
+      r.offset = i - YAMD_PICK4T(k, p.kd_bt, t);
+      r.pool_index = YAMD_PICK4T(k, p.kd_idx, t);
       r.candidate = p.cand_index != nullptr ? p.cand_index[c] : (uint32_t)c;
-      if (at < p.out_cap) p.out[at] = r;
+      if (at + t < p.out_cap) p.out[at + t] = r;
     }
   } else if (keep != 0) {
     verify_one<1>(p, c, lds, codebuf, keep, head, o + pre, n);
@@ -982,9 +995,9 @@ __global__ __launch_bounds__(256) void verify_write_kernel(VerifyParams p) {
     uint32_t keep = 0, n = 0, head = 0;
     const uint32_t k = (cls[q] >> 2) & 3u;
     if (cls[q] & kClassKept) {
-      n = p.kd_n[k];
+      n = YAMD_PICK4(k, p.kd_n);
       keep = (1u << n) - 1u;
-      head = p.kd_head[k];
+      head = YAMD_PICK4(k, p.kd_head);
     } else if (c < p.count && !(cls[q] & kClassDead)) {
       keep = p.keep[c];   // (pass 0 wrote it for live candidates only)
       if (keep != 0) {
@@ -994,14 +1007,16 @@ __global__ __launch_bounds__(256) void verify_write_kernel(VerifyParams p) {
     }
     const uint32_t pre = wave_exclusive(n);
     if ((cls[q] & kClassKept) && n <= kKeptDirect) {
-      uint64_t at = o[q] + pre;
+      const uint64_t at = o[q] + pre;
       const uint32_t cand = p.cand_index != nullptr ? p.cand_index[c] : (uint32_t)c;
-      for (uint32_t t = 0; t < n; ++t, ++at) {
+#pragma unroll
+      for (uint32_t t = 0; t < kKeptDirect; ++t) {
+        if (t >= n) break;
         VerifyRec r;
-        r.offset = i[q] - p.kd_bt[k][t];
-        r.pool_index = p.kd_idx[k][t];
+        r.offset = i[q] - YAMD_PICK4T(k, p.kd_bt, t);
+        r.pool_index = YAMD_PICK4T(k, p.kd_idx, t);
         r.candidate = cand;
-        if (at < p.out_cap) p.out[at] = r;
+        if (at + t < p.out_cap) p.out[at + t] = r;
       }
     } else if (keep != 0) {
       verify_one<1, true>(p, c, 0u, 0u, keep, head, o[q] + pre, n);
@@ -1099,7 +1114,7 @@ __global__ __launch_bounds__(1024) void group_scan_kernel(uint64_t* block_off, u
 #pragma unroll
       for (int b = 0; b < 4; ++b) {
         const uint32_t x = (word >> (8 * b)) & 0xFFu;
-        v += (x & kClassKept) ? kept.n[(x >> 2) & 3u] : 0u;
+        v += (x & kClassKept) ? YAMD_PICK4((x >> 2) & 3u, kept.n) : 0u;
       }
     };
     if (c1 - c0 == kGroup) {   // a whole group: four 16-byte loads
