@@ -72,13 +72,6 @@ constexpr uint32_t kScanLdsBytes = kFilterBytes + kQueueBytes + kPendBytes;     
 // window there; one ending at an odd position k + 1 has its first 3 bytes as
 // the window ending at k.  Both are inserted in the left role, so a pass at
 // even k makes k and k + 1 filter hits; the exact stages are unchanged.
-// YAMD_PAIR1W=1 (A/B builds, DESIGN.md section 5 "Filter designs"): the pair
-// filter with ONE bit per window, the left role in the block's low word (bit
-// x[0..4]), the right role in its high word (bit d[0..4]): one shift per window
-// instead of three, ~5x the false passes.
-#ifndef YAMD_PAIR1W
-#define YAMD_PAIR1W 0
-#endif
 constexpr uint32_t kFilterPair = 0;
 constexpr uint32_t kFilterEven = 1;
 // kFilterEvenHash: the even-position filter with its block picked by a

@@ -1000,21 +1000,14 @@ __device__ __forceinline__ uint32_t stage1(const uint32_t (&S)[6], uint32_t lane
 #pragma unroll
     for (int j = 0; j < kPairs; ++j) {
       const uint32_t x = xs[j];
-      const uint32_t y = (j & 1) ? y2[j >> 1] >> 16 : y2[j >> 1];   // d | b << 8 (low 10 bits)
-      uint32_t& aq = a[j >> 2];
-#if YAMD_PAIR1W
-      // one bit per window: left in the low word, right in the high word
-      const uint32_t ul = ws[j].x >> (x & 31u), ur = ws[j].y >> (y & 31u);
-      if ((j & 3) == 0) aq = ul | ur;
-      else asm("v_or3_b32 %0, %1, %2, %0" : "+v"(aq) : "v"(ul), "v"(ur));
-#else
       const uint32_t ul = ws[j].x >> (x & 31u), vl = ws[j].y >> ((x >> 5) & 31u);
+      const uint32_t y = (j & 1) ? y2[j >> 1] >> 16 : y2[j >> 1];   // d | b << 8 (low 10 bits)
       const uint32_t ur = ws[j].x >> (y & 31u), vr = ws[j].y >> ((y >> 5) & 31u);
+      uint32_t& aq = a[j >> 2];
       if ((j & 3) == 0) aq = ul & vl;
       // acc |= u & v in one v_bitop3 (S0 = u, S1 = v, S2 = acc: 0xF0 & 0xCC | 0xAA)
       else asm("v_bitop3_b32 %0, %1, %2, %0 bitop3:0xea" : "+v"(aq) : "v"(ul), "v"(vl));
       asm("v_bitop3_b32 %0, %1, %2, %0 bitop3:0xea" : "+v"(aq) : "v"(ur), "v"(vr));
-#endif
     }
     if constexpr (MODE == 2 || MODE == 4 || MODE == 5) {   // ablations: no ring
       asm volatile("" ::"v"(a[0] | a[1]));
@@ -1053,18 +1046,11 @@ __device__ __forceinline__ uint32_t stage1(const uint32_t (&S)[6], uint32_t lane
       acc[k & 3] ^= ws[j].x ^ ws[j].y;
     } else {
       const uint32_t x = xs[j];
-      const uint32_t y = (j & 1) ? y2[j >> 1] >> 16 : y2[j >> 1];   // d | b << 8 (low 10 bits)
-#if YAMD_PAIR1W
-      const uint32_t ul = ws[j].x >> (x & 31u);
-      YAMD_SDWA_AND(k, ul, ul);
-      const uint32_t ur = ws[j].y >> (y & 31u);
-      YAMD_SDWA_AND(k + 1, ur, ur);
-#else
       const uint32_t ul = ws[j].x >> (x & 31u), vl = ws[j].y >> ((x >> 5) & 31u);
       YAMD_SDWA_AND(k, ul, vl);
+      const uint32_t y = (j & 1) ? y2[j >> 1] >> 16 : y2[j >> 1];   // d | b << 8 (low 10 bits)
       const uint32_t ur = ws[j].x >> (y & 31u), vr = ws[j].y >> ((y >> 5) & 31u);
       YAMD_SDWA_AND(k + 1, ur, vr);
-#endif
     }
   }
 #undef YAMD_SDWA_AND

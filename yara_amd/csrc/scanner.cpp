@@ -1301,7 +1301,9 @@ int yr_amd_verify_device(yr_amd_scanner* s, uint64_t data_base, const yr_amd_ver
     return YR_AMD_INVALID_ARGUMENT;
   if (v.count > 0) {
     if (v.data == nullptr) return YR_AMD_INVALID_ARGUMENT;
-    int r = grow(s->d_vcount, s->vcount_cap, 2 * v.count);
+    // (d_vcount: the live list's dense copy behind the counts, only when the
+    // scan made one -- a 2^32-candidate stream has none and needs 16 GiB less)
+    int r = grow(s->d_vcount, s->vcount_cap, (v.live != nullptr ? 2 : 1) * v.count);
     if (!r) r = grow(s->d_vkeep, s->vkeep_cap, 2 * v.count);
     if (!r) r = grow(s->d_vblock, s->vblock_cap, verify_groups(v.count) + 1);
     if (!r) r = grow(s->d_vchunk, s->vchunk_cap, verify_chunks(v.count) + 1);
@@ -1312,7 +1314,7 @@ int yr_amd_verify_device(yr_amd_scanner* s, uint64_t data_base, const yr_amd_ver
     if (!r) r = grow(s->d_vrec, s->vrec_cap, std::min<uint64_t>(v.count / 16 + 1, 1u << 20));
     if (r) return r;
     v.counts = s->d_vcount;
-    v.live_dense = s->d_vcount + v.count;   // (d_vcount: 2 x count, below)
+    v.live_dense = v.live != nullptr ? s->d_vcount + v.count : nullptr;
     v.keep = s->d_vkeep;
     v.heads = s->d_vkeep + v.count;
     v.block_off = s->d_vblock;

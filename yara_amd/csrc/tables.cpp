@@ -47,14 +47,8 @@ void filter_put(std::vector<uint32_t>& f, const FilterProbe& fp) {
   f[2 * fp.block + 1] |= 1u << fp.b_hi;
 }
 void filter_set(std::vector<uint32_t>& f, uint32_t w3) {
-#if YAMD_PAIR1W
-  const FilterProbe l = filter_probe_left(w3), r = filter_probe_right(w3);
-  f[2 * l.block] |= 1u << l.b_lo;
-  f[2 * r.block + 1] |= 1u << r.b_lo;
-#else
   filter_put(f, filter_probe_left(w3));
   filter_put(f, filter_probe_right(w3));
-#endif
 }
 
 // Two-choice, 4-way bucketed cuckoo table of non-zero keys.  Load <= 1/2 to
@@ -387,13 +381,7 @@ int flatten_tables(const uint32_t* T, const uint32_t* M, uint32_t n_slots,
       };
       // (+12 per 2-byte key tested as half-words: 3 per dword, like a 1-byte key)
       const double s_pair = pair_test ? 12.0 * out.keys_by_len[2] : 0.0;
-      #if YAMD_PAIR1W
-      uint64_t set1 = 0;
-      for (uint32_t w : out.filter) set1 += (uint64_t)__builtin_popcount(w);
-      const double c_pair = cost(55.0, 100.0, set1 * 16.0 / 16777216.0, kBytesPerLane);
-#else
       const double c_pair = cost(91.0, 100.0, pass_sum(out.filter) / 16777216.0, kBytesPerLane);
-#endif
       const double c_even[2] = {cost(55.0 + s_pair, 89.0, pass_plain_new / 16777216.0, kBytesPerLane / 2),
                                 cost(63.0 + s_pair, 89.0, pass[1] / 16777216.0, kBytesPerLane / 2)};
       const int h = c_even[1] < c_even[0] ? 1 : 0;

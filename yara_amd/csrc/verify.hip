@@ -902,6 +902,14 @@ __device__ __forceinline__ uint32_t wave_exclusive(uint32_t v) {
   }
   return inc - v;
 }
+// The exclusive prefix of the lanes' record counts; when every lane has the
+// same count (the dense "kept" keys' groups: one record per candidate) it is
+// lane * n, with no cross-lane scan (six dependent ds_bpermute round trips).
+__device__ __forceinline__ uint32_t records_before(uint32_t n) {
+  const uint32_t n0 = __builtin_amdgcn_readfirstlane(n);
+  if (__ballot(n != n0) == 0) return (threadIdx.x & 63u) * n0;
+  return wave_exclusive(n);
+}
 __device__ __forceinline__ uint32_t wave_in_block() {
   return __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
 }
@@ -936,7 +944,7 @@ __device__ __forceinline__ void verify_group(const VerifyParams& p, uint64_t g, 
       head = p.heads[c];
     }
   }
-  const uint32_t pre = wave_exclusive(n);
+  const uint32_t pre = records_before(n);
   if ((cls & kClassKept) && n <= kKeptDirect) {
     // every call of the key's list, from the key's own list copy: no pool
     // records, no list walk (the dense "kept" keys' candidates)
@@ -1005,7 +1013,7 @@ __global__ __launch_bounds__(256) void verify_write_kernel(VerifyParams p) {
         head = p.heads[c];
       }
     }
-    const uint32_t pre = wave_exclusive(n);
+    const uint32_t pre = records_before(n);
     if ((cls[q] & kClassKept) && n <= kKeptDirect) {
       const uint64_t at = o[q] + pre;
       const uint32_t cand = p.cand_index != nullptr ? p.cand_index[c] : (uint32_t)c;
