@@ -22,7 +22,7 @@ for rules, gib in (("rx", 1), ("fuzz0", 1)):
 g = L.yr_amd__diag_key_classes; g.argtypes = [ctypes.c_void_p, ctypes.POINTER(ctypes.c_uint32)]
 for name in sorted(os.listdir("tests/golden/tables")):
     t = yara_amd.Tables.from_npz(os.path.join("tests/golden/tables", name), device=0, strings=True)
-    o = (ctypes.c_uint32 * 32)()
+    o = (ctypes.c_uint32 * 40)()
     g(t._h, o)
     if o[2]:
         print(name[:-4], "kx_end", o[0], "keys", [hex(o[1] >> (8 * k) & 255) for k in range(o[2])],

@@ -13,7 +13,7 @@ from conftest import tables_npz, case_data, golden, ref_tables
 L=yara_amd._lib.lib()
 rules=sys.argv[1]; case=sys.argv[2]
 t=yara_amd.Tables.from_npz(tables_npz(rules), device=0, strings=True)
-o=(ctypes.c_uint32*32)()
+o=(ctypes.c_uint32*40)()
 L.yr_amd__diag_key_classes.argtypes=[ctypes.c_void_p, ctypes.POINTER(ctypes.c_uint32)]
 print(L.yr_amd__diag_key_classes(t._h, o))
 kx_end, byte_keys, nk = o[0], o[1], o[2]

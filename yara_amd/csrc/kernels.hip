@@ -293,7 +293,7 @@ static_assert(kQueueCap == kWave, "a drain takes the whole ring, one entry per l
 // the packed key bytes and reads its record (two ds_read_b128) instead of
 // selecting every field over the keys.
 struct KeyClassRec {
-  uint32_t info, m, v, x0, x1, min_pos, pad0, pad1;
+  uint32_t info, m, v, x0, x1, min_pos, bm, bv;
 };
 // last = the last valid byte of w (4: the five kept bytes; 7: eight bytes the
 // compaction read from the input, the key at byte 2).  *more (if given) is
@@ -329,22 +329,47 @@ __device__ __forceinline__ uint32_t key_class(const ScanParams& p, Rec rec, uint
     }
   }
   if (info & 4u) return pos >= min_pos ? (kClassKept | kidx << 2) : 0u;
-  // shift jj tests w bytes s0 + jj + t for the t <= tmax with mask byte t set
-  const int32_t g = (int32_t)(int8_t)(info >> 8), s0 = kp + g;
-  const uint32_t span = (info >> 16) & 15u, tmax = (info >> 20) & 3u;
-  // (the scan read nothing past byte_end: a range of a larger block has zeros there)
-  const int64_t end = (int64_t)pos + (int8_t)(info >> 24);
-  if (end > (int64_t)p.byte_end) return 0;
-  if (s0 < 0 || s0 + (int32_t)(span + tmax) > last) {
-    if (more && 2 + g >= 0 && 2 + g + (int32_t)(span + tmax) <= 7) *more = true;
-    return 0;
-  }
-  bool hit = false;
-  // (not vectorized: the vectorizer's masked form of this short loop cost the
-  // compaction ~30 spilled SGPRs)
+  // Each guard: shift jj tests w bytes s0 + jj + t for the t <= tmax with mask
+  // byte t set; a guard that fails proves the call dead, one whose bytes are
+  // not all in w (or in the scanned range) decides nothing.
+  // the forward guard
+  {
+    const int32_t g = (int32_t)(int8_t)(info >> 8), s0 = kp + g;
+    const uint32_t span = (info >> 16) & 15u, tmax = (info >> 20) & 3u;
+    // (the scan read nothing past byte_end: a range of a larger block has zeros there)
+    const int64_t end = (int64_t)pos + (int8_t)(info >> 24);
+    if (end > (int64_t)p.byte_end) {
+      // undecided
+    } else if (s0 < 0 || s0 + (int32_t)(span + tmax) > last) {
+      if (more && 2 + g >= 0 && 2 + g + (int32_t)(span + tmax) <= 7) *more = true;
+    } else {
+      bool hit = false;
+      // (not vectorized: the vectorizer's masked form of this short loop cost the
+      // compaction ~30 spilled SGPRs)
 #pragma clang loop vectorize(disable) interleave(disable)
-  for (uint32_t jj = 0; jj <= span; ++jj) hit |= ((uint32_t)(w >> (8 * ((uint32_t)s0 + jj))) & m) == v;
-  return hit ? 0u : kClassDead;
+      for (uint32_t jj = 0; jj <= span; ++jj) hit |= ((uint32_t)(w >> (8 * ((uint32_t)s0 + jj))) & m) == v;
+      if (!hit) return kClassDead;
+    }
+  }
+  // the backward guard (info bit 3; min_pos: its first tested byte relative to
+  // the key byte (int8), span << 8, last tested byte << 12): bytes before the
+  // key, all at or after byte_begin
+  if (info & 8u) {
+    const int32_t g = (int32_t)(int8_t)min_pos, s0 = kp + g;
+    const uint32_t span = (min_pos >> 8) & 15u, tmax = (min_pos >> 12) & 3u;
+    if ((int64_t)pos - 1 + g < (int64_t)p.byte_begin) {
+      // undecided
+    } else if (s0 < 0 || s0 + (int32_t)(span + tmax) > last) {
+      if (more && 2 + g >= 0 && 2 + g + (int32_t)(span + tmax) <= 7) *more = true;
+    } else {
+      bool hit = false;
+#pragma clang loop vectorize(disable) interleave(disable)
+      for (uint32_t jj = 0; jj <= span; ++jj)
+        hit |= ((uint32_t)(w >> (8 * ((uint32_t)s0 + jj))) & r.bm) == r.bv;
+      if (!hit) return kClassDead;
+    }
+  }
+  return 0u;   // (passing and undecided guards alike leave the call live)
 }
 
 // Key k's class record in the scan kernel (k lane-varying): lane 8k + f of
@@ -353,7 +378,7 @@ __device__ __forceinline__ uint32_t key_class(const ScanParams& p, Rec rec, uint
 __device__ __forceinline__ KeyClassRec scan_key_rec(uint32_t kcv, uint32_t k) {
   const int b = (int)(k * 32u);   // ds_bpermute byte address of lane 8k
   auto f = [&](int i) { return (uint32_t)__builtin_amdgcn_ds_bpermute(b + 4 * i, (int)kcv); };
-  return KeyClassRec{f(0), f(1), f(2), f(3), f(4), f(5), 0u, 0u};
+  return KeyClassRec{f(0), f(1), f(2), f(3), f(4), f(5), f(6), f(7)};
 }
 
 // Bucket-probe every pending hit (one lane each) and append the survivors,
@@ -1424,7 +1449,8 @@ __global__ __launch_bounds__(W * kWave) void seg_scatter_kernel(
   const bool classes = p.dead != nullptr;   // (uniform)
   if (threadIdx.x < kMaxByteKeys) {
     const uint32_t k = threadIdx.x;
-    kc[k] = KeyClassRec{p.kd_info[k], p.kd_m[k], p.kd_v[k], p.kd_x0[k], p.kd_x1[k], p.kd_min_pos[k], 0u, 0u};
+    kc[k] = KeyClassRec{p.kd_info[k], p.kd_m[k], p.kd_v[k], p.kd_x0[k], p.kd_x1[k], p.kd_min_pos[k],
+                        p.kd_bm[k], p.kd_bv[k]};
   }
   if (threadIdx.x == 0) lcount = 0;
   __syncthreads();

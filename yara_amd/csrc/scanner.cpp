@@ -97,6 +97,7 @@ struct yr_amd_tables {
   uint32_t kd_m[4] = {0, 0, 0, 0}, kd_v[4] = {0, 0, 0, 0}, kd_info[4] = {0, 0, 0, 0};
   uint32_t kd_x0[4] = {0, 0, 0, 0}, kd_x1[4] = {0, 0, 0, 0};
   uint32_t kd_n[4] = {0, 0, 0, 0}, kd_head[4] = {0, 0, 0, 0}, kd_min_pos[4] = {0, 0, 0, 0};
+  uint32_t kd_bm[4] = {0, 0, 0, 0}, kd_bv[4] = {0, 0, 0, 0};   // backward guards (ScanParams)
   uint32_t kd_idx[4][4] = {}, kd_bt[4][4] = {};   // a kept key's first list entries (VerifyParams)
   bool kd_any = false;
   bool kd_guard = false;              // some key's class is guard-decided (can be dead)
@@ -111,6 +112,9 @@ struct yr_amd_tables {
   uint8_t* d_re_code = nullptr;       // yr_amd_tables_set_re_code
   std::vector<DevPoolRec> h_pool;     // host copy of the records (set_re_code fills .re)
   std::vector<uint32_t> h_str_flags, h_pool_string;   // host copies (validation)
+  // per pool entry: its yr_re_exec forward program cannot fail with
+  // ERROR_TOO_MANY_RE_FIBERS (re_fiber_safe; set_re_code)
+  std::vector<uint8_t> h_fwd_fiber_safe;
   uint64_t max_str_bytes = 0;     // max over strings of the bytes a comparison reads
 };
 
@@ -505,7 +509,7 @@ int64_t yr_amd__diag_dead_count(yr_amd_scanner* s) {
   return n;
 }
 
-// The key classes of a table (key_classes): out[0] = kx_end, [1] = the
+// The key classes of a table (key_classes), out[40]: out[0] = kx_end, [1] = the
 // 1-byte keys, [2] = their count, [3..6] = kd_info, [7..10] = kd_m, [11..14] = kd_v.
 int yr_amd__diag_key_classes(const yr_amd_tables* t, uint32_t* out) {
   if (t == nullptr || out == nullptr) return YR_AMD_INVALID_ARGUMENT;
@@ -517,6 +521,8 @@ int yr_amd__diag_key_classes(const yr_amd_tables* t, uint32_t* out) {
   for (int k = 0; k < 4; ++k) out[15 + k] = t->kd_x0[k], out[19 + k] = t->kd_x1[k], out[23 + k] = t->kd_min_pos[k];
   out[27] = t->kx_deep;
   out[28] = t->kx_next;
+  // [32..35] kd_bm, [36..39] kd_bv
+  for (int k = 0; k < 4; ++k) out[32 + k] = t->kd_bm[k], out[36 + k] = t->kd_bv[k];
   return YR_AMD_SUCCESS;
 }
 
@@ -638,6 +644,8 @@ int yr_amd_scan_window(yr_amd_scanner* s, const uint8_t* d_window, uint64_t wind
     p.kd_n[k] = t->kd_n[k];
     p.kd_head[k] = t->kd_head[k];
     p.kd_min_pos[k] = t->kd_min_pos[k];
+    p.kd_bm[k] = t->kd_bm[k];
+    p.kd_bv[k] = t->kd_bv[k];
   }
   p.filter_mode = t->flat.filter_mode;
   // verified-only: the byte-key kernel decides the certain candidates' classes
@@ -967,6 +975,34 @@ bool general_guard(const uint8_t* c, uint32_t len, uint32_t skip, bool backwards
 }  // namespace
 
 namespace {
+// Whether yr_re_exec running `code` (re.c:1693-2072) provably stays below
+// RE_MAX_FIBERS (limits.h: 1024), so that it cannot fail with
+// ERROR_TOO_MANY_RE_FIBERS (re.c:1228-1229).  Without REPEAT_START/END the
+// fibers' stacks stay empty, and live fibers are distinct in (ip, rc) after
+// each step (_yr_re_fiber_exists, re.c:1278-1310; rc in -1..max of a
+// REPEAT_ANY, re.c:1586-1625): at most ops x (max + 2).  A step's syncs grow
+// each of them by at most one fiber per SPLIT / REPEAT_ANY before the next
+// dedup (_yr_re_fiber_sync, re.c:1441-1560).  Bound both, conservatively.
+bool re_fiber_safe(const uint8_t* c, uint32_t len) {
+  uint64_t ops = 0, forks = 0, mx = 0;
+  for (uint32_t n = 0; n < len;) {
+    const uint8_t op = c[n];
+    const uint32_t sz = re_op_size(op);
+    if (sz == 0 || n + sz > len) return false;
+    if (op == kOpRepeatStartGreedy || op == kOpRepeatEndGreedy || op == kOpRepeatStartUngreedy ||
+        op == kOpRepeatEndUngreedy)
+      return false;
+    if (op == kOpSplitA || op == kOpSplitB) ++forks;
+    if (op == kOpRepeatAnyGreedy || op == kOpRepeatAnyUngreedy) {
+      ++forks;
+      mx = std::max<uint64_t>(mx, re_u16(c + n + 3));
+    }
+    ++ops;
+    n += sz;
+  }
+  return ops * (mx + 2) * (forks + 2) < 1024;
+}
+
 // The 1-byte keys whose calls the scan kernel can classify (kernels.hip
 // key_class).  The key's state is its own node unless the byte before it is
 // one of at most 8 bytes x with a trie node of depth >= 2 ending in x, key (a
@@ -1016,7 +1052,7 @@ void key_classes(yr_amd_tables* t) {
     for (int e = 0; e < 4; ++e) t->kd_idx[k][e] = t->kd_bt[k][e] = 0;
   for (int k = 0; k < 4; ++k)
     t->kd_m[k] = t->kd_v[k] = t->kd_info[k] = t->kd_x0[k] = t->kd_x1[k] = t->kd_n[k] =
-        t->kd_head[k] = t->kd_min_pos[k] = 0;
+        t->kd_head[k] = t->kd_min_pos[k] = t->kd_bm[k] = t->kd_bv[k] = 0;
   if (f.root_accepting || t->h_pool.empty() || diag_env("YAMD_NO_KEY_CLASSES") != nullptr) return;
   // Per key the class it can have, then the five bytes the scan keeps beside
   // its certain candidates (kernels.hip key_class): lane bytes key - kp ..
@@ -1025,9 +1061,9 @@ void key_classes(yr_amd_tables* t) {
   // also test the byte before it against the key's exclusions (kx_deep), so
   // the five bytes may all lie after the key.
   struct Desc {
-    bool ok = false, kept = false;
-    uint32_t nx = 0, xs0 = 0, xs1 = 0, m = 0, v = 0, n = 0, head = 0, min_pos = 0;
-    int rs = 0, span = 0, tmax = 0, end = 0;
+    bool ok = false, kept = false, bok = false;
+    uint32_t nx = 0, xs0 = 0, xs1 = 0, m = 0, v = 0, n = 0, head = 0, min_pos = 0, bm = 0, bv = 0;
+    int rs = 0, span = 0, tmax = 0, end = 0, bs = 0, bspan = 0, btmax = 0;
   } d[4];
   const uint32_t nk = std::min<uint32_t>(f.n_byte_keys, 4);
   for (uint32_t k = 0; k < nk; ++k) {
@@ -1082,6 +1118,27 @@ void key_classes(yr_amd_tables* t) {
     o.m = e.fguard.m;
     o.v = e.fguard.v;
     o.ok = true;
+    // The backward guard as well: with a backward program, a call whose
+    // backward run fails never reaches _yr_scan_match_callback
+    // (_yr_scan_verify_re_match, scan.c:843-880; verify.hip re_call_matters),
+    // and the guard's bytes are that run's single-fiber prefix.  The backward
+    // run comes after the forward one, so a yr_re_exec program only when its
+    // forward run cannot end in ERROR_TOO_MANY_RE_FIBERS (a scan error the host
+    // must still see); yr_re_fast_exec has no such error.
+    const size_t q = (size_t)(head - 1);
+    if (e.re.bwd_len > 0 && e.bguard.m != 0 &&
+        ((fl & kStrFastRegexp) || (q < t->h_fwd_fiber_safe.size() && t->h_fwd_fiber_safe[q]))) {
+      // region [offset - L, offset), offset = key byte + 1 - backtrack; byte
+      // tmin of the guard's four is its lowest tested one
+      const int L = (e.bguard_bs & 15) + (e.bguard_bs >> 4) + 4;
+      const int tmin = __builtin_ctz(e.bguard.m) >> 3, tmx = (31 - __builtin_clz(e.bguard.m)) >> 3;
+      o.bs = 1 - (int)e.backtrack - L + tmin;
+      o.bspan = e.bguard_bs >> 4;
+      o.btmax = tmx - tmin;
+      o.bm = e.bguard.m >> (8 * tmin);
+      o.bv = e.bguard.v >> (8 * tmin);
+      o.bok = o.bs >= -128 && o.bs < 0;
+    }
   }
   // a key is decided at place kp if its identity, the byte before it (with
   // exclusions; or the scan's test of it) and every byte its guard tests lie
@@ -1117,6 +1174,12 @@ void key_classes(yr_amd_tables* t) {
     } else {
       t->kd_m[k] = o.m;
       t->kd_v[k] = o.v;
+      if (o.bok) {
+        info |= 8u;
+        t->kd_min_pos[k] = (uint32_t)(uint8_t)(int8_t)o.bs | (uint32_t)o.bspan << 8 | (uint32_t)o.btmax << 12;
+        t->kd_bm[k] = o.bm;
+        t->kd_bv[k] = o.bv;
+      }
       t->kd_guard = true;
       t->kx_next = 1;   // (a guard's bytes may run past the lane: keep the next lane's two)
       info |= ((uint32_t)(uint8_t)(int8_t)o.rs << 8) | ((uint32_t)o.span << 16) |
@@ -1131,8 +1194,9 @@ void key_classes(yr_amd_tables* t) {
   // classes at all (the scan then keeps every candidate: still exact)
   uint32_t kc[32] = {};
   for (int k = 0; k < 4; ++k) {
-    const uint32_t r[6] = {t->kd_info[k], t->kd_m[k], t->kd_v[k], t->kd_x0[k], t->kd_x1[k], t->kd_min_pos[k]};
-    for (int f = 0; f < 6; ++f) kc[8 * k + f] = r[f];
+    const uint32_t r[8] = {t->kd_info[k], t->kd_m[k], t->kd_v[k], t->kd_x0[k],
+                           t->kd_x1[k], t->kd_min_pos[k], t->kd_bm[k], t->kd_bv[k]};
+    for (int f = 0; f < 8; ++f) kc[8 * k + f] = r[f];
   }
   if ((t->d_kc == nullptr && hipMalloc((void**)&t->d_kc, sizeof(kc)) != hipSuccess) ||
       hipMemcpy(t->d_kc, kc, sizeof(kc), hipMemcpyHostToDevice) != hipSuccess) {
@@ -1207,6 +1271,7 @@ int yr_amd_tables_set_re_code(yr_amd_tables* t, uint32_t n_pool, const uint32_t*
   // (the forward program starts at the atom: its first `backtrack` bytes are
   // the atom's)
   const bool no_guards = diag_env("YAMD_NO_GUARDS") != nullptr;   // A/B measurements only
+  t->h_fwd_fiber_safe.assign(n_pool, 0);
   for (uint32_t k = 0; k < n_pool; ++k) {
     DevPoolRec& e = t->h_pool[k];
     e.re = re[k];
@@ -1224,6 +1289,7 @@ int yr_amd_tables_set_re_code(yr_amd_tables* t, uint32_t n_pool, const uint32_t*
     };
     guard(re[k].fwd_off, re[k].fwd_len, e.backtrack, false, e.fguard, e.fguard_bs);
     if (re[k].bwd_len > 0) guard(re[k].bwd_off, re[k].bwd_len, 0, true, e.bguard, e.bguard_bs);
+    if (!(sflags & kStrFastRegexp)) t->h_fwd_fiber_safe[k] = re_fiber_safe(code + re[k].fwd_off, re[k].fwd_len);
   }
   if (n_pool > 0 && hipMemcpy(t->d_pool, t->h_pool.data(), n_pool * sizeof(DevPoolRec),
                               hipMemcpyHostToDevice) != hipSuccess)
