@@ -228,8 +228,12 @@ int yr_amd_scan_device_result(
  * calls can have an effect out of the result: yr_amd_scan_device_result then
  * returns that reduced stream, while the records of yr_amd_verify_device are
  * unchanged -- the same calls, and the candidate field still indexes the FULL
- * stream (yr_amd_scan_device_stream_length).  No effect on other rule sets
- * or with yr_amd_tables_set_profiling.  Default 0.
+ * stream (yr_amd_scan_device_stream_length).  yr_amd_scan_device_result of
+ * a verified-only scan returns as soon as the counts are known, before the
+ * compaction has written the positions: they are complete in the scanner's
+ * stream order (yr_amd_verify_device queues behind them), and a reader on
+ * another stream or on the host must synchronise that stream first.  No
+ * effect on other rule sets or with yr_amd_tables_set_profiling.  Default 0.
  */
 int yr_amd_scanner_set_verified_only(yr_amd_scanner* scanner, int enable);
 

@@ -174,6 +174,11 @@ struct yr_amd_scanner {
   // this scan only, so scanners sharing a stream can have the next scan queued
   hipEvent_t ev_done = nullptr;
   hipEvent_t last_done = nullptr;   // ev_done, or ev_compact when the scan was timed
+  // verified-only scans: recorded behind the offsets kernels, so that
+  // yr_amd_scan_device_result has the counts (host-mapped summary) while the
+  // scatter still runs and pre-verification queues behind it with no gap
+  hipEvent_t ev_counted = nullptr;
+  hipEvent_t last_counted = nullptr;   // ev_counted for the pending scan, else null
   bool ev_valid = false;
 
   int diag_mode = 0;   // profiling ablation of the scan kernel (0 = product)
@@ -310,6 +315,11 @@ int run_scan(yr_amd_scanner* s) {
     HIP_TRY(launch_scan(p, s->last_grid, s->stream, s->diag_mode));
   }
   HIP_TRY(launch_compact(p, s->d_seg_offset, s->d_hsum, nullptr, false, s->stream));
+  s->last_counted = nullptr;
+  if (s->verified_only) {
+    HIP_TRY(hipEventRecord(s->ev_counted, s->stream));
+    s->last_counted = s->ev_counted;
+  }
   HIP_TRY(launch_compact(p, s->d_seg_offset, s->d_hsum, s->d_positions, true, s->stream));
   // one event marks the end of the scan's work: the timed one when timing (a
   // second event record at the same point would add a ~5 us gap per scan on
@@ -433,7 +443,8 @@ int yr_amd_scanner_create(yr_amd_tables* tables, void* stream, yr_amd_scanner** 
           hipSuccess ||
       hipHostGetDevicePointer((void**)&s->d_hsum, s->h_summary, 0) != hipSuccess ||
       hipMalloc((void**)&s->d_summary, 2 * sizeof(uint64_t)) != hipSuccess ||
-      hipEventCreateWithFlags(&s->ev_done, hipEventDisableTiming) != hipSuccess) {
+      hipEventCreateWithFlags(&s->ev_done, hipEventDisableTiming) != hipSuccess ||
+      hipEventCreateWithFlags(&s->ev_counted, hipEventDisableTiming) != hipSuccess) {
     yr_amd_scanner_destroy(s);
     return YR_AMD_INTERNAL_FATAL_ERROR;
   }
@@ -459,6 +470,7 @@ int yr_amd_scanner_destroy(yr_amd_scanner* s) {
   if (s->ev_end) (void)hipEventDestroy(s->ev_end);
   if (s->ev_compact) (void)hipEventDestroy(s->ev_compact);
   if (s->ev_done) (void)hipEventDestroy(s->ev_done);
+  if (s->ev_counted) (void)hipEventDestroy(s->ev_counted);
   if (s->own_stream && s->stream) (void)hipStreamDestroy(s->stream);
   delete s;
   return YR_AMD_SUCCESS;
@@ -681,7 +693,10 @@ int yr_amd_scan_device_result(yr_amd_scanner* s, const uint64_t** d_positions, u
     if (count) *count = 0;
     return YR_AMD_SUCCESS;
   }
-  HIP_TRY(hipEventSynchronize(s->last_done ? s->last_done : s->ev_done));
+  // (verified-only: the counts are final once the offsets kernels ran; the
+  // scatter's positions, classes and live lists follow in stream order)
+  HIP_TRY(hipEventSynchronize(s->last_counted ? s->last_counted
+                                              : (s->last_done ? s->last_done : s->ev_done)));
   uint64_t total = s->h_summary[0];
   const uint64_t maxc = s->h_summary[1];
   static const bool no_learn = diag_env("YAMD_NO_CAP_LEARN") != nullptr;   // A/B only
@@ -1449,8 +1464,8 @@ int yr_amd_scan_block_verified(yr_amd_scanner* s, const uint8_t* data, size_t si
   const bool was = s->verified_only;
   s->verified_only = true;
   int r = yr_amd_scan_device(s, s->d_block, size, 0, size);
-  s->verified_only = was;
   if (!r) r = yr_amd_scan_device_result(s, nullptr, nullptr, nullptr);
+  s->verified_only = was;
   const yr_amd_verify_rec* d_rec = nullptr;
   uint64_t n = 0;
   if (!r) r = yr_amd_verify_device(s, data_base, &d_rec, &n);

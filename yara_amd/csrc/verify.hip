@@ -23,6 +23,9 @@
 // walk the pool list, compare.  Candidates are ~0.015% of positions (config
 // C): this is latency-bound pointer chasing in L2, microseconds per block, so
 // the kernels are simple two-pass (count, exclusive scan, write).
+#include <mutex>
+#include <vector>
+
 #include "internal.h"
 #include "re_program.h"
 #include "verify.h"
@@ -1196,13 +1199,27 @@ __global__ __launch_bounds__(1024) void block_offsets_kernel(uint64_t* block_off
 
 // Grid of the persistent kernels: as many 256-thread blocks as the device
 // keeps resident (a second wave of blocks would finish late).
+// (Queried once per kernel and device: the occupancy query costs microseconds
+// of host time between launches that the GPU would spend idle.)
 static uint32_t resident_blocks(const void* kernel) {
-  int dev = 0, cus = 0, per = 0;
-  if (hipGetDevice(&dev) != hipSuccess ||
-      hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess ||
+  int dev = 0;
+  if (hipGetDevice(&dev) != hipSuccess) return 256;
+  struct Entry { const void* k; int dev; uint32_t n; };
+  static std::mutex mu;
+  static std::vector<Entry> cache;
+  {
+    std::lock_guard<std::mutex> lk(mu);
+    for (const Entry& e : cache)
+      if (e.k == kernel && e.dev == dev) return e.n;
+  }
+  int cus = 0, per = 0;
+  if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess ||
       hipOccupancyMaxActiveBlocksPerMultiprocessor(&per, kernel, 256, 0) != hipSuccess)
     return 256;
-  return (uint32_t)std::max(1, cus * std::max(1, per));
+  const uint32_t n = (uint32_t)std::max(1, cus * std::max(1, per));
+  std::lock_guard<std::mutex> lk(mu);
+  cache.push_back(Entry{kernel, dev, n});
+  return n;
 }
 
 hipError_t launch_verify(const VerifyParams& p, int pass, hipStream_t s) {
