@@ -15,7 +15,9 @@ the scan kernel) and the median per-round ratio to the first variant.
 --strings attaches the rule set's string records and regexp programs (as
 tools/ruleset_rates.py does), so the compaction also decides the 1-byte-key
 candidates' classes and builds the live list; --verify (implies --strings)
-also times the on-device pre-verification after each scan (wall clock).
+also times the on-device pre-verification after each scan (wall clock);
+--verified-only (implies --verify) runs the scanners in verified-only mode
+(yr_amd_scanner_set_verified_only) and reports the whole step's wall time.
 """
 import argparse
 import ctypes
@@ -64,7 +66,9 @@ def main():
     ap.add_argument("--warm-s", type=float, default=1.0)
     ap.add_argument("--strings", action="store_true")
     ap.add_argument("--verify", action="store_true")
+    ap.add_argument("--verified-only", action="store_true")
     a = ap.parse_args()
+    a.verify = a.verify or a.verified_only
     a.strings = a.strings or a.verify
     import torch
     names = a.variants.split(",")
@@ -121,13 +125,18 @@ def main():
                                                    code.ctypes.data, re_n) == 0
         assert L.yr_amd_scanner_create(t, None, ctypes.byref(s)) == 0
         L.yr_amd_scanner_set_timing(s, 1)
+        if a.verified_only:
+            L.yr_amd_scanner_set_verified_only.argtypes = [_vp, ctypes.c_int]
+            assert L.yr_amd_scanner_set_verified_only(s, 1) == 0
         scanners.append((L, t, s))
 
     import time
+    wall = {v: [] for v in names}
 
     def scan(i):
         L, _, s = scanners[i]
         cnt = ctypes.c_uint64()
+        w0 = time.perf_counter()
         assert L.yr_amd_scan_device(s, _vp(buf.data_ptr()), n, 0, n) == 0
         assert L.yr_amd_scan_device_result(s, None, ctypes.byref(cnt), None) == 0
         km, sm = ctypes.c_float(), ctypes.c_float()
@@ -139,6 +148,7 @@ def main():
             t0 = time.perf_counter()
             assert L.yr_amd_verify_device(s, 0, None, ctypes.byref(nrec)) == 0
             vms = (time.perf_counter() - t0) * 1e3
+        wall[names[i]].append((time.perf_counter() - w0) * 1e3)
         return km.value, sm.value, cnt.value, vms
 
     t0 = time.perf_counter()
@@ -147,6 +157,7 @@ def main():
         scan(k % len(names))
         k += 1
     kern = {v: [] for v in names}
+    wall.update({v: [] for v in names})
     scanms = {v: [] for v in names}
     verms = {v: [] for v in names}
     counts = {}
@@ -173,7 +184,8 @@ def main():
                               "kernel_min_ms": round(min(kern[v]), 4),
                               "scan_median_ms": round(statistics.median(scanms[v]), 4),
                               "ratio_to_first_median": round(statistics.median(ratios[v]), 4),
-                              **({"verify_median_ms": round(statistics.median(verms[v]), 4)} if a.verify else {}),
+                              **({"verify_median_ms": round(statistics.median(verms[v]), 4),
+                                  "step_wall_median_ms": round(statistics.median(wall[v]), 4)} if a.verify else {}),
                               "candidates": counts[v]}
     print(json.dumps(out, indent=1))
 

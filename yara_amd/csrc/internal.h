@@ -223,8 +223,9 @@ struct ScanParams {
   // before the key that the call's backward program tests first: mask / value
   // (shifted so that their lowest tested byte is byte 0), and in kd_min_pos
   // (unused by such keys) the first tested byte relative to the key byte
-  // (int8) | span << 8 | last tested byte << 12
+  // (int8) | last tested byte << 12 (guards at one position only)
   uint32_t kd_bm[4], kd_bv[4];
+  uint32_t kd_bguard;       // some key has a backward guard (info bit 3)
   uint32_t* seg_x;          // null, or beside seg_out: a certain candidate's first four
                             // bytes (lane bytes s .. s + 3, s = min(key + kx_end - 3, 11))
   uint32_t kx_end;          // 2..4 (scanner.cpp key_classes)

@@ -237,6 +237,12 @@ constexpr int kModeByteKeysNextEvenHash = 29;
 constexpr int kDropModes = 1000;
 template <int MODE>
 constexpr bool kDrop = MODE >= kDropModes;
+// MODE + kDropBgModes: the drop instance for tables whose key classes include
+// backward guards (ScanParams::kd_bguard) -- kept apart because the extra test,
+// inlined at every drain site, costs the other tables' drop kernels ~4 %
+constexpr int kDropBgModes = 2000;
+template <int MODE>
+constexpr bool kDropBg = MODE >= kDropBgModes;
 template <int MODE>
 constexpr int kBase = MODE % kDropModes >= 100 ? MODE % 100 : MODE % kDropModes;
 template <int MODE>
@@ -301,7 +307,7 @@ struct KeyClassRec {
 // w, and eight bytes with the key at byte 2 would hold them.
 // rec(k): key k's KeyClassRec (the compaction: an LDS table; the scan kernel:
 // selects over its arguments, scan_key_rec).
-template <typename Rec>
+template <bool kBg = true, typename Rec>
 __device__ __forceinline__ uint32_t key_class(const ScanParams& p, Rec rec, uint64_t w,
                                               int32_t kp, bool deep, uint64_t pos, int32_t last = 4,
                                               bool* more = nullptr) {
@@ -332,53 +338,59 @@ __device__ __forceinline__ uint32_t key_class(const ScanParams& p, Rec rec, uint
   // Each guard: shift jj tests w bytes s0 + jj + t for the t <= tmax with mask
   // byte t set; a guard that fails proves the call dead, one whose bytes are
   // not all in w (or in the scanned range) decides nothing.
-  // the forward guard
-  {
-    const int32_t g = (int32_t)(int8_t)(info >> 8), s0 = kp + g;
-    const uint32_t span = (info >> 16) & 15u, tmax = (info >> 20) & 3u;
-    // (the scan read nothing past byte_end: a range of a larger block has zeros there)
-    const int64_t end = (int64_t)pos + (int8_t)(info >> 24);
-    if (end > (int64_t)p.byte_end) {
-      // undecided
-    } else if (s0 < 0 || s0 + (int32_t)(span + tmax) > last) {
-      if (more && 2 + g >= 0 && 2 + g + (int32_t)(span + tmax) <= 7) *more = true;
-    } else {
-      bool hit = false;
-      // (not vectorized: the vectorizer's masked form of this short loop cost the
-      // compaction ~30 spilled SGPRs)
-#pragma clang loop vectorize(disable) interleave(disable)
-      for (uint32_t jj = 0; jj <= span; ++jj) hit |= ((uint32_t)(w >> (8 * ((uint32_t)s0 + jj))) & m) == v;
-      if (!hit) return kClassDead;
-    }
-  }
-  // the backward guard (info bit 3; min_pos: its first tested byte relative to
-  // the key byte (int8), span << 8, last tested byte << 12): bytes before the
-  // key, all at or after byte_begin
-  if (info & 8u) {
+  // The backward guard (info bit 3; min_pos: its first tested byte relative
+  // to the key byte (int8) | last tested byte << 12; one position,
+  // scanner.cpp key_classes): bytes before the key, all at or after
+  // byte_begin.  Computed without branches (the scan kernel inlines this at
+  // every drain site, where new exec masks spill its SGPRs) and folded into
+  // the forward guard's result at the end.
+  bool bdead = false, bmore = false;
+  if constexpr (kBg) {
+    const bool on = p.kd_bguard != 0u && (info & 8u) != 0u;
     const int32_t g = (int32_t)(int8_t)min_pos, s0 = kp + g;
-    const uint32_t span = (min_pos >> 8) & 15u, tmax = (min_pos >> 12) & 3u;
-    if ((int64_t)pos - 1 + g < (int64_t)p.byte_begin) {
-      // undecided
-    } else if (s0 < 0 || s0 + (int32_t)(span + tmax) > last) {
-      if (more && 2 + g >= 0 && 2 + g + (int32_t)(span + tmax) <= 7) *more = true;
-    } else {
-      bool hit = false;
-#pragma clang loop vectorize(disable) interleave(disable)
-      for (uint32_t jj = 0; jj <= span; ++jj)
-        hit |= ((uint32_t)(w >> (8 * ((uint32_t)s0 + jj))) & r.bm) == r.bv;
-      if (!hit) return kClassDead;
-    }
+    const int32_t tmax = (int32_t)((min_pos >> 12) & 3u);
+    const bool inrange = (int64_t)pos - 1 + g >= (int64_t)p.byte_begin;
+    const bool inw = s0 >= 0 && s0 + tmax <= last;
+    const uint32_t x = (uint32_t)(w >> (8 * (uint32_t)(inw ? s0 : 0)));
+    bdead = on && inrange && inw && (x & r.bm) != r.bv;
+    bmore = on && inrange && !inw && 2 + g >= 0 && 2 + g + tmax <= 7;
   }
-  return 0u;   // (passing and undecided guards alike leave the call live)
+  // the forward guard
+  const int32_t g = (int32_t)(int8_t)(info >> 8), s0 = kp + g;
+  const uint32_t span = (info >> 16) & 15u, tmax = (info >> 20) & 3u;
+  // (the scan read nothing past byte_end: a range of a larger block has zeros there)
+  const int64_t end = (int64_t)pos + (int8_t)(info >> 24);
+  uint32_t res = 0u;
+  if (end > (int64_t)p.byte_end) {
+    // undecided
+  } else if (s0 < 0 || s0 + (int32_t)(span + tmax) > last) {
+    if (more && 2 + g >= 0 && 2 + g + (int32_t)(span + tmax) <= 7) *more = true;
+  } else {
+    bool hit = false;
+    // (not vectorized: the vectorizer's masked form of this short loop cost the
+    // compaction ~30 spilled SGPRs)
+#pragma clang loop vectorize(disable) interleave(disable)
+    for (uint32_t jj = 0; jj <= span; ++jj) hit |= ((uint32_t)(w >> (8 * ((uint32_t)s0 + jj))) & m) == v;
+    res = hit ? 0u : kClassDead;
+  }
+  if (more && bmore) *more = true;
+  return bdead ? kClassDead : res;
 }
 
 // Key k's class record in the scan kernel (k lane-varying): lane 8k + f of
 // kcv holds field f of key k (ScanParams::kc, loaded once per kernel), fetched
 // by lane permutes -- no memory access, and no SGPRs held for 24 arguments.
-__device__ __forceinline__ KeyClassRec scan_key_rec(uint32_t kcv, uint32_t k) {
+// (bg: the table has backward guards -- wave-uniform, so the two permutes for
+// them run with every lane active or not at all)
+__device__ __forceinline__ KeyClassRec scan_key_rec(uint32_t kcv, uint32_t k, bool bg) {
   const int b = (int)(k * 32u);   // ds_bpermute byte address of lane 8k
   auto f = [&](int i) { return (uint32_t)__builtin_amdgcn_ds_bpermute(b + 4 * i, (int)kcv); };
-  return KeyClassRec{f(0), f(1), f(2), f(3), f(4), f(5), f(6), f(7)};
+  KeyClassRec r{f(0), f(1), f(2), f(3), f(4), f(5), 0u, 0u};
+  if (bg) {
+    r.bm = f(6);
+    r.bv = f(7);
+  }
+  return r;
 }
 
 // Bucket-probe every pending hit (one lane each) and append the survivors,
@@ -684,9 +696,9 @@ __device__ __forceinline__ uint32_t scan_class_entry(const ScanParams& p, uint32
   const uint32_t key = (uint32_t)(w >> 16) & 0xFFu;
   const uint32_t t = p.byte_keys ^ (key * 0x01010101u);
   const uint32_t z = (t - 0x01010101u) & ~t & 0x80808080u;
-  const KeyClassRec r = scan_key_rec(kcv_, (uint32_t)__builtin_ctz(z | 0x80000000u) >> 3);
+  const KeyClassRec r = scan_key_rec(kcv_, (uint32_t)__builtin_ctz(z | 0x80000000u) >> 3, kDropBg<MODE>);
   bool more = false;
-  const uint32_t cls = key_class(p, [r](uint32_t) { return r; }, w, 2, false, seg_start + off + 1,
+  const uint32_t cls = key_class<kDropBg<MODE>>(p, [r](uint32_t) { return r; }, w, 2, false, seg_start + off + 1,
                                  min(have, 8) - 1, &more);
   return off | (cls == 0u && more ? kClassFetch : cls) << kOutByteShift |
          kOutPlaceScanClass << kOutKeyShift;
@@ -1677,10 +1689,13 @@ hipError_t launch_scan(const ScanParams& p, int grid, hipStream_t s, int mode, h
     case 12: YAMD_LAUNCH_SCAN(scan_segments_kernel<D + kModeByteKeysEvenHash>); break;            \
     default: YAMD_LAUNCH_SCAN(scan_segments_kernel<D + kModeByteKeysNextEvenHash>); break;        \
   }
-        if (p.drop_dead != 0u)
+        if (p.drop_dead != 0u && p.kd_bguard != 0u) {
+          YAMD_BK_CASES(kDropBgModes)
+        } else if (p.drop_dead != 0u) {
           YAMD_BK_CASES(kDropModes)
-        else
+        } else {
           YAMD_BK_CASES(0)
+        }
 #undef YAMD_BK_CASES
       } else if (p.filter_mode == kFilterEven)
         YAMD_LAUNCH_SCAN(scan_segments_kernel<kModeEven>);
@@ -1750,6 +1765,12 @@ hipError_t configure_scan_kernel() {
                         (const void*)scan_segments_kernel<kDropModes + kModeByteKeysEvenHash>,
                         (const void*)scan_segments_kernel<kDropModes + kModeByteKeysNextEven>,
                         (const void*)scan_segments_kernel<kDropModes + kModeByteKeysNextEvenHash>,
+                        (const void*)scan_segments_kernel<kDropBgModes + kModeByteKeys>,
+                        (const void*)scan_segments_kernel<kDropBgModes + kModeByteKeysNext>,
+                        (const void*)scan_segments_kernel<kDropBgModes + kModeByteKeysEven>,
+                        (const void*)scan_segments_kernel<kDropBgModes + kModeByteKeysEvenHash>,
+                        (const void*)scan_segments_kernel<kDropBgModes + kModeByteKeysNextEven>,
+                        (const void*)scan_segments_kernel<kDropBgModes + kModeByteKeysNextEvenHash>,
 #if YAMD_DIAG
                         (const void*)scan_segments_kernel<1>,
                         (const void*)scan_segments_kernel<2>, (const void*)scan_segments_kernel<3>,

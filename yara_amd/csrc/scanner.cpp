@@ -659,6 +659,7 @@ int yr_amd_scan_window(yr_amd_scanner* s, const uint8_t* d_window, uint64_t wind
     p.kd_bm[k] = t->kd_bm[k];
     p.kd_bv[k] = t->kd_bv[k];
   }
+  p.kd_bguard = ((t->kd_info[0] | t->kd_info[1] | t->kd_info[2] | t->kd_info[3]) & 8u) ? 1u : 0u;
   p.filter_mode = t->flat.filter_mode;
   // verified-only: the byte-key kernel decides the certain candidates' classes
   // and leaves the dead ones out (kd_any: 1-byte keys with classes; never with
@@ -1152,7 +1153,8 @@ void key_classes(yr_amd_tables* t) {
       o.btmax = tmx - tmin;
       o.bm = e.bguard.m >> (8 * tmin);
       o.bv = e.bguard.v >> (8 * tmin);
-      o.bok = o.bs >= -128 && o.bs < 0;
+      // (one position only: the scan kernel tests it with one compare)
+      o.bok = o.bs >= -128 && o.bs < 0 && o.bspan == 0;
     }
   }
   // a key is decided at place kp if its identity, the byte before it (with
@@ -1191,7 +1193,7 @@ void key_classes(yr_amd_tables* t) {
       t->kd_v[k] = o.v;
       if (o.bok) {
         info |= 8u;
-        t->kd_min_pos[k] = (uint32_t)(uint8_t)(int8_t)o.bs | (uint32_t)o.bspan << 8 | (uint32_t)o.btmax << 12;
+        t->kd_min_pos[k] = (uint32_t)(uint8_t)(int8_t)o.bs | (uint32_t)o.btmax << 12;
         t->kd_bm[k] = o.bm;
         t->kd_bv[k] = o.bv;
       }
