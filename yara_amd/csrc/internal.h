@@ -221,11 +221,10 @@ struct ScanParams {
   uint32_t kd_n[4], kd_head[4], kd_min_pos[4];
   // with info bit 3 (guard-decided keys): a backward guard too -- the bytes
   // before the key that the call's backward program tests first: mask / value
-  // (shifted so that their lowest tested byte is byte 0), and in kd_min_pos
-  // (unused by such keys) the first tested byte relative to the key byte
-  // (int8) | last tested byte << 12 (guards at one position only)
-  uint32_t kd_bm[4], kd_bv[4];
-  uint32_t kd_bguard;       // some key has a backward guard (info bit 3)
+  // (shifted so that their lowest tested byte is byte 0) in fields 6 and 7 of
+  // the key's record in kc (below), and in kd_min_pos (unused by such keys)
+  // the first tested byte relative to the key byte (int8) | last tested byte
+  // << 12 (guards at one position only)
   uint32_t* seg_x;          // null, or beside seg_out: a certain candidate's first four
                             // bytes (lane bytes s .. s + 3, s = min(key + kx_end - 3, 11))
   uint32_t kx_end;          // 2..4 (scanner.cpp key_classes)
@@ -254,6 +253,7 @@ struct ScanParams {
   // every output candidate into cand_index (only if some candidate was left
   // out: seg_full_offset[n_segments] != the output total).
   uint32_t drop_dead;
+  uint32_t kd_bguard;       // some key has a backward guard (info bit 3)
   const uint32_t* kc;       // [32]: key k's class record (kd_info, kd_m, kd_v, kd_x0, kd_x1,
                             // kd_min_pos, kd_bm, kd_bv) at [8k, 8k + 8) -- the scan kernel reads it
                             // into one VGPR and fetches fields by lane permutes

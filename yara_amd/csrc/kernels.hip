@@ -1461,8 +1461,9 @@ __global__ __launch_bounds__(W * kWave) void seg_scatter_kernel(
   const bool classes = p.dead != nullptr;   // (uniform)
   if (threadIdx.x < kMaxByteKeys) {
     const uint32_t k = threadIdx.x;
+    // (the backward guards from the scan kernel's record table, kc fields 6, 7)
     kc[k] = KeyClassRec{p.kd_info[k], p.kd_m[k], p.kd_v[k], p.kd_x0[k], p.kd_x1[k], p.kd_min_pos[k],
-                        p.kd_bm[k], p.kd_bv[k]};
+                        p.kc != nullptr ? p.kc[8 * k + 6] : 0u, p.kc != nullptr ? p.kc[8 * k + 7] : 0u};
   }
   if (threadIdx.x == 0) lcount = 0;
   __syncthreads();

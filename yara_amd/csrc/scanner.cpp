@@ -656,8 +656,6 @@ int yr_amd_scan_window(yr_amd_scanner* s, const uint8_t* d_window, uint64_t wind
     p.kd_n[k] = t->kd_n[k];
     p.kd_head[k] = t->kd_head[k];
     p.kd_min_pos[k] = t->kd_min_pos[k];
-    p.kd_bm[k] = t->kd_bm[k];
-    p.kd_bv[k] = t->kd_bv[k];
   }
   p.kd_bguard = ((t->kd_info[0] | t->kd_info[1] | t->kd_info[2] | t->kd_info[3]) & 8u) ? 1u : 0u;
   p.filter_mode = t->flat.filter_mode;
