@@ -1151,8 +1151,10 @@ void key_classes(yr_amd_tables* t) {
       o.btmax = tmx - tmin;
       o.bm = e.bguard.m >> (8 * tmin);
       o.bv = e.bguard.v >> (8 * tmin);
-      // (one position only: the scan kernel tests it with one compare)
-      o.bok = o.bs >= -128 && o.bs < 0 && o.bspan == 0;
+      // (one position only: the scan kernel tests it with one compare; and
+      // within the two bytes before the key that its eight-byte windows hold
+      // -- a guard further back would only cost the drop kernel its test)
+      o.bok = o.bs >= -2 && o.bs < 0 && o.bspan == 0;
     }
   }
   // a key is decided at place kp if its identity, the byte before it (with
