@@ -118,10 +118,16 @@ def main():
                         ws.append((t2 - t0) * 1e3)
                     sc.set_timing(False)
                     km, sm, vm = statistics.median(ks), statistics.median(ss), statistics.median(vv)
+                    # (a verified-only scan's pre-verification is queued while its
+                    # compaction still runs, so scan_ms + verify_ms counts that
+                    # overlap twice: step_wall_ms, the whole step on the host's
+                    # clock, is the measure of the verified path)
+                    wm = statistics.median(ws)
                     rec[mode] = {"kernel_ms": round(km, 4), "scan_ms": round(sm, 4),
                                  "verify_ms": round(vm, 4), "scan_plus_verify_ms": round(sm + vm, 4),
                                  "frac_scan_plus_verify": round(n / ((sm + vm) * 1e-3) / 1e9 / HBM_PEAK_GBS, 4),
-                                 "step_wall_ms": round(statistics.median(ws), 4),
+                                 "step_wall_ms": round(wm, 4),
+                                 "frac_step_wall": round(n / (wm * 1e-3) / 1e9 / HBM_PEAK_GBS, 4),
                                  "candidates": int(cnt), "stream_length": int(sc.stream_length()),
                                  "records": int(nrec)}
                 sc.set_verified_only(False)
