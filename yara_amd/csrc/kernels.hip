@@ -435,6 +435,7 @@ __device__ __forceinline__ void flush_pending(const ScanParams& p, WaveQueue& q,
     const uint32_t idx = found + __builtin_amdgcn_mbcnt_hi((uint32_t)(b >> 32),
                                                            __builtin_amdgcn_mbcnt_lo((uint32_t)b, 0u));
     if (idx < p.seg_cap) {
+      // (plain stores: non-temporal ones cost the dense sets' kernels 2-4 %, r5h25)
       out[idx] = off;
       if (kByteKeys<MODE> && p.seg_x != nullptr) p.seg_x[(out - p.seg_out) + idx] = xv;
     }
@@ -1438,7 +1439,7 @@ __global__ __launch_bounds__(1024) void seg_offsets_kernel(const uint32_t* seg_c
   }
 }
 
-constexpr uint32_t kScatterWaves = 8;   // waves per segment in the scatter (dense segments)
+constexpr uint32_t kScatterWaves = 8;   // waves per segment in the scatter (dense segments; 4, 16: no better, r5h24)
 
 // The compaction reads the input bytes a certain candidate's class needs when
 // the scan's five kept bytes do not hold them (key_class's `more`):
@@ -1511,7 +1512,9 @@ __global__ __launch_bounds__(W * kWave) void seg_scatter_kernel(
         if (classes) x = sx[i + kStride];
       }
       const uint64_t pos = base + (ec & kOutOffsetMask);
-      if (valid) dst[i] = pos;
+      // (non-temporal: short's verified step -2 %, fuzz3's -1 %, the
+      // pre-verification that reads them back included, gpurun r5h24)
+      if (valid) __builtin_nontemporal_store(pos, dst + i);
       if (valid && cidx != nullptr) cidx[i] = full0 + xc;   // (mod 2^32, as the records')
       if (!classes) continue;
       // the certain candidates' classes from the bytes the scan kept beside them
