@@ -219,6 +219,10 @@ int flatten_tables(const uint32_t* T, const uint32_t* M, uint32_t n_slots,
     if (n.depth < 2) continue;
     const uint32_t last = (n.bytes >> (8 * (n.depth - 1))) & 0xFFu;
     const uint32_t prev = (n.bytes >> (8 * (n.depth - 2))) & 0xFFu;
+    // the depth-1 node of `last`, if any (its slot from the root's row)
+    const uint32_t t1 = T[last + 1];
+    const bool has1 = (t1 & 0x1FFu) == last + 1;
+    if (has1 && M[n.slot] == M[t1 >> 9]) continue;   // the same calls as `last` alone
     out.deep_last[last >> 5] |= 1u << (last & 31);
     out.deep_pair[last * 8 + (prev >> 5)] |= 1u << (prev & 31);
   }

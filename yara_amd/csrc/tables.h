@@ -46,11 +46,15 @@ struct FlatTables {
   // they end at an odd position, instead of as the filter's (*, *, p) windows
   // (which would pass every byte p)
   uint32_t pair_keys[2] = {0, 0}, n_pair_keys = 0;
-  // bit b set: some trie node of depth >= 2 ends with byte b (so a position
-  // whose last byte is the 1-byte key b may have a deeper state than b's node)
+  // bit b set: some trie node of depth >= 2 ends with byte b and has another
+  // match list than b's own node (so at a position whose last byte is the
+  // 1-byte key b the calls may differ from b's list)
   uint32_t deep_last[8] = {0, 0, 0, 0, 0, 0, 0, 0};
   // bit x of row b (8 words a row): some trie node of depth >= 2 ends with the
-  // bytes x, b -- such a position's state may be that node instead of b's
+  // bytes x, b and its match list (M, ahocorasick.c: its own matches, then its
+  // failure state's) is not b's -- such a position's calls may differ from
+  // b's.  Deeper nodes whose lists ARE b's (no matches of their own along the
+  // failure chain down to b) make the same calls, so they do not count.
   std::vector<uint32_t> deep_pair;   // 256 x 8
 
   // accepting trie nodes -> match-list head M[slot], by the node's string
