@@ -1408,9 +1408,7 @@ int yr_amd_verify_device(yr_amd_scanner* s, uint64_t data_base, const yr_amd_ver
     // summary) -> write pass, then one wait
     if (v.live != nullptr) {
       // the scan's live list: only its candidates are decided, their record
-      // counts added to the groups' (zeroed here)
-      HIP_TRY(hipMemsetAsync(v.block_off, 0, (verify_groups(v.count) + 1) * sizeof(uint64_t),
-                             s->stream));
+      // counts added to the groups' (zeroed by the live list's gather)
       HIP_TRY(launch_verify_live(v, s->d_summary, s->stream));
     } else {
       HIP_TRY(launch_verify(v, 0, s->stream));

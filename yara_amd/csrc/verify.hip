@@ -1086,13 +1086,21 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(5))) void v
 
 // The scan segments' live lists concatenated (live_off: their offsets, from
 // launch_counts_offsets): one wave per segment, persistent over the segments.
+// Each wave also zeroes the record counts of the groups its segment's
+// candidates fall in (verify_live_kernel adds to them; a group shared by two
+// segments is zeroed by both, before either adds) -- no separate memset.
 __global__ __launch_bounds__(256) void live_gather_kernel(VerifyParams p) {
   const uint32_t waves = gridDim.x * (blockDim.x / 64), lane = threadIdx.x & 63u;
+  const uint64_t groups = (p.count + kGroup - 1) / kGroup;
   for (uint32_t seg = blockIdx.x * (blockDim.x / 64) + wave_in_block(); seg < p.live_segs; seg += waves) {
     const uint32_t n = p.live_count[seg];
     const uint32_t* src = p.live + p.live_first[seg];
     uint32_t* dst = p.live_dense + p.live_off[seg];
     for (uint32_t h = lane; h < n; h += 64) dst[h] = src[h];
+    const uint64_t c0 = p.live_first[seg], c1 = min(p.live_first[seg + 1], p.count);
+    if (c1 > c0)
+      for (uint64_t g = c0 / kGroup + lane; g <= (c1 - 1) / kGroup; g += 64) p.block_off[g] = 0;
+    if (seg == p.live_segs - 1 && lane == 0) p.block_off[groups] = 0;   // (past the last group)
   }
 }
 
@@ -1270,7 +1278,9 @@ hipError_t launch_verify(const VerifyParams& p, int pass, hipStream_t s) {
 hipError_t launch_counts_offsets(const uint32_t* counts, uint32_t n, uint64_t* offsets, uint64_t* summary,
                                  hipStream_t s);   // (kernels.hip)
 hipError_t launch_verify_live(const VerifyParams& p, uint64_t* summary, hipStream_t s) {
-  if (p.count == 0 || p.live_segs == 0) return hipSuccess;
+  if (p.count == 0) return hipSuccess;
+  if (p.live_segs == 0)   // (no segments: nothing to gather, the counts zeroed here)
+    return hipMemsetAsync(p.block_off, 0, (verify_groups(p.count) + 1) * sizeof(uint64_t), s);
   hipError_t e = launch_counts_offsets(p.live_count, p.live_segs, p.live_off, summary, s);
   if (e != hipSuccess) return e;
   hipLaunchKernelGGL(live_gather_kernel, dim3((p.live_segs + 3) / 4), dim3(256), 0, s, p);
