@@ -112,9 +112,6 @@ struct yr_amd_tables {
   uint8_t* d_re_code = nullptr;       // yr_amd_tables_set_re_code
   std::vector<DevPoolRec> h_pool;     // host copy of the records (set_re_code fills .re)
   std::vector<uint32_t> h_str_flags, h_pool_string;   // host copies (validation)
-  // per pool entry: its yr_re_exec forward program cannot fail with
-  // ERROR_TOO_MANY_RE_FIBERS (re_fiber_safe; set_re_code)
-  std::vector<uint8_t> h_fwd_fiber_safe;
   uint64_t max_str_bytes = 0;     // max over strings of the bytes a comparison reads
 };
 
@@ -807,7 +804,7 @@ int yr_amd_tables_set_strings(yr_amd_tables* t, const uint32_t* pool_string, uin
     DevPoolRec& e = t->h_pool[k];
     e.next = f.pool_next[k];
     e.backtrack = f.pool_backtrack[k];
-    e.flags = x.flags;
+    e.flags = x.flags & ~kPoolFwdFiberSafe;   // (that bit is the device's own)
     e.length = x.length;
     e.fixed_offset = x.fixed_offset;
     e.bytes_off = x.bytes_offset;
@@ -1139,9 +1136,7 @@ void key_classes(yr_amd_tables* t) {
     // run comes after the forward one, so a yr_re_exec program only when its
     // forward run cannot end in ERROR_TOO_MANY_RE_FIBERS (a scan error the host
     // must still see); yr_re_fast_exec has no such error.
-    const size_t q = (size_t)(head - 1);
-    if (e.re.bwd_len > 0 && e.bguard.m != 0 &&
-        ((fl & kStrFastRegexp) || (q < t->h_fwd_fiber_safe.size() && t->h_fwd_fiber_safe[q]))) {
+    if (e.re.bwd_len > 0 && e.bguard.m != 0 && ((fl & kStrFastRegexp) || (fl & kPoolFwdFiberSafe))) {
       // region [offset - L, offset), offset = key byte + 1 - backtrack; byte
       // tmin of the guard's four is its lowest tested one
       const int L = (e.bguard_bs & 15) + (e.bguard_bs >> 4) + 4;
@@ -1288,7 +1283,6 @@ int yr_amd_tables_set_re_code(yr_amd_tables* t, uint32_t n_pool, const uint32_t*
   // (the forward program starts at the atom: its first `backtrack` bytes are
   // the atom's)
   const bool no_guards = diag_env("YAMD_NO_GUARDS") != nullptr;   // A/B measurements only
-  t->h_fwd_fiber_safe.assign(n_pool, 0);
   for (uint32_t k = 0; k < n_pool; ++k) {
     DevPoolRec& e = t->h_pool[k];
     e.re = re[k];
@@ -1306,7 +1300,9 @@ int yr_amd_tables_set_re_code(yr_amd_tables* t, uint32_t n_pool, const uint32_t*
     };
     guard(re[k].fwd_off, re[k].fwd_len, e.backtrack, false, e.fguard, e.fguard_bs);
     if (re[k].bwd_len > 0) guard(re[k].bwd_off, re[k].bwd_len, 0, true, e.bguard, e.bguard_bs);
-    if (!(sflags & kStrFastRegexp)) t->h_fwd_fiber_safe[k] = re_fiber_safe(code + re[k].fwd_off, re[k].fwd_len);
+    e.flags &= ~kPoolFwdFiberSafe;
+    if (!(sflags & kStrFastRegexp) && re_fiber_safe(code + re[k].fwd_off, re[k].fwd_len))
+      e.flags |= kPoolFwdFiberSafe;
   }
   if (n_pool > 0 && hipMemcpy(t->d_pool, t->h_pool.data(), n_pool * sizeof(DevPoolRec),
                               hipMemcpyHostToDevice) != hipSuccess)

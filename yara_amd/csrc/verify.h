@@ -21,6 +21,11 @@ constexpr uint32_t kStrUnmodelled = 0x200000 | 0x400000;
 
 constexpr uint32_t kStrFastRegexp = 0x40;
 constexpr uint32_t kStrDotAll = 0x20000;
+// DevPoolRec.flags only (above every STRING_FLAGS_* bit, types.h:66-88): the
+// entry's yr_re_exec forward program provably cannot fail with
+// ERROR_TOO_MANY_RE_FIBERS (scanner.cpp re_fiber_safe), so a failing backward
+// guard decides the call without running the forward search first
+constexpr uint32_t kPoolFwdFiberSafe = 0x80000000u;
 constexpr uint32_t kStrBase64Any = 0x200000 | 0x400000;
 
 // Fast-exec RE programs (hex strings) of one pool entry: forward code at

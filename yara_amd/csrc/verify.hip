@@ -721,6 +721,11 @@ __device__ bool re_call_matters(const VerifyParams& p, const DevPoolRec& e, uint
     if (w == 0 ? !try_ascii : !try_wide) continue;
     if (w == 0 && e.fguard.m != 0 && !guard_ok(p, d, offset, false, e.fguard_bs, e.fguard, lds, near))
       continue;
+    // a forward run that cannot fail (kPoolFwdFiberSafe) leaves the backward
+    // guard to decide first: no forward search for a call it rules out
+    if (w == 0 && (e.flags & kPoolFwdFiberSafe) && r.bwd_len > 0 && e.bguard.m != 0 &&
+        !guard_ok(p, d, offset, true, e.bguard_bs, e.bguard, lds, near))
+      continue;
     const int f = general_re_reachable(fwd, r.fwd_len, d, p.size - offset, offset, false, w == 1,
                                        nocase, dotall, p.lowercase);
     if (f == kPathUnknown) return true;
