@@ -13,6 +13,7 @@
 #include <string.h>
 
 #include <algorithm>
+#include <cmath>
 #include <new>
 #include <vector>
 
@@ -1150,6 +1151,21 @@ void key_classes(yr_amd_tables* t) {
       // within the two bytes before the key that its eight-byte windows hold
       // -- a guard further back would only cost the drop kernel its test)
       o.bok = o.bs >= -2 && o.bs < 0 && o.bspan == 0;
+      // ... and only where the forward guard alone leaves many candidates
+      // undecided: the backward-guard drop instance costs the scan kernel
+      // 4-7 % (profiles/r05_ab_inproc.json r5h30: rx, whose forward guard
+      // passes 1 in 256, lost more there than its live list gained when a
+      // wider window let its guard five bytes back in).  Undecided = passing
+      // the forward guard on random bytes (its tested bits, less the key's own
+      // byte) or lying past the eight bytes of the window.
+      if (o.bok) {
+        int bits = __builtin_popcount(o.m);
+        if (o.rs <= 0 && o.rs + 3 >= 0 && ((o.m >> (8 * -o.rs)) & 0xFFu) != 0u) bits -= 8;
+        const double pass = std::min(1.0, (o.span + 1) * std::ldexp(1.0, -std::max(bits, 0)));
+        const int hi = o.rs + o.span + o.tmax;   // last tested byte after the key
+        const double outside = o.rs < -2 ? 1.0 : std::min(1.0, std::max(0, hi - 2) / 16.0);
+        o.bok = pass + outside >= 0.02;
+      }
     }
   }
   // a key is decided at place kp if its identity, the byte before it (with
