@@ -33,6 +33,7 @@ _vp = ctypes.c_void_p
 
 
 def load(name):
+    name = name.split(":")[0]   # (a ":vo" suffix: that variant's scanner in verified-only mode)
     path = (os.path.join(REPO, "yara_amd", "libyara_amd.so") if name == "base"
             else os.path.join(REPO, "yara_amd", "_variants", name + ".so"))
     L = ctypes.CDLL(path, mode=getattr(os, "RTLD_LOCAL", 0) | os.RTLD_NOW)
@@ -125,7 +126,7 @@ def main():
                                                    code.ctypes.data, re_n) == 0
         assert L.yr_amd_scanner_create(t, None, ctypes.byref(s)) == 0
         L.yr_amd_scanner_set_timing(s, 1)
-        if a.verified_only:
+        if a.verified_only or names[len(scanners)].endswith(":vo"):
             L.yr_amd_scanner_set_verified_only.argtypes = [_vp, ctypes.c_int]
             assert L.yr_amd_scanner_set_verified_only(s, 1) == 0
         scanners.append((L, t, s))
