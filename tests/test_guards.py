@@ -200,3 +200,39 @@ def test_general_guard_follows_jumps_and_stops_at_splits():
     assert guard(bytes([SPLITA, 0, 6, 0, LIT, 0x41, LIT, 0x42, MATCH]), general=True) is None
     # nocase literals compare through the host's case folding: untested
     assert guard(bytes([LIT, 0x41, LIT, 0x42, MATCH]), general=True, nocase=True) is None
+
+
+# --- fiber safety of yr_re_exec forward programs (scanner.cpp re_fiber_safe) --
+REPSTARTG, REPENDG = 0xC3, 0xC4
+
+
+def fiber_safe(code):
+    L = _lib.lib()
+    f = L.yr_amd__re_fiber_safe
+    f.restype = ctypes.c_int
+    f.argtypes = [ctypes.c_char_p, ctypes.c_uint32]
+    r = f(bytes(code), len(code))
+    assert r in (0, 1)
+    return bool(r)
+
+
+def test_fiber_safe_bound():
+    """A forward program may let a key class test the call's backward guard
+    first only if yr_re_exec cannot end in ERROR_TOO_MANY_RE_FIBERS
+    (re.c:1228-1229): no REPEAT_START / REPEAT_END (fiber stacks stay empty),
+    and ops x (largest REPEAT_ANY max + 2) x (SPLITs + REPEAT_ANYs + 2) below
+    RE_MAX_FIBERS = 1024 (limits.h:168)."""
+    # fuzz0's key `_` (golden tables): LIT 5F, JUMP +9, dead LITs, REPEAT_ANY {0, 4}, LIT 3E, MATCH
+    fuzz0 = [LIT, 0x5F, JUMP, 9, 0, LIT, 0x61, LIT, 0x62, LIT, 0x31, REPANY, 0, 0, 4, 0, LIT, 0x3E, MATCH]
+    assert fiber_safe(fuzz0)                      # 8 ops x 6 x 3 = 144
+    assert fiber_safe([LIT, 0x41, MATCH])
+    # a counted loop: its counter stacks make fibers distinct beyond (ip, rc)
+    assert not fiber_safe([REPSTARTG, 2, 0, 5, 0, 9, 0, 0, 0, LIT, 0x41,
+                           REPENDG, 2, 0, 5, 0, 0xF7, 0xFF, 0xFF, 0xFF, MATCH])
+    # a wide jump: 3 ops x (1000 + 2) x 3 > 1024
+    assert not fiber_safe([LIT, 0x41, REPANY, 0, 0, 0xE8, 0x03, LIT, 0x42, MATCH])
+    # many ops: 200 literals x (4 + 2) x 3
+    assert not fiber_safe([LIT, 0x41] * 199 + [REPANY, 0, 0, 4, 0, MATCH])
+    # unknown opcode or a truncated instruction: not provably safe
+    assert not fiber_safe([0x99, MATCH])
+    assert not fiber_safe([LIT])

@@ -777,9 +777,11 @@ int upload(T*& d, const T* h, size_t n) {
 }  // namespace
 }  // extern "C++"
 
+extern "C++" {   // (internal helpers: C++ linkage, not exported)
 namespace {
 void key_classes(yr_amd_tables* t);
-}
+}  // namespace
+}  // extern "C++"
 
 int yr_amd_tables_set_strings(yr_amd_tables* t, const uint32_t* pool_string, uint32_t n_pool,
                               const yr_amd_string* strings, uint32_t n_strings,
@@ -831,6 +833,7 @@ int yr_amd_tables_set_strings(yr_amd_tables* t, const uint32_t* pool_string, uin
   return YR_AMD_SUCCESS;
 }
 
+extern "C++" {   // (internal helpers: C++ linkage, not exported)
 namespace {
 // Length of a linear fast-exec program (opcodes of yr_re_fast_exec,
 // re.c:2150-2391) that ends with MATCH exactly at `len`, else 0.
@@ -985,7 +988,9 @@ bool general_guard(const uint8_t* c, uint32_t len, uint32_t skip, bool backwards
   return pick_guard(head, tail, repeat, mn, mx, skip, backwards, g, bs);
 }
 }  // namespace
+}  // extern "C++"
 
+extern "C++" {   // (internal helpers: C++ linkage, not exported)
 namespace {
 // Whether yr_re_exec running `code` (re.c:1693-2072) provably stays below
 // RE_MAX_FIBERS (limits.h: 1024), so that it cannot fail with
@@ -1236,6 +1241,15 @@ void key_classes(yr_amd_tables* t) {
   }
 }
 }  // namespace
+}  // extern "C++"
+
+// Not declared in include/yara_amd.h: re_fiber_safe on one yr_re_exec
+// program, for the CPU tests (tests/test_guards.py): 1 if its run provably
+// stays below RE_MAX_FIBERS, else 0.
+int yr_amd__re_fiber_safe(const uint8_t* code, uint32_t len) {
+  if (code == nullptr) return -1;
+  return re_fiber_safe(code, len) ? 1 : 0;
+}
 
 // Not declared in include/yara_amd.h: the guard compiler on one program, for
 // the CPU tests (tests/test_guards.py).  Returns 1 and the guard (verify.h
@@ -1603,6 +1617,7 @@ int yr_amd_replay(const yr_amd_tables* t, const uint8_t* data, size_t size,
 // xorshift64 jump-ahead: the generator is linear over GF(2)^64, so the state
 // after m steps is A^m x0; chunk start states are computed on the host.
 // ---------------------------------------------------------------------------
+extern "C++" {   // (internal helpers: C++ linkage, not exported)
 namespace {
 struct Mat64 {
   uint64_t col[64];
@@ -1638,6 +1653,7 @@ Mat64 power(uint64_t m) {
   return acc;
 }
 }  // namespace
+}  // extern "C++"
 
 int yr_amd_fill_xorshift64(void* d_buf, uint64_t n, uint64_t seed, uint64_t offset, void* stream) {
   if (n == 0) return YR_AMD_SUCCESS;
