@@ -146,7 +146,7 @@ hipError_t launch_block_offsets(uint64_t* block_off, uint64_t* chunk_off, uint64
                                 uint64_t* total, const uint8_t* cls, const KeptLists& kept,
                                 hipStream_t s);
 constexpr uint64_t kGroup = 64;           // candidates per group (one wave)
-constexpr uint64_t kChunkGroups = 1024;   // groups per chunk of the offsets scan
+constexpr uint64_t kChunkGroups = 256;    // groups per chunk of the offsets scan (4 threads each)
 uint64_t verify_groups(uint64_t count);
 uint64_t verify_chunks(uint64_t count);
 
