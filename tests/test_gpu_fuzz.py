@@ -32,7 +32,9 @@ from conftest import REPO
 from oracle.tables import read_tables
 
 REFDUMP = os.path.join(REPO, "oracle", "_ref", "refdump")
-SEEDS = range(300, 348)
+# (YAMD_FUZZ_SEEDS="a-b": another range, for an extended one-off run)
+_seeds = os.environ.get("YAMD_FUZZ_SEEDS", "300-347").split("-")
+SEEDS = range(int(_seeds[0]), int(_seeds[1]) + 1)
 SIZE = 1 << 20
 
 pytestmark = [pytest.mark.gpu,
@@ -68,11 +70,27 @@ def test_fresh_rule_set_on_gpu(tmp_path, seed):
     np.testing.assert_array_equal(recs["offset"].astype(np.int64), want_off)
     np.testing.assert_array_equal(recs["pool_index"], vidx[keep])
 
+    # (verify_calls runs yr_amd_scan_block_verified: a verified-only scan, the
+    # libyara path's mode, whose byte-key kernels decide classes and drop dead
+    # candidates.)  The same records from a full device scan, candidate
+    # indices included: the verified-only records index the full stream.
+    import torch
+    from yara_amd._hip import memcpy
+    d = torch.from_numpy(np.ascontiguousarray(data)).cuda()
+    sv = yara_amd.Scanner(sc.tables)
+    sv.scan_device(d.data_ptr(), SIZE)
+    sv.device_result()
+    ptr, cnt = sv.verify_device(0)
+    h = torch.empty(max(cnt, 1) * 16, dtype=torch.uint8, device="cuda")
+    memcpy(h.data_ptr(), ptr, cnt * 16, 3)
+    vo = np.frombuffer(h[:cnt * 16].cpu().numpy().tobytes(), dtype=yara_amd._lib.VERIFY_REC_DTYPE)
+    np.testing.assert_array_equal(vo["offset"].astype(np.int64), want_off)
+    np.testing.assert_array_equal(vo["pool_index"], vidx[keep])
+    np.testing.assert_array_equal(vo["candidate"], recs["candidate"])
+
     if t.M[0] != 0:
         return
-    import torch
     from yara_amd import dist as ydist
-    from yara_amd._hip import memcpy
     before, after = ydist.tables_halos(sc.tables)
     got = []
     for r in range(3):
