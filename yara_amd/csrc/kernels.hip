@@ -188,6 +188,7 @@ struct WaveQueue {
   uint32_t pend_n;  // wave-uniform
   uint32_t full;    // wave-uniform (byte-key kernels): candidates of the segment's full
                     // stream flushed so far (verified-only scans leave the dead out)
+  uint32_t dacc;    // wave-uniform (kDrainClass): the drains' dead not yet in `full`
   uint32_t kcv;     // per lane (byte-key kernels): the key class records (scan_key_rec)
   bool defer;       // wave-uniform: the per-lane hits below await their words
   uint32_t facc;    // per lane (byte-key kernels, kBkSkipF): OR of the stage-1 filter
@@ -403,20 +404,23 @@ __device__ __forceinline__ void flush_pending(const ScanParams& p, WaveQueue& q,
                                               uint64_t seg_start, uint32_t* out, uint32_t& found) {
   __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
   bool keep = false, dead = false;
-  uint32_t off = 0, xv = 0;
+  uint32_t off = 0, xv = 0, dx = 0;
   if constexpr (kByteKeys<MODE>) {
     // confirmed entries need no probe; a flush of nothing else makes no
     // memory round trip at all
     u32x2 e = {0u, 0u};
     if (lane < q.pend_n) e = lds_load<u32x2>(q.pend + 8 * lane);
     const bool conf = (e.y & kCertainMask) != 0u;
-    off = e.y;   // (a certain entry's bits for key_class with it)
+    // (a certain entry's bits for key_class with it; a non-certain one's dead
+    // count, kDrainClass, in the class byte's place)
+    off = conf ? e.y : e.y & kOutOffsetMask;
     const bool probe = lane < q.pend_n && !conf;
     dead = kDrop<MODE> && lane < q.pend_n && conf &&
            ((e.y >> kOutByteShift) & 0xFFu) == kClassDead;
     keep = lane < q.pend_n && conf && !dead;
     if (__ballot(probe) != 0 && probe) keep = exact_check(e.x, seg_start + off + 1, p);
     xv = e.x;
+    dx = conf ? e.x : (e.y >> kOutByteShift) & 0xFFu;   // (kDrop: the dead its drain dropped before it)
   } else if (lane < q.pend_n) {
     const u32x2 e = lds_load<u32x2>(q.pend + 8 * lane);
     off = e.y;
@@ -427,8 +431,8 @@ __device__ __forceinline__ void flush_pending(const ScanParams& p, WaveQueue& q,
   if constexpr (kByteKeys<MODE>) {
     if constexpr (kDrop<MODE>) {
       bf = __ballot(keep || dead);
-      xv = q.full + __builtin_amdgcn_mbcnt_hi((uint32_t)(bf >> 32),
-                                              __builtin_amdgcn_mbcnt_lo((uint32_t)bf, 0u));
+      xv = q.full + dx +
+           __builtin_amdgcn_mbcnt_hi((uint32_t)(bf >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)bf, 0u));
     }
   }
   if (keep) {
@@ -667,6 +671,210 @@ __device__ __forceinline__ void certain_entry(const ScanParams& p, uint32_t ent,
 // offset, DESIGN.md section 5 "Measurement method".)
 template <int MODE>
 constexpr bool kBkResolve = kByteKeys<MODE>;
+
+// A raw pending entry's first word: the ring entry's LDS address (< 2^18), the
+// lane byte j, and -- drain classes, below -- how many candidates of the same
+// drain before it were dropped as dead (< 1024: 64 entries of 16 bytes).
+static_assert(kFilterBytes + kQueueBytes + kWavesPerWG * kWave * 8 <= (1u << 18),
+              "raw pending entries hold LDS addresses in 18 bits");
+__device__ __forceinline__ uint32_t raw_x(uint32_t ent, uint32_t j, uint32_t d) {
+  return ent | j << 18 | d << 22;
+}
+__device__ __forceinline__ uint32_t raw_ent(uint32_t x) { return x & 0x3FFFFu; }
+__device__ __forceinline__ uint32_t raw_j(uint32_t x) { return (x >> 18) & 15u; }
+__device__ __forceinline__ uint32_t raw_dead(uint32_t x) { return x >> 22; }
+
+// Drain classes (verified-only scans, the drop instances): the drain decides
+// the classes of its entries' certain candidates itself, sixteen positions at
+// a time, from the bytes the entry holds -- key_class's decision in byte-wise
+// SWAR form.  Dead candidates never reach the pending list (only counted, for
+// the full stream's indices); kept / undecided ones whose bytes all lie in the
+// entry go there resolved, so the drain needs no resolve_pending for them.  The
+// rest (a guard's bytes past the entry, a block edge) stay raw for
+// scan_class_entry.  (The upper bound, every certain candidate dropped in the
+// drain: rx's kernel 1.028 -> 0.769 ms, fuzz0's 1.043 -> 0.844, gpurun r5h41.)
+#ifndef YAMD_DRAIN_CLASS
+#define YAMD_DRAIN_CLASS 1
+#endif
+template <int MODE>
+constexpr bool kDrainClass = kDrop<MODE> && YAMD_DRAIN_CLASS;
+
+// bit 7 of each byte set iff that byte of t is 0 (exact for every byte)
+__device__ __forceinline__ uint32_t zero_flags(uint32_t t) {
+  return ~(((t & 0x7F7F7F7Fu) + 0x7F7F7F7Fu) | t) & 0x80808080u;
+}
+// Bit-7 flags of lane bytes 4d .. 4d + 3 in z[d] -> bit j <=> lane byte j
+// (byte_keys_mask's v_dot4 gather).
+__device__ __forceinline__ uint32_t gather16(const uint32_t (&z)[4]) {
+  const uint32_t lo = __builtin_amdgcn_udot4(z[1], 0x80402010u, __builtin_amdgcn_udot4(z[0], 0x08040201u, 0u, false),
+                                             false);
+  const uint32_t hi = __builtin_amdgcn_udot4(z[3], 0x80402010u, __builtin_amdgcn_udot4(z[2], 0x08040201u, 0u, false),
+                                             false);
+  return (lo >> 7) | (hi << 1);
+}
+// Byte tests over a drain entry's 24 bytes, lane bytes -4 .. 19 (the context
+// dword, the lane's sixteen, the next lane's dword -- its first two bytes, or
+// zeros): bit b + 4 of the result <=> (byte b & mt) == vt, for one mask / value
+// byte pair and all 24 bytes at once (six zero-byte tests and a v_dot4
+// gather).  A test at offset o from each of the sixteen positions is then a
+// shift: bit j of (T >> (o + 4)).  (Shifting bytes instead -- a select of
+// dwords per offset and v_alignbyte -- cost as much as the drain saved.)
+__device__ __forceinline__ uint32_t byte_test24(const uint32_t (&E)[6], uint32_t mt, uint32_t vt) {
+  const uint32_t M = mt * 0x01010101u, V = vt * 0x01010101u;
+  const uint32_t z0 = zero_flags((E[0] & M) ^ V), z1 = zero_flags((E[1] & M) ^ V);
+  const uint32_t z2 = zero_flags((E[2] & M) ^ V), z3 = zero_flags((E[3] & M) ^ V);
+  const uint32_t z4 = zero_flags((E[4] & M) ^ V), z5 = zero_flags((E[5] & M) ^ V);
+  const uint32_t lo = __builtin_amdgcn_udot4(z1, 0x80402010u, __builtin_amdgcn_udot4(z0, 0x08040201u, 0u, false),
+                                             false);
+  const uint32_t mid = __builtin_amdgcn_udot4(z3, 0x80402010u, __builtin_amdgcn_udot4(z2, 0x08040201u, 0u, false),
+                                              false);
+  const uint32_t hi = __builtin_amdgcn_udot4(z5, 0x80402010u, __builtin_amdgcn_udot4(z4, 0x08040201u, 0u, false),
+                                             false);
+  return (lo >> 7) | (mid << 1) | (hi << 9);
+}
+
+// bit b + 4 <=> lane byte b (-4 .. 15) is one of the bytes of x0, x1 (the
+// exclusions: the first one repeated to fill), OR-ed before one gather
+__device__ __forceinline__ uint32_t byte_set_test20(const uint32_t (&E)[6], uint32_t x0, uint32_t x1) {
+  uint32_t z0 = 0u, z1 = 0u, z2 = 0u, z3 = 0u, z4 = 0u;
+  auto acc = [](uint32_t& z, uint32_t t) { z |= ~(((t & 0x7F7F7F7Fu) + 0x7F7F7F7Fu) | t); };
+#pragma unroll 1
+  for (uint32_t i = 0; i < 8; ++i) {
+    const uint32_t b = ((i < 4 ? x0 : x1) >> (8 * (i & 3u))) & 0xFFu;
+    if (i != 0 && b == (x0 & 0xFFu)) break;
+    const uint32_t V = b * 0x01010101u;
+    acc(z0, E[0] ^ V);
+    acc(z1, E[1] ^ V);
+    acc(z2, E[2] ^ V);
+    acc(z3, E[3] ^ V);
+    acc(z4, E[4] ^ V);
+  }
+  const uint32_t k = 0x80808080u;
+  const uint32_t lo = __builtin_amdgcn_udot4(z1 & k, 0x80402010u, __builtin_amdgcn_udot4(z0 & k, 0x08040201u, 0u, false),
+                                             false);
+  const uint32_t mid = __builtin_amdgcn_udot4(z3 & k, 0x80402010u,
+                                              __builtin_amdgcn_udot4(z2 & k, 0x08040201u, 0u, false), false);
+  const uint32_t hi = __builtin_amdgcn_udot4(z4 & k, 0x08040201u, 0u, false);
+  return (lo >> 7) | (mid << 1) | (hi << 9);
+}
+
+// One drain entry's certain candidates (m: its hits, tail-masked, all of them
+// certain; pos0: the block position of lane byte 0): dead = decided dead;
+// res = decided and kept (class kept if in `kept`, the key index's bits in kid
+// -- bit j: bit 0, bit 16 + j: bit 1 -- else class 0).  key_class (kp = 2) for
+// sixteen positions at a time, on the same records (kcv, read by v_readlane:
+// the key loop is wave-uniform); what it cannot decide is in neither mask.
+struct DrainClasses {
+  uint32_t dead, res, kept, kid, fetch;
+};
+template <int MODE>
+__device__ __forceinline__ DrainClasses drain_classes(const ScanParams& p, uint32_t kcv, uint32_t ent,
+                                                      const uint32_t (&S)[6], uint32_t eidx, uint32_t m,
+                                                      uint64_t pos0) {
+  DrainClasses c{0u, 0u, 0u, 0u, 0u};
+  // the next lane's first two bytes: kept by the kernels with kNextBytes,
+  // except in a tile's last lane
+  const bool nx = kNextBytes<MODE> && (eidx & (kWave - 1)) != kWave - 1;
+  const uint32_t E[6] = {S[0], S[1], S[2], S[3], S[4], nx ? eidx >> 16 : 0u};
+  const int32_t last = nx ? 17 : 15;   // last lane byte held
+  uint32_t seen = 0u;                  // the keys' candidates so far
+  // one test remembered across keys and guards (rx: both keys test the byte
+  // after them against 0xC3)
+  uint32_t cm = 0u, cv = 0u, ct = 0u;
+  auto test = [&](uint32_t mt, uint32_t vt) {
+    if (mt != cm || vt != cv) {
+      cm = mt;
+      cv = vt;
+      ct = byte_test24(E, mt, vt);
+    }
+    return ct;
+  };
+  // (rolled loops, over the keys and the tested bytes: unrolled, with the
+  // test's reuse branch, the drop kernels' code grew four-fold)
+  const uint32_t nk = uniform_count(p.n_byte_keys);
+#pragma unroll 1
+  for (uint32_t k = 0; k < nk; ++k) {
+    auto f = [&](uint32_t i) { return (uint32_t)__builtin_amdgcn_readlane((int)kcv, (int)(8 * k + i)); };
+    const uint32_t key = (p.byte_keys >> (8 * k)) & 0xFFu;
+    uint32_t K;   // this key's candidates (the last key: the rest of m)
+    if (k + 1 == nk) {
+      K = m & ~seen;
+    } else {
+      uint32_t z[4];
+#pragma unroll
+      for (int d = 0; d < 4; ++d) z[d] = zero_flags(S[1 + d] ^ key * 0x01010101u);
+      K = gather16(z) & m;
+      seen |= K;
+    }
+    const uint32_t info = f(0);
+    if (!(info & 1u)) {   // no class: 0
+      c.res |= K;
+      continue;
+    }
+    uint32_t Kn = K;
+    if (info & 2u) {   // the byte before the key among the exclusions (a deeper trie state): class 0
+      const uint32_t X = byte_set_test20(E, f(3), f(4)) >> 3 & K;
+      c.res |= X;
+      Kn = K & ~X;
+    }
+    if (info & 4u) {   // kept, from min_pos on (pos >= min_pos for every j of the entry)
+      if (pos0 + 1 >= (uint64_t)f(5)) {
+        c.res |= Kn;
+        c.kept |= Kn;
+        c.kid |= ((k & 1u) ? Kn : 0u) | ((k & 2u) ? Kn << 16 : 0u);
+      }
+      continue;
+    }
+    // the forward guard: dead iff no shift jj <= span passes; decided where its
+    // bytes lie in the entry (avail) and end <= byte_end for every j of the
+    // entry (rng)
+    const uint32_t gm = f(1), gv = f(2);
+    const int32_t rs = (int32_t)(int8_t)(info >> 8);
+    const uint32_t span = (info >> 16) & 15u, tmax = (info >> 20) & 3u;
+    const int64_t endo = (int8_t)(info >> 24);
+    // A: bit j <=> position j passes every tested byte at shift 0 (rs + t + 4
+    // >= 0: rs >= -1, fits() in scanner.cpp); shift jj is A >> jj
+    uint32_t A = ~0u;
+#pragma unroll 1
+    for (uint32_t t = 0; t <= tmax; ++t) {
+      const uint32_t mt = (gm >> (8 * t)) & 0xFFu, vt = (gv >> (8 * t)) & 0xFFu;
+      // (a test of the key byte itself holds at every candidate)
+      if (mt == 0u || (rs + (int32_t)t == 0 && mt == 0xFFu && vt == key)) continue;
+      A &= test(mt, vt) >> (uint32_t)(rs + (int32_t)t + 4);
+    }
+    uint32_t fp = 0u;
+#pragma unroll 1
+    for (uint32_t jj = 0; jj <= span; ++jj) fp |= A >> jj;
+    const int32_t lim = last - (rs + (int32_t)(span + tmax));   // held: j <= lim
+    const uint32_t avail = lim < 0 ? 0u : lim >= 15 ? 0xFFFFu : (2u << lim) - 1u;
+    const uint32_t rng = (int64_t)pos0 + 16 + endo > (int64_t)p.byte_end ? 0u : 0xFFFFu;
+    uint32_t dead = Kn & ~fp & avail & rng;
+    // the backward guard (one position, its bytes before the key: always held)
+    if (p.kd_bguard != 0u && (info & 8u)) {
+      const uint32_t mp = f(5), bm = f(6), bv = f(7);
+      const int32_t g = (int32_t)(int8_t)mp;
+      const uint32_t btmax = (mp >> 12) & 3u;
+      if ((int64_t)pos0 + g >= (int64_t)p.byte_begin) {
+        uint32_t a = ~0u;
+#pragma unroll 1
+        for (uint32_t t = 0; t <= btmax; ++t) {
+          const uint32_t mt = (bm >> (8 * t)) & 0xFFu, vt = (bv >> (8 * t)) & 0xFFu;
+          if (mt == 0u) continue;
+          a &= test(mt, vt) >> (uint32_t)(g + (int32_t)t + 4);
+        }
+        dead |= Kn & ~a;
+      }
+    }
+    c.dead |= dead;
+    // alive: class 0 where the guard's bytes were held, else (within byte_end)
+    // kClassFetch -- key_class's "more": the compaction's eight bytes around
+    // the key hold them (fits(): rs >= -1, rs + span + tmax <= 5)
+    c.res |= Kn & rng & ~dead;
+    c.fetch |= Kn & rng & ~avail & ~dead;
+  }
+  return c;
+}
+
 // Verified-only scans: the class of the certain candidate at lane byte j of
 // ring entry ent (key_class over the eight lane bytes j - 2 .. j + 5, the key at
 // byte 2 -- lane bytes 16, 17 are the next lane's first two, kept in the
@@ -715,13 +923,15 @@ __device__ __forceinline__ void resolve_pending(const ScanParams& p, WaveQueue& 
     // scan_class_entry's permutes need their source lanes active; an idle
     // lane computes on pending entry `from`'s (raw) entry and stores nothing
     const u32x2 e = lds_load<u32x2>(q.pend + 8 * (act ? lane : from));
-    const uint32_t ent = e.x & 0xFFFFFFu, j = e.x >> 24;
+    const uint32_t ent = raw_ent(e.x), j = raw_j(e.x);
     const uint32_t yc = scan_class_entry<MODE>(p, q.kcv, ent, j, e.y & 0x7FFFFFFFu, seg_start);
-    if (act) {
-      uint32_t x = 0u, y = yc;
-      if (!(e.y >> 31)) {
+    // (entries the drain resolved itself, kDrainClass, stay as they are; an
+    // idle lane's entry may be one of them: its reads stay inside the LDS)
+    if (act && (e.y & kCertainMask) == 0u) {
+      uint32_t x = raw_dead(e.x), y = yc;
+      if (!(e.y >> 31)) {   // non-certain: the dead count (< 256) in the class byte's place
         x = window4(ent, j);
-        y = e.y;
+        y = e.y | raw_dead(e.x) << kOutByteShift;
       }
       lds_store2(q.pend + 8 * lane, x, y);
     }
@@ -729,7 +939,7 @@ __device__ __forceinline__ void resolve_pending(const ScanParams& p, WaveQueue& 
   }
   if (act) {
     const u32x2 e = lds_load<u32x2>(q.pend + 8 * lane);
-    const uint32_t ent = e.x & 0xFFFFFFu, j = e.x >> 24;
+    const uint32_t ent = raw_ent(e.x), j = raw_j(e.x);
     uint32_t x = 0u, y = e.y & 0x7FFFFFFFu;
     if (e.y >> 31) certain_entry<MODE>(p, ent, j, x, y);
     else x = window4(ent, j);
@@ -794,15 +1004,21 @@ __device__ __forceinline__ void drain(const ScanParams& p, WaveQueue& q, uint32_
   __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
   uint32_t maybe = 0, off0 = 0, m = 0;   // m: bit j = lane byte j passes the filter
   uint32_t kmask = 0;                    // bit j = lane byte j is a 1-byte key (certain)
+  DrainClasses dc{0u, 0u, 0u, 0u, 0u};   // (kDrainClass)
   const uint32_t ent = q.ring + lane * (kQueueEntryWords * 4);
+  uint32_t S[6] = {0u, 0u, 0u, 0u, 0u, 0u}, eidx = 0u;
   if (lane < n) {
     // the entry's 16 positions again, now with a per-position result: the
     // same pair tests as stage 1 over the entry's window context
     const u32x2 e01 = lds_load<u32x2>(ent);
     const u32x2 e23 = lds_load<u32x2>(ent + 8);
     const u32x2 e45 = lds_load<u32x2>(ent + 16);
-    const uint32_t S[6] = {e01.x, e01.y, e23.x, e23.y, e45.x, 0u};
-    const uint32_t eidx = e45.y;
+    S[0] = e01.x;
+    S[1] = e01.y;
+    S[2] = e23.x;
+    S[3] = e23.y;
+    S[4] = e45.x;
+    eidx = e45.y;
     off0 = (eidx & 0xFFFFu) * kBytesPerLane;
     if (need_f) {
       if constexpr (kEven<MODE>) {
@@ -823,6 +1039,9 @@ __device__ __forceinline__ void drain(const ScanParams& p, WaveQueue& q, uint32_
       m &= lim >= 16u ? 0xFFFFu : (1u << lim) - 1u;
     }
   }
+  // (kDrainClass: nc = some lane holds a filter hit, a non-certain entry)
+  const bool nc = kDrainClass<MODE> && __ballot((m & ~kmask) != 0u) != 0;
+  if (kDrainClass<MODE> && lane < n) dc = drain_classes<MODE>(p, q.kcv, ent, S, eidx, m & kmask, seg_start + off0);
   if constexpr (kDeferFl<MODE> && kAsync) {
     const uint32_t m2 = m & (m - 1u);
     if ((p.len_mask & 6u) == 0u && __ballot((m2 & (m2 - 1u)) != 0u) == 0) {
@@ -877,46 +1096,109 @@ __device__ __forceinline__ void drain(const ScanParams& p, WaveQueue& q, uint32_
       maybe |= (uint32_t)hit << j;
     }
   }
-  const uint32_t c = __popc(maybe);
-  const uint32_t incl = wave_inclusive_scan(c);
+  // (kDrainClass: the dead are counted, per lane dd = how many, dbase = how
+  // many in the lanes below, dtotal = in the drain -- one scan for both sums)
+  uint32_t dd = 0u, dbase = 0u, dtotal = 0u;
+  const uint32_t maybe0 = maybe;
+  if constexpr (kDrainClass<MODE>) {
+    maybe &= ~dc.dead;
+    dd = __popc(dc.dead);
+  }
+  uint32_t c = __popc(maybe);
+  uint32_t incl;
+  if constexpr (kDrainClass<MODE>) {
+    const uint32_t both = wave_inclusive_scan(c | dd << 16);   // (sums <= 1024)
+    incl = both & 0xFFFFu;
+    dbase = (both >> 16) - dd;
+    dtotal = __builtin_amdgcn_readlane(both, kWave - 1) >> 16;
+    if (nc && dtotal >= 256u) {
+      // a non-certain entry carries its dead count in 8 bits: a drain with
+      // more dead than that and a filter hit keeps all of its entries (rare:
+      // 16 dead per lane of a dense 1-byte key)
+      dc = DrainClasses{0u, 0u, 0u, 0u, 0u};
+      maybe = maybe0;
+      c = __popc(maybe);
+      incl = wave_inclusive_scan(c);
+      dd = dbase = dtotal = 0u;
+    }
+  } else {
+    incl = wave_inclusive_scan(c);
+  }
   if constexpr (MODE == 1 || MODE == 9 || MODE == 10) {   // ablations: output as is
     append_hits(p, maybe, c, incl, off0, out, found);
     return;
   }
   const uint32_t total = __builtin_amdgcn_readlane(incl, kWave - 1);
-  if (total == 0) return;
-  // in order to the pending list, bucket-probed (one round trip for 64 hits)
-  // each time it fills up -- dense true hits (1-byte keys) can yield up to 16
-  // per lane; probing them in place would cost one round trip per hit
-  const uint32_t end = q.pend_n + total;
-  uint32_t idx = q.pend_n + incl - c;
-  uint32_t from = q.pend_n;   // (kBkResolve: the first pending entry still raw)
-  for (uint32_t base = 0;; base += kWave) {
-    while (maybe != 0u && idx < base + kWave) {
-      const uint32_t j = (uint32_t)__builtin_ctz(maybe);
-      maybe &= maybe - 1;
-      uint32_t y = off0 + j, x;
-      if constexpr (kBkResolve<MODE>) {
-        // raw: the ring entry, the lane byte and "certain"; resolved below
-        x = ent | j << 24;
-        y |= ((kmask >> j) & 1u) << 31;
-      } else if (kByteKeys<MODE> && ((kmask >> j) & 1u)) {
-        certain_entry<MODE>(p, ent, j, x, y);
-      } else {
-        x = window4(ent, j);
+  if (total != 0) {
+    // any entry left raw (kDrainClass: a drain that resolved all of its own
+    // entries skips resolve_pending)
+    const bool raw = !kDrainClass<MODE> || __ballot((maybe & ~dc.res) != 0u) != 0;
+    if constexpr (kDrainClass<MODE>) {
+      // the dead not yet counted (q.dacc) join the full stream before any
+      // entry that cannot carry their number -- a non-certain one past 8 bits
+      // of it, a raw one past 10 -- after the pending entries before them
+      if (q.dacc != 0u && ((nc && q.dacc + dtotal >= 256u) || (raw && q.dacc + dtotal >= 1024u))) {
+        if (q.pend_n != 0u) flush_pending<MODE>(p, q, lane, seg_start, out, found);
+        q.full += q.dacc;
+        q.dacc = 0u;
       }
-      lds_store2(q.pend + 8 * (idx - base), x, y);
-      ++idx;
     }
-    if (end <= base + kWave) {
-      q.pend_n = end - base;
-      if constexpr (kBkResolve<MODE>) resolve_pending<MODE>(p, q, lane, from, seg_start);
-      return;
+    // in order to the pending list, bucket-probed (one round trip for 64 hits)
+    // each time it fills up -- dense true hits (1-byte keys) can yield up to 16
+    // per lane; probing them in place would cost one round trip per hit
+    const uint32_t end = q.pend_n + total;
+    uint32_t idx = q.pend_n + incl - c;
+    uint32_t from = q.pend_n;   // (kBkResolve: the first pending entry still raw)
+    for (uint32_t base = 0;; base += kWave) {
+      while (maybe != 0u && idx < base + kWave) {
+        const uint32_t j = (uint32_t)__builtin_ctz(maybe);
+        maybe &= maybe - 1;
+        uint32_t y = off0 + j, x;
+        if constexpr (kBkResolve<MODE>) {
+          // the dead of this drain before the candidate
+          const uint32_t dj = kDrainClass<MODE> ? q.dacc + dbase + __popc(dc.dead & ((1u << j) - 1u)) : 0u;
+          if (kDrainClass<MODE> && ((dc.res >> j) & 1u)) {
+            // resolved here: scan_class_entry's output entry, the dead count in x
+            const uint32_t kidx = ((dc.kid >> j) & 1u) | ((dc.kid >> (15 + j)) & 2u);
+            const uint32_t cls = ((dc.kept >> j) & 1u)    ? (kClassKept | kidx << 2)
+                                 : ((dc.fetch >> j) & 1u) ? kClassFetch
+                                                          : 0u;
+            x = dj;
+            y |= cls << kOutByteShift | kOutPlaceScanClass << kOutKeyShift;
+          } else {
+            // raw: the ring entry, the lane byte and "certain"; resolved below
+            x = raw_x(ent, j, dj);
+            y |= ((kmask >> j) & 1u) << 31;
+          }
+        } else if (kByteKeys<MODE> && ((kmask >> j) & 1u)) {
+          certain_entry<MODE>(p, ent, j, x, y);
+        } else {
+          x = window4(ent, j);
+        }
+        lds_store2(q.pend + 8 * (idx - base), x, y);
+        ++idx;
+      }
+      if (end <= base + kWave) {
+        q.pend_n = end - base;
+        if constexpr (kBkResolve<MODE>)
+          if (raw) resolve_pending<MODE>(p, q, lane, from, seg_start);
+        break;
+      }
+      q.pend_n = kWave;
+      if constexpr (kBkResolve<MODE>)
+        if (raw) resolve_pending<MODE>(p, q, lane, from, seg_start);
+      from = 0;
+      flush_pending<MODE>(p, q, lane, seg_start, out, found);
     }
-    q.pend_n = kWave;
-    if constexpr (kBkResolve<MODE>) resolve_pending<MODE>(p, q, lane, from, seg_start);
-    from = 0;
-    flush_pending<MODE>(p, q, lane, seg_start, out, found);
+  }
+  if constexpr (kDrainClass<MODE>) {
+    // the drain's dead, counted into the full stream once no pending entry
+    // precedes them (each pending entry carries the number before it)
+    q.dacc += dtotal;
+    if (q.pend_n == 0u) {
+      q.full += q.dacc;
+      q.dacc = 0u;
+    }
   }
 }
 
@@ -1277,6 +1559,7 @@ __device__ __forceinline__ void scan_segment(const ScanParams& p, WaveQueue& q, 
   q.count = 0;
   q.pend_n = 0;
   q.full = 0;
+  q.dacc = 0;
   q.defer = false;
   q.facc = 0u;
   q.ia = q.ib = 0u;
@@ -1314,7 +1597,7 @@ __device__ __forceinline__ void scan_segment(const ScanParams& p, WaveQueue& q, 
   if (q.pend_n != 0) flush_pending<MODE>(p, q, lane, st.seg_start, st.out, st.found);
   if (lane == 0) {
     p.seg_count[seg] = st.found;
-    if (kDrop<MODE>) p.seg_full[seg] = q.full;
+    if (kDrop<MODE>) p.seg_full[seg] = q.full + q.dacc;
   }
 }
 
