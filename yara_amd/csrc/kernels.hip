@@ -782,7 +782,10 @@ __device__ __forceinline__ DrainClasses drain_classes(const ScanParams& p, uint3
   // after them against 0xC3)
   uint32_t cm = 0u, cv = 0u, ct = 0u;
   auto test = [&](uint32_t mt, uint32_t vt) {
-    if (mt != cm || vt != cv) {
+    // (readfirstlane: provably uniform, so the reuse test is a scalar branch)
+    mt = __builtin_amdgcn_readfirstlane(mt);
+    vt = __builtin_amdgcn_readfirstlane(vt);
+    if (mt != __builtin_amdgcn_readfirstlane(cm) || vt != __builtin_amdgcn_readfirstlane(cv)) {
       cm = mt;
       cv = vt;
       ct = byte_test24(E, mt, vt);
@@ -1041,7 +1044,9 @@ __device__ __forceinline__ void drain(const ScanParams& p, WaveQueue& q, uint32_
   }
   // (kDrainClass: nc = some lane holds a filter hit, a non-certain entry)
   const bool nc = kDrainClass<MODE> && __ballot((m & ~kmask) != 0u) != 0;
-  if (kDrainClass<MODE> && lane < n) dc = drain_classes<MODE>(p, q.kcv, ent, S, eidx, m & kmask, seg_start + off0);
+  // (every lane, in uniform control flow -- lanes without an entry have no
+  // hits: the class code's wave-uniform values stay in SGPRs)
+  if constexpr (kDrainClass<MODE>) dc = drain_classes<MODE>(p, q.kcv, ent, S, eidx, m & kmask, seg_start + off0);
   if constexpr (kDeferFl<MODE> && kAsync) {
     const uint32_t m2 = m & (m - 1u);
     if ((p.len_mask & 6u) == 0u && __ballot((m2 & (m2 - 1u)) != 0u) == 0) {
