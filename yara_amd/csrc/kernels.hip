@@ -569,11 +569,23 @@ __device__ __forceinline__ uint32_t pair_keys_mask(const uint32_t (&S)[6], const
 // Exact zero-byte flags (bit 7 of each byte of z_d) OR-ed over the keys, then
 // each dword's four flags gathered by one v_dot4_u32_u8 against the place
 // values 2^r (two dwords per chain: bytes of 0x80 times 1..128 stay below 2^16).
-__device__ __forceinline__ uint32_t byte_keys_mask(const uint32_t (&S)[6], const ScanParams& p) {
+// (first: if given and the table has more than one key, the first key's own
+// mask -- the drain classes' per-key split)
+__device__ __forceinline__ uint32_t byte_keys_mask(const uint32_t (&S)[6], const ScanParams& p,
+                                                   uint32_t* first = nullptr) {
   uint32_t z[4] = {0u, 0u, 0u, 0u};
 #pragma unroll
   for (uint32_t k = 0; k < kMaxByteKeys; ++k) {
     if (k != 0 && k >= uniform_count(p.n_byte_keys)) break;
+    if (k == 1 && first != nullptr) {
+      const uint32_t lo = __builtin_amdgcn_udot4(z[1] & 0x80808080u, 0x80402010u,
+                                                 __builtin_amdgcn_udot4(z[0] & 0x80808080u, 0x08040201u, 0u, false),
+                                                 false);
+      const uint32_t hi = __builtin_amdgcn_udot4(z[3] & 0x80808080u, 0x80402010u,
+                                                 __builtin_amdgcn_udot4(z[2] & 0x80808080u, 0x08040201u, 0u, false),
+                                                 false);
+      *first = (lo >> 7) | (hi << 1);
+    }
     const uint32_t v = ((p.byte_keys >> (8 * k)) & 0xFFu) * 0x01010101u;   // (k: a constant)
 #pragma unroll
     for (int d = 0; d < 4; ++d) {
@@ -721,9 +733,14 @@ __device__ __forceinline__ uint32_t gather16(const uint32_t (&z)[4]) {
 // dwords per offset and v_alignbyte -- cost as much as the drain saved.)
 __device__ __forceinline__ uint32_t byte_test24(const uint32_t (&E)[6], uint32_t mt, uint32_t vt) {
   const uint32_t M = mt * 0x01010101u, V = vt * 0x01010101u;
-  const uint32_t z0 = zero_flags((E[0] & M) ^ V), z1 = zero_flags((E[1] & M) ^ V);
-  const uint32_t z2 = zero_flags((E[2] & M) ^ V), z3 = zero_flags((E[3] & M) ^ V);
-  const uint32_t z4 = zero_flags((E[4] & M) ^ V), z5 = zero_flags((E[5] & M) ^ V);
+  uint32_t z0, z1, z2, z3, z4, z5;
+  if (mt == 0xFFu) {   // (wave-uniform: no mask, one instruction less per dword)
+    z0 = zero_flags(E[0] ^ V), z1 = zero_flags(E[1] ^ V), z2 = zero_flags(E[2] ^ V);
+    z3 = zero_flags(E[3] ^ V), z4 = zero_flags(E[4] ^ V), z5 = zero_flags(E[5] ^ V);
+  } else {
+    z0 = zero_flags((E[0] & M) ^ V), z1 = zero_flags((E[1] & M) ^ V), z2 = zero_flags((E[2] & M) ^ V);
+    z3 = zero_flags((E[3] & M) ^ V), z4 = zero_flags((E[4] & M) ^ V), z5 = zero_flags((E[5] & M) ^ V);
+  }
   const uint32_t lo = __builtin_amdgcn_udot4(z1, 0x80402010u, __builtin_amdgcn_udot4(z0, 0x08040201u, 0u, false),
                                              false);
   const uint32_t mid = __builtin_amdgcn_udot4(z3, 0x80402010u, __builtin_amdgcn_udot4(z2, 0x08040201u, 0u, false),
@@ -770,7 +787,7 @@ struct DrainClasses {
 template <int MODE>
 __device__ __forceinline__ DrainClasses drain_classes(const ScanParams& p, uint32_t kcv, uint32_t ent,
                                                       const uint32_t (&S)[6], uint32_t eidx, uint32_t m,
-                                                      uint64_t pos0) {
+                                                      uint32_t first, uint64_t pos0) {
   DrainClasses c{0u, 0u, 0u, 0u, 0u};
   // the next lane's first two bytes: kept by the kernels with kNextBytes,
   // except in a tile's last lane
@@ -799,9 +816,12 @@ __device__ __forceinline__ DrainClasses drain_classes(const ScanParams& p, uint3
   for (uint32_t k = 0; k < nk; ++k) {
     auto f = [&](uint32_t i) { return (uint32_t)__builtin_amdgcn_readlane((int)kcv, (int)(8 * k + i)); };
     const uint32_t key = (p.byte_keys >> (8 * k)) & 0xFFu;
-    uint32_t K;   // this key's candidates (the last key: the rest of m)
+    uint32_t K;   // this key's candidates (the first: byte_keys_mask's; the last: the rest of m)
     if (k + 1 == nk) {
       K = m & ~seen;
+    } else if (k == 0) {
+      K = first;
+      seen = K;
     } else {
       uint32_t z[4];
 #pragma unroll
@@ -1008,6 +1028,7 @@ __device__ __forceinline__ void drain(const ScanParams& p, WaveQueue& q, uint32_
   uint32_t maybe = 0, off0 = 0, m = 0;   // m: bit j = lane byte j passes the filter
   uint32_t kmask = 0;                    // bit j = lane byte j is a 1-byte key (certain)
   DrainClasses dc{0u, 0u, 0u, 0u, 0u};   // (kDrainClass)
+  uint32_t kfirst = 0u;                  // (kDrainClass, tables with 2+ keys: bits of the first one)
   const uint32_t ent = q.ring + lane * (kQueueEntryWords * 4);
   uint32_t S[6] = {0u, 0u, 0u, 0u, 0u, 0u}, eidx = 0u;
   if (lane < n) {
@@ -1032,7 +1053,7 @@ __device__ __forceinline__ void drain(const ScanParams& p, WaveQueue& q, uint32_
       }
     }
     if constexpr (kByteKeys<MODE>) {
-      kmask = byte_keys_mask(S, p);
+      kmask = byte_keys_mask(S, p, kDrainClass<MODE> ? &kfirst : nullptr);
       m |= kmask;
     }
     // the segment's partial last tile (its entries are appended after the main
@@ -1046,7 +1067,8 @@ __device__ __forceinline__ void drain(const ScanParams& p, WaveQueue& q, uint32_
   const bool nc = kDrainClass<MODE> && __ballot((m & ~kmask) != 0u) != 0;
   // (every lane, in uniform control flow -- lanes without an entry have no
   // hits: the class code's wave-uniform values stay in SGPRs)
-  if constexpr (kDrainClass<MODE>) dc = drain_classes<MODE>(p, q.kcv, ent, S, eidx, m & kmask, seg_start + off0);
+  if constexpr (kDrainClass<MODE>)
+    dc = drain_classes<MODE>(p, q.kcv, ent, S, eidx, m & kmask, kfirst & m, seg_start + off0);
   if constexpr (kDeferFl<MODE> && kAsync) {
     const uint32_t m2 = m & (m - 1u);
     if ((p.len_mask & 6u) == 0u && __ballot((m2 & (m2 - 1u)) != 0u) == 0) {
