@@ -334,11 +334,34 @@ def _device_records(sc, d, n, lo=0, hi=None):
     return out, cnt, sc.stream_length()
 
 
+def _dense_key_buffer(rules):
+    """8 MiB for the drain classes' edge cases (kernels.hip drain_classes): runs
+    of the rule set's 1-byte key (a dead candidate at every position, more
+    dead per drain than a filter-hit entry's 8-bit count holds), the key
+    followed by bytes its guard accepts, zeros, and slices of the rule set's
+    planted golden case every 4 KiB (filter hits and live calls inside the
+    dense runs)."""
+    key = {"rx": 0x5B, "fuzz0": 0x5F, "short": 0x61}[rules]
+    planted = case_data(CASES[{"rx": "rx_1M", "fuzz0": "fuzz0_256K", "short": "short_1M"}[rules]])
+    d = oracle.xorshift(8 << 20, 7).copy()
+    M = 1 << 20
+    d[1 * M:3 * M] = key
+    alive = {"rx": b"\x5b\xc3", "fuzz0": b"d_>", "short": b"ab"}[rules]
+    d[3 * M:4 * M] = np.resize(np.frombuffer(alive, dtype=np.uint8), M)
+    d[4 * M:5 * M] = 0
+    d[5 * M:6 * M] = np.resize(np.frombuffer(bytes([key]) * 7 + alive, dtype=np.uint8), M)
+    for at in range(1 * M, 6 * M, 4096):
+        o = (at * 2654435761) % (len(planted) - 256)
+        d[at + 1000:at + 1256] = planted[o:o + 256]
+    return d
+
+
 @pytest.mark.gpu
 @pytest.mark.parametrize("rules,case", [
     ("rx", "rx_1M"), ("fuzz0", "fuzz0_256K"), ("fuzz3", "fuzz3_256K"), ("short", "short_1M"),
     ("lit", "lit_1M"), ("C", "C_planted16M"),
-    ("rx", "xs64M"), ("fuzz0", "xs64M"), ("fuzz3", "xs64M"), ("short", "xs64M")])
+    ("rx", "xs64M"), ("fuzz0", "xs64M"), ("fuzz3", "xs64M"), ("short", "xs64M"),
+    ("rx", "dense"), ("fuzz0", "dense"), ("short", "dense")])
 def test_verified_only_scan_keeps_records_and_candidate_indices(rules, case):
     """Verified-only scans (yr_amd_scanner_set_verified_only: the scan kernel
     decides the 1-byte keys' classes from eight bytes around the key and leaves
@@ -348,7 +371,12 @@ def test_verified_only_scan_keeps_records_and_candidate_indices(rules, case):
     records are pinned to the reference by the tests above)."""
     import torch
     import yara_amd
-    data = oracle.xorshift(64 << 20, 1) if case == "xs64M" else case_data(CASES[case])
+    if case == "xs64M":
+        data = oracle.xorshift(64 << 20, 1)
+    elif case == "dense":
+        data = _dense_key_buffer(rules)
+    else:
+        data = case_data(CASES[case])
     n = len(data)
     d = torch.from_numpy(data.copy()).cuda()
     tab = yara_amd.Tables.from_npz(tables_npz(rules), device=0, strings=True)

@@ -28,6 +28,8 @@ def main():
     ap.add_argument("--sets", default="C,B,E,lit,hex,rx,short,fuzz0,fuzz3,fuzz7,root")
     ap.add_argument("--reps", type=int, default=10)
     ap.add_argument("--no-verify", action="store_true")
+    ap.add_argument("--warm-s", type=float, default=1.0)
+    ap.add_argument("--step-reps", type=int, default=30)
     a = ap.parse_args()
     import torch
     import yara_amd
@@ -98,13 +100,18 @@ def main():
                     # (a scanner per mode: each learns its own output capacity)
                     sc = yara_amd.Scanner(t)
                     sc.set_verified_only(mode == "verified_only")
-                    for _ in range(5):
+                    # whole steps for --warm-s first: a step idles the GPU while
+                    # the host waits, and five of them left the clocks below
+                    # their steady state (rx's verified-only kernel 1.02 ms here
+                    # against 0.94 in tools/ab_inproc.py, gpurun r5h53)
+                    t0 = time.perf_counter()
+                    while time.perf_counter() - t0 < a.warm_s:
                         sc.scan_device(buf.data_ptr(), n)
                         sc.device_result()
                         sc.verify_device(0)
                     sc.set_timing(True)
                     ks, ss, ws, vv = [], [], [], []
-                    for _ in range(a.reps):
+                    for _ in range(a.step_reps):
                         torch.cuda.synchronize()
                         t0 = time.perf_counter()
                         sc.scan_device(buf.data_ptr(), n)
