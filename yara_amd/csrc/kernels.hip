@@ -775,19 +775,20 @@ __device__ __forceinline__ uint32_t byte_set_test20(const uint32_t (&E)[6], uint
   return (lo >> 7) | (mid << 1) | (hi << 9);
 }
 
-// One drain entry's certain candidates (m: its hits, tail-masked, all of them
-// certain; pos0: the block position of lane byte 0): dead = decided dead;
+// One drain entry's certain candidates (m: its 1-byte-key hits, tail-masked;
+// first: those of the first key, with two or more keys; pos0: the block
+// position of lane byte 0): dead = decided dead;
 // res = decided and kept (class kept if in `kept`, the key index's bits in kid
-// -- bit j: bit 0, bit 16 + j: bit 1 -- else class 0).  key_class (kp = 2) for
+// -- bit j: bit 0, bit 16 + j: bit 1 --, kClassFetch if in `fetch`, else class
+// 0).  key_class (kp = 2) for
 // sixteen positions at a time, on the same records (kcv, read by v_readlane:
 // the key loop is wave-uniform); what it cannot decide is in neither mask.
 struct DrainClasses {
   uint32_t dead, res, kept, kid, fetch;
 };
 template <int MODE>
-__device__ __forceinline__ DrainClasses drain_classes(const ScanParams& p, uint32_t kcv, uint32_t ent,
-                                                      const uint32_t (&S)[6], uint32_t eidx, uint32_t m,
-                                                      uint32_t first, uint64_t pos0) {
+__device__ __forceinline__ DrainClasses drain_classes(const ScanParams& p, uint32_t kcv, const uint32_t (&S)[6],
+                                                      uint32_t eidx, uint32_t m, uint32_t first, uint64_t pos0) {
   DrainClasses c{0u, 0u, 0u, 0u, 0u};
   // the next lane's first two bytes: kept by the kernels with kNextBytes,
   // except in a tile's last lane
@@ -1068,7 +1069,7 @@ __device__ __forceinline__ void drain(const ScanParams& p, WaveQueue& q, uint32_
   // (every lane, in uniform control flow -- lanes without an entry have no
   // hits: the class code's wave-uniform values stay in SGPRs)
   if constexpr (kDrainClass<MODE>)
-    dc = drain_classes<MODE>(p, q.kcv, ent, S, eidx, m & kmask, kfirst & m, seg_start + off0);
+    dc = drain_classes<MODE>(p, q.kcv, S, eidx, m & kmask, kfirst & m, seg_start + off0);
   if constexpr (kDeferFl<MODE> && kAsync) {
     const uint32_t m2 = m & (m - 1u);
     if ((p.len_mask & 6u) == 0u && __ballot((m2 & (m2 - 1u)) != 0u) == 0) {
