@@ -351,6 +351,35 @@ def main():
                            "frac": round(shard / (k_o * 1e-3) / 1e9 / HBM_PEAK_GBS, 4),
                            "candidates": int(c_o)}
             del s_o, t_o
+            if name in ("rx", "short", "fuzz0", "fuzz3"):
+                # the verified path of the dense sets (tools/ruleset_rates.py's
+                # verified-only leg): tables with their string records, scan +
+                # result + on-device pre-verification per step, host clock,
+                # median of 20 steps after 0.5 s of them (clock ramp)
+                t_v = yara_amd.Tables.from_npz(os.path.join(REPO, "tests", "golden", "tables",
+                                                            "%s.npz" % name), device=dev.index, strings=True)
+                s_v = yara_amd.Scanner(t_v, stream=stream.cuda_stream)
+                s_v.set_verified_only(True)
+
+                def v_step():
+                    s_v.scan_device(buf.data_ptr(), total)
+                    s_v.device_result()
+                    return s_v.verify_device(0)[1]
+                t_w = time.perf_counter()
+                while time.perf_counter() - t_w < 0.5:
+                    v_step()
+                ws = []
+                for _ in range(20):
+                    torch.cuda.synchronize()
+                    t_s = time.perf_counter()
+                    n_v = v_step()
+                    ws.append((time.perf_counter() - t_s) * 1e3)
+                ws.sort()
+                w_med = (ws[9] + ws[10]) / 2
+                other[name]["verified_step_ms"] = round(w_med, 4)
+                other[name]["verified_frac"] = round(shard / (w_med * 1e-3) / 1e9 / HBM_PEAK_GBS, 4)
+                other[name]["verified_records"] = int(n_v)
+                del s_v, t_v
 
     # The verification-complete step, timed separately over the same number of
     # steps (not the bench value): scan + compaction + on-device
