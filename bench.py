@@ -12,7 +12,10 @@ one logical 4N GiB buffer, rank r owns bytes [4r, 4r+4) GiB and holds them
 plus the rule set's verify halos, yara_amd/dist.py; weak scaling).  The
 line's "verified_step" times the verification-complete step separately: the
 same plus on-device pre-verification per rank and, for N > 1, the gather of
-the pre-verified {offset, pool index} records.
+the pre-verified {offset, pool index} records.  "other_rule_sets" (N = 1):
+the scan kernel of other rule-set shapes, and for the dense 1-byte-key sets
+(rx, short, fuzz0, fuzz3) their verified-only step (verified_step_ms: scan,
+result and pre-verification on the host's clock).
 
     python bench.py [--gpus N] [--steps K] [--warmup W]
     torchrun --nproc-per-node N bench.py --gpus N ...
