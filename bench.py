@@ -20,6 +20,11 @@ result and pre-verification on the host's clock).
     python bench.py [--gpus N] [--steps K] [--warmup W]
     torchrun --nproc-per-node N bench.py --gpus N ...
 
+With --gpus N > 1 and no launcher around it (WORLD_SIZE unset) bench.py starts
+the N rank processes itself, before anything touches the GPU, with torchrun's
+environment (RANK, LOCAL_RANK, WORLD_SIZE, MASTER_ADDR=127.0.0.1, ...), and
+exits with the worst rank's code; --launch-only prints those environments.
+
 Clocks: from idle the scan kernel's first launches take up to 1.2 ms and
 settle at ~0.86 ms after ~25 ms of kernel time.  Every rank, for every N,
 first scans back to back for --clock-warmup-s seconds (default 0.4 s, ~450
@@ -30,7 +35,9 @@ Rank 0 prints one JSON line.  value = total bytes scanned by all ranks per
 second (decimal GB/s).  roofline = the scan kernel's algorithmic HBM bytes
 (1 B per input byte) per launch / its HIP-event duration, vs
 the 8.0 TB/s HBM3E peak.  cpu_baseline = the stock reference libyara
-(oracle/_ref, yr_rules_scan_mem) on the host, 1 thread, bounded sample.
+(oracle/_ref) on the host, one YR_SCANNER per thread, a bounded sample, at the
+faster of: every CPU the process may run on, and the CPUs its cgroup grants;
+the 1-thread stock yr_rules_scan_mem beside it.
 """
 import argparse
 import ctypes
@@ -68,7 +75,84 @@ def parse():
                          "process may run on)")
     ap.add_argument("--clock-warmup-s", type=float, default=0.4,
                     help="back-to-back scans before the measured legs, on every rank")
+    ap.add_argument("--launch-only", action="store_true",
+                    help="with --gpus N > 1 and no launcher: print the N rank environments "
+                         "this process would start, as one JSON line, and exit")
+    ap.add_argument("--rank-probe", action="store_true",
+                    help="(test hook) each rank prints its rank environment as JSON and exits "
+                         "before importing torch; --rank-probe-fail R makes rank R exit 3")
+    ap.add_argument("--rank-probe-fail", type=int, default=-1, help=argparse.SUPPRESS)
     return ap.parse_args()
+
+
+RANK_ENV = ("RANK", "LOCAL_RANK", "WORLD_SIZE", "LOCAL_WORLD_SIZE", "GROUP_RANK",
+            "MASTER_ADDR", "MASTER_PORT")
+
+
+def _free_port() -> int:
+    import socket
+    with socket.socket(socket.AF_INET, socket.SOCK_STREAM) as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def rank_envs(n: int, port: int):
+    """The environments of the N rank processes of one node, as torchrun sets
+    them (one process per GPU, rendezvous on 127.0.0.1)."""
+    return [{"RANK": str(r), "LOCAL_RANK": str(r), "WORLD_SIZE": str(n),
+             "LOCAL_WORLD_SIZE": str(n), "GROUP_RANK": "0", "MASTER_ADDR": "127.0.0.1",
+             "MASTER_PORT": str(port)} for r in range(n)]
+
+
+def spawn_ranks(args) -> int:
+    """`bench.py --gpus N` (N > 1) run without a launcher: start the N ranks
+    here, as fresh child processes of this script with torchrun's environment,
+    BEFORE this process touches the GPU (it never does: torch is not even
+    imported), wait for all of them and return the worst exit code.  Rank 0's
+    stdout carries the JSON line.  A rank that fails ends the others (their
+    exact PIDs), so no rank is left waiting in a collective; a rank that cannot
+    be started is a non-zero exit -- never a 1-GPU line for --gpus N."""
+    import signal
+    import subprocess
+    port = _free_port()
+    envs = rank_envs(args.gpus, port)
+    cmd = [sys.executable, os.path.abspath(__file__)] + sys.argv[1:]
+    if args.launch_only:
+        print(json.dumps({"launcher": "bench.py", "cmd": cmd, "ranks": envs}), flush=True)
+        return 0
+    procs = []
+    try:
+        for e in envs:
+            env = dict(os.environ)
+            env.update(e)
+            procs.append(subprocess.Popen(cmd, env=env))
+    except OSError as ex:
+        print("bench.py: could not start rank %d: %s" % (len(procs), ex), file=sys.stderr)
+        for p in procs:
+            p.send_signal(signal.SIGTERM)
+        for p in procs:
+            p.wait()
+        return 1
+    worst = 0
+    live = list(procs)
+    term_at = None
+    while live:
+        for p in list(live):
+            rc = p.poll()
+            if rc is None:
+                continue
+            live.remove(p)
+            if rc != 0 and term_at is None:
+                worst = rc if rc > 0 else 128 - rc
+                term_at = time.monotonic()
+                for q in live:               # the rest would wait in a collective
+                    q.send_signal(signal.SIGTERM)
+        if live and term_at is not None and time.monotonic() - term_at > 30:
+            for q in live:
+                q.kill()
+            term_at = float("inf")
+        time.sleep(0.05)
+    return worst
 
 
 def cpu_model() -> str:
@@ -134,6 +218,9 @@ def cpu_baseline(rules: str, data, seed: int):
         t0 = time.perf_counter()
         rc = L.yr_rules_scan_mem(rules_h, data.ctypes.data, n, 0, cb, None, 0)
         dt = time.perf_counter() - t0
+        L.yr_compiler_destroy(comp)
+        L.yr_rules_destroy(rules_h)
+        L.yr_finalize()                           # paired with yr_initialize above
         assert rc == 0, rc
         kind, what = "reference", "stock libyara 4.2.1 yr_rules_scan_mem (oracle/_ref)"
     else:
@@ -221,18 +308,28 @@ def load_traffic(kernel_bytes):
 
 def main():
     args = parse()
+    if args.gpus < 1:
+        raise SystemExit("--gpus must be >= 1")
+    if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
+        # no launcher (torchrun) around us: start the N ranks ourselves
+        sys.exit(spawn_ranks(args))
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world != args.gpus:
+        raise SystemExit("--gpus %d but WORLD_SIZE=%d" % (args.gpus, world))
+    if args.rank_probe:
+        print(json.dumps({k: os.environ.get(k) for k in RANK_ENV}), flush=True)
+        if args.rank_probe_fail >= 0 and rank != args.rank_probe_fail:
+            time.sleep(120)                  # stands for a rank waiting in a collective
+        sys.exit(3 if rank == args.rank_probe_fail else 0)
+
     sys.path.insert(0, os.path.join(REPO, "tests"))
     import torch
     import torch.distributed as dist
 
     import yara_amd
     from yara_amd._hip import memcpy
-
-    world = int(os.environ.get("WORLD_SIZE", "1"))
-    rank = int(os.environ.get("RANK", "0"))
-    local = int(os.environ.get("LOCAL_RANK", "0"))
-    if world != args.gpus and world > 1:
-        raise SystemExit("--gpus %d but WORLD_SIZE=%d" % (args.gpus, world))
     # the N > 1 code path: a process group, per-rank attribution, the gathers
     # (--dist: also at world size 1, e.g. RCCL on one GPU)
     use_dist = world > 1 or args.dist
@@ -241,6 +338,12 @@ def main():
                      ("WORLD_SIZE", "1")):
             os.environ.setdefault(k, v)
     ndev = torch.cuda.device_count()
+    if ndev < 1:
+        raise SystemExit("bench.py: no GPU visible")
+    if use_dist and args.backend == "nccl" and world > ndev:
+        # two RCCL ranks cannot share one device; rehearse with --backend gloo
+        raise SystemExit("bench.py: --gpus %d with backend nccl but only %d GPU(s) visible"
+                         % (world, ndev))
     dev = torch.device("cuda", local % ndev)   # % ndev: gloo rehearsals on fewer GPUs
     torch.cuda.set_device(dev)
     if use_dist:
@@ -521,13 +624,34 @@ def main():
         if world == 1 and not args.no_cpu:
             import oracle
             sample = oracle.xorshift(args.cpu_sample_mib << 20, args.seed)
-            threads = args.cpu_threads or cpu_info()["affinity"]
+            info = cpu_info()
+            threads = args.cpu_threads or info["affinity"]
             # the CPU comparator: stock libyara on every CPU of the host this
-            # process may use (SURVEY.md §8d "nproc threads"); the 1-thread
-            # stock scan and the restatement's slice walkers beside it
-            cpu = cpu_stock_threads(args.rules, sample, args.seed, threads)
+            # process may use (SURVEY.md §8d "nproc threads") and at the CPUs
+            # the host actually grants it (min(affinity, ceil(cgroup quota)):
+            # a GPU box's cgroup may grant far fewer than it shows); the faster
+            # of the two is cpu_baseline.  The 1-thread stock scan and the
+            # restatement's slice walkers beside them.
+            granted = threads
+            if not args.cpu_threads and "cgroup_cpus" in info:
+                granted = max(1, min(info["affinity"], int(-(-info["cgroup_cpus"] // 1))))
+            cpu_all = cpu_stock_threads(args.rules, sample, args.seed, threads)
+            cpu_granted = (cpu_stock_threads(args.rules, sample, args.seed, granted)
+                           if granted != threads else None)
+            legs = [c for c in (cpu_all, cpu_granted) if c and "value" in c]
+            cpu = max(legs, key=lambda c: c["value"]) if legs else cpu_all
+            if legs:
+                pick = "granted" if cpu is cpu_granted else "affinity"
+                cpu = dict(cpu)
+                cpu["legs"] = {"affinity": {"threads": threads,
+                                            "GB/s": (cpu_all or {}).get("value")},
+                               "granted": {"threads": granted, "GB/s": (
+                                   cpu_granted or cpu_all or {}).get("value")}}
+                cpu["chosen"] = pick + (" (min(affinity, ceil(cgroup CPU quota)) threads)"
+                                        if pick == "granted" else " (every CPU in the "
+                                        "process's affinity mask)")
             cpu1 = cpu_baseline(args.rules, sample, args.seed)
-            cpu_par = cpu_parallel(args.rules, sample, threads)
+            cpu_par = cpu_parallel(args.rules, sample, granted)
             if cpu is None:
                 cpu, cpu1 = cpu1, None
             del sample

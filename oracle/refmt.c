@@ -63,11 +63,9 @@ static void* worker_main(void* arg) {
 // Returns 0 and fills *gbps (owned bytes scanned per second, decimal GB/s,
 // over the passes every thread completed) and *passes (minimum completed
 // passes over the threads), or a libyara error code / -1.
-int refmt_scan(const char* rules_src, const uint8_t* data, size_t n, int threads, double min_seconds,
-               double* gbps, uint64_t* passes, double* seconds) {
-  if (threads < 1 || n == 0) return -1;
-  int rc = yr_initialize();
-  if (rc != ERROR_SUCCESS) return rc;
+static int scan_initialized(const char* rules_src, const uint8_t* data, size_t n, int threads,
+                            double min_seconds, double* gbps, uint64_t* passes, double* seconds) {
+  int rc;
   YR_COMPILER* comp = NULL;
   YR_RULES* rules = NULL;
   rc = yr_compiler_create(&comp);
@@ -134,5 +132,17 @@ int refmt_scan(const char* rules_src, const uint8_t* data, size_t n, int threads
     *passes = min_p;
     *seconds = dt;
   }
+  return rc;
+}
+
+// yr_initialize / yr_finalize are paired on every call (libyara counts them,
+// libyara.c), so repeated bench legs leave no global state behind.
+int refmt_scan(const char* rules_src, const uint8_t* data, size_t n, int threads, double min_seconds,
+               double* gbps, uint64_t* passes, double* seconds) {
+  if (threads < 1 || n == 0) return -1;
+  int rc = yr_initialize();
+  if (rc != ERROR_SUCCESS) return rc;
+  rc = scan_initialized(rules_src, data, n, threads, min_seconds, gbps, passes, seconds);
+  yr_finalize();
   return rc;
 }

@@ -97,12 +97,21 @@ def _edge_worker(rank, world, port, q):
                     ok &= out.tolist() == want
                 else:
                     ok &= out is None
-        with_bad = torch.tensor([0 if rank else 1 << 40], dtype=torch.int64)
+        # only the last rank's input is bad: every rank must raise, none may be
+        # left waiting in the collective
+        n = 1 << 20
+        bounds = [ydist.shard_bounds(n, world, r, align=16) for r in range(world)]
+        good = 0 if rank == 0 else bounds[rank][0] + 1
+        with_bad = torch.tensor([1 << 40 if rank == world - 1 else good], dtype=torch.int64)
         try:
-            ydist.gather_positions(with_bad, begins=[0] * world, end=1 << 20)
+            ydist.gather_positions(with_bad, begins=[b for b, _ in bounds], end=n)
             ok = False
         except ValueError:
             pass
+        # and the group is still usable afterwards
+        ok &= ydist.gather_positions(torch.tensor([good], dtype=torch.int64),
+                                     begins=[b for b, _ in bounds], end=n,
+                                     dst=0) is not None or rank != 0
         q.put((rank, bool(ok)))
     finally:
         dist.destroy_process_group()

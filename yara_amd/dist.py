@@ -65,11 +65,16 @@ def _gather_backend(group):
     return "gather" if dist.get_backend(group) in ("nccl", "gloo") else "all_gather"
 
 
-def gather_rows(local: torch.Tensor, group=None, dst: int = 0, split: bool = False):
+def gather_rows(local: torch.Tensor, group=None, dst: int = 0, split: bool = False,
+                error: str = None):
     """Gather every rank's int64 rows [m_r, w] to `dst`: all_gather of the
     counts, one padded gather (payloads are KB-MB, far below what the xGMI
     links move per microsecond).  Returns the rank-ordered concatenation on
-    `dst` (with ``split``: the list of every rank's rows), None elsewhere."""
+    `dst` (with ``split``: the list of every rank's rows), None elsewhere.
+
+    ``error``: this rank's input is bad.  The rank still enters the counts
+    all-gather, with a count of -1, so EVERY rank learns of it there and
+    raises ValueError together -- none is left waiting in the payload gather."""
     if local.dim() != 2 or local.dtype not in (torch.int64, torch.int32):
         raise ValueError("rows must be a 2-d int64 or int32 tensor")
     world = dist.get_world_size(group)
@@ -77,10 +82,13 @@ def gather_rows(local: torch.Tensor, group=None, dst: int = 0, split: bool = Fal
     if dist.get_backend(group) == "gloo":
         local = local.cpu()                  # gloo collectives run on host tensors
     w = local.shape[1]
-    n = torch.tensor([local.shape[0]], dtype=torch.int64, device=local.device)
+    n = torch.tensor([-1 if error else local.shape[0]], dtype=torch.int64, device=local.device)
     counts_t = torch.empty(world, dtype=torch.int64, device=local.device)
     dist.all_gather_into_tensor(counts_t, n, group=group)
     counts = counts_t.tolist()               # one host sync for all ranks' counts
+    if min(counts) < 0:
+        bad = [r for r, c in enumerate(counts) if c < 0]
+        raise ValueError(error if error else "rank(s) %s reported bad input to the gather" % bad)
     width = max(max(counts), 1)
     if local.shape[0] == width:
         padded = local.contiguous()
@@ -127,11 +135,13 @@ def gather_positions(local: torch.Tensor, group=None, dst: int = 0, begins=None,
         out = gather_rows(local.reshape(-1, 1).to(torch.int64), group, dst)
         return None if out is None else out.reshape(-1)
     loc = local.to(torch.int64)
+    error = None
     if loc.numel() and (int(loc.min()) < bases[rank] or int(loc.max()) > ends[rank]):
-        raise ValueError("rank %d: positions outside its shard [%d, %d]"
-                         % (rank, bases[rank], ends[rank]))
+        # raised inside gather_rows, on every rank at once (a rank raising
+        # here alone would leave the others waiting in the collective)
+        error = "rank %d: positions outside its shard [%d, %d]" % (rank, bases[rank], ends[rank])
     off = (loc - bases[rank]).to(torch.int32)   # (wraps past 2^31; restored below)
-    rows = gather_rows(off.reshape(-1, 1), group, dst, split=True)
+    rows = gather_rows(off.reshape(-1, 1), group, dst, split=True, error=error)
     if rows is None:
         return None
     return torch.cat([(part.reshape(-1).to(torch.int64) & 0xFFFFFFFF) + bases[r]
