@@ -15,12 +15,17 @@ restatement of the device's decisions (oracle.literal_effect: the records
 yr_amd_verify_device returns, pinned by tests/test_preverify.py).  The stock
 yr_rules_scan_mem of the same block is timed beside it.
 
-    python tools/replay_profile.py [--sets short,fuzz3] [--mib 1024] > profiles/r05_replay_profile.json
+    python tools/replay_profile.py [--sets short,fuzz3] [--mib 1024] [--reps 7] > profiles/r06_replay_profile.json
+
+Each mode runs once per repetition, the modes interleaved in a rotating order;
+the tool reports medians with their spread and exits non-zero if a part (the
+libyara calls alone, the shim's own work alone) measures longer than the whole.
 """
 import argparse
 import ctypes
 import json
 import os
+import statistics
 import subprocess
 import sys
 import tempfile
@@ -40,7 +45,7 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--sets", default="short,fuzz3")
     ap.add_argument("--mib", type=int, default=1024)
-    ap.add_argument("--reps", type=int, default=3)
+    ap.add_argument("--reps", type=int, default=7)
     a = ap.parse_args()
     import gen_rules
     import oracle
@@ -58,6 +63,7 @@ def main():
             return fuzz_rules.gen(int(name[4:]))
         p = os.path.join(REPO, "tests", "golden", "rules", name + ".yar")
         return open(p).read() if os.path.exists(p) else gen_rules.gen(name)
+    bad = []
     for name in a.sets.split(","):
         src = text(name)
         with tempfile.TemporaryDirectory() as td:
@@ -90,28 +96,53 @@ def main():
                                                ctypes.c_size_t, ctypes.c_int, ctypes.c_uint64,
                                                ctypes.POINTER(ctypes.c_double)]
         res = {"records": int(len(recs)), "stock_verify_calls": int(len(v))}
-        for label, mode, tmo in (("shim", 0, 0), ("shim_timeout", 0, 10 ** 15), ("shim_only", 1, 0),
-                                 ("shim_only_timeout", 1, 10 ** 15), ("libyara", 2, 0)):
-            best = None
-            for _ in range(a.reps):
+        modes = (("shim", 0, 0), ("shim_timeout", 0, 10 ** 15), ("shim_only", 1, 0),
+                 ("shim_only_timeout", 1, 10 ** 15), ("libyara", 2, 0))
+        times = {label: [] for label, _, _ in modes}
+        # the modes interleaved, the order rotated every repetition (one pass
+        # of each per repetition), so that a slow stretch of a shared host or a
+        # cache warmed by the previous mode lands on every mode alike
+        for r in range(a.reps):
+            for q in range(len(modes)):
+                label, mode, tmo = modes[(q + r) % len(modes)]
                 sec = ctypes.c_double()
                 rc = shim.yr_gpu_replay_profile(scanner, recs.ctypes.data, len(recs), data.ctypes.data, n,
                                                 mode, tmo, ctypes.byref(sec))
                 assert rc == 0, (label, rc)
-                best = sec.value if best is None else min(best, sec.value)
-            res[label + "_s"] = round(best, 4)
-            res[label + "_ns_per_record"] = round(best / max(len(recs), 1) * 1e9, 1)
+                times[label].append(sec.value)
+        for label, _, _ in modes:
+            t = sorted(times[label])
+            med = statistics.median(t)
+            res[label + "_s"] = {"median": round(med, 4), "min": round(t[0], 4), "max": round(t[-1], 4),
+                                 "spread": round((t[-1] - t[0]) / med, 3)}
+            res[label + "_ns_per_record"] = round(med / max(len(recs), 1) * 1e9, 1)
+        # shares: medians of the per-repetition ratios (each repetition's parts
+        # against the same repetition's whole) and their range
+        for part, whole in (("libyara", "shim"), ("shim_only", "shim")):
+            q = sorted(x / y for x, y in zip(times[part], times[whole]))
+            res["share_%s_of_%s" % (part, whole)] = {"median": round(statistics.median(q), 4),
+                                                    "min": round(q[0], 4), "max": round(q[-1], 4)}
         ref.yr_rules_scan_mem.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_size_t, ctypes.c_int, CB,
                                           ctypes.c_void_p, ctypes.c_int]
         t0 = time.perf_counter()
         assert ref.yr_rules_scan_mem(rules, data.ctypes.data, n, 0, cb, None, 0) == 0
         res["stock_scan_s"] = round(time.perf_counter() - t0, 3)
-        res["share_inside_libyara"] = round(res["libyara_s"] / res["shim_s"], 4)
+        res["share_inside_libyara"] = res["share_libyara_of_shim"]["median"]
+        # a part cannot take longer than the whole it is part of: a median share
+        # above 1 means the measurement is noise, not a profile
+        if res["share_inside_libyara"] > 1.0 or res["share_shim_only_of_shim"]["median"] > 1.0:
+            bad.append(name)
         out["sets"][name] = res
         print(name, res, file=sys.stderr, flush=True)
         ref.yr_scanner_destroy(scanner)
         ref.yr_rules_destroy(rules)
+    out["reps"] = a.reps
+    out["method"] = ("each mode once per repetition, interleaved, order rotated per repetition; "
+                     "medians, min/max and spread = (max - min) / median over the repetitions; "
+                     "shares = medians of per-repetition ratios")
     print(json.dumps(out, indent=1))
+    if bad:
+        sys.exit("replay_profile: a part measured longer than the whole for %s" % ",".join(bad))
 
 
 if __name__ == "__main__":
