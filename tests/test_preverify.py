@@ -393,3 +393,34 @@ def test_verified_only_scan_keeps_records_and_candidate_indices(rules, case):
             np.testing.assert_array_equal(got[f], full[f], err_msg="%s [%d, %d)" % (f, lo, hi))
         if rules in ("rx", "fuzz0") and case == "xs64M":   # dense candidates, most of them dead
             assert cnt < cnt_full // 2, (cnt, cnt_full)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("rules", ["rx", "fuzz0", "short", "fuzz3"])
+def test_verified_only_first_scan_of_a_fresh_scanner(rules):
+    """A verified-only scan as a FRESH scanner's first scan: its
+    segments still have the default capacity, so the dense key runs overflow
+    them and the scan is re-run at exact offsets under the verified-only
+    instance (the dropped candidates' full-stream counts, the candidate index
+    rebuilt; with kept keys, the segment write pass over the re-run's
+    layout).  Records and candidate indices equal a separate full-scan
+    scanner's."""
+    import torch
+    import yara_amd
+    data = _dense_key_buffer(rules if rules != "fuzz3" else "short")
+    n = len(data)
+    d = torch.from_numpy(data.copy()).cuda()
+    tab = yara_amd.Tables.from_npz(tables_npz(rules), device=0, strings=True)
+    vo = yara_amd.Scanner(tab)
+    vo.set_verified_only(True)
+    got, cnt, length = _device_records(vo, d, n)
+    full, cnt_full, len_full = _device_records(yara_amd.Scanner(tab), d, n)
+    assert length == cnt_full == len_full and cnt <= cnt_full
+    for f in ("offset", "pool_index", "candidate"):
+        np.testing.assert_array_equal(got[f], full[f], err_msg=f)
+    # and again on the same (now learned-capacity) scanner, over a byte range
+    cut = (n // 3) & ~15
+    got2, _, _ = _device_records(vo, d, n, cut, n)
+    full2, _, _ = _device_records(yara_amd.Scanner(tab), d, n, cut, n)
+    for f in ("offset", "pool_index", "candidate"):
+        np.testing.assert_array_equal(got2[f], full2[f], err_msg=f)

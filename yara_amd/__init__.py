@@ -278,7 +278,12 @@ class Scanner:
                                                  window_end, block_size, byte_begin, byte_end))
 
     def device_result(self):
-        """(device pointer to uint64 positions, count, all_positions)."""
+        """(device pointer to uint64 positions, count, all_positions) --
+        yr_amd_scan_device_result.  The positions are complete in the
+        scanner's stream order: a reader on another stream (or the host) must
+        synchronise that stream first.  On a verified-only scanner
+        (set_verified_only) the call returns before the compaction has written
+        them: such a scan serves verify_device, which queues behind them."""
         p = ctypes.c_void_p()
         cnt = ctypes.c_uint64()
         allp = ctypes.c_int()

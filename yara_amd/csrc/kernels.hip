@@ -190,7 +190,9 @@ struct WaveQueue {
                     // stream flushed so far (verified-only scans leave the dead out)
   uint32_t dacc;    // wave-uniform (kDrainClass): the drains' dead not yet in `full`
   uint32_t kcv;     // per lane (byte-key kernels): the key class records (scan_key_rec)
-  bool defer;       // wave-uniform: the per-lane hits below await their words
+  uint32_t defer;   // wave-uniform: kDeferKey while the per-lane hits below await their
+                    // words, else 0 (a count above the ring's capacity: ring_append
+                    // tests "ring full or a drain to complete" with one scalar compare)
   uint32_t facc;    // per lane (byte-key kernels, kBkSkipF): OR of the stage-1 filter
                     // and 2-byte-key tests of the tiles queued since the last drain
   // per lane, the first (a) and second (b) deferred hit: window, segment
@@ -209,6 +211,7 @@ __device__ __forceinline__ uint32_t uniform_count(uint32_t n) {
 }
 
 constexpr uint32_t kNoHit = 0xFFFFFFFFu;
+constexpr uint32_t kDeferKey = 256u;   // WaveQueue::defer (> kQueueCap + kWave)
 // Kernel variant: the product kernel for rule sets whose 1-byte keys are tested
 // byte by byte in stage 1 (byte_keys_any below) instead of in the filter.
 constexpr int kModeByteKeys = 20;
@@ -272,6 +275,10 @@ constexpr int kStage1Mode = !(kByteKeys<MODE> || MODE == 24 || MODE == 25) ? kBa
 // not even detected.  Both on a 1-byte-key rule set; output wrong by construction.
 template <int MODE>
 constexpr bool kByteKeyAblation = MODE == 24 || MODE == 25;
+// The ring entry's index word holds the lane's byte offset in the segment
+// (else its 16-byte unit index, with the next lane's first two bytes on top)
+template <int MODE>
+constexpr bool kIdxBytes = !kNextBytes<MODE>;
 // A pending entry's offset with this bit set is a certain candidate (its last
 // byte is a 1-byte key): no bucket probe.  (Segment offsets are < 2^20.)
 // a pending entry becomes the output entry: certain iff its key place is set
@@ -978,7 +985,7 @@ __device__ __forceinline__ void drain_complete(const ScanParams& p, WaveQueue& q
                                                uint64_t seg_start, uint32_t* out, uint32_t& found) {
   const bool ha = q.oa != kNoHit && first_level_test(q.da, q.wa);
   const bool hb = q.ob != kNoHit && first_level_test(q.db, q.wb);
-  q.defer = false;
+  q.defer = 0u;
   q.ia = q.ib = 0u;
   // each lane's a-hit precedes its b-hit: lane L's first slot is the number of
   // a- and b-hits in the lanes below it (two ballots and their mbcnts instead
@@ -1044,7 +1051,7 @@ __device__ __forceinline__ void drain(const ScanParams& p, WaveQueue& q, uint32_
     S[3] = e23.y;
     S[4] = e45.x;
     eidx = e45.y;
-    off0 = (eidx & 0xFFFFu) * kBytesPerLane;
+    off0 = kIdxBytes<MODE> ? eidx : (eidx & 0xFFFFu) * kBytesPerLane;
     if (need_f) {
       if constexpr (kEven<MODE>) {
         m = even_mask<kEvenHash<MODE>>(S);
@@ -1101,7 +1108,7 @@ __device__ __forceinline__ void drain(const ScanParams& p, WaveQueue& q, uint32_
           q.ib = fl_word(q.wb) * 4u;
         }
       }
-      q.defer = true;
+      q.defer = kDeferKey;
       return;
     }
   }
@@ -1412,9 +1419,10 @@ __device__ __forceinline__ uint32_t stage1(const uint32_t (&S)[6], uint32_t lane
 }
 
 // One ring entry: the 16-byte unit's bytes S[1..4] (as loaded: no register
-// moves), the 4 bytes before them S[0], and the unit's index in the segment
-// (offset / 16; byte-key kernels: the next unit's first two bytes in the top
-// half).
+// moves), the 4 bytes before them S[0], and the unit's place in the segment:
+// its byte offset (kIdxBytes: one VOP2 from the tile offset in an SGPR and the
+// lane's loop-invariant offset), or, for the kernels that keep the next lane's
+// first two bytes in the top half (kNextBytes), its index (offset / 16).
 template <int MODE>
 __device__ __forceinline__ void write_entry(uint32_t ent, const uint32_t (&S)[6], uint32_t unit) {
   const uint32_t idx = unit | (kNextBytes<MODE> ? S[5] << 16 : 0u);
@@ -1433,6 +1441,13 @@ __device__ __forceinline__ void write_entry(uint32_t ent, const uint32_t (&S)[6]
 
 // The ordered append of a tile's hits to the wave ring.  TAIL: the segment's
 // last, partial tile (positions past seg_len are masked off).
+// The common path (~98 % of config C's tiles: some lane passes, the ring has
+// room, no deferred drain to complete) is straight-line scalar code: ONE
+// compare covers both rare paths (q.defer is kDeferKey, above any count, while
+// a deferred drain awaits its words), and a tile without a passing lane takes
+// it too -- its masked-off writes cost less than a branch around them
+// (tools/stage2_cost.sh: a SALU or branch instruction per tile costs config C
+// 2.5 us per 4 GiB, a VOP2 4.5 us).
 template <int MODE, bool TAIL>
 __device__ __forceinline__ void ring_append(const ScanParams& p, WaveQueue& q, SegState& st,
                                             const uint32_t (&S)[6], uint32_t any,
@@ -1443,31 +1458,37 @@ __device__ __forceinline__ void ring_append(const ScanParams& p, WaveQueue& q, S
     if (lane_off >= st.seg_len) any = 0u;   // lanes wholly past the segment end
   }
   const uint64_t lanes = __ballot(any != 0);
-  if (YAMD_EXPECT(lanes != 0, 1)) {   // (~98 % of config C's tiles)
-    const uint32_t n = (uint32_t)__popcll(lanes);
-    if (YAMD_EXPECT(q.count + n > kQueueCap, 0)) {
-      __builtin_amdgcn_s_setprio(0);   // (streaming waves first)
+  const uint32_t n = (uint32_t)__popcll(lanes);
+  if (YAMD_EXPECT(q.count + n + q.defer > kQueueCap, 0)) {
+    __builtin_amdgcn_s_setprio(0);   // (streaming waves first)
+    // (drain completes a deferred drain first; a deferred drain alone, its
+    // words loaded by the previous tile step, is completed here)
+    if (q.count + n > kQueueCap) {
       drain<MODE, true>(p, q, lane, st.seg_start, st.seg_len, st.out, st.found);
-      __builtin_amdgcn_s_setprio(1);
+    } else if constexpr (kDeferFl<MODE>) {
+      drain_complete<MODE>(p, q, lane, st.seg_start, st.out, st.found);
     }
-    if (any != 0) {
-      // slot = count (scalar, folded into the base) + the appending lanes below
-      const uint32_t below = __builtin_amdgcn_mbcnt_hi(
-          (uint32_t)(lanes >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)lanes, 0u));
-      static_assert(kQueueEntryWords * 4 == 24, "entry size is the asm's inline constant");
-      const uint32_t base = q.ring + q.count * (kQueueEntryWords * 4);   // scalar
-      uint32_t ent;   // (asm: the compiler would re-associate into a 64-bit mad)
-      asm("v_mad_u32_u24 %0, %1, 24, %2" : "=v"(ent) : "v"(below), "s"(base));
-      // 24-byte entry: the lane's 16 bytes (as loaded: no register moves),
-      // the 4 bytes before them, the lane index in the segment
-      if constexpr (MODE == 8) {   // ablation: the append's slot arithmetic, no LDS writes
-        asm volatile("" ::"v"(ent), "v"((tile_off >> 4) + lane));
-      } else {
-        write_entry<MODE>(ent, S, (tile_off >> 4) + lane);
-      }
-    }
-    q.count += n;
+    __builtin_amdgcn_s_setprio(1);
   }
+  if (any != 0) {
+    // slot = count (scalar, folded into the base) + the appending lanes below
+    // (gfx950's VOP3 reads one SGPR: count as the mbcnt's addend would cost a
+    // v_mov instead of the two SALU of the base)
+    const uint32_t below = __builtin_amdgcn_mbcnt_hi(
+        (uint32_t)(lanes >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)lanes, 0u));
+    static_assert(kQueueEntryWords * 4 == 24, "entry size is the asm's inline constant");
+    const uint32_t base = q.ring + q.count * (kQueueEntryWords * 4);   // scalar
+    uint32_t ent;   // (asm: the compiler would re-associate into a 64-bit mad)
+    asm("v_mad_u32_u24 %0, %1, 24, %2" : "=v"(ent) : "v"(below), "s"(base));
+    // 24-byte entry: the lane's 16 bytes (as loaded: no register moves),
+    // the 4 bytes before them, the lane's place in the segment
+    if constexpr (MODE == 8) {   // ablation: the append's slot arithmetic, no LDS writes
+      asm volatile("" ::"v"(ent), "v"(lane_off));
+    } else {
+      write_entry<MODE>(ent, S, kIdxBytes<MODE> ? lane_off : (tile_off >> 4) + lane);
+    }
+  }
+  q.count += n;
 }
 
 // The lane's window context: the previous lane's last dword (lane 0: the
@@ -1532,15 +1553,43 @@ __device__ __forceinline__ void tile_step(const ScanParams& p, WaveQueue& q, Seg
     else if constexpr (kAbl<MODE> != 4) any |= byte_keys_any(S, p);
   }
   if constexpr (MODE == 24) asm volatile("" ::"v"(byte_keys_any(S, p)));
-  if constexpr (kDeferFl<MODE>)
-    if (YAMD_EXPECT(q.defer, 0)) {   // (~1 tile in 16)
-      __builtin_amdgcn_s_setprio(0);
-      drain_complete<MODE>(p, q, lane, st.seg_start, st.out, st.found);
-      __builtin_amdgcn_s_setprio(1);
-    }
+#if defined(YAMD_PAD_VOP2) || defined(YAMD_PAD_VOP3) || defined(YAMD_PAD_SALU) || defined(YAMD_PAD_NOP)
+  // cost model (tools/stage2_cost.sh, variant builds only): N extra instructions
+  // of one issue class per tile step of the product kernel, on four independent
+  // dummy chains -- the marginal cost of one instruction of that class per tile
+  if constexpr (MODE == 0) {
+    uint32_t t0 = S[1], t1 = S[2], t2 = S[3], t3 = S[4];
+#ifdef YAMD_PAD_VOP2
+#pragma unroll
+    for (int i = 0; i < YAMD_PAD_VOP2; i += 4)
+      asm volatile("v_add_u32_e32 %0, 1, %0\n v_add_u32_e32 %1, 1, %1\n v_add_u32_e32 %2, 1, %2\n v_add_u32_e32 %3, 1, %3"
+                   : "+v"(t0), "+v"(t1), "+v"(t2), "+v"(t3));
+#endif
+#ifdef YAMD_PAD_VOP3
+#pragma unroll
+    for (int i = 0; i < YAMD_PAD_VOP3; i += 4)
+      asm volatile("v_add3_u32 %0, %0, 1, 2\n v_add3_u32 %1, %1, 1, 2\n v_add3_u32 %2, %2, 1, 2\n v_add3_u32 %3, %3, 1, 2"
+                   : "+v"(t0), "+v"(t1), "+v"(t2), "+v"(t3));
+#endif
+#ifdef YAMD_PAD_NOP
+#pragma unroll
+    for (int i = 0; i < YAMD_PAD_NOP; ++i) asm volatile("s_nop 0");
+#endif
+    asm volatile("" ::"v"(t0 ^ t1 ^ t2 ^ t3));
+#ifdef YAMD_PAD_SALU
+    uint32_t u0 = tile_off, u1 = tile_off + 1, u2 = tile_off + 2, u3 = tile_off + 3;
+#pragma unroll
+    for (int i = 0; i < YAMD_PAD_SALU; i += 4)
+      asm volatile("s_add_u32 %0, %0, 1\n s_add_u32 %1, %1, 1\n s_add_u32 %2, %2, 1\n s_add_u32 %3, %3, 1"
+                   : "+s"(u0), "+s"(u1), "+s"(u2), "+s"(u3) : : "scc");
+    asm volatile("" ::"s"(u0 ^ u1 ^ u2 ^ u3));
+#endif
+  }
+#endif
   if constexpr (kAbl<MODE> == 1) {   // ablation: stage 1 only
     asm volatile("" ::"v"(any));
   } else {
+    // (a deferred drain is completed inside, on the append's rare path)
     ring_append<MODE, TAIL>(p, q, st, S, any, tile_off, lane);
   }
   // (after the append: a drain inside it takes only the earlier tiles' entries)
@@ -1588,7 +1637,7 @@ __device__ __forceinline__ void scan_segment(const ScanParams& p, WaveQueue& q, 
   q.pend_n = 0;
   q.full = 0;
   q.dacc = 0;
-  q.defer = false;
+  q.defer = 0u;
   q.facc = 0u;
   q.ia = q.ib = 0u;
   q.da = q.db = 0u;
@@ -1597,7 +1646,7 @@ __device__ __forceinline__ void scan_segment(const ScanParams& p, WaveQueue& q, 
 
   const uint32_t n_full = st.seg_len / kTile;            // tiles needing no mask / bounds
   if (n_full > 0) {
-    const uint32_t last = (n_full - 1) * kTile;
+    const uint32_t full_end = n_full * kTile;
     const __amdgpu_buffer_rsrc_t rsrc = segment_rsrc(base);
     const uint32_t lane16 = lane * kBytesPerLane;
     uint4 a = load_tile_full(rsrc, 0, lane16), b;
@@ -1605,15 +1654,28 @@ __device__ __forceinline__ void scan_segment(const ScanParams& p, WaveQueue& q, 
     // a load pending on a (the loop's wait for its input tile would
     // otherwise cover the deferred first-level loads too)
     asm volatile("" : "+v"(a.x), "+v"(a.y), "+v"(a.z), "+v"(a.w));
-    uint32_t i = 0;
-    // the last step's prefetch re-reads the last tile rather than branch
-    for (; i + 2 <= n_full; i += 2) {
-      b = load_tile_full(rsrc, (i + 1) * kTile, lane16);
-      tile_step<MODE, false>(p, q, st, a, i * kTile, lane);
-      a = load_tile_full(rsrc, min((i + 2) * kTile, last), lane16);
-      tile_step<MODE, false>(p, q, st, b, (i + 1) * kTile, lane);
+    // the loop runs on the tile's byte offset (the loads' SGPR offset; the
+    // second tile's + 1 KiB folds into the instruction's offset field) and
+    // only while its prefetch stays inside the full tiles: no clamp per step,
+    // the last one or two tiles after it
+    uint32_t off = 0;
+    if (full_end > 2 * kTile) {
+      const uint32_t lim = full_end - 2 * kTile;   // (a bottom-tested loop: one compare per pair)
+      do {
+        b = load_tile_full(rsrc, off + kTile, lane16);
+        tile_step<MODE, false>(p, q, st, a, off, lane);
+        a = load_tile_full(rsrc, off + 2 * kTile, lane16);
+        tile_step<MODE, false>(p, q, st, b, off + kTile, lane);
+        off += 2 * kTile;
+      } while (off < lim);
     }
-    if (i < n_full) tile_step<MODE, false>(p, q, st, a, i * kTile, lane);
+    if (off + kTile < full_end) {
+      b = load_tile_full(rsrc, off + kTile, lane16);
+      tile_step<MODE, false>(p, q, st, a, off, lane);
+      tile_step<MODE, false>(p, q, st, b, off + kTile, lane);
+    } else {
+      tile_step<MODE, false>(p, q, st, a, off, lane);
+    }
   }
   if (st.seg_len % kTile != 0)   // the ragged tail tile
     tile_step<MODE, true>(p, q, st, load_tile(base, n_full * kTile, lane, avail), n_full * kTile,
