@@ -133,6 +133,20 @@ def spawn_ranks(args) -> int:
         for p in procs:
             p.wait()
         return 1
+    # a launcher that stops us (timeout, Ctrl-C) stops the ranks too: no rank
+    # is left holding a GPU
+    def forward(signum, _frame):
+        for p in procs:
+            if p.poll() is None:
+                p.send_signal(signal.SIGTERM)
+        for p in procs:
+            try:
+                p.wait(timeout=30)
+            except subprocess.TimeoutExpired:
+                p.kill()
+        sys.exit(128 + signum)
+    signal.signal(signal.SIGTERM, forward)
+    signal.signal(signal.SIGINT, forward)
     worst = 0
     live = list(procs)
     term_at = None

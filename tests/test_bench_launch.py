@@ -66,6 +66,24 @@ def test_failing_rank_ends_the_others_and_sets_exit_code():
     assert time.monotonic() - t0 < 60
 
 
+def test_terminating_the_launcher_ends_its_ranks():
+    # --rank-probe-fail 9 names no rank: all three ranks sleep (standing for
+    # ranks at work), so all are alive when the launcher is stopped
+    import signal
+    p = subprocess.Popen([sys.executable, BENCH, "--gpus", "3", "--rank-probe", "--rank-probe-fail", "9"],
+                         stdout=subprocess.PIPE, stderr=subprocess.PIPE, text=True, env=_env())
+    seen = 0
+    while seen < 3:   # every rank has printed its environment: all started
+        line = p.stdout.readline()
+        assert line, p.stderr.read()
+        seen += 1
+    t0 = time.monotonic()
+    p.send_signal(signal.SIGTERM)
+    rc = p.wait(timeout=60)
+    assert rc == 128 + signal.SIGTERM
+    assert time.monotonic() - t0 < 40
+
+
 def test_world_size_mismatch_is_an_error():
     env = _env()
     env.update({"WORLD_SIZE": "2", "RANK": "0", "LOCAL_RANK": "0"})
