@@ -83,9 +83,12 @@ def test_multi_block_iterator(case):
 
 @pytest.mark.parametrize("rules", ["B", "C", "E", "short"])
 @pytest.mark.parametrize("size", [0, 1, 2, 3, 4, 5, 15, 16, 17, 100, 1023, 1024, 1025,
-                                  4095, 4097, 65535, 65536, 65537, 262144 + 7, 3_000_001])
+                                  2047, 2048, 2049, 3071, 3072, 3073,
+                                  4095, 4097, 5121, 65535, 65536, 65537, 262144 + 7, 3_000_001])
 def test_ragged_sizes_vs_oracle(rules, size):
-    """Empty and ragged blocks, tile/segment edges, tails not multiple of 16."""
+    """Empty and ragged blocks, tile/segment edges, tails not multiple of 16
+    (2047 .. 3073: segments of 1, 2 and 3 full tiles with and without a tail --
+    the tile loop's peeled last one or two tiles)."""
     if rules == "short":
         x = oracle.xorshift(size, 17)
         data = np.frombuffer(b"abcdxyzHeloC\x00\x01\xff", np.uint8)[x % 15]
