@@ -316,26 +316,45 @@ static pthread_mutex_t _sig_mu = PTHREAD_MUTEX_INITIALIZER;
 static int _sig_users = 0;
 static struct sigaction _sig_old_bus, _sig_old_segv;
 
+static void _sig_install(struct sigaction* old_bus, struct sigaction* old_segv)
+{
+  struct sigaction act;
+  memset(&act, 0, sizeof(act));
+  act.sa_handler = exception_handler;
+  act.sa_flags = 0;
+  sigfillset(&act.sa_mask);
+  sigaction(SIGBUS, &act, old_bus);
+  sigaction(SIGSEGV, &act, old_segv);
+}
+
+static int _sig_is_ours(void)
+{
+  struct sigaction bus, segv;
+  sigaction(SIGBUS, NULL, &bus);
+  sigaction(SIGSEGV, NULL, &segv);
+  return bus.sa_handler == exception_handler && segv.sa_handler == exception_handler;
+}
+
 static void _sig_enter(void)
 {
   pthread_mutex_lock(&_sig_mu);
   if (_sig_users++ == 0)
-  {
-    struct sigaction act;
-    memset(&act, 0, sizeof(act));
-    act.sa_handler = exception_handler;
-    act.sa_flags = 0;
-    sigfillset(&act.sa_mask);
-    sigaction(SIGBUS, &act, &_sig_old_bus);
-    sigaction(SIGSEGV, &act, &_sig_old_segv);
-  }
+    _sig_install(&_sig_old_bus, &_sig_old_segv);
+  else if (!_sig_is_ours())
+    /* a stock YR_TRYCATCH on another thread ended meanwhile and restored
+     * what it had saved: install ours again for this copy (the saved actions
+     * stay those found by the first copy in) */
+    _sig_install(NULL, NULL);
   pthread_mutex_unlock(&_sig_mu);
 }
 
 static void _sig_leave(void)
 {
   pthread_mutex_lock(&_sig_mu);
-  if (--_sig_users == 0)
+  /* the last copy out restores what the first one found -- unless the
+   * handler is no longer ours: then the application (or another YR_TRYCATCH)
+   * installed its own meanwhile, and that one stays */
+  if (--_sig_users == 0 && _sig_is_ours())
   {
     sigaction(SIGBUS, &_sig_old_bus, NULL);
     sigaction(SIGSEGV, &_sig_old_segv, NULL);

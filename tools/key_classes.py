@@ -3,15 +3,16 @@ of golden tables, decoded (diagnostic build's yr_amd__diag_key_classes).
 GPU box:  python tools/key_classes.py rx fuzz0 ...
 """
 import ctypes, json, os, sys
-sys.path.insert(0, os.getcwd())
-os.environ["YARA_AMD_LIB"] = os.path.join(os.getcwd(), "yara_amd/_diag/libyara_amd.so")
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, REPO)
+os.environ["YARA_AMD_LIB"] = os.path.join(REPO, "yara_amd", "_diag", "libyara_amd.so")
 import yara_amd
 L = yara_amd._lib.lib()
 g = L.yr_amd__diag_key_classes
 g.argtypes = [ctypes.c_void_p, ctypes.POINTER(ctypes.c_uint32)]
 s8 = lambda x: x - 256 if x >= 128 else x
 for name in sys.argv[1:]:
-    t = yara_amd.Tables.from_npz(os.path.join("tests/golden/tables", name + ".npz"), device=0, strings=True)
+    t = yara_amd.Tables.from_npz(os.path.join(REPO, "tests", "golden", "tables", name + ".npz"), device=0, strings=True)
     o = (ctypes.c_uint32 * 40)()
     g(t._h, o)
     keys = []

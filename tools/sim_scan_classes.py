@@ -5,9 +5,10 @@ against the oracle's kept calls (a dead class on a kept call is a bug).
     python tools/sim_scan_classes.py <rules> <case|xs>
 """
 import sys, ctypes, numpy as np
-sys.path[:0]=['/root/repo','/root/repo/tests','/root/repo/tests/golden']
 import os
-os.environ['YARA_AMD_LIB']='/root/repo/yara_amd/_diag/libyara_amd.so'
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path[:0]=[REPO, os.path.join(REPO, 'tests'), os.path.join(REPO, 'tests', 'golden')]
+os.environ['YARA_AMD_LIB']=os.path.join(REPO, 'yara_amd', '_diag', 'libyara_amd.so')
 import yara_amd, oracle
 from conftest import tables_npz, case_data, golden, ref_tables
 L=yara_amd._lib.lib()
