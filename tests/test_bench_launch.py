@@ -93,16 +93,29 @@ def test_world_size_mismatch_is_an_error():
 
 
 @pytest.mark.gpu
-def test_bench_two_ranks_without_launcher_on_one_gpu():
+@pytest.mark.parametrize("world", [2, 3])
+def test_bench_ranks_without_launcher_on_one_gpu(world):
     # gloo: two RCCL ranks cannot share the box's one device
-    r = _run(["--gpus", "2", "--backend", "gloo", "--steps", "2", "--warmup", "1",
+    r = _run(["--gpus", str(world), "--backend", "gloo", "--steps", "2", "--warmup", "1",
               "--no-cpu", "--no-other"], timeout=600)
     assert r.returncode == 0, r.stderr[-4000:]
     lines = [s for s in r.stdout.splitlines() if s.startswith("{")]
     assert len(lines) == 1, r.stdout[-4000:]
     line = json.loads(lines[0])
-    assert line["n_gpus"] == 2
-    assert line["config"]["parallelism"] == "shard2"
+    assert line["n_gpus"] == world
+    assert line["config"]["parallelism"] == "shard%d" % world
+    # every rank's 4 GiB shard against its stock golden (tests/golden/config_d.json)
     assert line["check"]["match_golden"] is True, line["check"]
     assert line["check"]["ascending"] is True
-    assert line["multi"]["per_rank_step_ms"]["by_rank"].__len__() == 2
+    assert len(line["multi"]["per_rank_step_ms"]["by_rank"]) == world
+
+
+@pytest.mark.gpu
+def test_bench_nccl_ranks_beyond_the_visible_gpus_fail():
+    # two RCCL ranks on a one-GPU box: a non-zero exit, never a 1-GPU line
+    import torch
+    if torch.cuda.device_count() >= 2:
+        pytest.skip("more than one GPU visible")
+    r = _run(["--gpus", "2", "--steps", "1", "--warmup", "1", "--no-cpu", "--no-other"], timeout=300)
+    assert r.returncode != 0
+    assert not [s for s in r.stdout.splitlines() if s.startswith("{")], r.stdout[-2000:]
