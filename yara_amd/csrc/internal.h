@@ -185,6 +185,10 @@ constexpr uint32_t kClassKept = 2u;
 constexpr uint32_t kClassFetch = 0xFFu;   // (verified-only scans) undecided from the scan's
                                           // eight bytes: the compaction reads the input
 constexpr uint32_t kOutPlaceScanClass = 7u;   // key place of an entry carrying its class
+// ScanParams::kc: 32 words of key class records (8 per key), then the plan of
+// the one-plan drop instance (scanner.cpp key_plan): info, forward tests m / v
+constexpr uint32_t kKcPlan = 32;
+constexpr uint32_t kKcWords = 36;
 
 struct ScanParams {
   const uint8_t* data;      // block base in HBM (16-byte aligned)
@@ -260,6 +264,14 @@ struct ScanParams {
   uint32_t* seg_full;
   uint64_t* seg_full_offset;   // [n_segments + 1], written by the offsets kernel
   uint32_t* cand_index;
+  // The one-plan drop instance (kernels.hip kDropPlanModes; scanner.cpp
+  // key_plan): every 1-byte key's class is the same forward guard once the
+  // test of the key byte itself is left out (rx: both keys test the byte after
+  // them against 0xC3), so the drain decides all certain candidates of an
+  // entry at once, in straight-line code -- not per key from the records.  The
+  // plan's words follow the records in kc (kKcPlan..): read by scalar loads in
+  // each drain, so they hold no SGPRs across the tile loop.
+  uint32_t kp_on;
 };
 
 }  // namespace yamd

@@ -246,7 +246,14 @@ constexpr bool kDrop = MODE >= kDropModes;
 // inlined at every drain site, costs the other tables' drop kernels ~4 %
 constexpr int kDropBgModes = 2000;
 template <int MODE>
-constexpr bool kDropBg = MODE >= kDropBgModes;
+constexpr bool kDropBg = MODE >= kDropBgModes && MODE < 3000;
+// MODE + kDropPlanModes: the drop instance for tables whose keys all share one
+// forward guard (ScanParams::kp_on, scanner.cpp key_plan): the drain's classes
+// in straight-line code (rx's drop kernel 0.94 -> 0.87 ms, gpurun r06q; with
+// the plan's parameters as compile-time constants 0.81, r06x)
+constexpr int kDropPlanModes = 3000;
+template <int MODE>
+constexpr bool kDropPlan = MODE >= kDropPlanModes;
 template <int MODE>
 constexpr int kBase = MODE % kDropModes >= 100 ? MODE % 100 : MODE % kDropModes;
 template <int MODE>
@@ -802,6 +809,35 @@ __device__ __forceinline__ DrainClasses drain_classes(const ScanParams& p, uint3
   const bool nx = kNextBytes<MODE> && (eidx & (kWave - 1)) != kWave - 1;
   const uint32_t E[6] = {S[0], S[1], S[2], S[3], S[4], nx ? eidx >> 16 : 0u};
   const int32_t last = nx ? 17 : 15;   // last lane byte held
+  if constexpr (kDropPlan<MODE>) {
+    // one forward guard for every key (scanner.cpp key_plan): the loop below
+    // for all of m at once, its parameters from two scalar loads (kc[kKcPlan..],
+    // a wave-uniform address) instead of lane reads of the records, no per-key
+    // split of m, no test-reuse branch
+    (void)first;
+    (void)kcv;
+    const uint4 w = *reinterpret_cast<const uint4*>(p.kc + kKcPlan);
+    const uint32_t info = w.x, pm = w.y, pv = w.z;
+    const int32_t rs = (int32_t)(int8_t)(info >> 8);
+    const uint32_t span = (info >> 16) & 15u, tmax = (info >> 20) & 3u;
+    const int64_t endo = (int8_t)(info >> 24);
+    uint32_t A = ~0u;
+#pragma unroll
+    for (uint32_t t = 0; t < 4; ++t) {
+      const uint32_t mt = (pm >> (8 * t)) & 0xFFu, vt = (pv >> (8 * t)) & 0xFFu;
+      if (t <= tmax && mt != 0u) A &= byte_test24(E, mt, vt) >> (uint32_t)(rs + (int32_t)t + 4);
+    }
+    uint32_t fp = A;
+#pragma unroll 1
+    for (uint32_t jj = 1; jj <= span; ++jj) fp |= A >> jj;
+    const int32_t lim = last - (rs + (int32_t)(span + tmax));
+    const uint32_t avail = lim < 0 ? 0u : lim >= 15 ? 0xFFFFu : (2u << lim) - 1u;
+    const uint32_t rng = (int64_t)pos0 + 16 + endo > (int64_t)p.byte_end ? 0u : 0xFFFFu;
+    c.dead = m & ~fp & avail & rng;
+    c.res = m & rng & ~c.dead;
+    c.fetch = m & rng & ~avail & ~c.dead;
+    return c;
+  }
   uint32_t seen = 0u;                  // the keys' candidates so far
   // one test remembered across keys and guards (rx: both keys test the byte
   // after them against 0xC3)
@@ -936,9 +972,10 @@ __device__ __forceinline__ uint32_t scan_class_entry(const ScanParams& p, uint32
   const uint32_t key = (uint32_t)(w >> 16) & 0xFFu;
   const uint32_t t = p.byte_keys ^ (key * 0x01010101u);
   const uint32_t z = (t - 0x01010101u) & ~t & 0x80808080u;
-  const KeyClassRec r = scan_key_rec(kcv_, (uint32_t)__builtin_ctz(z | 0x80000000u) >> 3, kDropBg<MODE>);
+  constexpr bool kBg = kDropBg<MODE>;
+  const KeyClassRec r = scan_key_rec(kcv_, (uint32_t)__builtin_ctz(z | 0x80000000u) >> 3, kBg);
   bool more = false;
-  const uint32_t cls = key_class<kDropBg<MODE>>(p, [r](uint32_t) { return r; }, w, 2, false, seg_start + off + 1,
+  const uint32_t cls = key_class<kBg>(p, [r](uint32_t) { return r; }, w, 2, false, seg_start + off + 1,
                                  min(have, 8) - 1, &more);
   return off | (cls == 0u && more ? kClassFetch : cls) << kOutByteShift |
          kOutPlaceScanClass << kOutKeyShift;
@@ -2066,7 +2103,9 @@ hipError_t launch_scan(const ScanParams& p, int grid, hipStream_t s, int mode, h
     case 12: YAMD_LAUNCH_SCAN(scan_segments_kernel<D + kModeByteKeysEvenHash>); break;            \
     default: YAMD_LAUNCH_SCAN(scan_segments_kernel<D + kModeByteKeysNextEvenHash>); break;        \
   }
-        if (p.drop_dead != 0u && p.kd_bguard != 0u) {
+        if (p.drop_dead != 0u && p.kp_on != 0u) {
+          YAMD_BK_CASES(kDropPlanModes)
+        } else if (p.drop_dead != 0u && p.kd_bguard != 0u) {
           YAMD_BK_CASES(kDropBgModes)
         } else if (p.drop_dead != 0u) {
           YAMD_BK_CASES(kDropModes)
@@ -2148,6 +2187,12 @@ hipError_t configure_scan_kernel() {
                         (const void*)scan_segments_kernel<kDropBgModes + kModeByteKeysEvenHash>,
                         (const void*)scan_segments_kernel<kDropBgModes + kModeByteKeysNextEven>,
                         (const void*)scan_segments_kernel<kDropBgModes + kModeByteKeysNextEvenHash>,
+                        (const void*)scan_segments_kernel<kDropPlanModes + kModeByteKeys>,
+                        (const void*)scan_segments_kernel<kDropPlanModes + kModeByteKeysNext>,
+                        (const void*)scan_segments_kernel<kDropPlanModes + kModeByteKeysEven>,
+                        (const void*)scan_segments_kernel<kDropPlanModes + kModeByteKeysEvenHash>,
+                        (const void*)scan_segments_kernel<kDropPlanModes + kModeByteKeysNextEven>,
+                        (const void*)scan_segments_kernel<kDropPlanModes + kModeByteKeysNextEvenHash>,
 #if YAMD_DIAG
                         (const void*)scan_segments_kernel<1>,
                         (const void*)scan_segments_kernel<2>, (const void*)scan_segments_kernel<3>,

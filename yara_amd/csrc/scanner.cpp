@@ -103,10 +103,12 @@ struct yr_amd_tables {
   bool kd_any = false;
   bool kd_guard = false;              // some key's class is guard-decided (can be dead)
   bool kd_kept = false;               // some key's class is "kept" (every call a record)
+  // one class plan for every key (key_plan; ScanParams::kp_on, kc[kKcPlan..])
+  uint32_t kp_on = 0, kp_info = 0, kp_m = 0, kp_v = 0;
   uint32_t max_list = 0;              // the longest match list (pool chain)
   uint32_t kx_end = 2, kx_deep = 0, kx_next = 0;   // ScanParams::kx_end / kx_deep / kx_next
   uint32_t* d_nodes = nullptr;        // accepting nodes by string (FlatTables::nodes)
-  uint32_t* d_kc = nullptr;           // [32] the key class records (ScanParams::kc)
+  uint32_t* d_kc = nullptr;           // [kKcWords] the key class records + the plan (ScanParams::kc)
   DevPoolRec* d_pool = nullptr;       // per pool entry: link, backtrack, string, programs
   uint8_t* d_str_bytes = nullptr;
   uint8_t* d_lowercase = nullptr;
@@ -656,6 +658,7 @@ int yr_amd_scan_window(yr_amd_scanner* s, const uint8_t* d_window, uint64_t wind
     p.kd_min_pos[k] = t->kd_min_pos[k];
   }
   p.kd_bguard = ((t->kd_info[0] | t->kd_info[1] | t->kd_info[2] | t->kd_info[3]) & 8u) ? 1u : 0u;
+  p.kp_on = t->kp_on;
   p.filter_mode = t->flat.filter_mode;
   // verified-only: the byte-key kernel decides the certain candidates' classes
   // and leaves the dead ones out (kd_any: 1-byte keys with classes; never with
@@ -1036,8 +1039,53 @@ bool re_fiber_safe(const uint8_t* c, uint32_t len) {
 //    the compaction tests it.  (YR_AC_MATCH offsets: the call's offset is
 //    position - backtrack, the guard's region starts `base` bytes after it.)
 // Pre-verification then never reads the input for such candidates.
+// One class plan for every 1-byte key (the drop kernels' kDropPlanModes
+// instance): every key's class is a forward guard -- no key without a class,
+// none "kept", no exclusions, no backward guard -- with the same region and
+// the same tests once each key's test of its own byte (a full-mask compare
+// with the key at the key byte, which every candidate of that key passes:
+// drain_classes skips it too) is left out.  Then the drain decides all
+// certain candidates of an entry at once, whatever their key, in straight-line
+// code (rx: both keys test the byte after them against 0xC3).  Measured, one
+// process, both orders (profiles/r06_key_plan_ab/): rx's drop kernel 0.94 ->
+// 0.87 ms; the same plan with exclusions and a backward guard (fuzz0) was 2 %
+// slower than the per-key loop, and as a drop kernel for a "kept" key (short,
+// fuzz3) 7-8 % slower than their non-drop kernel: neither shape takes it.
+void key_plan(yr_amd_tables* t) {
+  t->kp_on = 0;
+  const uint32_t nk = std::min<uint32_t>(t->flat.n_byte_keys, 4);
+  if (!t->kd_any || nk == 0) return;
+  uint32_t m0 = 0, v0 = 0;
+  for (uint32_t k = 0; k < nk; ++k) {
+    const uint32_t info = t->kd_info[k];
+    if (!(info & 1u) || (info & (2u | 4u | 8u))) return;
+    const uint32_t key = (t->flat.byte_keys >> (8 * k)) & 0xFFu;
+    const int rs = (int)(int8_t)(info >> 8);
+    const uint32_t tmax = (info >> 20) & 3u;
+    uint32_t m = t->kd_m[k], v = t->kd_v[k];
+    for (uint32_t q = 0; q <= tmax; ++q) {
+      const uint32_t mt = (m >> (8 * q)) & 0xFFu, vt = (v >> (8 * q)) & 0xFFu;
+      if (rs + (int)q == 0 && mt == 0xFFu && vt == key) {
+        m &= ~(0xFFu << (8 * q));
+        v &= ~(0xFFu << (8 * q));
+      }
+    }
+    v &= m;
+    if (k == 0) {
+      m0 = m, v0 = v;
+    } else if (info != t->kd_info[0] || m != m0 || v != v0) {
+      return;
+    }
+  }
+  t->kp_info = t->kd_info[0];
+  t->kp_m = m0;
+  t->kp_v = v0;
+  t->kp_on = diag_env("YAMD_NO_KEY_PLAN") != nullptr ? 0u : 1u;
+}
+
 void key_classes(yr_amd_tables* t) {
   const FlatTables& f = t->flat;
+  t->kp_on = 0;
   t->kd_any = false;
   t->kd_guard = false;
   t->kd_kept = false;
@@ -1223,19 +1271,24 @@ void key_classes(yr_amd_tables* t) {
     t->kd_x1[k] = o.xs1;
     t->kd_any = true;
   }
+  key_plan(t);
   // the records the scan kernel reads (ScanParams::kc); without them, no
   // classes at all (the scan then keeps every candidate: still exact)
-  uint32_t kc[32] = {};
+  uint32_t kc[kKcWords] = {};
   for (int k = 0; k < 4; ++k) {
     const uint32_t r[8] = {t->kd_info[k], t->kd_m[k], t->kd_v[k], t->kd_x0[k],
                            t->kd_x1[k], t->kd_min_pos[k], t->kd_bm[k], t->kd_bv[k]};
     for (int f = 0; f < 8; ++f) kc[8 * k + f] = r[f];
   }
+  kc[kKcPlan] = t->kp_info;
+  kc[kKcPlan + 1] = t->kp_m;
+  kc[kKcPlan + 2] = t->kp_v;
   if ((t->d_kc == nullptr && hipMalloc((void**)&t->d_kc, sizeof(kc)) != hipSuccess) ||
       hipMemcpy(t->d_kc, kc, sizeof(kc), hipMemcpyHostToDevice) != hipSuccess) {
     if (t->d_kc) (void)hipFree(t->d_kc);
     t->d_kc = nullptr;
     t->kd_any = false;
+    t->kp_on = 0;
     t->kd_guard = false;
     t->kd_kept = false;
   }
