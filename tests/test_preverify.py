@@ -424,3 +424,24 @@ def test_verified_only_first_scan_of_a_fresh_scanner(rules):
     full2, _, _ = _device_records(yara_amd.Scanner(tab), d, n, cut, n)
     for f in ("offset", "pool_index", "candidate"):
         np.testing.assert_array_equal(got2[f], full2[f], err_msg=f)
+
+
+@pytest.mark.gpu
+def test_one_plan_drop_instance_selection():
+    """scanner.cpp key_plan: rx's two 1-byte keys ('[' and ']') share one forward
+    guard once each key's test of its own byte is left out -- the byte after
+    the key is 0xC3 -- so its verified-only scans run the one-plan drop
+    instance (kernels.hip kDropPlanModes); fuzz0 (exclusions, a backward guard)
+    and the kept-key sets short / fuzz3 keep their own kernels.  (The records
+    of every one of these sets are pinned by the verified-only tests above.)"""
+    import ctypes
+    import yara_amd
+    g = yara_amd._lib.lib().yr_amd__diag_key_classes
+    g.argtypes = [ctypes.c_void_p, ctypes.POINTER(ctypes.c_uint32)]
+    for name, plan in (("rx", 1), ("fuzz0", 0), ("short", 0), ("fuzz3", 0)):
+        t = yara_amd.Tables.from_npz(tables_npz(name), device=0, strings=True)
+        o = (ctypes.c_uint32 * 40)()
+        assert g(t._h, o) == 0
+        assert o[29] == plan, name
+        if plan:
+            assert (o[30], o[31]) == (0xFF00, 0xC300), (hex(o[30]), hex(o[31]))

@@ -533,6 +533,10 @@ int yr_amd__diag_key_classes(const yr_amd_tables* t, uint32_t* out) {
   for (int k = 0; k < 4; ++k) out[15 + k] = t->kd_x0[k], out[19 + k] = t->kd_x1[k], out[23 + k] = t->kd_min_pos[k];
   out[27] = t->kx_deep;
   out[28] = t->kx_next;
+  // [29] the one-plan drop instance (key_plan), [30] / [31] its forward tests
+  out[29] = t->kp_on;
+  out[30] = t->kp_m;
+  out[31] = t->kp_v;
   // [32..35] kd_bm, [36..39] kd_bv
   for (int k = 0; k < 4; ++k) out[32 + k] = t->kd_bm[k], out[36 + k] = t->kd_bv[k];
   return YR_AMD_SUCCESS;
