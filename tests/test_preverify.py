@@ -433,15 +433,20 @@ def test_one_plan_drop_instance_selection():
     the key is 0xC3 -- so its verified-only scans run the one-plan drop
     instance (kernels.hip kDropPlanModes); fuzz0 (exclusions, a backward guard)
     and the kept-key sets short / fuzz3 keep their own kernels.  (The records
-    of every one of these sets are pinned by the verified-only tests above.)"""
-    import ctypes
-    import yara_amd
-    g = yara_amd._lib.lib().yr_amd__diag_key_classes
-    g.argtypes = [ctypes.c_void_p, ctypes.POINTER(ctypes.c_uint32)]
-    for name, plan in (("rx", 1), ("fuzz0", 0), ("short", 0), ("fuzz3", 0)):
-        t = yara_amd.Tables.from_npz(tables_npz(name), device=0, strings=True)
-        o = (ctypes.c_uint32 * 40)()
-        assert g(t._h, o) == 0
-        assert o[29] == plan, name
-        if plan:
-            assert (o[30], o[31]) == (0xFF00, 0xC300), (hex(o[30]), hex(o[31]))
+    of every one of these sets are pinned by the verified-only tests above.)
+    Read through the diagnostic build's yr_amd__diag_key_classes."""
+    from conftest import run_diag_child
+    code = (
+        "import ctypes, yara_amd\n"
+        "from conftest import tables_npz\n"
+        "g = yara_amd._lib.lib().yr_amd__diag_key_classes\n"
+        "g.argtypes = [ctypes.c_void_p, ctypes.POINTER(ctypes.c_uint32)]\n"
+        "for name in ('rx', 'fuzz0', 'short', 'fuzz3'):\n"
+        "  t = yara_amd.Tables.from_npz(tables_npz(name), device=0, strings=True)\n"
+        "  o = (ctypes.c_uint32 * 40)()\n"
+        "  assert g(t._h, o) == 0\n"
+        "  print('plan', name, o[29], hex(o[30]), hex(o[31]))\n")
+    got = {ln.split()[1]: ln.split()[2:] for ln in run_diag_child(code).splitlines()
+           if ln.startswith("plan ")}
+    assert got["rx"] == ["1", "0xff00", "0xc300"], got
+    assert [got[n][0] for n in ("fuzz0", "short", "fuzz3")] == ["0", "0", "0"], got

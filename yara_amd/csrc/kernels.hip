@@ -802,7 +802,8 @@ struct DrainClasses {
 };
 template <int MODE>
 __device__ __forceinline__ DrainClasses drain_classes(const ScanParams& p, uint32_t kcv, const uint32_t (&S)[6],
-                                                      uint32_t eidx, uint32_t m, uint32_t first, uint64_t pos0) {
+                                                      uint32_t eidx, uint32_t m, uint32_t first, uint64_t pos0,
+                                                      uint4 plan) {
   DrainClasses c{0u, 0u, 0u, 0u, 0u};
   // the next lane's first two bytes: kept by the kernels with kNextBytes,
   // except in a tile's last lane
@@ -811,13 +812,12 @@ __device__ __forceinline__ DrainClasses drain_classes(const ScanParams& p, uint3
   const int32_t last = nx ? 17 : 15;   // last lane byte held
   if constexpr (kDropPlan<MODE>) {
     // one forward guard for every key (scanner.cpp key_plan): the loop below
-    // for all of m at once, its parameters from two scalar loads (kc[kKcPlan..],
-    // a wave-uniform address) instead of lane reads of the records, no per-key
-    // split of m, no test-reuse branch
+    // for all of m at once, its parameters from one scalar load at the drain's
+    // start (kc[kKcPlan..], a wave-uniform address: `plan`) instead of lane
+    // reads of the records, no per-key split of m, no test-reuse branch
     (void)first;
     (void)kcv;
-    const uint4 w = *reinterpret_cast<const uint4*>(p.kc + kKcPlan);
-    const uint32_t info = w.x, pm = w.y, pv = w.z;
+    const uint32_t info = plan.x, pm = plan.y, pv = plan.z;
     const int32_t rs = (int32_t)(int8_t)(info >> 8);
     const uint32_t span = (info >> 16) & 15u, tmax = (info >> 20) & 3u;
     const int64_t endo = (int8_t)(info >> 24);
@@ -1063,6 +1063,16 @@ __device__ __forceinline__ void drain(const ScanParams& p, WaveQueue& q, uint32_
     if (q.defer) drain_complete<MODE>(p, q, lane, seg_start, out, found);
   const uint32_t n = q.count;   // <= kQueueCap = kWave
   q.count = 0;
+  // (the one-plan instance: its words loaded first, so the scalar load
+  // overlaps the entries' re-test -- drain_classes needs them last)
+  uint4 plan = make_uint4(0u, 0u, 0u, 0u);
+  if constexpr (kDropPlan<MODE>) {
+    // (an opaque copy of the pointer: the load stays in the drain instead of
+    // being hoisted to the kernel's start, where its SGPRs would be spilled)
+    const uint32_t* kc = p.kc;
+    asm volatile("" : "+s"(kc));
+    plan = *reinterpret_cast<const uint4*>(kc + kKcPlan);
+  }
   bool need_f = true;   // (kBkSkipF: some queued tile passed the filter / a 2-byte key)
   if constexpr (kBkSkipF<MODE>) {
     need_f = __ballot(q.facc != 0u) != 0;
@@ -1113,7 +1123,7 @@ __device__ __forceinline__ void drain(const ScanParams& p, WaveQueue& q, uint32_
   // (every lane, in uniform control flow -- lanes without an entry have no
   // hits: the class code's wave-uniform values stay in SGPRs)
   if constexpr (kDrainClass<MODE>)
-    dc = drain_classes<MODE>(p, q.kcv, S, eidx, m & kmask, kfirst & m, seg_start + off0);
+    dc = drain_classes<MODE>(p, q.kcv, S, eidx, m & kmask, kfirst & m, seg_start + off0, plan);
   if constexpr (kDeferFl<MODE> && kAsync) {
     const uint32_t m2 = m & (m - 1u);
     if ((p.len_mask & 6u) == 0u && __ballot((m2 & (m2 - 1u)) != 0u) == 0) {
