@@ -186,7 +186,8 @@ constexpr uint32_t kClassFetch = 0xFFu;   // (verified-only scans) undecided fro
                                           // eight bytes: the compaction reads the input
 constexpr uint32_t kOutPlaceScanClass = 7u;   // key place of an entry carrying its class
 // ScanParams::kc: 32 words of key class records (8 per key), then the plan of
-// the one-plan drop instance (scanner.cpp key_plan): info, forward tests m / v
+// the one-plan drop instance (scanner.cpp key_plan): info, the one compared
+// byte's value replicated to four bytes, its shift in byte_test24's mask
 constexpr uint32_t kKcPlan = 32;
 constexpr uint32_t kKcWords = 36;
 

@@ -802,8 +802,7 @@ struct DrainClasses {
 };
 template <int MODE>
 __device__ __forceinline__ DrainClasses drain_classes(const ScanParams& p, uint32_t kcv, const uint32_t (&S)[6],
-                                                      uint32_t eidx, uint32_t m, uint32_t first, uint64_t pos0,
-                                                      uint4 plan) {
+                                                      uint32_t eidx, uint32_t m, uint32_t first, uint64_t pos0) {
   DrainClasses c{0u, 0u, 0u, 0u, 0u};
   // the next lane's first two bytes: kept by the kernels with kNextBytes,
   // except in a tile's last lane
@@ -811,22 +810,28 @@ __device__ __forceinline__ DrainClasses drain_classes(const ScanParams& p, uint3
   const uint32_t E[6] = {S[0], S[1], S[2], S[3], S[4], nx ? eidx >> 16 : 0u};
   const int32_t last = nx ? 17 : 15;   // last lane byte held
   if constexpr (kDropPlan<MODE>) {
-    // one forward guard for every key (scanner.cpp key_plan): the loop below
-    // for all of m at once, its parameters from one scalar load at the drain's
-    // start (kc[kKcPlan..], a wave-uniform address: `plan`) instead of lane
-    // reads of the records, no per-key split of m, no test-reuse branch
+    // one forward guard -- one full-byte compare -- for every key (scanner.cpp
+    // key_plan): the per-key loop below in one pass over all of m, its three
+    // parameters read from the records' VGPR (kc[kKcPlan..] sit in lanes 32..34
+    // of kcv: no memory access in the drain, no SGPRs held across the tile
+    // loop), no per-key split of m, no loop over tested bytes, no test-reuse branch
     (void)first;
-    (void)kcv;
-    const uint32_t info = plan.x, pm = plan.y, pv = plan.z;
+    const uint32_t info = (uint32_t)__builtin_amdgcn_readlane((int)kcv, (int)kKcPlan);
+    const uint32_t V = (uint32_t)__builtin_amdgcn_readlane((int)kcv, (int)kKcPlan + 1);
+    const uint32_t sh = (uint32_t)__builtin_amdgcn_readlane((int)kcv, (int)kKcPlan + 2);
     const int32_t rs = (int32_t)(int8_t)(info >> 8);
     const uint32_t span = (info >> 16) & 15u, tmax = (info >> 20) & 3u;
     const int64_t endo = (int8_t)(info >> 24);
-    uint32_t A = ~0u;
-#pragma unroll
-    for (uint32_t t = 0; t < 4; ++t) {
-      const uint32_t mt = (pm >> (8 * t)) & 0xFFu, vt = (pv >> (8 * t)) & 0xFFu;
-      if (t <= tmax && mt != 0u) A &= byte_test24(E, mt, vt) >> (uint32_t)(rs + (int32_t)t + 4);
-    }
+    // the one full-byte compare, on all 24 bytes (byte_test24's unmasked form)
+    const uint32_t z0 = zero_flags(E[0] ^ V), z1 = zero_flags(E[1] ^ V), z2 = zero_flags(E[2] ^ V);
+    const uint32_t z3 = zero_flags(E[3] ^ V), z4 = zero_flags(E[4] ^ V), z5 = zero_flags(E[5] ^ V);
+    const uint32_t lo = __builtin_amdgcn_udot4(z1, 0x80402010u, __builtin_amdgcn_udot4(z0, 0x08040201u, 0u, false),
+                                               false);
+    const uint32_t mid = __builtin_amdgcn_udot4(z3, 0x80402010u, __builtin_amdgcn_udot4(z2, 0x08040201u, 0u, false),
+                                                false);
+    const uint32_t hi = __builtin_amdgcn_udot4(z5, 0x80402010u, __builtin_amdgcn_udot4(z4, 0x08040201u, 0u, false),
+                                               false);
+    const uint32_t A = ((lo >> 7) | (mid << 1) | (hi << 9)) >> sh;
     uint32_t fp = A;
 #pragma unroll 1
     for (uint32_t jj = 1; jj <= span; ++jj) fp |= A >> jj;
@@ -1063,16 +1068,6 @@ __device__ __forceinline__ void drain(const ScanParams& p, WaveQueue& q, uint32_
     if (q.defer) drain_complete<MODE>(p, q, lane, seg_start, out, found);
   const uint32_t n = q.count;   // <= kQueueCap = kWave
   q.count = 0;
-  // (the one-plan instance: its words loaded first, so the scalar load
-  // overlaps the entries' re-test -- drain_classes needs them last)
-  uint4 plan = make_uint4(0u, 0u, 0u, 0u);
-  if constexpr (kDropPlan<MODE>) {
-    // (an opaque copy of the pointer: the load stays in the drain instead of
-    // being hoisted to the kernel's start, where its SGPRs would be spilled)
-    const uint32_t* kc = p.kc;
-    asm volatile("" : "+s"(kc));
-    plan = *reinterpret_cast<const uint4*>(kc + kKcPlan);
-  }
   bool need_f = true;   // (kBkSkipF: some queued tile passed the filter / a 2-byte key)
   if constexpr (kBkSkipF<MODE>) {
     need_f = __ballot(q.facc != 0u) != 0;
@@ -1123,7 +1118,7 @@ __device__ __forceinline__ void drain(const ScanParams& p, WaveQueue& q, uint32_
   // (every lane, in uniform control flow -- lanes without an entry have no
   // hits: the class code's wave-uniform values stay in SGPRs)
   if constexpr (kDrainClass<MODE>)
-    dc = drain_classes<MODE>(p, q.kcv, S, eidx, m & kmask, kfirst & m, seg_start + off0, plan);
+    dc = drain_classes<MODE>(p, q.kcv, S, eidx, m & kmask, kfirst & m, seg_start + off0);
   if constexpr (kDeferFl<MODE> && kAsync) {
     const uint32_t m2 = m & (m - 1u);
     if ((p.len_mask & 6u) == 0u && __ballot((m2 & (m2 - 1u)) != 0u) == 0) {
@@ -1765,7 +1760,7 @@ __global__ __launch_bounds__(kWGThreads, 1) void scan_segments_kernel(ScanParams
   uint32_t seg = blockIdx.x * kWavesPerWG + wid;
   uint32_t kcv = 0u;
   if constexpr (kDrop<MODE>)
-    if (lane < 32u) kcv = p.kc[lane];
+    if (lane < kKcWords) kcv = p.kc[lane];   // (the records, and the plan in lanes 32..)
   while (seg < p.n_segments) {
     WaveQueue q;   // (per segment: its per-lane state then stays in registers)
     q.kcv = kcv;

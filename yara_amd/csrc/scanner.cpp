@@ -104,7 +104,7 @@ struct yr_amd_tables {
   bool kd_guard = false;              // some key's class is guard-decided (can be dead)
   bool kd_kept = false;               // some key's class is "kept" (every call a record)
   // one class plan for every key (key_plan; ScanParams::kp_on, kc[kKcPlan..])
-  uint32_t kp_on = 0, kp_info = 0, kp_m = 0, kp_v = 0;
+  uint32_t kp_on = 0, kp_info = 0, kp_m = 0, kp_v = 0, kp_t = 0;
   uint32_t max_list = 0;              // the longest match list (pool chain)
   uint32_t kx_end = 2, kx_deep = 0, kx_next = 0;   // ScanParams::kx_end / kx_deep / kx_next
   uint32_t* d_nodes = nullptr;        // accepting nodes by string (FlatTables::nodes)
@@ -1048,7 +1048,7 @@ bool re_fiber_safe(const uint8_t* c, uint32_t len) {
 // none "kept", no exclusions, no backward guard -- with the same region and
 // the same tests once each key's test of its own byte (a full-mask compare
 // with the key at the key byte, which every candidate of that key passes:
-// drain_classes skips it too) is left out.  Then the drain decides all
+// drain_classes skips it too) is left out, and that is one full-byte compare.  Then the drain decides all
 // certain candidates of an entry at once, whatever their key, in straight-line
 // code (rx: both keys test the byte after them against 0xC3).  Measured, one
 // process, both orders (profiles/r06_key_plan_ab/): rx's drop kernel 0.94 ->
@@ -1081,9 +1081,20 @@ void key_plan(yr_amd_tables* t) {
       return;
     }
   }
+  // ... and one full-byte compare left (rx: the byte after the key is 0xC3):
+  // the drain's one byte_test24 then needs no mask and no loop over the bytes
+  int tested = -1;
+  for (int q = 0; q < 4; ++q) {
+    const uint32_t mt = (m0 >> (8 * q)) & 0xFFu;
+    if (mt == 0u) continue;
+    if (mt != 0xFFu || tested >= 0) return;
+    tested = q;
+  }
+  if (tested < 0) return;
   t->kp_info = t->kd_info[0];
   t->kp_m = m0;
   t->kp_v = v0;
+  t->kp_t = (uint32_t)tested;
   t->kp_on = diag_env("YAMD_NO_KEY_PLAN") != nullptr ? 0u : 1u;
 }
 
@@ -1284,9 +1295,14 @@ void key_classes(yr_amd_tables* t) {
                            t->kd_x1[k], t->kd_min_pos[k], t->kd_bm[k], t->kd_bv[k]};
     for (int f = 0; f < 8; ++f) kc[8 * k + f] = r[f];
   }
-  kc[kKcPlan] = t->kp_info;
-  kc[kKcPlan + 1] = t->kp_m;
-  kc[kKcPlan + 2] = t->kp_v;
+  // the plan (kernels.hip drain_classes): info, the compared byte's value
+  // replicated, its shift (rs + t + 4)
+  if (t->kp_on) {
+    const int32_t rs = (int32_t)(int8_t)(t->kp_info >> 8);
+    kc[kKcPlan] = t->kp_info;
+    kc[kKcPlan + 1] = ((t->kp_v >> (8 * t->kp_t)) & 0xFFu) * 0x01010101u;
+    kc[kKcPlan + 2] = (uint32_t)(rs + (int32_t)t->kp_t + 4);
+  }
   if ((t->d_kc == nullptr && hipMalloc((void**)&t->d_kc, sizeof(kc)) != hipSuccess) ||
       hipMemcpy(t->d_kc, kc, sizeof(kc), hipMemcpyHostToDevice) != hipSuccess) {
     if (t->d_kc) (void)hipFree(t->d_kc);
