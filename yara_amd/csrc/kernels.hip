@@ -249,7 +249,7 @@ template <int MODE>
 constexpr bool kDropBg = MODE >= kDropBgModes && MODE < 3000;
 // MODE + kDropPlanModes: the drop instance for tables whose keys all share one
 // forward guard (ScanParams::kp_on, scanner.cpp key_plan): the drain's classes
-// in straight-line code (rx's drop kernel 0.94 -> 0.87 ms, gpurun r06q; with
+// in straight-line code (rx's drop kernel 0.94 -> 0.825 ms, gpurun r06v2; with
 // the plan's parameters as compile-time constants 0.81, r06x)
 constexpr int kDropPlanModes = 3000;
 template <int MODE>

@@ -1048,11 +1048,11 @@ bool re_fiber_safe(const uint8_t* c, uint32_t len) {
 // none "kept", no exclusions, no backward guard -- with the same region and
 // the same tests once each key's test of its own byte (a full-mask compare
 // with the key at the key byte, which every candidate of that key passes:
-// drain_classes skips it too) is left out, and that is one full-byte compare.  Then the drain decides all
-// certain candidates of an entry at once, whatever their key, in straight-line
-// code (rx: both keys test the byte after them against 0xC3).  Measured, one
-// process, both orders (profiles/r06_key_plan_ab/): rx's drop kernel 0.94 ->
-// 0.87 ms; the same plan with exclusions and a backward guard (fuzz0) was 2 %
+// drain_classes skips it too) is left out, and that is one full-byte compare.
+// Then the drain decides all certain candidates of an entry at once, whatever
+// their key, in straight-line code (rx: both keys test the byte after them
+// against 0xC3).  Measured, one process, both orders
+// (profiles/r06_key_plan_ab/): rx's drop kernel 0.94 -> 0.825 ms; the same plan with exclusions and a backward guard (fuzz0) was 2 %
 // slower than the per-key loop, and as a drop kernel for a "kept" key (short,
 // fuzz3) 7-8 % slower than their non-drop kernel: neither shape takes it.
 void key_plan(yr_amd_tables* t) {
