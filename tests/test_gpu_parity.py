@@ -101,6 +101,28 @@ def test_ragged_sizes_vs_oracle(rules, size):
     np.testing.assert_array_equal(pos, oracle.candidates(tab, data))
 
 
+@pytest.mark.parametrize("rules", ["B", "C", "E", "rx", "short"])
+def test_segment_tile_counts(rules):
+    """Segments of 4 to 13 full tiles, with and without a ragged tail: every
+    entry and exit of the tile loop (kernels.hip scan_segment: the rounds of
+    kPf + 1 steps with kPf tiles in flight, the remaining tiles one ahead,
+    the one-ahead loop of segments too short for a round).  A block of
+    waves x T KiB makes segments of T tiles (scanner.cpp choose_seg_bytes)."""
+    torch = _torch()
+    waves = torch.cuda.get_device_properties(0).multi_processor_count * 16
+    tab = ref_tables(rules)
+    sc = yara_amd.Scanner(dev_tables(rules))
+    for t in range(4, 13):
+        for extra in (0, 777):
+            n = waves * t * 1024 + extra
+            data = oracle.xorshift(n, 100 + t)
+            if rules == "short":
+                data = np.frombuffer(b"abcdxyzHeloC\x00\x01\xff", np.uint8)[data % 15]
+            pos, allp = sc.candidates(data)
+            assert not allp
+            np.testing.assert_array_equal(pos, oracle.candidates(tab, data), err_msg=str((t, extra)))
+
+
 @pytest.mark.parametrize("hot_mib", [1, 3])
 def test_skewed_candidate_density(hot_mib):
     """One dense region (every byte a candidate of a 1-byte key) inside random

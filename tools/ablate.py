@@ -21,7 +21,7 @@ NAMES = {0: "product", 1: "no-exact-check", 2: "stage1-only", 3: "stream-only",
          4: "stage1-conflict-free-lds", 5: "stage1-valu-no-lds",
          6: "stage1-lds-no-test", 7: "stage1+appends-no-drain", 8: "stage1+append-arith-no-lds-writes",
          9: "drain-one-l2-load", 10: "drain-exact-valu-no-loads", 11: "product-reads-first",
-         12: "first-level-only", 24: "bytekeys-detected-not-appended", 25: "bytekeys-not-detected",
+         12: "first-level-only", 13: "stage1+appends-index-dword-only", 24: "bytekeys-detected-not-appended", 25: "bytekeys-not-detected",
          # ablations of the byte-key variant the product runs for the rule set (its filter)
          101: "bk-stage1-only", 102: "bk-appends-drains-drop", 103: "bk-keys-detected-not-appended",
          104: "bk-keys-not-detected"}

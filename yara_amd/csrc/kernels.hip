@@ -641,8 +641,31 @@ constexpr bool kHoldFl = !kEven<MODE>;
 // their drains never defer (the deferral needs len_mask & 6 == 0): they carry
 // none of its per-tile machinery (the two first-level loads, the
 // deferred-drain test): rx -4.7 %, short -4.6 % (profiles/r04_ab_inproc.json h23).
+// Tiles in flight ahead of the one in the tile step (scan_segment).  Two
+// instead of one: C -4 %, rx -8 %, E -2 % (profiles/r06_prefetch_ab/) --
+// once the drains check the first level themselves instead of deferring its
+// loads to the next tile step (kDeferFl): vmcnt retires in issue order, so a
+// step that consumed the words loaded at the end of the previous one also
+// waited for the tile issued after them, and two tiles in flight measured no
+// faster with the deferral (round 2; r07c).  The deferral itself is worth
+// nothing now (C equal without it, r07c), so no kernel defers; the plain
+// even-position filter kernel without 1-byte keys (B) stays at one tile ahead
+// (two: +2 %).
+// (YAMD_PF / YAMD_PF_EVEN / YAMD_DEFER_FL: variant builds.)
+#ifndef YAMD_PF
+#define YAMD_PF 2
+#endif
+#ifndef YAMD_PF_EVEN
+#define YAMD_PF_EVEN 1
+#endif
+#ifndef YAMD_DEFER_FL
+#define YAMD_DEFER_FL 0
+#endif
 template <int MODE>
-constexpr bool kDeferFl = kAbl<MODE> != 1 && (MODE == 0 || MODE == 12 || kEven<MODE>) &&
+constexpr uint32_t kPf = kBase<MODE> == kModeEven ? YAMD_PF_EVEN : YAMD_PF;
+template <int MODE>
+constexpr bool kDeferFl = YAMD_DEFER_FL && kAbl<MODE> != 1 && kPf<MODE> == 1 &&
+                          (MODE == 0 || MODE == 12 || kEven<MODE>) &&
                           !(kByteKeys<MODE> || kByteKeyAblation<MODE>);
 // Byte-key drains re-test the filter and the 2-byte keys only when some tile
 // queued since the last drain passed them in stage 1 (a per-lane OR, one
@@ -1073,7 +1096,7 @@ __device__ __forceinline__ void drain(const ScanParams& p, WaveQueue& q, uint32_
     need_f = __ballot(q.facc != 0u) != 0;
     q.facc = 0u;
   }
-  if constexpr (MODE == 7 || MODE == 8 || kAbl<MODE> == 2) return;   // ablations: entries dropped
+  if constexpr (MODE == 7 || MODE == 8 || MODE == 13 || kAbl<MODE> == 2) return;   // ablations: entries dropped
   __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
   uint32_t maybe = 0, off0 = 0, m = 0;   // m: bit j = lane byte j passes the filter
   uint32_t kmask = 0;                    // bit j = lane byte j is a 1-byte key (certain)
@@ -1526,6 +1549,8 @@ __device__ __forceinline__ void ring_append(const ScanParams& p, WaveQueue& q, S
     // the 4 bytes before them, the lane's place in the segment
     if constexpr (MODE == 8) {   // ablation: the append's slot arithmetic, no LDS writes
       asm volatile("" ::"v"(ent), "v"(lane_off));
+    } else if constexpr (MODE == 13) {   // ablation: an entry of the index dword only
+      *reinterpret_cast<__attribute__((address_space(3))) uint32_t*>((uintptr_t)(ent + kEntIdx)) = lane_off;
     } else {
       write_entry<MODE>(ent, S, kIdxBytes<MODE> ? lane_off : (tile_off >> 4) + lane);
     }
@@ -1651,7 +1676,8 @@ __device__ __forceinline__ void tile_step(const ScanParams& p, WaveQueue& q, Seg
 // ring appends, drains drop the entries, 8 = 7 without the ring's LDS writes, 9 = exact check replaced by one L2 dword
 // load per hit, 10 = exact-check VALU with the bucket loads replaced by values,
 // 11 = product with all 8 filter reads of a tile issued before any test,
-// 12 = product without the bucket probes (first level only).
+// 12 = product without the bucket probes (first level only), 13 = 7 with
+// ring entries of the index dword only (what an offset-only entry would cost).
 //
 // (An earlier version rotated each segment's tile order so that the waves of
 // the chip would not read the same offsets of their equal segments at the
@@ -1696,27 +1722,58 @@ __device__ __forceinline__ void scan_segment(const ScanParams& p, WaveQueue& q, 
     // a load pending on a (the loop's wait for its input tile would
     // otherwise cover the deferred first-level loads too)
     asm volatile("" : "+v"(a.x), "+v"(a.y), "+v"(a.z), "+v"(a.w));
-    // the loop runs on the tile's byte offset (the loads' SGPR offset; the
-    // second tile's + 1 KiB folds into the instruction's offset field) and
-    // only while its prefetch stays inside the full tiles: no clamp per step,
-    // the last one or two tiles after it
     uint32_t off = 0;
-    if (full_end > 2 * kTile) {
-      const uint32_t lim = full_end - 2 * kTile;   // (a bottom-tested loop: one compare per pair)
+    // kPf tiles in flight ahead of the one in the step: kPf + 1 tile registers
+    // in rotation, the loop unrolled over them; a segment too short for one
+    // round of it takes the one-ahead loop
+    constexpr uint32_t kP = kPf<MODE>, kR = kP + 1;
+    if (kP > 1 && full_end >= (2 * kR - 1) * kTile) {
+      uint4 t[kR];
+      t[0] = a;
+#pragma unroll
+      for (uint32_t i = 1; i < kP; ++i) t[i] = load_tile_full(rsrc, i * kTile, lane16);
+      const uint32_t lim = full_end - (2 * kR - 1) * kTile;   // (every load of a round inside)
       do {
+#pragma unroll
+        for (uint32_t i = 0; i < kR; ++i) {
+          t[(i + kP) % kR] = load_tile_full(rsrc, off + (i + kP) * kTile, lane16);
+          tile_step<MODE, false>(p, q, st, t[i], off + i * kTile, lane);
+        }
+        off += kR * kTile;
+      } while (off <= lim);
+      // t[0 .. kP - 1] hold the tiles at off ..; fewer than 2 kR tiles remain
+      // after them, one ahead at a time (a copy per step: no pair unrolling)
+      const uint32_t rest = off + kP * kTile;
+      if (rest < full_end) a = load_tile_full(rsrc, rest, lane16);
+#pragma unroll
+      for (uint32_t i = 0; i < kP; ++i) tile_step<MODE, false>(p, q, st, t[i], off + i * kTile, lane);
+      for (off = rest; off < full_end; off += kTile) {
+        if (off + kTile < full_end) b = load_tile_full(rsrc, off + kTile, lane16);
+        tile_step<MODE, false>(p, q, st, a, off, lane);
+        a = b;
+      }
+    } else {
+      // the loop runs on the tile's byte offset (the loads' SGPR offset; the
+      // second tile's + 1 KiB folds into the instruction's offset field) and
+      // only while its prefetch stays inside the full tiles: no clamp per
+      // step, the last one or two tiles after it
+      if (full_end > 2 * kTile) {
+        const uint32_t lim = full_end - 2 * kTile;   // (a bottom-tested loop: one compare per pair)
+        do {
+          b = load_tile_full(rsrc, off + kTile, lane16);
+          tile_step<MODE, false>(p, q, st, a, off, lane);
+          a = load_tile_full(rsrc, off + 2 * kTile, lane16);
+          tile_step<MODE, false>(p, q, st, b, off + kTile, lane);
+          off += 2 * kTile;
+        } while (off < lim);
+      }
+      if (off + kTile < full_end) {
         b = load_tile_full(rsrc, off + kTile, lane16);
         tile_step<MODE, false>(p, q, st, a, off, lane);
-        a = load_tile_full(rsrc, off + 2 * kTile, lane16);
         tile_step<MODE, false>(p, q, st, b, off + kTile, lane);
-        off += 2 * kTile;
-      } while (off < lim);
-    }
-    if (off + kTile < full_end) {
-      b = load_tile_full(rsrc, off + kTile, lane16);
-      tile_step<MODE, false>(p, q, st, a, off, lane);
-      tile_step<MODE, false>(p, q, st, b, off + kTile, lane);
-    } else {
-      tile_step<MODE, false>(p, q, st, a, off, lane);
+      } else {
+        tile_step<MODE, false>(p, q, st, a, off, lane);
+      }
     }
   }
   if (st.seg_len % kTile != 0)   // the ragged tail tile
@@ -2076,6 +2133,7 @@ hipError_t launch_scan(const ScanParams& p, int grid, hipStream_t s, int mode, h
     case 10: YAMD_LAUNCH_SCAN(scan_segments_kernel<10>); break;
     case 11: YAMD_LAUNCH_SCAN(scan_segments_kernel<11>); break;
     case 12: YAMD_LAUNCH_SCAN(scan_segments_kernel<12>); break;
+    case 13: YAMD_LAUNCH_SCAN(scan_segments_kernel<13>); break;
     case 24: YAMD_LAUNCH_SCAN(scan_segments_kernel<24>); break;
     case 25: YAMD_LAUNCH_SCAN(scan_segments_kernel<25>); break;
     case 101: case 102: case 103: case 104: {
@@ -2205,7 +2263,7 @@ hipError_t configure_scan_kernel() {
                         (const void*)scan_segments_kernel<6>, (const void*)scan_segments_kernel<7>,
                         (const void*)scan_segments_kernel<8>, (const void*)scan_segments_kernel<9>,
                         (const void*)scan_segments_kernel<10>, (const void*)scan_segments_kernel<11>,
-                        (const void*)scan_segments_kernel<12>,
+                        (const void*)scan_segments_kernel<12>, (const void*)scan_segments_kernel<13>,
                         (const void*)scan_segments_kernel<24>, (const void*)scan_segments_kernel<25>,
 #define YAMD_ABL_K(A) (const void*)scan_segments_kernel<100 * A + kModeByteKeys>,                  \
                       (const void*)scan_segments_kernel<100 * A + kModeByteKeysNext>,              \

@@ -543,7 +543,7 @@ int yr_amd__diag_key_classes(const yr_amd_tables* t, uint32_t* out) {
 }
 
 int yr_amd__diag_kernel_mode(yr_amd_scanner* s, int mode) {
-  if (s == nullptr || mode < 0 || (mode > 12 && mode != 24 && mode != 25 && (mode < 101 || mode > 104)))
+  if (s == nullptr || mode < 0 || (mode > 13 && mode != 24 && mode != 25 && (mode < 101 || mode > 104)))
     return YR_AMD_INVALID_ARGUMENT;
   s->diag_mode = mode;
   return YR_AMD_SUCCESS;
