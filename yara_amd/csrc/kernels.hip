@@ -19,13 +19,15 @@
 //   stage 2 (filter hits):  lanes that pass append their 20 bytes of window
 //             context, in position order, to a per-wave LDS ring; a drain
 //             (one entry per lane) re-tests the 16 positions, sends each hit
-//             through a first-level word filter (L2, loads deferred to the
-//             next tile step) and the survivors through bucketed two-choice
-//             tables (L2); exact hits are compacted in order (ballot + mbcnt /
-//             DPP prefix sums) into the segment's output.
+//             through a first-level word filter (L2) and the survivors
+//             through bucketed two-choice tables (L2); exact hits are
+//             compacted in order (ballot + mbcnt / DPP prefix sums) into the
+//             segment's output.
 //
 // Memory: the input is streamed once, 16 B per lane (1 KiB per wave per step,
-// buffer loads), tile t+1 in flight while tile t is filtered.  Roofline: HBM
+// buffer loads), tiles t+1 and t+2 in flight while tile t is filtered
+// (t+3 too in the 1-byte-key kernels, one ahead in the plain even-filter
+// kernel).  Roofline: HBM
 // read bandwidth (1 algorithmic byte per input byte); in practice the kernel
 // is VALU-issue bound.
 #include <hip/hip_ext.h>
@@ -170,17 +172,9 @@ __device__ __forceinline__ uint32_t pair_window(const uint32_t (&S)[6], uint32_t
 // dword per hit) over 64 entries; the few hits that pass it go, in order, to
 // a per-wave pending list of (window, offset) pairs, and the bucket probes
 // run once that list holds a wave's worth -- one lane per hit, one round
-// trip per 64 hits instead of one per drain.
-//
-// The first-level loads of a drain are not waited for in the drain: the
-// drain leaves each lane's (at most two) hit windows and the dword indices
-// to probe in the queue, every tile step issues exactly two first-level
-// loads at one program point (index 0, a harmless word, when nothing is
-// deferred), and the next tile step consumes them after its stage 1 -- the
-// L2 round trip overlaps a tile of filtering.  Issuing the loads
-// unconditionally keeps the vmcnt bookkeeping identical on every path, so
-// waiting for the next input tile never waits for them (loads complete in
-// order; a conditional load would make the compiler's merged wait cover it).
+// trip per 64 hits instead of one per drain.  (Rounds 1-5 deferred the
+// first-level loads to the next tile step; with more than one tile in flight
+// that costs more than it hides -- DESIGN.md section 5.2.)
 struct WaveQueue {
   uint32_t ring;    // LDS address: kQueueCap entries of kQueueEntryWords dwords
   uint32_t count;   // wave-uniform: entries in the ring (a drain takes all of them)
@@ -190,16 +184,8 @@ struct WaveQueue {
                     // stream flushed so far (verified-only scans leave the dead out)
   uint32_t dacc;    // wave-uniform (kDrainClass): the drains' dead not yet in `full`
   uint32_t kcv;     // per lane (byte-key kernels): the key class records (scan_key_rec)
-  uint32_t defer;   // wave-uniform: kDeferKey while the per-lane hits below await their
-                    // words, else 0 (a count above the ring's capacity: ring_append
-                    // tests "ring full or a drain to complete" with one scalar compare)
   uint32_t facc;    // per lane (byte-key kernels, kBkSkipF): OR of the stage-1 filter
                     // and 2-byte-key tests of the tiles queued since the last drain
-  // per lane, the first (a) and second (b) deferred hit: window, segment
-  // offset (kNoHit = none), byte offset into the first level (exact[kExactFl..]) that the next tile step
-  // loads (0 = none), the loaded word
-  uint32_t wa, oa, ia, da;
-  uint32_t wb, ob, ib, db;
 };
 
 // A key count read where it is tested: an opaque copy, so the compiler does not
@@ -210,8 +196,6 @@ __device__ __forceinline__ uint32_t uniform_count(uint32_t n) {
   return n;
 }
 
-constexpr uint32_t kNoHit = 0xFFFFFFFFu;
-constexpr uint32_t kDeferKey = 256u;   // WaveQueue::defer (> kQueueCap + kWave)
 // Kernel variant: the product kernel for rule sets whose 1-byte keys are tested
 // byte by byte in stage 1 (byte_keys_any below) instead of in the filter.
 constexpr int kModeByteKeys = 20;
@@ -620,65 +604,48 @@ __device__ __forceinline__ uint32_t byte_keys_mask(const uint32_t (&S)[6], const
 
 
 // Wave priorities: the streaming waves (stage 1, the appends) run at
-// s_setprio 1, a wave inside a drain or a deferred first-level completion at 0,
+// s_setprio 1, a wave inside a drain at 0,
 // so the arbiter issues the waves that keep the input stream going first while
 // a drain's long VALU burst fills the gaps (C -1.3 to -2.5 %, rx -2 %, B/E
 // within noise: profiles/r03_copy_prio_ab.json, r03_prio_ab.json,
 // r03_prio3_ab.json).
 //
-// Branch-weight hints on the tile step's rare paths (the deferred-drain
-// completion, an append that fills the ring, a tile without hits): the common
+// Branch-weight hints on the tile step's rare path (an append that fills the
+// ring): the common
 // path falls through with no taken branch (C -1.2 %).
 #define YAMD_EXPECT(c, v) __builtin_expect((c), (v))
-// The product and byte-key kernels hold the deferred words' registers until
-// the next loads are issued (issue_first_level): C 0.850 -> 0.835-0.843 ms,
-// the 1-byte-key sets 1.5-2 % faster; the even-position kernels not (B 2.7 %
-// slower, E equal), profiles/r02_hold_fl_ab.json.
-template <int MODE>
-constexpr bool kHoldFl = !kEven<MODE>;
-// Kernel variants whose drains defer their first-level loads (WaveQueue).  The
-// byte-key kernels run only for tables with 1-byte keys (launch_scan), so
-// their drains never defer (the deferral needs len_mask & 6 == 0): they carry
-// none of its per-tile machinery (the two first-level loads, the
-// deferred-drain test): rx -4.7 %, short -4.6 % (profiles/r04_ab_inproc.json h23).
 // Tiles in flight ahead of the one in the tile step (scan_segment).  Two
 // instead of one: C -4 %, rx -8 %, E -2 % (profiles/r06_prefetch_ab/) --
 // once the drains check the first level themselves instead of deferring its
-// loads to the next tile step (kDeferFl): vmcnt retires in issue order, so a
+// loads to the next tile step (rounds 1-5): vmcnt retires in issue order, so a
 // step that consumed the words loaded at the end of the previous one also
 // waited for the tile issued after them, and two tiles in flight measured no
-// faster with the deferral (round 2; r07c).  The deferral itself is worth
-// nothing now (C equal without it, r07c), so no kernel defers; the plain
+// faster with the deferral (round 2; r07c).  The deferral itself was worth
+// nothing by then (C equal without it, r07c) and is gone; the plain
 // even-position filter kernel without 1-byte keys (B) stays at one tile ahead
-// (two: +2 %).
-// (YAMD_PF / YAMD_PF_EVEN / YAMD_DEFER_FL: variant builds.)
+// (two: +2 %).  (YAMD_PF / YAMD_PF_EVEN / YAMD_PF_BK / YAMD_NO_PRIO:
+// variant builds; without the wave priorities C is 2-4 %
+// slower, rx and fuzz3 2-3 %, r07k.)
 #ifndef YAMD_PF
 #define YAMD_PF 2
 #endif
 #ifndef YAMD_PF_EVEN
 #define YAMD_PF_EVEN 1
 #endif
-#ifndef YAMD_DEFER_FL
-#define YAMD_DEFER_FL 0
+#ifndef YAMD_PF_BK
+#define YAMD_PF_BK 3   // (the 1-byte-key kernels: three ahead, rx -1.5-2 %, fuzz3 -1.3 % against two, r07k)
+#endif
+#ifndef YAMD_NO_PRIO
+#define YAMD_NO_PRIO 0
 #endif
 template <int MODE>
-constexpr uint32_t kPf = kBase<MODE> == kModeEven ? YAMD_PF_EVEN : YAMD_PF;
-template <int MODE>
-constexpr bool kDeferFl = YAMD_DEFER_FL && kAbl<MODE> != 1 && kPf<MODE> == 1 &&
-                          (MODE == 0 || MODE == 12 || kEven<MODE>) &&
-                          !(kByteKeys<MODE> || kByteKeyAblation<MODE>);
+constexpr uint32_t kPf = kBase<MODE> == kModeEven ? YAMD_PF_EVEN : kByteKeys<MODE> ? YAMD_PF_BK : YAMD_PF;
 // Byte-key drains re-test the filter and the 2-byte keys only when some tile
 // queued since the last drain passed them in stage 1 (a per-lane OR, one
 // v_or per tile, balloted once per drain): rx's drains skip ~90 of their ~140
 // VALU nearly always (its ring holds 1-byte-key hits).
 template <int MODE>
 constexpr bool kBkSkipF = kByteKeys<MODE> && kAbl<MODE> == 0;
-// Deferring drains without divergent branches (kernels other than the
-// even-filter byte-key ones, which measured 0.5-1.4 % slower with them): the
-// tile loop loses a loop-carried lane mask (six SALU per tile); C -0.6 %,
-// fuzz0 / fuzz3 -3 % (profiles/r04_ab_inproc.json call h22)
-template <int MODE>
-constexpr bool kAsyncFlat = !(kEven<MODE> && kByteKeys<MODE>);
 
 // The output entry of a certain candidate (its last byte a 1-byte key) at lane
 // byte j of ring entry ent: it needs no window for the exact check, so the scan
@@ -1043,52 +1010,13 @@ __device__ __forceinline__ void resolve_pending(const ScanParams& p, WaveQueue& 
   }
 }
 
-// Consume a deferred drain's first-level words: the lanes' hits that pass go,
-// in order, to the pending list.
-template <int MODE>
-__device__ __forceinline__ void drain_complete(const ScanParams& p, WaveQueue& q, uint32_t lane,
-                                               uint64_t seg_start, uint32_t* out, uint32_t& found) {
-  const bool ha = q.oa != kNoHit && first_level_test(q.da, q.wa);
-  const bool hb = q.ob != kNoHit && first_level_test(q.db, q.wb);
-  q.defer = 0u;
-  q.ia = q.ib = 0u;
-  // each lane's a-hit precedes its b-hit: lane L's first slot is the number of
-  // a- and b-hits in the lanes below it (two ballots and their mbcnts instead
-  // of a DPP scan)
-  const uint64_t ma = __ballot(ha), mb = __ballot(hb);
-  const uint32_t total = (uint32_t)(__popcll(ma) + __popcll(mb));
-  if (total == 0) return;
-  // in order to the pending list, bucket-probed (one round trip for 64 hits)
-  // each time it fills up
-  const uint32_t end = q.pend_n + total;
-  const uint32_t below = __builtin_amdgcn_mbcnt_hi(
-      (uint32_t)(mb >> 32),
-      __builtin_amdgcn_mbcnt_lo((uint32_t)mb,
-                                __builtin_amdgcn_mbcnt_hi((uint32_t)(ma >> 32),
-                                                          __builtin_amdgcn_mbcnt_lo((uint32_t)ma, q.pend_n))));
-  const uint32_t i0 = below, i1 = i0 + (uint32_t)ha;
-  for (uint32_t base = 0;; base += kWave) {
-    if (ha && i0 - base < kWave) lds_store2(q.pend + 8 * (i0 - base), q.wa, q.oa);
-    if (hb && i1 - base < kWave) lds_store2(q.pend + 8 * (i1 - base), q.wb, q.ob);
-    if (end <= base + kWave) {
-      q.pend_n = end - base;
-      return;
-    }
-    q.pend_n = kWave;
-    flush_pending<MODE>(p, q, lane, seg_start, out, found);
-  }
-}
-
 // First-level check of the hits of up to 64 ring entries; survivors go to
-// the pending list.  kAsync (drains inside a tile step): when no lane
-// has more than two hits, only compute the first-level indices and leave the
-// loads to the tile step (WaveQueue).
-template <int MODE, bool kAsync = false>
+// the pending list.  kInLoop: a drain inside the tile loop (a full ring),
+// whose entries all lie in full tiles.
+template <int MODE, bool kInLoop = false>
 __device__ __forceinline__ void drain(const ScanParams& p, WaveQueue& q, uint32_t lane,
                                       uint64_t seg_start, uint32_t seg_len, uint32_t* out,
                                       uint32_t& found) {
-  if constexpr (kDeferFl<MODE>)
-    if (q.defer) drain_complete<MODE>(p, q, lane, seg_start, out, found);
   const uint32_t n = q.count;   // <= kQueueCap = kWave
   q.count = 0;
   bool need_f = true;   // (kBkSkipF: some queued tile passed the filter / a 2-byte key)
@@ -1131,7 +1059,7 @@ __device__ __forceinline__ void drain(const ScanParams& p, WaveQueue& q, uint32_
     }
     // the segment's partial last tile (its entries are appended after the main
     // loop's last drain, so only the final drain can hold them)
-    if (!kAsync && off0 + kBytesPerLane > seg_len) {
+    if (!kInLoop && off0 + kBytesPerLane > seg_len) {
       const uint32_t lim = off0 >= seg_len ? 0u : seg_len - off0;
       m &= lim >= 16u ? 0xFFFFu : (1u << lim) - 1u;
     }
@@ -1142,41 +1070,6 @@ __device__ __forceinline__ void drain(const ScanParams& p, WaveQueue& q, uint32_
   // hits: the class code's wave-uniform values stay in SGPRs)
   if constexpr (kDrainClass<MODE>)
     dc = drain_classes<MODE>(p, q.kcv, S, eidx, m & kmask, kfirst & m, seg_start + off0);
-  if constexpr (kDeferFl<MODE> && kAsync) {
-    const uint32_t m2 = m & (m - 1u);
-    if ((p.len_mask & 6u) == 0u && __ballot((m2 & (m2 - 1u)) != 0u) == 0) {
-      if constexpr (kAsyncFlat<MODE>) {
-        // without branches (no lane mask for the compiler to carry through the
-        // tile loop): a lane without a hit reads its entry's byte 16 window, a
-        // harmless in-entry read, and keeps kNoHit / index 0
-        const uint32_t ja = (uint32_t)__builtin_ctz(m | 0x10000u), jb = (uint32_t)__builtin_ctz(m2 | 0x10000u);
-        q.wa = window4(ent, ja);
-        q.wb = window4(ent, jb);
-        q.oa = m != 0u ? off0 + ja : kNoHit;
-        q.ob = m2 != 0u ? off0 + jb : kNoHit;
-        q.ia = m != 0u ? fl_word(q.wa) * 4u : 0u;   // (issue_first_level adds kExactFl)
-        q.ib = m2 != 0u ? fl_word(q.wb) * 4u : 0u;
-      } else {
-        q.oa = q.ob = kNoHit;
-        q.wa = q.wb = 0u;
-        q.ia = q.ib = 0u;
-        if (m != 0u) {
-          const uint32_t j = (uint32_t)__builtin_ctz(m);
-          q.wa = window4(ent, j);
-          q.oa = off0 + j;
-          q.ia = fl_word(q.wa) * 4u;   // (issue_first_level adds kExactFl)
-        }
-        if (m2 != 0u) {
-          const uint32_t j = (uint32_t)__builtin_ctz(m2);
-          q.wb = window4(ent, j);
-          q.ob = off0 + j;
-          q.ib = fl_word(q.wb) * 4u;
-        }
-      }
-      q.defer = kDeferKey;
-      return;
-    }
-  }
   if ((MODE == 0 || kByteKeys<MODE> || kByteKeyAblation<MODE>) && (p.len_mask & 6u) != 0u) {
     maybe = m;   // 1-/2-byte keys: no first level, every hit goes to the buckets
   } else {
@@ -1507,10 +1400,9 @@ __device__ __forceinline__ void write_entry(uint32_t ent, const uint32_t (&S)[6]
 // The ordered append of a tile's hits to the wave ring.  TAIL: the segment's
 // last, partial tile (positions past seg_len are masked off).
 // The common path (~98 % of config C's tiles: some lane passes, the ring has
-// room, no deferred drain to complete) is straight-line scalar code: ONE
-// compare covers both rare paths (q.defer is kDeferKey, above any count, while
-// a deferred drain awaits its words), and a tile without a passing lane takes
-// it too -- its masked-off writes cost less than a branch around them
+// room) is straight-line scalar code: one compare for the rare path, and a
+// tile without a passing lane takes the common path too -- its masked-off
+// writes cost less than a branch around them
 // (tools/stage2_cost.sh: a SALU or branch instruction per tile costs config C
 // 2.5 us per 4 GiB, a VOP2 4.5 us).
 template <int MODE, bool TAIL>
@@ -1524,16 +1416,10 @@ __device__ __forceinline__ void ring_append(const ScanParams& p, WaveQueue& q, S
   }
   const uint64_t lanes = __ballot(any != 0);
   const uint32_t n = (uint32_t)__popcll(lanes);
-  if (YAMD_EXPECT(q.count + n + q.defer > kQueueCap, 0)) {
-    __builtin_amdgcn_s_setprio(0);   // (streaming waves first)
-    // (drain completes a deferred drain first; a deferred drain alone, its
-    // words loaded by the previous tile step, is completed here)
-    if (q.count + n > kQueueCap) {
-      drain<MODE, true>(p, q, lane, st.seg_start, st.seg_len, st.out, st.found);
-    } else if constexpr (kDeferFl<MODE>) {
-      drain_complete<MODE>(p, q, lane, st.seg_start, st.out, st.found);
-    }
-    __builtin_amdgcn_s_setprio(1);
+  if (YAMD_EXPECT(q.count + n > kQueueCap, 0)) {
+    if (!YAMD_NO_PRIO) __builtin_amdgcn_s_setprio(0);   // (streaming waves first)
+    drain<MODE, true>(p, q, lane, st.seg_start, st.seg_len, st.out, st.found);
+    if (!YAMD_NO_PRIO) __builtin_amdgcn_s_setprio(1);
   }
   if (any != 0) {
     // slot = count (scalar, folded into the base) + the appending lanes below
@@ -1577,28 +1463,6 @@ __device__ __forceinline__ void tile_context(SegState& st, const uint4& cur, uin
   S[3] = cur.z;
   S[4] = cur.w;
   S[5] = 0u;
-}
-
-// Every tile step: the two first-level loads of a drain it deferred, or of
-// word 0 (see WaveQueue).  (Relaxed wavefront-scope atomic loads: plain
-// global_load_dword, but "ordered", so the compiler cannot sink them into the
-// consumer's conditional block -- they must issue here.)
-template <int MODE>
-__device__ __forceinline__ void issue_first_level(const ScanParams& p, WaveQueue& q) {
-  if constexpr (kDeferFl<MODE>) {
-    if constexpr (kHoldFl<MODE>) {
-      // keep the previous words' registers live up to here, so the loads below
-      // land in registers nothing else in the tile step writes (otherwise the
-      // compiler reuses them, e.g. for the ring entry's lane index, and that
-      // write must wait for a possibly still outstanding load)
-      asm volatile("" : "+v"(q.da), "+v"(q.db));
-    }
-    const char* ex = reinterpret_cast<const char*>(p.exact + kExactFl);
-    q.da = __hip_atomic_load(reinterpret_cast<const uint32_t*>(ex + q.ia), __ATOMIC_RELAXED,
-                             __HIP_MEMORY_SCOPE_WAVEFRONT);
-    q.db = __hip_atomic_load(reinterpret_cast<const uint32_t*>(ex + q.ib), __ATOMIC_RELAXED,
-                             __HIP_MEMORY_SCOPE_WAVEFRONT);
-  }
 }
 
 // One 1 KiB tile: stage-1 filter over its 1024 byte positions, then the ordered
@@ -1656,12 +1520,10 @@ __device__ __forceinline__ void tile_step(const ScanParams& p, WaveQueue& q, Seg
   if constexpr (kAbl<MODE> == 1) {   // ablation: stage 1 only
     asm volatile("" ::"v"(any));
   } else {
-    // (a deferred drain is completed inside, on the append's rare path)
     ring_append<MODE, TAIL>(p, q, st, S, any, tile_off, lane);
   }
   // (after the append: a drain inside it takes only the earlier tiles' entries)
   if constexpr (kBkSkipF<MODE>) q.facc |= any_f;
-  issue_first_level<MODE>(p, q);
 }
 
 // Stream one segment [seg_start, seg_start + seg_len) of the block: full tiles
@@ -1698,19 +1560,14 @@ __device__ __forceinline__ void scan_segment(const ScanParams& p, WaveQueue& q, 
 
   // 4 bytes before the segment (warm-up halo); zeros before the block start.
   // (readfirstlane: waited for here, so no load is pending on the carry's
-  // register when the tile loop starts -- see WaveQueue on vmcnt)
+  // register when the tile loop starts)
   st.carry = __builtin_amdgcn_readfirstlane(
       st.seg_start >= 4 ? *reinterpret_cast<const uint32_t*>(base - 4) : 0u);
   q.count = 0;
   q.pend_n = 0;
   q.full = 0;
   q.dacc = 0;
-  q.defer = 0u;
   q.facc = 0u;
-  q.ia = q.ib = 0u;
-  q.da = q.db = 0u;
-  q.wa = q.wb = 0u;
-  q.oa = q.ob = kNoHit;
 
   const uint32_t n_full = st.seg_len / kTile;            // tiles needing no mask / bounds
   if (n_full > 0) {
@@ -1718,9 +1575,8 @@ __device__ __forceinline__ void scan_segment(const ScanParams& p, WaveQueue& q, 
     const __amdgpu_buffer_rsrc_t rsrc = segment_rsrc(base);
     const uint32_t lane16 = lane * kBytesPerLane;
     uint4 a = load_tile_full(rsrc, 0, lane16), b;
-    // waited for before the loop, so that no path into the loop arrives with
-    // a load pending on a (the loop's wait for its input tile would
-    // otherwise cover the deferred first-level loads too)
+    // waited for before the loop: no path into the loop arrives with a load
+    // pending on a (without the wait: equal, profiles/r06_prefetch_ab/r07m_*)
     asm volatile("" : "+v"(a.x), "+v"(a.y), "+v"(a.z), "+v"(a.w));
     uint32_t off = 0;
     // kPf tiles in flight ahead of the one in the step: kPf + 1 tile registers
@@ -1781,8 +1637,6 @@ __device__ __forceinline__ void scan_segment(const ScanParams& p, WaveQueue& q, 
                           lane);
   // everything queued to the segment's output, in order
   if (q.count != 0) drain<MODE>(p, q, lane, st.seg_start, st.seg_len, st.out, st.found);
-  if constexpr (kDeferFl<MODE>)
-    if (q.defer) drain_complete<MODE>(p, q, lane, st.seg_start, st.out, st.found);
   if (q.pend_n != 0) flush_pending<MODE>(p, q, lane, st.seg_start, st.out, st.found);
   if (lane == 0) {
     p.seg_count[seg] = st.found;
