@@ -1574,20 +1574,22 @@ __device__ __forceinline__ void scan_segment(const ScanParams& p, WaveQueue& q, 
     const uint32_t full_end = n_full * kTile;
     const __amdgpu_buffer_rsrc_t rsrc = segment_rsrc(base);
     const uint32_t lane16 = lane * kBytesPerLane;
-    uint4 a = load_tile_full(rsrc, 0, lane16), b;
-    // waited for before the loop: no path into the loop arrives with a load
-    // pending on a (without the wait: equal, profiles/r06_prefetch_ab/r07m_*)
-    asm volatile("" : "+v"(a.x), "+v"(a.y), "+v"(a.z), "+v"(a.w));
-    uint32_t off = 0;
     // kPf tiles in flight ahead of the one in the step: kPf + 1 tile registers
-    // in rotation, the loop unrolled over them; a segment too short for one
-    // round of it takes the one-ahead loop
+    // in rotation, the main loop unrolled over them (no copies, so no wait is
+    // attached to a copy); the loop runs on the tile's byte offset (the loads'
+    // SGPR offset; the tile's place in the round folds into the instruction's
+    // offset field), only while a round's loads stay inside the full tiles
     constexpr uint32_t kP = kPf<MODE>, kR = kP + 1;
-    if (kP > 1 && full_end >= (2 * kR - 1) * kTile) {
-      uint4 t[kR];
-      t[0] = a;
+    uint4 t[kR];
 #pragma unroll
-      for (uint32_t i = 1; i < kP; ++i) t[i] = load_tile_full(rsrc, i * kTile, lane16);
+    for (uint32_t i = 0; i < kP; ++i)
+      if (i * kTile < full_end) t[i] = load_tile_full(rsrc, i * kTile, lane16);
+    // the first tile waited for before the loop: no path into the loop
+    // arrives with a load pending on t[0] (without the wait: equal,
+    // profiles/r06_prefetch_ab/r07m_*)
+    asm volatile("" : "+v"(t[0].x), "+v"(t[0].y), "+v"(t[0].z), "+v"(t[0].w));
+    uint32_t off = 0;
+    if (full_end >= (2 * kR - 1) * kTile) {
       const uint32_t lim = full_end - (2 * kR - 1) * kTile;   // (every load of a round inside)
       do {
 #pragma unroll
@@ -1597,39 +1599,19 @@ __device__ __forceinline__ void scan_segment(const ScanParams& p, WaveQueue& q, 
         }
         off += kR * kTile;
       } while (off <= lim);
-      // t[0 .. kP - 1] hold the tiles at off ..; fewer than 2 kR tiles remain
-      // after them, one ahead at a time (a copy per step: no pair unrolling)
-      const uint32_t rest = off + kP * kTile;
-      if (rest < full_end) a = load_tile_full(rsrc, rest, lane16);
+    }
+    // the rest (fewer than 2 kR tiles; short segments all of theirs): the
+    // same rotation with every load and step guarded (scalar tests)
+    while (off < full_end) {
 #pragma unroll
-      for (uint32_t i = 0; i < kP; ++i) tile_step<MODE, false>(p, q, st, t[i], off + i * kTile, lane);
-      for (off = rest; off < full_end; off += kTile) {
-        if (off + kTile < full_end) b = load_tile_full(rsrc, off + kTile, lane16);
-        tile_step<MODE, false>(p, q, st, a, off, lane);
-        a = b;
+      for (uint32_t i = 0; i < kR; ++i) {
+        if (off + i * kTile < full_end) {
+          if (off + (i + kP) * kTile < full_end)
+            t[(i + kP) % kR] = load_tile_full(rsrc, off + (i + kP) * kTile, lane16);
+          tile_step<MODE, false>(p, q, st, t[i], off + i * kTile, lane);
+        }
       }
-    } else {
-      // the loop runs on the tile's byte offset (the loads' SGPR offset; the
-      // second tile's + 1 KiB folds into the instruction's offset field) and
-      // only while its prefetch stays inside the full tiles: no clamp per
-      // step, the last one or two tiles after it
-      if (full_end > 2 * kTile) {
-        const uint32_t lim = full_end - 2 * kTile;   // (a bottom-tested loop: one compare per pair)
-        do {
-          b = load_tile_full(rsrc, off + kTile, lane16);
-          tile_step<MODE, false>(p, q, st, a, off, lane);
-          a = load_tile_full(rsrc, off + 2 * kTile, lane16);
-          tile_step<MODE, false>(p, q, st, b, off + kTile, lane);
-          off += 2 * kTile;
-        } while (off < lim);
-      }
-      if (off + kTile < full_end) {
-        b = load_tile_full(rsrc, off + kTile, lane16);
-        tile_step<MODE, false>(p, q, st, a, off, lane);
-        tile_step<MODE, false>(p, q, st, b, off + kTile, lane);
-      } else {
-        tile_step<MODE, false>(p, q, st, a, off, lane);
-      }
+      off += kR * kTile;
     }
   }
   if (st.seg_len % kTile != 0)   // the ragged tail tile
