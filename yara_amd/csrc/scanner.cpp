@@ -824,7 +824,13 @@ int yr_amd_tables_set_strings(yr_amd_tables* t, const uint32_t* pool_string, uin
   int r = YR_AMD_SUCCESS;
   if (!r) r = upload(t->d_nodes, f.nodes.data(), f.nodes.size());
   if (!r) r = upload(t->d_pool, t->h_pool.data(), t->h_pool.size());
-  if (!r) r = upload(t->d_str_bytes, bytes, n_bytes);
+  {
+    // 64 bytes of padding: verify.hip stage_str reads three aligned 16-byte
+    // chunks from a string's start (one 16-byte chunk below it at most)
+    std::vector<uint8_t> padded((size_t)n_bytes + 64, 0);
+    if (n_bytes > 0) memcpy(padded.data(), bytes, (size_t)n_bytes);
+    if (!r) r = upload(t->d_str_bytes, padded.data(), padded.size());
+  }
   if (!r) r = upload(t->d_lowercase, lowercase, 256);
   if (r) return r;   // partial uploads are freed with the tables
   t->h_pool_string.assign(pool_string, pool_string + n_pool);

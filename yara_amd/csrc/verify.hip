@@ -126,6 +126,11 @@ __device__ __forceinline__ uint32_t node_head(const VerifyParams& p, uint64_t i,
 // covering the 32 bytes after (forward) or before (backward) the start; reads
 // outside it, or any read when the window would leave the block, go to memory.
 constexpr int kWinBytes = 48;
+#ifndef YAMD_STAGE_STR
+#define YAMD_STAGE_STR 1
+#endif
+constexpr uint32_t kCodeBytes = 48;   // (stage_code, stage_str: a second buffer per lane)
+constexpr uint32_t kNoLds = 0xFFFFFFFFu;
 struct ByteWindow {
   const uint8_t* lo;   // block address of window byte 0 (null: no window)
   uint32_t lds;        // LDS byte address of this lane's window
@@ -174,28 +179,59 @@ struct DirWindow {
   }
 };
 
+// A literal's string bytes for the comparisons below: its first bytes staged
+// like the input window -- three aligned 16-byte loads into this lane's code
+// buffer (a literal call stages no regexp code), issued with the window's --
+// so a comparison that runs past the atom's bytes costs no dependent load per
+// character.  (The string blob carries kCodeBytes of padding: the aligned
+// loads never leave it.)
+struct StrBytes {
+  const uint8_t* s;
+  uint32_t lds;   // LDS address of string byte 0 (kNoLds: none staged)
+  uint32_t n;     // bytes staged from s on
+};
+__device__ __forceinline__ StrBytes stage_str(const uint8_t* s, uint32_t buf) {
+  if (buf == kNoLds) return {s, kNoLds, 0u};
+  const uintptr_t a = (uintptr_t)s, lo = a & ~(uintptr_t)15;
+  typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
+  const u32x4* g = reinterpret_cast<const u32x4*>(lo);
+  const u32x4 c0 = g[0], c1 = g[1], c2 = g[2];
+  typedef __attribute__((address_space(3))) u32x4 lds_u4;
+  lds_u4* d = reinterpret_cast<lds_u4*>((uintptr_t)buf);
+  d[0] = c0;
+  d[1] = c1;
+  d[2] = c2;
+  const uint32_t head = (uint32_t)(a - lo);
+  return {s, buf + head, kCodeBytes - head};
+}
+__device__ __forceinline__ uint8_t str_byte(const StrBytes& t, uint32_t i) {
+  if (i < t.n)
+    return *reinterpret_cast<const __attribute__((address_space(3))) uint8_t*>((uintptr_t)(t.lds + i));
+  return t.s[i];
+}
+
 // _yr_scan_compare / _yr_scan_icompare (scan.c:142-179): forward match length
 // of the ascii form, 0 if none.
-__device__ bool cmp_ascii(const uint8_t* d, uint64_t avail, const uint8_t* s, uint32_t n,
+__device__ bool cmp_ascii(const uint8_t* d, uint64_t avail, const StrBytes& s, uint32_t n,
                           const uint8_t* lower, const ByteWindow& w) {
   if (avail < n) return false;
   if (lower == nullptr) {
     for (uint32_t i = 0; i < n; ++i)
-      if (window_byte(w, d + i) != s[i]) return false;
+      if (window_byte(w, d + i) != str_byte(s, i)) return false;
   } else {
     for (uint32_t i = 0; i < n; ++i)
-      if (lower[window_byte(w, d + i)] != lower[s[i]]) return false;
+      if (lower[window_byte(w, d + i)] != lower[str_byte(s, i)]) return false;
   }
   return true;
 }
 
 // _yr_scan_wcompare / _yr_scan_wicompare (scan.c:181-255): the wide form
 // (every character followed by 0x00).
-__device__ bool cmp_wide(const uint8_t* d, uint64_t avail, const uint8_t* s, uint32_t n,
+__device__ bool cmp_wide(const uint8_t* d, uint64_t avail, const StrBytes& s, uint32_t n,
                          const uint8_t* lower, const ByteWindow& w) {
   if (avail < 2ull * n) return false;
   for (uint32_t i = 0; i < n; ++i) {
-    const uint8_t a = window_byte(w, d + 2 * i), b = s[i];
+    const uint8_t a = window_byte(w, d + 2 * i), b = str_byte(s, i);
     if ((lower == nullptr ? a != b : lower[a] != lower[b]) || window_byte(w, d + 2 * i + 1) != 0)
       return false;
   }
@@ -204,17 +240,17 @@ __device__ bool cmp_wide(const uint8_t* d, uint64_t avail, const uint8_t* s, uin
 
 // _yr_scan_xor_compare (scan.c:62-101) and _yr_scan_xor_wcompare (:103-140):
 // key k = data[0] ^ string[0], then every byte (and, wide, every 0x00 ^ k).
-__device__ bool cmp_xor(const uint8_t* d, uint64_t avail, const uint8_t* s, uint32_t n, bool wide,
+__device__ bool cmp_xor(const uint8_t* d, uint64_t avail, const StrBytes& s, uint32_t n, bool wide,
                         const ByteWindow& w) {
   if (avail < (wide ? 2ull * n : (uint64_t)n)) return false;
   if (n == 0) return false;   // both reference loops yield 0 for an empty string
-  const uint8_t k = window_byte(w, d) ^ s[0];
+  const uint8_t k = window_byte(w, d) ^ str_byte(s, 0);
   for (uint32_t i = 0; i < n; ++i) {
     if (wide) {
-      if (window_byte(w, d + 2 * i) != (uint8_t)(s[i] ^ k) ||
+      if (window_byte(w, d + 2 * i) != (uint8_t)(str_byte(s, i) ^ k) ||
           (uint8_t)(window_byte(w, d + 2 * i + 1) ^ k) != 0)
         return false;
-    } else if (window_byte(w, d + i) != (uint8_t)(s[i] ^ k)) {
+    } else if (window_byte(w, d + i) != (uint8_t)(str_byte(s, i) ^ k)) {
       return false;
     }
   }
@@ -382,8 +418,6 @@ __device__ int fast_re_set(const Code code, uint32_t len, const uint8_t* __restr
 // independent 16-byte loads into this lane's kCodeBytes of LDS -- and
 // interpreted from there.  (The code blob is allocated with kCodeBytes of
 // padding, so the aligned loads never leave it.)
-constexpr uint32_t kCodeBytes = 48;
-constexpr uint32_t kNoLds = 0xFFFFFFFFu;
 __device__ __forceinline__ uint32_t stage_code(const uint8_t* code, uint32_t len, uint32_t buf) {
   const uintptr_t a = (uintptr_t)code, lo = a & ~(uintptr_t)15;
   const uint32_t head = (uint32_t)(a - lo);
@@ -771,7 +805,7 @@ __device__ bool call_matters(const VerifyParams& p, const DevPoolRec& st, uint64
   // _yr_scan_verify_literal_match, scan.c:907-972
   const uint8_t* d = p.data + offset;
   const uint64_t avail = p.size - offset;
-  const uint8_t* s = p.str_bytes + st.bytes_off;
+  const uint8_t* sp = p.str_bytes + st.bytes_off;
   const uint32_t n = st.length;
   uint64_t fm = 0;   // forward_matches
   ByteWindow w = {nullptr, lds};
@@ -781,6 +815,7 @@ __device__ bool call_matters(const VerifyParams& p, const DevPoolRec& st, uint64
     // the compared bytes from LDS (one round trip of 16-byte loads) instead of
     // one dependent byte load per character
     w = stage_window(p, d, false, lds);
+    const StrBytes s = YAMD_STAGE_STR ? stage_str(sp, codebuf) : StrBytes{sp, kNoLds, 0u};
     const uint8_t* lower = (st.flags & kStrNoCase) ? p.lowercase : nullptr;
     if ((st.flags & kStrAscii) && cmp_ascii(d, avail, s, n, lower, w)) fm = n;
     if (fm == 0 && (st.flags & kStrWide) && cmp_wide(d, avail, s, n, lower, w)) fm = 2ull * n;
